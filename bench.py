@@ -1,0 +1,242 @@
+#!/usr/bin/env python3
+"""bench.py — RBL iterations/sec on the north-star workload (BASELINE.json `metric`).
+
+Workload: seeded symmetric hash-window matrix, n = 1e7, ~100 nnz/row
+(half-width 64, density 0.7734), planted top spectrum, b = 32, k = 20, generated on the
+device (no host copy).  One bench "step" = one fixed-length RBL run: rbl_start (A*Omega +
+QR) and the m_max = ceil(1200/b) = 38 block iterations of RBL_gpu.jl:162 with convergence
+checks off (partial-reorth cost grows with i, so the step range is fixed).
+value = block iterations per second of the whole job.  Time-to-k=20 (convergence on, from
+start through Ritz vectors) is reported beside it.
+
+Multi-GPU: one process per GPU (torch.distributed.run); rows are partitioned over ranks
+(strong scaling: n fixed), SpMM halos and Gram all-reduces go over RCCL inside
+librbl_hip.so; torch.distributed (gloo) only carries the RCCL id, barriers and the max-time.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "gpu-randomized-block-lanczos_amd")
+for _p in (ROOT, PKG):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import numpy as np  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md)
+FP64_MFMA_PEAK_TF = 78.6     # MI355X dense fp64 matrix spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--n", type=int, default=10_000_000)
+    ap.add_argument("--b", type=int, default=32)
+    ap.add_argument("--k", type=int, default=20)
+    ap.add_argument("--halfwidth", type=int, default=64)
+    ap.add_argument("--density", type=float, default=0.7734)
+    ap.add_argument("--seed", type=int, default=20261015)
+    ap.add_argument("--kryl", type=int, default=1200)
+    ap.add_argument("--cpu-sample-n", type=int, default=100_000)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-ttk", action="store_true")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    ap.add_argument("--spmm-kernel", type=int, default=0)
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    def allmax(x: float) -> float:
+        if dist is None:
+            return x
+        import torch
+        t = torch.tensor([x], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def allsum(x: int) -> int:
+        if dist is None:
+            return x
+        import torch
+        t = torch.tensor([x], dtype=torch.int64)
+        dist.all_reduce(t)
+        return int(t.item())
+
+    import rbl
+    from rbl import _lib
+    uid = None
+    if world > 1:
+        buf = np.zeros(128, np.uint8)
+        if rank == 0:
+            st = _lib.lib.rbl_get_unique_id(_lib.u8ptr(buf))
+            assert st == 0, "rbl_get_unique_id failed"
+        obj = [bytes(buf)]
+        dist.broadcast_object_list(obj, src=0)
+        uid = obj[0]
+    ctx = rbl.Context(local_rank, nranks=world, rank=rank, unique_id=uid)
+
+    n, b, k = args.n, args.b, args.k
+    plant = np.array([100.0 * (2 * k + 1 - l) for l in range(1, 2 * k + 1)])
+    t0 = time.perf_counter()
+    ctx.gen_hashwindow(n, args.halfwidth, args.density, args.seed, plant)
+    gen_s = time.perf_counter() - t0
+    _, r0, r1, nnz_loc = ctx.matrix_info()
+    nloc = r1 - r0
+    nnz = allsum(nnz_loc)
+    ctx.set_option(_lib.RBL_OPT_TIMERS, 1)
+    ctx.set_option(_lib.RBL_OPT_SPMM_KERNEL, args.spmm_kernel)
+    m_max = rbl.rbl_gpu.max_steps_for(args.kryl, b)
+
+    def one_run():
+        rbl.lanczos(ctx, k, b, kryl_sz=args.kryl, seed=args.seed + 1, check=False, ritz=False)
+
+    for _ in range(args.warmup):
+        one_run()
+    barrier()
+    ctx.synchronize()
+    ctx.reset_timers()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        one_run()
+    ctx.synchronize()
+    barrier()
+    elapsed = allmax(time.perf_counter() - t0)
+    stage = ctx.timers()
+    K = args.steps
+    iters = K * m_max
+    value = iters / elapsed
+    stage_per_run = {s: v / K for s, v in stage.items()}
+
+    # ---- roofline: SpMM (HBM) and partial reorth (fp64 MFMA), live from HIP events ----
+    spmm_launches = K * (m_max + 1)               # rbl_start + one per block step
+    spmm_ms = stage["AQ"] / spmm_launches
+    # algorithmic bytes: nnz*(8+4) + (n+1)*8 + read Q + write U
+    # (+ read Q_{i-1} for the fused 3-term epilogue on the m_max step launches)
+    bytes_step = nnz_loc * 12 + (nloc + 1) * 8 + 3 * nloc * b * 8
+    bytes_start = nnz_loc * 12 + (nloc + 1) * 8 + 2 * nloc * b * 8
+    spmm_bytes = (m_max * bytes_step + bytes_start) / (m_max + 1)
+    spmm_gbs = spmm_bytes / (spmm_ms * 1e-3) / 1e9
+    reorth_flops = sum(8.0 * nloc * b * b * (i - 2) for i in range(4, m_max + 1, 2))
+    reorth_ms = stage_per_run["part reorth"]
+    reorth_tf = reorth_flops / (reorth_ms * 1e-3) / 1e12 if reorth_ms > 0 else 0.0
+    traffic = None
+    try:
+        with open(args.traffic_json) as f:
+            tj = json.load(f)
+        if tj.get("config", {}).get("n") == n and tj.get("config", {}).get("b") == b:
+            traffic = tj.get("spmm_hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        pass
+    roof_spmm = {"kernel": "spmm (AQ stage)", "bound": "hbm", "achieved": round(spmm_gbs, 1),
+                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(spmm_gbs / HBM_PEAK_GBS, 4),
+                 "traffic": traffic, "algorithmic_bytes_per_launch": int(spmm_bytes),
+                 "ms_per_launch": round(spmm_ms, 4)}
+    roof_reorth = {"kernel": "partial reorth (gram+update)", "bound": "mfma",
+                   "achieved": round(reorth_tf, 2), "peak": FP64_MFMA_PEAK_TF, "unit": "TFLOP/s",
+                   "frac": round(reorth_tf / FP64_MFMA_PEAK_TF, 4), "traffic": None,
+                   "algorithmic_flops_per_run": reorth_flops, "ms_per_run": round(reorth_ms, 3)}
+    if stage["part reorth"] > stage["AQ"]:
+        roofline, roofline2 = roof_reorth, roof_spmm
+    else:
+        roofline, roofline2 = roof_spmm, roof_reorth
+
+    # ---- time-to-k (convergence on, start -> converged Ritz vectors) ----
+    ttk = None
+    if not args.no_ttk:
+        barrier()
+        ctx.synchronize()
+        t0 = time.perf_counter()
+        D, V, info = rbl.lanczos(ctx, k, b, kryl_sz=args.kryl, seed=args.seed + 2, check=True,
+                                 ritz=True)
+        ctx.synchronize()
+        barrier()
+        ttk_s = allmax(time.perf_counter() - t0)
+        ttk = {"seconds": round(ttk_s, 4), "iters": info.iters, "converged": info.converged,
+               "k": k, "top_eigenvalues": [round(float(x), 6) for x in D[:3]]}
+
+    # ---- CPU baseline: the oracle (port of RBL.jl) on a bounded sample, rank 0, N = 1 ----
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args, m_max, plant)
+
+    if rank == 0:
+        line = {
+            "metric": "RBL iters/sec (n=1e7, nnz/row~100, b=32, 38 fixed block steps)",
+            "value": round(value, 3),
+            "unit": "block iterations/s",
+            "n_gpus": world,
+            "steps": K,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / K * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (seeded hash-window symmetric matrix generated on device)",
+            "config": {"workload": "C4a hash-window SpMM-Lanczos", "n": n, "nnz": nnz, "b": b,
+                       "k": k, "halfwidth": args.halfwidth, "density": args.density,
+                       "block_steps_per_run": m_max, "parallelism": f"rows{world}"},
+            "roofline": roofline,
+            "roofline_secondary": roofline2,
+            "stage_ms_per_run": {s: round(v, 3) for s, v in stage_per_run.items()},
+            "time_to_k": ttk,
+            "matrix_gen_s": round(gen_s, 3),
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    ctx.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(args, m_max, plant):
+    """Time the oracle (NumPy/SciPy port of RBL.jl) on n_s rows of the same generator for the
+    same 38 fixed block steps, and scale per-iteration time linearly to n (every stage of a
+    block step is O(n) at fixed b and m)."""
+    from oracle import matgen
+    from oracle import rbl_oracle as o
+    try:
+        from threadpoolctl import threadpool_info
+        threads = max([d.get("num_threads", 1) for d in threadpool_info()] or [1])
+    except Exception:
+        threads = 1
+    ns = args.cpu_sample_n
+    A = matgen.hashwindow_csr(ns, args.halfwidth, args.density, args.seed, plant)
+    omega = np.random.default_rng(0).standard_normal((ns, args.b))
+    t0 = time.perf_counter()
+    o.RBL_gpu_semantics(A, args.k, args.b, omega=omega, kryl_sz=args.kryl, check=False)
+    t = time.perf_counter() - t0
+    scale = args.n / ns
+    return {"value": round(m_max / (t * scale), 5), "unit": "block iterations/s",
+            "cores": threads, "kind": "port",
+            "sample": f"oracle RBL (RBL.jl restated, NumPy/SciPy; SpMM single-threaded) on the "
+                      f"same generator at n={ns} for the same {m_max} block steps in {t:.2f} s, "
+                      f"scaled x{scale:.0f} to n={args.n}",
+            "sample_seconds": round(t, 3)}
+
+
+if __name__ == "__main__":
+    main()

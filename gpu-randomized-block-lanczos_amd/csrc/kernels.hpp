@@ -1,0 +1,87 @@
+// kernels.hpp — host launchers for the gfx950 RBL kernels (implemented in *.hip).
+#pragma once
+#include "rbl_common.hpp"
+
+namespace rbl {
+
+// A list of n x w row-major panels ("blocks"): panel t starts at ptr[t] (t < count).
+// Used for Krylov blocks (w = b), the pair [Q_i, Q_{i-1}] and the Ritz output (w = k).
+struct Panels {
+  static constexpr int kMax = 2;
+  const double* ptr[kMax] = {nullptr, nullptr};
+  int count = 0;
+  int w = 0;              // width of each panel (leading dimension = w)
+};
+// Contiguous run of `count` panels of width w, panel j at base + j*stride (Krylov basis).
+struct PanelRun {
+  const double* base = nullptr;
+  int64_t stride = 0;
+  int count = 0;
+  int w = 0;
+};
+
+// CSR rows [0,nrows) of the local slice; columns are global ids; Q row c lives at
+// Qin + (c - col_off) * b.
+struct CsrDev {
+  int64_t nrows = 0;
+  int64_t nnz = 0;
+  const int64_t* rowptr = nullptr;
+  const int32_t* col = nullptr;
+  const double* val = nullptr;
+  // LDS-window metadata (per row tile): min/max column, and whether every tile fits.
+  const int64_t* tile_cmin = nullptr;
+  const int64_t* tile_cmax = nullptr;
+  int tile_rows = 0;
+  bool window_ok = false;
+};
+
+// --- spmm.hip ----------------------------------------------------------------------------
+// U = A * Qin  (+ epilogue U -= Qprev * Bt^T with Bt = B_i row-major b x b, if Qprev).
+// variant: 0 auto, 1 global gather, 2 LDS window.
+void spmm(const CsrDev& A, const double* Qin, int64_t col_off, int b, double* U,
+          const double* Qprev, const double* Bi, int variant, hipStream_t s);
+
+// --- tsmm.hip ----------------------------------------------------------------------------
+// Partial Gram:  slab[s][a][c] = sum over rows of split s of W[r][a] * X[r][c]
+//   W: run of nW panels (a in [0, nW*w)), X: panels (c in [0, X.count*X.w)).
+// Returns the number of splits used; slab must hold splits * (nW*w) * (X.count*X.w).
+int gram_splits(int64_t nrows, int nW, int w, int xcols);
+void gram_partial(int64_t nrows, const PanelRun& W, const Panels& X, double* slab, int splits,
+                  const int* skip, hipStream_t s);
+// out[e] = sum_s slab[s][e], e < len.
+void reduce_slab(const double* slab, int splits, int64_t len, double* out, const int* skip,
+                 hipStream_t s);
+// Y = beta*Y + alpha * X * C, X a run of panels (k = nX*X.w), C row-major k x (Y.count*Y.w)
+// with leading dimension ldc.  Y may alias X's panels row-for-row (in-place apply).
+void tsmm(int64_t nrows, const PanelRun& X, const double* C, int ldc, const Panels& Y,
+          double alpha, double beta, const int* skip, hipStream_t s);
+
+// --- smallmat.hip ------------------------------------------------------------------------
+// Cholesky step of (shifted) CholQR on the b x b Gram G (row-major, symmetric):
+//   mode 0: first pass — try unshifted; on breakdown or estimated cond > 3e7 use the
+//           Fukaya shift and set need3[0] = 1, need3[1] = 0 (so a third pass runs;
+//           need3[1] is the `skip` word of the third pass' kernels);
+//   mode 1: later pass — unshifted (falls back to shift if it still breaks).
+// Writes R (upper), Rinv, and Rtot = R * Rtot_prev (first pass: Rtot = R).
+// If *skip != 0 the kernel does nothing (used for the conditional third pass).
+void chol_step(const double* G, int b, int64_t nglobal, int mode, double* R, double* Rinv,
+               double* Rtot, int* need3, int* status, const int* skip, hipStream_t s);
+// dst = src (b x b), used to stash B_i for the next step's epilogue.
+void copy_small(const double* src, double* dst, int64_t len, hipStream_t s);
+
+// --- gen.hip ---------------------------------------------------------------------------
+// Hash-window matrix rows [r0,r1): counts per row, then fill given rowptr (0-based, local).
+void hw_count(int64_t n, int64_t W, double p, uint64_t seed, int64_t r0, int64_t r1,
+              int32_t* counts, hipStream_t s);
+void hw_fill(int64_t n, int64_t W, double p, uint64_t seed, int64_t r0, int64_t r1,
+             const int64_t* rowptr, int nplant, const double* plant_dev, int32_t* col,
+             double* val, hipStream_t s);
+// N(0,1) block, row-major n_local x b, global row offset r0, counter-based from seed.
+void randn_block(double* Q, int64_t nrows, int b, int64_t r0, uint64_t seed, hipStream_t s);
+// Per-tile column range of the CSR (tile = `tile_rows` rows), for the LDS-window SpMM.
+void tile_col_range(const CsrDev& A, int tile_rows, int64_t* cmin, int64_t* cmax, hipStream_t s);
+// column-major (ld = nrows) <-> row-major (ld = w) transposes for the boundary
+void colmajor_to_rowmajor(const double* src, int64_t nrows, int w, double* dst, hipStream_t s);
+void rowmajor_to_colmajor(const double* src, int64_t nrows, int w, double* dst, hipStream_t s);
+
+}  // namespace rbl

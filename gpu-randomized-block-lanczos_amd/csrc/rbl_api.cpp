@@ -1,0 +1,803 @@
+// rbl_api.cpp — the C-ABI of librbl_hip.so (include/rbl_hip.h).
+//
+// Host orchestration of one block Lanczos step on one GPU (or one rank of a row-partitioned
+// job).  Mirrors the device part of Julia/RBL_gpu.jl:134-203; the CPU part (T_j band,
+// dsbev, sort, convergence — Julia/common.jl) stays with the caller.
+//
+// HBM plan: A (CSR, int64 rowptr / int32 col / fp64 val), the WHOLE Krylov basis
+// (max_blocks+1 slots of n_local x b, row-major), U, one scratch block, the Gram slab and
+// b x b scalars.  Nothing but b x b blocks crosses PCIe per step.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/rbl_hip.h"
+#include "kernels.hpp"
+
+using namespace rbl;
+
+struct rbl_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  int nranks = 1, rank = 0;
+  ncclComm_t comm = nullptr;
+  std::string err;
+
+  // matrix (local rows [r0,r1) of an n x n symmetric matrix)
+  int64_t n = 0, r0 = 0, r1 = 0, nloc = 0, nnz = 0;
+  int64_t* d_rowptr = nullptr;
+  int32_t* d_col = nullptr;
+  double* d_val = nullptr;
+  int64_t* d_tcmin = nullptr;
+  int64_t* d_tcmax = nullptr;
+  int tile_rows = 256;
+  bool window_ok = false;
+  std::vector<int64_t> bounds;            // nranks+1
+  std::vector<int64_t> need_lo, need_hi;  // rows I need from rank q
+  std::vector<int64_t> give_lo, give_hi;  // rows rank q needs from me
+  int64_t ext_lo = 0, ext_hi = 0;         // global rows held in d_qext
+
+  // Krylov run
+  int b = 0, max_blocks = 0, nblocks = 0;
+  double* d_basis = nullptr;  // (max_blocks+1) slots
+  int64_t slot = 0;           // nloc * b
+  double* d_U = nullptr;
+  double* d_T = nullptr;      // scratch n_local x max(b,k)
+  int64_t T_cols = 0;
+  double* d_qext = nullptr;   // halo-extended Q_i (multi-rank)
+  double* d_slab = nullptr;
+  size_t slab_elems = 0;
+  double* d_C = nullptr;      // Gram result (<= (max_blocks)*b x 2b)
+  size_t C_elems = 0;
+  double* d_small = nullptr;  // R, Rinv, Rtot, Bprev, Ai, G (b x b each)
+  int* d_flags = nullptr;     // [need3, skip3, status0, status1]
+  double* h_pin = nullptr;    // pinned staging: Ai, Rtot (2 b x b)
+  bool have_bprev = false;
+
+  // options
+  bool timers = false;
+  int reorth_order = 0;
+  int spmm_variant = 0;
+  double stage_ms[RBL_NUM_STAGES] = {0};
+  struct Mark { int stage; hipEvent_t a, b; };
+  std::vector<Mark> marks;
+  std::vector<hipEvent_t> ev_pool;
+  size_t ev_used = 0;
+};
+
+namespace {
+
+const char* kStageNames[RBL_NUM_STAGES] = {"AQ", "3-term", "qr", "part reorth", "loc reorth",
+                                           "Ritz vectors", "comm"};
+
+int fail(rbl_ctx* c, int code, const std::string& msg) {
+  if (c) c->err = msg;
+  return code;
+}
+
+#define HIPC(expr)                                                                    \
+  do {                                                                                \
+    hipError_t _e = (expr);                                                           \
+    if (_e != hipSuccess)                                                             \
+      return fail(ctx, _e == hipErrorOutOfMemory ? RBL_ERR_OOM : RBL_ERR_HIP,          \
+                  std::string(#expr) + ": " + hipGetErrorString(_e));                 \
+  } while (0)
+#define NCCLC(expr)                                                                   \
+  do {                                                                                \
+    ncclResult_t _r = (expr);                                                         \
+    if (_r != ncclSuccess)                                                            \
+      return fail(ctx, RBL_ERR_RCCL, std::string(#expr) + ": " + ncclGetErrorString(_r)); \
+  } while (0)
+#define CHK(expr)             \
+  do {                        \
+    int _s = (expr);          \
+    if (_s < 0) return _s;    \
+  } while (0)
+
+double* slotp(rbl_ctx* ctx, int j) { return ctx->d_basis + (int64_t)j * ctx->slot; }
+
+CsrDev csr(rbl_ctx* ctx) {
+  CsrDev A;
+  A.nrows = ctx->nloc;
+  A.nnz = ctx->nnz;
+  A.rowptr = ctx->d_rowptr;
+  A.col = ctx->d_col;
+  A.val = ctx->d_val;
+  A.tile_cmin = ctx->d_tcmin;
+  A.tile_cmax = ctx->d_tcmax;
+  A.tile_rows = ctx->tile_rows;
+  A.window_ok = ctx->window_ok;
+  return A;
+}
+
+// ---- timers --------------------------------------------------------------------------
+hipEvent_t next_event(rbl_ctx* ctx) {
+  if (ctx->ev_used == ctx->ev_pool.size()) {
+    hipEvent_t e;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    ctx->ev_pool.push_back(e);
+  }
+  return ctx->ev_pool[ctx->ev_used++];
+}
+struct StageScope {
+  rbl_ctx* ctx;
+  int stage;
+  hipEvent_t a = nullptr;
+  StageScope(rbl_ctx* c, int s) : ctx(c), stage(s) {
+    if (ctx->timers) {
+      a = next_event(ctx);
+      if (a) hipEventRecord(a, ctx->stream);
+    }
+  }
+  ~StageScope() {
+    if (ctx->timers && a) {
+      hipEvent_t b = next_event(ctx);
+      if (b) {
+        hipEventRecord(b, ctx->stream);
+        ctx->marks.push_back({stage, a, b});
+      }
+    }
+  }
+};
+void harvest_timers(rbl_ctx* ctx) {  // after a stream sync
+  for (auto& m : ctx->marks) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, m.a, m.b) == hipSuccess) ctx->stage_ms[m.stage] += ms;
+  }
+  ctx->marks.clear();
+  ctx->ev_used = 0;
+}
+
+// ---- collectives ---------------------------------------------------------------------
+int allreduce(rbl_ctx* ctx, double* buf, size_t count) {
+  if (ctx->nranks == 1) return RBL_OK;
+  StageScope t(ctx, RBL_STAGE_COMM);
+  NCCLC(ncclAllReduce(buf, buf, count, ncclDouble, ncclSum, ctx->comm, ctx->stream));
+  return RBL_OK;
+}
+
+// Gram C = W^T X over all ranks.  C layout [nW*w][X.count*X.w].
+int gram(rbl_ctx* ctx, const PanelRun& W, const Panels& X, double* C, const int* skip) {
+  const int xcols = X.count * X.w;
+  const int splits = gram_splits(ctx->nloc, W.count, W.w, xcols);
+  const int64_t len = (int64_t)W.count * W.w * xcols;
+  if ((size_t)splits * len > ctx->slab_elems)
+    return fail(ctx, RBL_ERR_INVALID, "internal: Gram slab too small");
+  if (ctx->nloc > 0) {
+    gram_partial(ctx->nloc, W, X, ctx->d_slab, splits, skip, ctx->stream);
+    reduce_slab(ctx->d_slab, splits, len, C, skip, ctx->stream);
+  } else {
+    HIPC(hipMemsetAsync(C, 0, len * sizeof(double), ctx->stream));
+  }
+  HIPC(hipGetLastError());
+  return allreduce(ctx, C, (size_t)len);
+}
+
+PanelRun run1(const double* p, int w) {
+  PanelRun r;
+  r.base = p;
+  r.stride = 0;
+  r.count = 1;
+  r.w = w;
+  return r;
+}
+Panels pan1(const double* p, int w) {
+  Panels x;
+  x.ptr[0] = p;
+  x.count = 1;
+  x.w = w;
+  return x;
+}
+Panels pan2(const double* p0, const double* p1, int w) {
+  Panels x;
+  x.ptr[0] = p0;
+  x.ptr[1] = p1;
+  x.count = 2;
+  x.w = w;
+  return x;
+}
+
+// small-buffer carve (b x b each)
+enum { S_R = 0, S_RINV, S_RTOT, S_BPREV, S_AI, S_G, S_NSMALL };
+double* smallp(rbl_ctx* ctx, int which) { return ctx->d_small + (int64_t)which * ctx->b * ctx->b; }
+
+int tsmm_checked(rbl_ctx* ctx, const PanelRun& X, const double* C, int ldc, const Panels& Y,
+                 double alpha, double beta, const int* skip) {
+  if (ctx->nloc <= 0) return RBL_OK;
+  tsmm(ctx->nloc, X, C, ldc, Y, alpha, beta, skip, ctx->stream);
+  HIPC(hipGetLastError());
+  return RBL_OK;
+}
+
+// Tall-skinny QR of U (n_local x b) into Qout; B = R (b x b, upper, row-major) in S_RTOT.
+int tsqr(rbl_ctx* ctx, const double* U, double* Qout) {
+  StageScope t(ctx, RBL_STAGE_QR);
+  const int b = ctx->b;
+  int* need3 = ctx->d_flags;      // [need3, skip3]
+  int* status = ctx->d_flags + 2; // [breakdown, shifted count]
+  double* G = smallp(ctx, S_G);
+  // pass 1 (shift decided on device)
+  CHK(gram(ctx, run1(U, b), pan1(U, b), G, nullptr));
+  chol_step(G, b, ctx->n, 0, smallp(ctx, S_R), smallp(ctx, S_RINV), smallp(ctx, S_RTOT), need3,
+            status, nullptr, ctx->stream);
+  CHK(tsmm_checked(ctx, run1(U, b), smallp(ctx, S_RINV), b, pan1(Qout, b), 1.0, 0.0, nullptr));
+  // pass 2
+  CHK(gram(ctx, run1(Qout, b), pan1(Qout, b), G, nullptr));
+  chol_step(G, b, ctx->n, 1, smallp(ctx, S_R), smallp(ctx, S_RINV), smallp(ctx, S_RTOT), need3,
+            status, nullptr, ctx->stream);
+  CHK(tsmm_checked(ctx, run1(Qout, b), smallp(ctx, S_RINV), b, pan1(Qout, b), 1.0, 0.0, nullptr));
+  // pass 3 only after a shifted first pass (device flag; kernels early-exit otherwise)
+  const int* skip3 = need3 + 1;
+  CHK(gram(ctx, run1(Qout, b), pan1(Qout, b), G, skip3));
+  chol_step(G, b, ctx->n, 1, smallp(ctx, S_R), smallp(ctx, S_RINV), smallp(ctx, S_RTOT), need3,
+            status, skip3, ctx->stream);
+  CHK(tsmm_checked(ctx, run1(Qout, b), smallp(ctx, S_RINV), b, pan1(Qout, b), 1.0, 0.0, skip3));
+  HIPC(hipGetLastError());
+  return RBL_OK;
+}
+
+// Bring Q (n_local x b, local rows) into the halo-extended buffer for SpMM.
+int halo_exchange(rbl_ctx* ctx, const double* Q, const double** Qin, int64_t* off) {
+  if (ctx->nranks == 1) {
+    *Qin = Q;
+    *off = 0;
+    return RBL_OK;
+  }
+  StageScope t(ctx, RBL_STAGE_COMM);
+  const int b = ctx->b;
+  double* ext = ctx->d_qext;
+  HIPC(hipMemcpyAsync(ext + (ctx->r0 - ctx->ext_lo) * b, Q, ctx->nloc * b * sizeof(double),
+                      hipMemcpyDeviceToDevice, ctx->stream));
+  NCCLC(ncclGroupStart());
+  for (int q = 0; q < ctx->nranks; ++q) {
+    if (q == ctx->rank) continue;
+    const int64_t gl = ctx->give_lo[q], gh = ctx->give_hi[q];
+    if (gh > gl)
+      NCCLC(ncclSend(Q + (gl - ctx->r0) * b, (size_t)(gh - gl) * b, ncclDouble, q, ctx->comm,
+                     ctx->stream));
+    const int64_t nl = ctx->need_lo[q], nh = ctx->need_hi[q];
+    if (nh > nl)
+      NCCLC(ncclRecv(ext + (nl - ctx->ext_lo) * b, (size_t)(nh - nl) * b, ncclDouble, q, ctx->comm,
+                     ctx->stream));
+  }
+  NCCLC(ncclGroupEnd());
+  *Qin = ext;
+  *off = ctx->ext_lo;
+  return RBL_OK;
+}
+
+void free_run(rbl_ctx* ctx) {
+  hipFree(ctx->d_basis); ctx->d_basis = nullptr;
+  hipFree(ctx->d_U); ctx->d_U = nullptr;
+  hipFree(ctx->d_T); ctx->d_T = nullptr;
+  hipFree(ctx->d_qext); ctx->d_qext = nullptr;
+  hipFree(ctx->d_slab); ctx->d_slab = nullptr;
+  hipFree(ctx->d_C); ctx->d_C = nullptr;
+  hipFree(ctx->d_small); ctx->d_small = nullptr;
+  hipFree(ctx->d_flags); ctx->d_flags = nullptr;
+  if (ctx->h_pin) hipHostFree(ctx->h_pin);
+  ctx->h_pin = nullptr;
+  ctx->nblocks = 0;
+  ctx->b = 0;
+  ctx->have_bprev = false;
+}
+
+void free_matrix(rbl_ctx* ctx) {
+  hipFree(ctx->d_rowptr); ctx->d_rowptr = nullptr;
+  hipFree(ctx->d_col); ctx->d_col = nullptr;
+  hipFree(ctx->d_val); ctx->d_val = nullptr;
+  hipFree(ctx->d_tcmin); ctx->d_tcmin = nullptr;
+  hipFree(ctx->d_tcmax); ctx->d_tcmax = nullptr;
+  ctx->n = ctx->nloc = ctx->nnz = 0;
+}
+
+// Exchange halo needs among ranks and size the extended buffer.
+int setup_halo(rbl_ctx* ctx) {
+  const int P = ctx->nranks;
+  ctx->give_lo.assign(P, 0);
+  ctx->give_hi.assign(P, 0);
+  ctx->ext_lo = ctx->r0;
+  ctx->ext_hi = ctx->r1;
+  if (P == 1) return RBL_OK;
+  for (int q = 0; q < P; ++q) {
+    if (q == ctx->rank || ctx->need_hi[q] <= ctx->need_lo[q]) continue;
+    ctx->ext_lo = std::min(ctx->ext_lo, ctx->need_lo[q]);
+    ctx->ext_hi = std::max(ctx->ext_hi, ctx->need_hi[q]);
+  }
+  // all-gather the (lo,hi) need tables: row p of the table = what rank p needs from each q
+  std::vector<int64_t> mine(2 * P);
+  for (int q = 0; q < P; ++q) {
+    mine[2 * q] = ctx->need_lo[q];
+    mine[2 * q + 1] = ctx->need_hi[q];
+  }
+  int64_t *d_in = nullptr, *d_out = nullptr;
+  HIPC(hipMalloc(&d_in, 2 * P * sizeof(int64_t)));
+  HIPC(hipMalloc(&d_out, 2 * P * P * sizeof(int64_t)));
+  HIPC(hipMemcpy(d_in, mine.data(), 2 * P * sizeof(int64_t), hipMemcpyHostToDevice));
+  NCCLC(ncclAllGather(d_in, d_out, 2 * P, ncclInt64, ctx->comm, ctx->stream));
+  std::vector<int64_t> all(2 * P * P);
+  HIPC(hipMemcpyAsync(all.data(), d_out, all.size() * sizeof(int64_t), hipMemcpyDeviceToHost,
+                      ctx->stream));
+  HIPC(hipStreamSynchronize(ctx->stream));
+  hipFree(d_in);
+  hipFree(d_out);
+  for (int p = 0; p < P; ++p) {
+    if (p == ctx->rank) continue;
+    ctx->give_lo[p] = all[(size_t)p * 2 * P + 2 * ctx->rank];
+    ctx->give_hi[p] = all[(size_t)p * 2 * P + 2 * ctx->rank + 1];
+  }
+  return RBL_OK;
+}
+
+// Upload a local CSR (0-based rowptr relative to the slice, global 0-based int64 columns).
+int upload_csr(rbl_ctx* ctx, int64_t n, int64_t r0, int64_t r1, const int64_t* rowptr,
+               const int64_t* colind, const double* val, int64_t base_ptr, int64_t base_idx) {
+  free_run(ctx);
+  free_matrix(ctx);
+  const int64_t m = r1 - r0;
+  const int64_t nnz = rowptr[m] - rowptr[0];
+  std::vector<int64_t> rp(m + 1);
+  for (int64_t i = 0; i <= m; ++i) rp[i] = rowptr[i] - rowptr[0];
+  std::vector<int32_t> ci(nnz);
+  const int64_t e0 = rowptr[0] - base_ptr;
+  for (int64_t e = 0; e < nnz; ++e) {
+    const int64_t c = colind[e0 + e] - base_idx;
+    if (c < 0 || c >= n) return fail(ctx, RBL_ERR_INVALID, "column index out of range");
+    if (c > INT32_MAX) return fail(ctx, RBL_ERR_INVALID, "n exceeds int32 column ids");
+    ci[e] = (int32_t)c;
+  }
+  // rows must be column-sorted (SparseArrays guarantees it; the window kernel relies on it)
+  for (int64_t i = 0; i < m; ++i)
+    for (int64_t e = rp[i] + 1; e < rp[i + 1]; ++e)
+      if (ci[e] < ci[e - 1]) return fail(ctx, RBL_ERR_INVALID, "row indices not sorted");
+  ctx->n = n;
+  ctx->r0 = r0;
+  ctx->r1 = r1;
+  ctx->nloc = m;
+  ctx->nnz = nnz;
+  HIPC(hipMalloc(&ctx->d_rowptr, (m + 1) * sizeof(int64_t)));
+  HIPC(hipMalloc(&ctx->d_col, std::max<int64_t>(nnz, 1) * sizeof(int32_t)));
+  HIPC(hipMalloc(&ctx->d_val, std::max<int64_t>(nnz, 1) * sizeof(double)));
+  HIPC(hipMemcpy(ctx->d_rowptr, rp.data(), (m + 1) * sizeof(int64_t), hipMemcpyHostToDevice));
+  if (nnz) {
+    HIPC(hipMemcpy(ctx->d_col, ci.data(), nnz * sizeof(int32_t), hipMemcpyHostToDevice));
+    HIPC(hipMemcpy(ctx->d_val, val + e0, nnz * sizeof(double), hipMemcpyHostToDevice));
+  }
+  // halo needs: column footprint per owning rank
+  const int P = ctx->nranks;
+  ctx->need_lo.assign(P, 0);
+  ctx->need_hi.assign(P, 0);
+  if (P > 1) {
+    std::vector<int64_t> lo(P), hi(P);
+    for (int q = 0; q < P; ++q) { lo[q] = INT64_MAX; hi[q] = -1; }
+    for (int64_t e = 0; e < nnz; ++e) {
+      const int64_t c = ci[e];
+      const int q = (int)(std::upper_bound(ctx->bounds.begin(), ctx->bounds.end(), c) -
+                          ctx->bounds.begin()) - 1;
+      lo[q] = std::min(lo[q], c);
+      hi[q] = std::max(hi[q], c + 1);
+    }
+    for (int q = 0; q < P; ++q) {
+      ctx->need_lo[q] = hi[q] < 0 ? 0 : lo[q];
+      ctx->need_hi[q] = hi[q] < 0 ? 0 : hi[q];
+    }
+  }
+  return setup_halo(ctx);
+}
+
+}  // namespace
+
+// =========================================================================================
+extern "C" {
+
+int rbl_abi_version(void) { return RBL_ABI_VERSION; }
+
+int rbl_create(rbl_ctx** out, int device) {
+  if (!out) return RBL_ERR_INVALID;
+  rbl_ctx* ctx = new rbl_ctx();
+  ctx->device = device;
+  *out = ctx;
+  HIPC(hipSetDevice(device));
+  HIPC(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
+  ctx->bounds = {0, 0};
+  return RBL_OK;
+}
+
+int rbl_get_unique_id(uint8_t unique_id[128]) {
+  ncclUniqueId id;
+  if (ncclGetUniqueId(&id) != ncclSuccess) return RBL_ERR_RCCL;
+  static_assert(sizeof(id) == 128, "ncclUniqueId size");
+  memcpy(unique_id, &id, 128);
+  return RBL_OK;
+}
+
+int rbl_create_dist(rbl_ctx** out, int device, int nranks, int rank, const uint8_t unique_id[128]) {
+  if (!out || nranks < 1 || rank < 0 || rank >= nranks) return RBL_ERR_INVALID;
+  int s = rbl_create(out, device);
+  if (s != RBL_OK) return s;
+  rbl_ctx* ctx = *out;
+  ctx->nranks = nranks;
+  ctx->rank = rank;
+  if (nranks > 1) {
+    ncclUniqueId id;
+    memcpy(&id, unique_id, 128);
+    NCCLC(ncclCommInitRank(&ctx->comm, nranks, id, rank));
+  }
+  return RBL_OK;
+}
+
+int rbl_free(rbl_ctx* ctx) {
+  if (!ctx) return RBL_OK;
+  hipSetDevice(ctx->device);
+  if (ctx->stream) hipStreamSynchronize(ctx->stream);
+  free_run(ctx);
+  free_matrix(ctx);
+  for (auto e : ctx->ev_pool) hipEventDestroy(e);
+  if (ctx->comm) ncclCommDestroy(ctx->comm);
+  if (ctx->stream) hipStreamDestroy(ctx->stream);
+  delete ctx;
+  return RBL_OK;
+}
+
+const char* rbl_last_error(const rbl_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int rbl_set_option(rbl_ctx* ctx, int option, int64_t value) {
+  if (!ctx) return RBL_ERR_INVALID;
+  switch (option) {
+    case RBL_OPT_TIMERS: ctx->timers = value != 0; return RBL_OK;
+    case RBL_OPT_REORTH_ORDER:
+      if (value < 0 || value > 1) return fail(ctx, RBL_ERR_INVALID, "reorth order must be 0|1");
+      ctx->reorth_order = (int)value;
+      return RBL_OK;
+    case RBL_OPT_SPMM_KERNEL:
+      if (value < 0 || value > 2) return fail(ctx, RBL_ERR_INVALID, "spmm kernel must be 0|1|2");
+      ctx->spmm_variant = (int)value;
+      return RBL_OK;
+    default: return fail(ctx, RBL_ERR_INVALID, "unknown option");
+  }
+}
+
+int rbl_set_matrix_csc(rbl_ctx* ctx, int64_t n, int64_t nnz, const int64_t* colptr,
+                       const int64_t* rowval, const double* nzval, int index_base) {
+  if (!ctx || n < 1 || nnz < 0 || !colptr || (nnz && (!rowval || !nzval)) ||
+      (index_base != 0 && index_base != 1))
+    return fail(ctx, RBL_ERR_INVALID, "rbl_set_matrix_csc: bad arguments");
+  if (colptr[n] - colptr[0] != nnz) return fail(ctx, RBL_ERR_INVALID, "colptr[n] != nnz");
+  HIPC(hipSetDevice(ctx->device));
+  // symmetric: column slice [r0,r1) of CSC == row slice of CSR
+  std::vector<int64_t> rp(n + 1);
+  for (int64_t i = 0; i <= n; ++i) rp[i] = colptr[i] - colptr[0];
+  ctx->bounds.assign(ctx->nranks + 1, 0);
+  rbl_plan_row_partition(n, rp.data(), ctx->nranks, ctx->bounds.data());
+  const int64_t r0 = ctx->bounds[ctx->rank], r1 = ctx->bounds[ctx->rank + 1];
+  return upload_csr(ctx, n, r0, r1, colptr + r0, rowval, nzval, index_base, index_base);
+}
+
+int rbl_set_matrix_csr_rows(rbl_ctx* ctx, int64_t n, int64_t row_begin, int64_t row_end,
+                            const int64_t* rowptr, const int64_t* colind, const double* val,
+                            int index_base) {
+  if (!ctx || n < 1 || row_begin < 0 || row_end < row_begin || row_end > n || !rowptr ||
+      (index_base != 0 && index_base != 1))
+    return fail(ctx, RBL_ERR_INVALID, "rbl_set_matrix_csr_rows: bad arguments");
+  HIPC(hipSetDevice(ctx->device));
+  // the partition is the callers' (every rank's [row_begin,row_end) must tile [0,n))
+  if (ctx->nranks > 1) {
+    int64_t *d = nullptr, *d_all = nullptr;
+    int64_t mine[2] = {row_begin, row_end};
+    HIPC(hipMalloc(&d, 2 * sizeof(int64_t)));
+    HIPC(hipMalloc(&d_all, 2 * ctx->nranks * sizeof(int64_t)));
+    HIPC(hipMemcpy(d, mine, sizeof(mine), hipMemcpyHostToDevice));
+    NCCLC(ncclAllGather(d, d_all, 2, ncclInt64, ctx->comm, ctx->stream));
+    std::vector<int64_t> all(2 * ctx->nranks);
+    HIPC(hipMemcpyAsync(all.data(), d_all, all.size() * sizeof(int64_t), hipMemcpyDeviceToHost,
+                        ctx->stream));
+    HIPC(hipStreamSynchronize(ctx->stream));
+    hipFree(d);
+    hipFree(d_all);
+    ctx->bounds.assign(ctx->nranks + 1, 0);
+    for (int p = 0; p < ctx->nranks; ++p) {
+      if (all[2 * p] != (p == 0 ? 0 : all[2 * p - 1]))
+        return fail(ctx, RBL_ERR_INVALID, "row slices must tile [0,n) in rank order");
+      ctx->bounds[p + 1] = all[2 * p + 1];
+    }
+    if (ctx->bounds[ctx->nranks] != n) return fail(ctx, RBL_ERR_INVALID, "row slices != n");
+  } else {
+    if (row_begin != 0 || row_end != n)
+      return fail(ctx, RBL_ERR_INVALID, "single rank must own all rows");
+    ctx->bounds = {0, n};
+  }
+  return upload_csr(ctx, n, row_begin, row_end, rowptr, colind, val, index_base, index_base);
+}
+
+int rbl_gen_matrix_hashwindow(rbl_ctx* ctx, int64_t n, int64_t halfwidth, double density,
+                              uint64_t seed, int nplant, const double* plant) {
+  if (!ctx || n < 1 || halfwidth < 0 || nplant < 0 || (nplant > 0 && !plant) || n > INT32_MAX)
+    return fail(ctx, RBL_ERR_INVALID, "rbl_gen_matrix_hashwindow: bad arguments");
+  HIPC(hipSetDevice(ctx->device));
+  free_run(ctx);
+  free_matrix(ctx);
+  const int P = ctx->nranks;
+  ctx->bounds.assign(P + 1, 0);
+  for (int p = 0; p <= P; ++p) ctx->bounds[p] = n * p / P;  // uniform rows: ~uniform nnz
+  const int64_t r0 = ctx->bounds[ctx->rank], r1 = ctx->bounds[ctx->rank + 1], m = r1 - r0;
+  ctx->n = n;
+  ctx->r0 = r0;
+  ctx->r1 = r1;
+  ctx->nloc = m;
+  int32_t* d_cnt = nullptr;
+  HIPC(hipMalloc(&d_cnt, std::max<int64_t>(m, 1) * sizeof(int32_t)));
+  hw_count(n, halfwidth, density, seed, r0, r1, d_cnt, ctx->stream);
+  std::vector<int32_t> cnt(m);
+  HIPC(hipMemcpyAsync(cnt.data(), d_cnt, m * sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
+  HIPC(hipStreamSynchronize(ctx->stream));
+  hipFree(d_cnt);
+  std::vector<int64_t> rp(m + 1, 0);
+  for (int64_t i = 0; i < m; ++i) rp[i + 1] = rp[i] + cnt[i];
+  ctx->nnz = rp[m];
+  HIPC(hipMalloc(&ctx->d_rowptr, (m + 1) * sizeof(int64_t)));
+  HIPC(hipMalloc(&ctx->d_col, std::max<int64_t>(ctx->nnz, 1) * sizeof(int32_t)));
+  HIPC(hipMalloc(&ctx->d_val, std::max<int64_t>(ctx->nnz, 1) * sizeof(double)));
+  HIPC(hipMemcpy(ctx->d_rowptr, rp.data(), (m + 1) * sizeof(int64_t), hipMemcpyHostToDevice));
+  double* d_plant = nullptr;
+  if (nplant > 0) {
+    HIPC(hipMalloc(&d_plant, nplant * sizeof(double)));
+    HIPC(hipMemcpy(d_plant, plant, nplant * sizeof(double), hipMemcpyHostToDevice));
+  }
+  hw_fill(n, halfwidth, density, seed, r0, r1, ctx->d_rowptr, nplant, d_plant, ctx->d_col,
+          ctx->d_val, ctx->stream);
+  HIPC(hipGetLastError());
+  HIPC(hipStreamSynchronize(ctx->stream));
+  hipFree(d_plant);
+  ctx->need_lo.assign(P, 0);
+  ctx->need_hi.assign(P, 0);
+  for (int q = 0; q < P; ++q) {  // analytic footprint of the window
+    const int64_t lo = std::max(ctx->bounds[q], std::max<int64_t>(0, r0 - halfwidth));
+    const int64_t hi = std::min(ctx->bounds[q + 1], std::min<int64_t>(n, r1 + halfwidth));
+    if (hi > lo && q != ctx->rank) {
+      ctx->need_lo[q] = lo;
+      ctx->need_hi[q] = hi;
+    }
+  }
+  return setup_halo(ctx);
+}
+
+int rbl_matrix_info(rbl_ctx* ctx, int64_t* n, int64_t* row_begin, int64_t* row_end,
+                    int64_t* nnz_local) {
+  if (!ctx) return RBL_ERR_INVALID;
+  if (n) *n = ctx->n;
+  if (row_begin) *row_begin = ctx->r0;
+  if (row_end) *row_end = ctx->r1;
+  if (nnz_local) *nnz_local = ctx->nnz;
+  return RBL_OK;
+}
+
+int rbl_get_matrix_csr(rbl_ctx* ctx, int64_t* rowptr, int32_t* colind, double* val) {
+  if (!ctx || !ctx->d_rowptr) return fail(ctx, RBL_ERR_STATE, "no matrix");
+  HIPC(hipSetDevice(ctx->device));
+  if (rowptr)
+    HIPC(hipMemcpy(rowptr, ctx->d_rowptr, (ctx->nloc + 1) * sizeof(int64_t), hipMemcpyDeviceToHost));
+  if (colind && ctx->nnz)
+    HIPC(hipMemcpy(colind, ctx->d_col, ctx->nnz * sizeof(int32_t), hipMemcpyDeviceToHost));
+  if (val && ctx->nnz)
+    HIPC(hipMemcpy(val, ctx->d_val, ctx->nnz * sizeof(double), hipMemcpyDeviceToHost));
+  return RBL_OK;
+}
+
+int rbl_start(rbl_ctx* ctx, int b, int max_blocks, int basis_bits, const double* omega,
+              uint64_t seed) {
+  if (!ctx) return RBL_ERR_INVALID;
+  if (!ctx->d_rowptr) return fail(ctx, RBL_ERR_STATE, "rbl_start: no matrix");
+  if (b < 1 || b > 64) return fail(ctx, RBL_ERR_INVALID, "block size must be in [1,64]");
+  if (max_blocks < 1) return fail(ctx, RBL_ERR_INVALID, "max_blocks must be >= 1");
+  if (basis_bits != 64) return fail(ctx, RBL_ERR_INVALID, "only the fp64 basis is implemented");
+  HIPC(hipSetDevice(ctx->device));
+  HIPC(hipStreamSynchronize(ctx->stream));
+  free_run(ctx);
+  ctx->b = b;
+  ctx->max_blocks = max_blocks;
+  ctx->slot = ctx->nloc * b;
+  const int64_t nl = std::max<int64_t>(ctx->nloc, 1);
+  HIPC(hipMalloc(&ctx->d_basis, (size_t)(max_blocks + 1) * nl * b * sizeof(double)));
+  HIPC(hipMalloc(&ctx->d_U, nl * b * sizeof(double)));
+  ctx->T_cols = b;
+  HIPC(hipMalloc(&ctx->d_T, nl * b * sizeof(double)));
+  if (ctx->nranks > 1)
+    HIPC(hipMalloc(&ctx->d_qext, std::max<int64_t>(ctx->ext_hi - ctx->ext_lo, 1) * b * sizeof(double)));
+  // Gram slab: the largest Gram is the partial-reorth one, (max_blocks-1) panels x 2b
+  size_t slab = 0;
+  for (int nW = 1; nW <= std::max(1, max_blocks - 1); ++nW)
+    for (int xc : {b, 2 * b}) {
+      const size_t sp = (size_t)gram_splits(ctx->nloc, nW, b, xc);
+      slab = std::max(slab, sp * nW * b * xc);
+    }
+  ctx->slab_elems = slab;
+  HIPC(hipMalloc(&ctx->d_slab, slab * sizeof(double)));
+  ctx->C_elems = (size_t)std::max(1, max_blocks) * b * 2 * b;
+  HIPC(hipMalloc(&ctx->d_C, ctx->C_elems * sizeof(double)));
+  HIPC(hipMalloc(&ctx->d_small, (size_t)S_NSMALL * b * b * sizeof(double)));
+  HIPC(hipMalloc(&ctx->d_flags, 4 * sizeof(int)));
+  HIPC(hipMemset(ctx->d_flags, 0, 4 * sizeof(int)));
+  HIPC(hipHostMalloc(&ctx->h_pin, 2 * b * b * sizeof(double), hipHostMallocDefault));
+
+  // Omega (row-major) in d_T
+  if (omega) {
+    double* d_tmp = slotp(ctx, 1 <= max_blocks ? 1 : 0);
+    HIPC(hipMemcpyAsync(d_tmp, omega, ctx->nloc * b * sizeof(double), hipMemcpyHostToDevice,
+                        ctx->stream));
+    colmajor_to_rowmajor(d_tmp, ctx->nloc, b, ctx->d_T, ctx->stream);
+  } else {
+    randn_block(ctx->d_T, ctx->nloc, b, ctx->r0, seed, ctx->stream);
+  }
+  // Q_1 = qr(A * Omega).Q   (RBL_gpu.jl:213-214)
+  const double* Qin = nullptr;
+  int64_t off = 0;
+  CHK(halo_exchange(ctx, ctx->d_T, &Qin, &off));
+  {
+    StageScope t(ctx, RBL_STAGE_AQ);
+    spmm(csr(ctx), Qin, off, b, ctx->d_U, nullptr, nullptr, ctx->spmm_variant, ctx->stream);
+    HIPC(hipGetLastError());
+  }
+  CHK(tsqr(ctx, ctx->d_U, slotp(ctx, 0)));
+  HIPC(hipStreamSynchronize(ctx->stream));
+  harvest_timers(ctx);
+  int flags[4];
+  HIPC(hipMemcpy(flags, ctx->d_flags, sizeof(flags), hipMemcpyDeviceToHost));
+  if (flags[2]) return fail(ctx, RBL_ERR_NUMERIC, "QR breakdown in rbl_start");
+  ctx->nblocks = 1;
+  return RBL_OK;
+}
+
+int rbl_step(rbl_ctx* ctx, int i, int part_reorth, double* A_out, double* B_out) {
+  if (!ctx) return RBL_ERR_INVALID;
+  if (!ctx->d_basis || ctx->nblocks < 1) return fail(ctx, RBL_ERR_STATE, "rbl_step before rbl_start");
+  if (i != ctx->nblocks) return fail(ctx, RBL_ERR_STATE, "rbl_step: i must equal the current block count");
+  if (i > ctx->max_blocks) return fail(ctx, RBL_ERR_STATE, "rbl_step: basis full (max_blocks)");
+  HIPC(hipSetDevice(ctx->device));
+  const int b = ctx->b;
+  double* Qi = slotp(ctx, i - 1);
+  double* Qm = i >= 2 ? slotp(ctx, i - 2) : nullptr;
+  HIPC(hipMemsetAsync(ctx->d_flags, 0, 4 * sizeof(int), ctx->stream));
+
+  // partial reorth of Q_i and Q_{i-1} against Q_1..Q_{i-2}   (RBL_gpu.jl:164-166, 59-81)
+  if (part_reorth && i >= 3) {
+    StageScope t(ctx, RBL_STAGE_PART_REORTH);
+    const int nW = i - 2;
+    if (ctx->reorth_order == 0) {  // block CGS: one Gram over every j, one update
+      PanelRun W;
+      W.base = slotp(ctx, 0);
+      W.stride = ctx->slot;
+      W.count = nW;
+      W.w = b;
+      CHK(gram(ctx, W, pan2(Qi, Qm, b), ctx->d_C, nullptr));
+      CHK(tsmm_checked(ctx, W, ctx->d_C, 2 * b, pan2(Qi, Qm, b), -1.0, 1.0, nullptr));
+    } else {  // ascending-j block MGS, exactly the reference order
+      for (int j = 0; j < nW; ++j) {
+        const PanelRun W = run1(slotp(ctx, j), b);
+        CHK(gram(ctx, W, pan2(Qi, Qm, b), ctx->d_C, nullptr));
+        CHK(tsmm_checked(ctx, W, ctx->d_C, 2 * b, pan2(Qi, Qm, b), -1.0, 1.0, nullptr));
+      }
+    }
+  }
+  // local reorth: Q_i -= Q_{i-1} (Q_{i-1}^T Q_i), one projection (RBL_gpu.jl:83-93, P1)
+  if (i >= 2) {
+    StageScope t(ctx, RBL_STAGE_LOC_REORTH);
+    CHK(gram(ctx, run1(Qm, b), pan1(Qi, b), ctx->d_C, nullptr));
+    CHK(tsmm_checked(ctx, run1(Qm, b), ctx->d_C, b, pan1(Qi, b), -1.0, 1.0, nullptr));
+  }
+  // U = A Q_i - Q_{i-1} B_i^T   (RBL_gpu.jl:176-177)
+  {
+    const double* Qin = nullptr;
+    int64_t off = 0;
+    CHK(halo_exchange(ctx, Qi, &Qin, &off));
+    StageScope t(ctx, RBL_STAGE_AQ);
+    if (ctx->nloc > 0)
+      spmm(csr(ctx), Qin, off, b, ctx->d_U, Qm, i >= 2 ? smallp(ctx, S_BPREV) : nullptr,
+           ctx->spmm_variant, ctx->stream);
+    HIPC(hipGetLastError());
+  }
+  // A_i = Q_i^T U ; U -= Q_i A_i   (RBL_gpu.jl:178-179)
+  {
+    StageScope t(ctx, RBL_STAGE_3TERM);
+    CHK(gram(ctx, run1(Qi, b), pan1(ctx->d_U, b), smallp(ctx, S_AI), nullptr));
+    CHK(tsmm_checked(ctx, run1(Qi, b), smallp(ctx, S_AI), b, pan1(ctx->d_U, b), -1.0, 1.0, nullptr));
+  }
+  // Q_{i+1} B_{i+1} = qr(U)   (RBL_gpu.jl:180-184)
+  CHK(tsqr(ctx, ctx->d_U, slotp(ctx, i)));
+  copy_small(smallp(ctx, S_RTOT), smallp(ctx, S_BPREV), (int64_t)b * b, ctx->stream);
+  HIPC(hipMemcpyAsync(ctx->h_pin, smallp(ctx, S_AI), (size_t)b * b * sizeof(double),
+                      hipMemcpyDeviceToHost, ctx->stream));
+  HIPC(hipMemcpyAsync(ctx->h_pin + b * b, smallp(ctx, S_RTOT), (size_t)b * b * sizeof(double),
+                      hipMemcpyDeviceToHost, ctx->stream));
+  int flags[4];
+  HIPC(hipMemcpyAsync(flags, ctx->d_flags, sizeof(flags), hipMemcpyDeviceToHost, ctx->stream));
+  HIPC(hipStreamSynchronize(ctx->stream));
+  harvest_timers(ctx);
+  // row-major device -> column-major host
+  for (int r = 0; r < b; ++r)
+    for (int c = 0; c < b; ++c) {
+      if (A_out) A_out[c * b + r] = ctx->h_pin[r * b + c];
+      if (B_out) B_out[c * b + r] = ctx->h_pin[b * b + r * b + c];
+    }
+  ctx->nblocks = i + 1;
+  if (flags[2]) return fail(ctx, RBL_ERR_NUMERIC, "QR breakdown (shifted CholQR failed)");
+  return flags[3] ? RBL_WARN_QR_SHIFTED : RBL_OK;
+}
+
+int rbl_ritz(rbl_ctx* ctx, int nblocks, int k, const double* S, double* V_out) {
+  if (!ctx || nblocks < 1 || k < 1 || !S) return fail(ctx, RBL_ERR_INVALID, "rbl_ritz: bad arguments");
+  if (nblocks > ctx->nblocks) return fail(ctx, RBL_ERR_INVALID, "rbl_ritz: more blocks than computed");
+  if (k > nblocks * ctx->b) return fail(ctx, RBL_ERR_INVALID, "rbl_ritz: k > nblocks*b");
+  HIPC(hipSetDevice(ctx->device));
+  const int b = ctx->b;
+  const int64_t rows = (int64_t)nblocks * b;
+  const int64_t nl = std::max<int64_t>(ctx->nloc, 1);
+  double *d_S = nullptr, *d_Scm = nullptr, *d_V = nullptr, *d_Vcm = nullptr;
+  HIPC(hipMalloc(&d_Scm, rows * k * sizeof(double)));
+  HIPC(hipMalloc(&d_S, rows * k * sizeof(double)));
+  HIPC(hipMalloc(&d_V, nl * k * sizeof(double)));
+  HIPC(hipMalloc(&d_Vcm, nl * k * sizeof(double)));
+  HIPC(hipMemcpyAsync(d_Scm, S, rows * k * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+  colmajor_to_rowmajor(d_Scm, rows, k, d_S, ctx->stream);
+  {
+    StageScope t(ctx, RBL_STAGE_RITZ);
+    PanelRun X;
+    X.base = slotp(ctx, 0);
+    X.stride = ctx->slot;
+    X.count = nblocks;
+    X.w = b;
+    CHK(tsmm_checked(ctx, X, d_S, k, pan1(d_V, k), 1.0, 0.0, nullptr));
+  }
+  rowmajor_to_colmajor(d_V, ctx->nloc, k, d_Vcm, ctx->stream);
+  if (V_out)
+    HIPC(hipMemcpyAsync(V_out, d_Vcm, ctx->nloc * k * sizeof(double), hipMemcpyDeviceToHost,
+                        ctx->stream));
+  HIPC(hipStreamSynchronize(ctx->stream));
+  harvest_timers(ctx);
+  hipFree(d_S);
+  hipFree(d_Scm);
+  hipFree(d_V);
+  hipFree(d_Vcm);
+  return RBL_OK;
+}
+
+int rbl_get_block(rbl_ctx* ctx, int j, double* Q_out) {
+  if (!ctx || j < 1 || j > ctx->nblocks || !Q_out) return fail(ctx, RBL_ERR_INVALID, "rbl_get_block: bad block");
+  HIPC(hipSetDevice(ctx->device));
+  const int b = ctx->b;
+  rowmajor_to_colmajor(slotp(ctx, j - 1), ctx->nloc, b, ctx->d_T, ctx->stream);
+  HIPC(hipMemcpyAsync(Q_out, ctx->d_T, ctx->nloc * b * sizeof(double), hipMemcpyDeviceToHost,
+                      ctx->stream));
+  HIPC(hipStreamSynchronize(ctx->stream));
+  return RBL_OK;
+}
+
+int rbl_num_blocks(rbl_ctx* ctx) { return ctx ? ctx->nblocks : 0; }
+
+int rbl_num_stages(void) { return RBL_NUM_STAGES; }
+const char* rbl_stage_name(int stage) {
+  return (stage >= 0 && stage < RBL_NUM_STAGES) ? kStageNames[stage] : "";
+}
+int rbl_timers(rbl_ctx* ctx, double* ms, int nstages) {
+  if (!ctx || !ms) return RBL_ERR_INVALID;
+  for (int s = 0; s < nstages && s < RBL_NUM_STAGES; ++s) ms[s] = ctx->stage_ms[s];
+  return RBL_OK;
+}
+int rbl_reset_timers(rbl_ctx* ctx) {
+  if (!ctx) return RBL_ERR_INVALID;
+  for (double& v : ctx->stage_ms) v = 0.0;
+  return RBL_OK;
+}
+int rbl_synchronize(rbl_ctx* ctx) {
+  if (!ctx) return RBL_ERR_INVALID;
+  HIPC(hipSetDevice(ctx->device));
+  HIPC(hipStreamSynchronize(ctx->stream));
+  harvest_timers(ctx);
+  return RBL_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,45 @@
+// rbl_common.hpp — shared definitions for the gfx950 RBL kernels and the C-ABI layer.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <cstddef>
+
+namespace rbl {
+
+constexpr int kWave = 64;  // CDNA wavefront width (gfx950); never 32.
+
+// ----------------------------------------------------------------------------------------
+// Seeded hash used by the synthetic "hash-window" matrix and the
+// device N(0,1) start block.  Integer-only so host and device produce identical bits.
+// ----------------------------------------------------------------------------------------
+__host__ __device__ inline uint64_t mix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+__host__ __device__ inline uint64_t pair_hash(uint64_t seed, int64_t lo, int64_t hi) {
+  return mix64(mix64(seed + (uint64_t)lo) ^ (uint64_t)hi);
+}
+// uniform [0,1) from the top 53 bits — exact in fp64
+__host__ __device__ inline double u53(uint64_t h) { return (double)(h >> 11) * 0x1.0p-53; }
+// entry (lo,hi) present?  (lo < hi)
+__host__ __device__ inline bool hw_present(uint64_t seed, int64_t lo, int64_t hi, double density) {
+  return u53(pair_hash(seed, lo, hi)) < density;
+}
+// value of entry (lo,hi), lo <= hi, uniform(-1,1)
+__host__ __device__ inline double hw_value(uint64_t seed, int64_t lo, int64_t hi) {
+  double u = u53(mix64(pair_hash(seed, lo, hi) ^ 0x5851F42D4C957F2Dull));
+  return (u + u) - 1.0;
+}
+
+inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// ----------------------------------------------------------------------------------------
+// Wave-level helpers
+// ----------------------------------------------------------------------------------------
+__device__ inline double shfl_xor_d(double v, int mask) {
+  return __shfl_xor(v, mask, kWave);
+}
+
+}  // namespace rbl

@@ -1,0 +1,136 @@
+// smallmat.hip — b x b work of the tall-skinny QR, on one workgroup, no host round trip.
+//
+// The reference factors every n x b block with cuSOLVER geqrf + orgqr (RBL_gpu.jl:155,
+// 180-184; CPU: LAPACK, RBL.jl:102-104).  The HIP path uses CholQR2 and, when the block is
+// (nearly) rank deficient — Krylov exhaustion in the reference's own tests —
+// shifted CholQR3 (Fukaya et al. 2020: shift s = 11 (n b + b (b+1)) u ||U||^2, then two
+// unshifted passes).  R has a non-negative diagonal.
+#include "kernels.hpp"
+
+namespace rbl {
+
+constexpr int kMaxB = 64;
+
+__global__ __launch_bounds__(256) void k_chol(const double* __restrict__ G, int b, int64_t nglob,
+                                              int mode, double* R, double* Rinv, double* Rtot,
+                                              int* need3, int* status, const int* skip) {
+  if (skip && *skip) return;
+  __shared__ double M[kMaxB][kMaxB + 1];
+  __shared__ double X[kMaxB][kMaxB + 1];
+  __shared__ int fail;
+  __shared__ double shift;
+  __shared__ int zero;
+  const int tid = threadIdx.x, nt = blockDim.x;
+
+  if (tid == 0) {
+    double tr = 0.0;
+    for (int j = 0; j < b; ++j) tr += G[j * b + j];
+    zero = !(tr > 0.0);
+    shift = 0.0;
+    // Fukaya shift, u = 2^-53; trace(G) >= ||U||_2^2
+    if (!zero) shift = 11.0 * ((double)nglob * b + (double)b * (b + 1)) * 0x1.0p-53 * tr;
+  }
+  __syncthreads();
+
+  int shifted = 0;
+  if (!zero) {
+    for (int attempt = 0; attempt < 2; ++attempt) {
+      const double sh = attempt ? shift : 0.0;
+      for (int e = tid; e < b * b; e += nt) {
+        const int r = e / b, c = e % b;
+        M[r][c] = (r <= c) ? G[r * b + c] + (r == c ? sh : 0.0) : 0.0;
+      }
+      if (tid == 0) fail = 0;
+      __syncthreads();
+      for (int j = 0; j < b; ++j) {
+        if (tid == 0) {
+          const double d = M[j][j];
+          const double gjj = G[j * b + j] + sh;
+          if (!(d > 0.0) || !isfinite(d)) {
+            fail = 1;
+          } else {
+            // relative pivot: sin^2 of the angle between u_j and span(u_<j); below 1e-15 the
+            // block's condition number exceeds ~3e7 and plain CholQR2 loses orthogonality
+            if (attempt == 0 && mode == 0 && d < 1e-15 * gjj) fail = 2;
+            M[j][j] = sqrt(d);
+          }
+        }
+        __syncthreads();
+        if (fail) break;
+        const double rjj = M[j][j];
+        for (int c = j + 1 + tid; c < b; c += nt) M[j][c] /= rjj;
+        __syncthreads();
+        const int m = b - j - 1;
+        for (int e = tid; e < m * m; e += nt) {
+          const int r = j + 1 + e / m, c = j + 1 + e % m;
+          if (r <= c) M[r][c] -= M[j][r] * M[j][c];
+        }
+        __syncthreads();
+      }
+      __syncthreads();
+      if (!fail) break;
+      shifted = 1;
+      __syncthreads();
+    }
+  }
+  __syncthreads();
+  const bool bad = !zero && fail;
+
+  // Rinv: column c by thread c (back substitution on the upper triangle)
+  if (!zero && !bad) {
+    for (int c = tid; c < b; c += nt) {
+      for (int i = 0; i < b; ++i) X[i][c] = 0.0;
+      X[c][c] = 1.0 / M[c][c];
+      for (int i = c - 1; i >= 0; --i) {
+        double acc = 0.0;
+        for (int k = i + 1; k <= c; ++k) acc += M[i][k] * X[k][c];
+        X[i][c] = -acc / M[i][i];
+      }
+    }
+  }
+  __syncthreads();
+  for (int e = tid; e < b * b; e += nt) {
+    const int r = e / b, c = e % b;
+    const bool up = r <= c;
+    const double rv = (zero || bad || !up) ? 0.0 : M[r][c];
+    const double xv = (zero || bad || !up) ? 0.0 : X[r][c];
+    R[e] = rv;
+    Rinv[e] = xv;
+  }
+  __syncthreads();
+  // Rtot = R * Rtot_prev (mode 1) or R (mode 0); reuse X as scratch for the product
+  if (mode == 0) {
+    for (int e = tid; e < b * b; e += nt) Rtot[e] = R[e];
+  } else {
+    for (int e = tid; e < b * b; e += nt) X[e / b][e % b] = Rtot[e];
+    __syncthreads();
+    for (int e = tid; e < b * b; e += nt) {
+      const int r = e / b, c = e % b;
+      double acc = 0.0;
+      if (r <= c && !zero && !bad)
+        for (int k = r; k <= c; ++k) acc += M[r][k] * X[k][c];
+      Rtot[e] = acc;
+    }
+  }
+  if (tid == 0) {
+    if (mode == 0) { need3[0] = shifted; need3[1] = !shifted; }
+    if (bad) status[0] = 1;
+    if (shifted) status[1] += 1;
+  }
+}
+
+void chol_step(const double* G, int b, int64_t nglobal, int mode, double* R, double* Rinv,
+               double* Rtot, int* need3, int* status, const int* skip, hipStream_t s) {
+  hipLaunchKernelGGL(k_chol, dim3(1), dim3(256), 0, s, G, b, nglobal, mode, R, Rinv, Rtot, need3,
+                     status, skip);
+}
+
+__global__ void k_copy(const double* __restrict__ src, double* __restrict__ dst, int64_t len) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < len) dst[e] = src[e];
+}
+void copy_small(const double* src, double* dst, int64_t len, hipStream_t s) {
+  hipLaunchKernelGGL(k_copy, dim3((unsigned)((len + 255) / 256)), dim3(256), 0, s, src, dst, len);
+}
+
+}  // namespace rbl

@@ -1,0 +1,274 @@
+// tsmm.hip — tall-skinny fp64 MFMA kernels for gfx950.
+//
+// These replace every cuBLAS gemm of the reference's block step:
+//   * Gram  C = W^T X   — A_i = Q_i^T U (RBL_gpu.jl:153,178), local-reorth coefficient
+//     (RBL_gpu.jl:87), partial-reorth coefficients against the Krylov basis
+//     (RBL_gpu.jl:33,39,50,52) and the CholQR Gram matrices that replace cuSOLVER geqrf.
+//   * update Y = beta Y + alpha X C — U -= Q_i A_i (:154,179), local / partial reorth
+//     updates (:88, :34,40,51,53), CholQR apply, and the Ritz projection (:121).
+//
+// Both are v_mfma_f64_16x16x4f64 tiles (one f64 per lane for A and B; C/D: col = lane&15,
+// row = (lane>>4) + 4*reg).  Memory layout: every n x w panel is row-major, so a 16-lane
+// quad reads 128 contiguous bytes.  Gram partials go to a slab [split][a][c] reduced in a
+// fixed order by reduce_slab (bitwise reproducible, no atomics).
+#include "kernels.hpp"
+
+namespace rbl {
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+__device__ inline d4 mfma16(double a, double b, d4 c) {
+  return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+
+// ----------------------------------------------------------------------------------------
+// Gram partials
+// ----------------------------------------------------------------------------------------
+template <int AT, int CT>
+__global__ __launch_bounds__(256) void k_gram(int64_t nrows, PanelRun W, Panels X, double* slab,
+                                              int splits, int ncg, int64_t rows_per,
+                                              const int* skip) {
+  if (skip && *skip) return;
+  const int lane = threadIdx.x & 63;
+  const int wid = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int njobs = W.count * ncg;
+  const int job = wid % njobs;
+  const int s = wid / njobs;
+  if (s >= splits) return;
+  const int j = job % W.count;
+  const int cg = job / W.count;
+  const int w = W.w, xw = X.w;
+  const int KC = X.count * xw;
+  const int KW = W.count * w;
+  const int li = lane & 15, q = lane >> 4;
+
+  const int64_t r_begin = (int64_t)s * rows_per;
+  const int64_t r_end = r_begin + rows_per < nrows ? r_begin + rows_per : nrows;
+
+  const double* wp[AT];
+  bool wv[AT];
+#pragma unroll
+  for (int at = 0; at < AT; ++at) {
+    const int a = at * 16 + li;
+    wv[at] = a < w;
+    wp[at] = W.base + (int64_t)j * W.stride + (wv[at] ? a : 0);
+  }
+  const double* xp[CT];
+  bool xv[CT];
+#pragma unroll
+  for (int ct = 0; ct < CT; ++ct) {
+    const int c = (cg * CT + ct) * 16 + li;
+    xv[ct] = c < KC;
+    const int t = xv[ct] ? c / xw : 0;
+    xp[ct] = X.ptr[t] + (xv[ct] ? c - t * xw : 0);
+  }
+  d4 acc[AT][CT];
+#pragma unroll
+  for (int at = 0; at < AT; ++at)
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) acc[at][ct] = d4{0.0, 0.0, 0.0, 0.0};
+
+  // main loop: 4 rows per MFMA k-step, lane quad q owns row r0 + q
+  int64_t r0 = r_begin;
+  for (; r0 + 4 <= r_end; r0 += 4) {
+    const int64_t row = r0 + q;
+    double av[AT], xv_[CT];
+#pragma unroll
+    for (int at = 0; at < AT; ++at) av[at] = wv[at] ? wp[at][row * w] : 0.0;
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) xv_[ct] = xv[ct] ? xp[ct][row * xw] : 0.0;
+#pragma unroll
+    for (int at = 0; at < AT; ++at)
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct) acc[at][ct] = mfma16(av[at], xv_[ct], acc[at][ct]);
+  }
+  if (r0 < r_end) {  // ragged tail (wave-uniform branch)
+    const int64_t row = r0 + q;
+    const bool rv = row < r_end;
+    double av[AT], xv_[CT];
+#pragma unroll
+    for (int at = 0; at < AT; ++at) av[at] = (rv && wv[at]) ? wp[at][row * w] : 0.0;
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) xv_[ct] = (rv && xv[ct]) ? xp[ct][row * xw] : 0.0;
+#pragma unroll
+    for (int at = 0; at < AT; ++at)
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct) acc[at][ct] = mfma16(av[at], xv_[ct], acc[at][ct]);
+  }
+
+  double* out = slab + (int64_t)s * KW * KC;
+#pragma unroll
+  for (int at = 0; at < AT; ++at)
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+      for (int reg = 0; reg < 4; ++reg) {
+        const int a = at * 16 + q + 4 * reg;
+        const int c = (cg * CT + ct) * 16 + li;
+        if (a < w && c < KC) out[(int64_t)(j * w + a) * KC + c] = acc[at][ct][reg];
+      }
+}
+
+static int tiles16(int x) { return (x + 15) / 16; }
+static int pick_at(int w) { int t = tiles16(w); return t <= 1 ? 1 : (t <= 2 ? 2 : 4); }
+
+int gram_splits(int64_t nrows, int nW, int w, int xcols) {
+  const int ctt = tiles16(xcols);
+  const int ct = ctt <= 1 ? 1 : (ctt <= 2 ? 2 : 4);
+  const int ncg = (ctt + ct - 1) / ct;
+  const int64_t njobs = (int64_t)nW * ncg;
+  int64_t splits = (4096 + njobs - 1) / njobs;
+  const int64_t max_by_rows = (nrows + 63) / 64;
+  if (splits > max_by_rows) splits = max_by_rows;
+  // keep the slab <= 256 MB
+  const int64_t per = (int64_t)nW * w * xcols * 8;
+  const int64_t max_by_mem = per > 0 ? (256ll << 20) / per : splits;
+  if (splits > max_by_mem) splits = max_by_mem;
+  if (splits < 1) splits = 1;
+  return (int)splits;
+}
+
+template <int AT, int CT>
+static void launch_gram_t(int64_t nrows, const PanelRun& W, const Panels& X, double* slab,
+                          int splits, int ncg, const int* skip, hipStream_t s) {
+  int64_t rows_per = (nrows + splits - 1) / splits;
+  rows_per = (rows_per + 3) / 4 * 4;
+  const int64_t waves = (int64_t)W.count * ncg * splits;
+  const int blocks = (int)((waves + 3) / 4);
+  hipLaunchKernelGGL((k_gram<AT, CT>), dim3(blocks), dim3(256), 0, s, nrows, W, X, slab, splits,
+                     ncg, rows_per, skip);
+}
+
+void gram_partial(int64_t nrows, const PanelRun& W, const Panels& X, double* slab, int splits,
+                  const int* skip, hipStream_t s) {
+  const int at = pick_at(W.w);
+  const int ctt = tiles16(X.count * X.w);
+  const int ct = ctt <= 1 ? 1 : (ctt <= 2 ? 2 : 4);
+  const int ncg = (ctt + ct - 1) / ct;
+#define RBL_GRAM_CASE(A_, C_) \
+  if (at == A_ && ct == C_) return launch_gram_t<A_, C_>(nrows, W, X, slab, splits, ncg, skip, s);
+  RBL_GRAM_CASE(1, 1) RBL_GRAM_CASE(1, 2) RBL_GRAM_CASE(1, 4)
+  RBL_GRAM_CASE(2, 1) RBL_GRAM_CASE(2, 2) RBL_GRAM_CASE(2, 4)
+  RBL_GRAM_CASE(4, 1) RBL_GRAM_CASE(4, 2) RBL_GRAM_CASE(4, 4)
+#undef RBL_GRAM_CASE
+}
+
+// ----------------------------------------------------------------------------------------
+// Deterministic slab reduction
+// ----------------------------------------------------------------------------------------
+__global__ void k_reduce(const double* __restrict__ slab, int splits, int64_t len,
+                         double* __restrict__ out, const int* skip) {
+  if (skip && *skip) return;
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= len) return;
+  double acc = 0.0;
+  for (int s = 0; s < splits; ++s) acc += slab[(int64_t)s * len + e];
+  out[e] = acc;
+}
+
+void reduce_slab(const double* slab, int splits, int64_t len, double* out, const int* skip,
+                 hipStream_t s) {
+  const int blocks = (int)((len + 255) / 256);
+  hipLaunchKernelGGL(k_reduce, dim3(blocks), dim3(256), 0, s, slab, splits, len, out, skip);
+}
+
+// ----------------------------------------------------------------------------------------
+// Y = beta*Y + alpha * X * C
+// ----------------------------------------------------------------------------------------
+template <int RT, int CT>
+__global__ __launch_bounds__(256) void k_tsmm(int64_t nrows, PanelRun X, const double* __restrict__ C,
+                                              int ldc, Panels Y, double alpha, double beta,
+                                              int ncg, const int* skip) {
+  if (skip && *skip) return;
+  const int lane = threadIdx.x & 63;
+  const int64_t wid = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int cg = (int)(wid % ncg);
+  const int64_t rg = wid / ncg;
+  const int64_t rowbase = rg * (16 * RT);
+  if (rowbase >= nrows) return;
+  const int li = lane & 15, q = lane >> 4;
+  const int xw = X.w;
+  const int K = X.count * xw;
+  const int KY = Y.count * Y.w;
+
+  bool rv[RT];
+  int64_t arow[RT];
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt) {
+    arow[rt] = rowbase + rt * 16 + li;
+    rv[rt] = arow[rt] < nrows;
+  }
+  int cc[CT];
+  bool cv[CT];
+#pragma unroll
+  for (int ct = 0; ct < CT; ++ct) {
+    cc[ct] = (cg * CT + ct) * 16 + li;
+    cv[ct] = cc[ct] < KY;
+  }
+  d4 acc[RT][CT];
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) acc[rt][ct] = d4{0.0, 0.0, 0.0, 0.0};
+
+  // k = panel*xw + col; lane quad q owns k = k0 + q
+  int panel = 0, col = q;          // running (panel, col) of k = k0 + q
+  while (col >= xw && panel < X.count) { col -= xw; ++panel; }
+  for (int k0 = 0; k0 < K; k0 += 4) {
+    const int k = k0 + q;
+    const bool kv = k < K;
+    const double* xpan = X.base + (int64_t)panel * X.stride;
+    double a[RT], bb[CT];
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) a[rt] = (kv && rv[rt]) ? xpan[arow[rt] * xw + col] : 0.0;
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) bb[ct] = (kv && cv[ct]) ? C[(int64_t)k * ldc + cc[ct]] : 0.0;
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct) acc[rt][ct] = mfma16(a[rt], bb[ct], acc[rt][ct]);
+    col += 4;
+    while (col >= xw) { col -= xw; ++panel; }
+  }
+
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+      for (int reg = 0; reg < 4; ++reg) {
+        const int64_t r = rowbase + rt * 16 + q + 4 * reg;
+        const int c = (cg * CT + ct) * 16 + li;
+        if (r < nrows && c < KY) {
+          const int t = c / Y.w;
+          double* yp = const_cast<double*>(Y.ptr[t]) + r * Y.w + (c - t * Y.w);
+          const double v = alpha * acc[rt][ct][reg];
+          *yp = beta == 0.0 ? v : beta * (*yp) + v;
+        }
+      }
+}
+
+template <int RT, int CT>
+static void launch_tsmm_t(int64_t nrows, const PanelRun& X, const double* C, int ldc,
+                          const Panels& Y, double alpha, double beta, int ncg, const int* skip,
+                          hipStream_t s) {
+  const int64_t rgs = (nrows + 16 * RT - 1) / (16 * RT);
+  const int64_t waves = rgs * ncg;
+  const int64_t blocks = (waves + 3) / 4;
+  hipLaunchKernelGGL((k_tsmm<RT, CT>), dim3((unsigned)blocks), dim3(256), 0, s, nrows, X, C, ldc,
+                     Y, alpha, beta, ncg, skip);
+}
+
+void tsmm(int64_t nrows, const PanelRun& X, const double* C, int ldc, const Panels& Y,
+          double alpha, double beta, const int* skip, hipStream_t s) {
+  const int ctt = tiles16(Y.count * Y.w);
+  const int ct = ctt <= 1 ? 1 : (ctt <= 2 ? 2 : 4);
+  const int ncg = (ctt + ct - 1) / ct;
+  // in-place use (Y aliasing X) is race-free only when one wave owns whole rows (ncg == 1,
+  // i.e. Y.count*Y.w <= 64); the API layer only aliases for the b x b CholQR apply.
+  if (ct == 1) return launch_tsmm_t<2, 1>(nrows, X, C, ldc, Y, alpha, beta, ncg, skip, s);
+  if (ct == 2) return launch_tsmm_t<2, 2>(nrows, X, C, ldc, Y, alpha, beta, ncg, skip, s);
+  return launch_tsmm_t<2, 4>(nrows, X, C, ldc, Y, alpha, beta, ncg, skip, s);
+}
+
+}  // namespace rbl

@@ -1,0 +1,239 @@
+"""Host driver mirroring the reference's ``RBL_gpu(A, k, b)`` (Julia/RBL_gpu.jl:205-221).
+
+The host keeps the loop control, the block-tridiagonal T_j and its LAPACK ``dsbev``
+(Julia/common.jl), exactly as the north star asks; every n-sized operation — SpMM, local and
+partial reorthogonalisation, tall-skinny QR, Ritz projection — runs in librbl_hip.so on the
+MI355X.  Per step only the two b x b blocks A_i, B_{i+1} cross PCIe.
+
+Semantics follow the GPU reference loop (RBL_gpu.jl:134-203):
+  * max Krylov size 1200 (RBL_gpu.jl:211), step i runs while i*b < kryl_sz (:162);
+  * partial reorth at even i (:164), local reorth every step (:167);
+  * eigensolve + convergence test when i*b > k and i % 4 == 0 (:186-191), absolute 1e-7;
+  * D returned in descending |lambda| (:202), V = [Q_1..Q_m] S in fp64 (RBL.jl:61-71, P3).
+Non-convergence (the reference's BoundsError) returns the last Ritz pairs
+with ``info.converged = False`` and status RBL_WARN_NOT_CONVERGED.
+"""
+from __future__ import annotations
+
+import math
+import time
+from dataclasses import dataclass, field
+
+import numpy as np
+import scipy.sparse as sp
+
+from . import _lib
+from ._lib import RBLError, dptr, i32ptr, i64ptr, lib, u8ptr
+from .host import TBand, check_convergence, dsbev, sort_eig_abs
+
+KRYL_SZ_GPU = 1200          # RBL_gpu.jl:211
+RESIDUAL_TOL = 1e-7         # RBL_gpu.jl:189
+
+
+class Context:
+    """One librbl_hip context: one GPU, or one rank of a row-partitioned job."""
+
+    def __init__(self, device: int = 0, nranks: int = 1, rank: int = 0,
+                 unique_id: bytes | None = None):
+        import ctypes as C
+        self._h = C.c_void_p()
+        if nranks == 1:
+            st = lib.rbl_create(C.byref(self._h), device)
+        else:
+            uid = np.frombuffer(unique_id, dtype=np.uint8).copy()
+            st = lib.rbl_create_dist(C.byref(self._h), device, nranks, rank, u8ptr(uid))
+        self.nranks, self.rank, self.device = nranks, rank, device
+        self._check(st, "rbl_create")
+        self.b = None
+
+    # -- plumbing -------------------------------------------------------------------------
+    def _check(self, st: int, what: str) -> int:
+        if st < 0:
+            msg = lib.rbl_last_error(self._h).decode() if self._h else ""
+            raise RBLError(st, f"{what}: {msg}")
+        return st
+
+    def close(self) -> None:
+        if self._h:
+            lib.rbl_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def set_option(self, opt: int, value: int) -> None:
+        self._check(lib.rbl_set_option(self._h, opt, int(value)), "rbl_set_option")
+
+    # -- matrix ---------------------------------------------------------------------------
+    def set_matrix(self, A) -> None:
+        """Upload a symmetric sparse matrix (any SciPy format). CSC arrays are passed as-is
+        (Julia SparseMatrixCSC layout, RBL_gpu.jl:209); symmetry makes them the CSR arrays."""
+        A = sp.csc_matrix(A)
+        A.sort_indices()
+        n = A.shape[1]
+        colptr = A.indptr.astype(np.int64)
+        rowval = A.indices.astype(np.int64)
+        nzval = A.data.astype(np.float64)
+        self._check(lib.rbl_set_matrix_csc(self._h, n, A.nnz, i64ptr(colptr), i64ptr(rowval),
+                                           dptr(nzval), 0), "rbl_set_matrix_csc")
+
+    def set_matrix_rows(self, n, row_begin, row_end, rowptr, colind, val, index_base=0) -> None:
+        rowptr = np.ascontiguousarray(rowptr, dtype=np.int64)
+        colind = np.ascontiguousarray(colind, dtype=np.int64)
+        val = np.ascontiguousarray(val, dtype=np.float64)
+        self._check(lib.rbl_set_matrix_csr_rows(self._h, n, row_begin, row_end, i64ptr(rowptr),
+                                                i64ptr(colind), dptr(val), index_base),
+                    "rbl_set_matrix_csr_rows")
+
+    def gen_hashwindow(self, n: int, halfwidth: int, density: float, seed: int,
+                       plant=None) -> None:
+        plant = np.ascontiguousarray(plant if plant is not None else np.zeros(0), np.float64)
+        self._check(lib.rbl_gen_matrix_hashwindow(self._h, n, halfwidth, density, seed,
+                                                  plant.size, dptr(plant) if plant.size else None),
+                    "rbl_gen_matrix_hashwindow")
+
+    def matrix_info(self):
+        v = [np.zeros(1, np.int64) for _ in range(4)]
+        self._check(lib.rbl_matrix_info(self._h, *[i64ptr(x) for x in v]), "rbl_matrix_info")
+        n, r0, r1, nnz = (int(x[0]) for x in v)
+        return n, r0, r1, nnz
+
+    def get_matrix_csr(self):
+        n, r0, r1, nnz = self.matrix_info()
+        rowptr = np.zeros(r1 - r0 + 1, np.int64)
+        col = np.zeros(max(nnz, 1), np.int32)
+        val = np.zeros(max(nnz, 1), np.float64)
+        self._check(lib.rbl_get_matrix_csr(self._h, i64ptr(rowptr), i32ptr(col), dptr(val)),
+                    "rbl_get_matrix_csr")
+        return rowptr, col[:nnz], val[:nnz]
+
+    # -- Krylov run -------------------------------------------------------------------------
+    def start(self, b: int, max_blocks: int, omega=None, seed: int = 0) -> None:
+        om = None
+        if omega is not None:
+            om = np.asfortranarray(omega, dtype=np.float64)
+        self._check(lib.rbl_start(self._h, b, max_blocks, 64, dptr(om), seed), "rbl_start")
+        self.b = b
+
+    def step(self, i: int, part_reorth: bool):
+        b = self.b
+        A = np.zeros((b, b), order="F")
+        B = np.zeros((b, b), order="F")
+        st = self._check(lib.rbl_step(self._h, i, int(bool(part_reorth)), dptr(A), dptr(B)),
+                         "rbl_step")
+        return A, B, st
+
+    def ritz(self, nblocks: int, k: int, S: np.ndarray) -> np.ndarray:
+        n, r0, r1, _ = self.matrix_info()
+        S = np.asfortranarray(S[: nblocks * self.b, :k], dtype=np.float64)
+        V = np.zeros((r1 - r0, k), order="F")
+        self._check(lib.rbl_ritz(self._h, nblocks, k, dptr(S), dptr(V)), "rbl_ritz")
+        return V
+
+    def get_block(self, j: int) -> np.ndarray:
+        n, r0, r1, _ = self.matrix_info()
+        Q = np.zeros((r1 - r0, self.b), order="F")
+        self._check(lib.rbl_get_block(self._h, j, dptr(Q)), "rbl_get_block")
+        return Q
+
+    def num_blocks(self) -> int:
+        return lib.rbl_num_blocks(self._h)
+
+    def timers(self) -> dict:
+        names = _lib.stage_names()
+        ms = np.zeros(len(names))
+        self._check(lib.rbl_timers(self._h, dptr(ms), len(names)), "rbl_timers")
+        return dict(zip(names, ms.tolist()))
+
+    def reset_timers(self) -> None:
+        self._check(lib.rbl_reset_timers(self._h), "rbl_reset_timers")
+
+    def synchronize(self) -> None:
+        self._check(lib.rbl_synchronize(self._h), "rbl_synchronize")
+
+
+@dataclass
+class RBLInfo:
+    iters: int = 0
+    nblocks: int = 0
+    converged: bool = False
+    status: int = 0
+    qr_shifted_steps: int = 0
+    eig_ms: float = 0.0
+    trace_A: list = field(default_factory=list)
+    trace_B: list = field(default_factory=list)
+
+
+def max_steps_for(kryl_sz: int, b: int) -> int:
+    """Number of block steps the loop `while i*b < kryl_sz` can run (RBL_gpu.jl:162)."""
+    return max(1, math.ceil(kryl_sz / b))
+
+
+def lanczos(ctx: Context, k: int, b: int, *, kryl_sz: int = KRYL_SZ_GPU, omega=None, seed=0,
+            check: bool = True, max_steps: int | None = None, tol: float = RESIDUAL_TOL,
+            trace: bool = False, ritz: bool = True):
+    """RBL_gpu.jl:134-203 + :219 on an already-loaded context.  Returns (D, V_local, info)."""
+    steps_cap = max_steps_for(kryl_sz, b)
+    if max_steps is not None:
+        steps_cap = min(steps_cap, max_steps)
+    ctx.start(b, steps_cap, omega=omega, seed=seed)
+    info = RBLInfo()
+    T = TBand(b, steps_cap)
+    D = np.zeros(0)
+    S = np.zeros((0, 0))
+
+    def _step(i, part):
+        A, B, st = ctx.step(i, part)
+        if st == _lib.RBL_WARN_QR_SHIFTED:
+            info.qr_shifted_steps += 1
+        if trace:
+            info.trace_A.append(A.copy())
+            info.trace_B.append(B.copy())
+        return A, B
+
+    Ai, Bi = _step(1, False)                       # first loop, RBL_gpu.jl:149-161
+    T.insert_A(Ai)
+    T.insert_B(Bi, 1)
+    i = 1
+    while i * b < kryl_sz and i < steps_cap:       # :162
+        i += 1
+        Ai, Bi = _step(i, i % 2 == 0)              # :164-184
+        T.insert_A(Ai)                             # :185
+        if check and i * b > k and i % 4 == 0:     # :186
+            t0 = time.perf_counter()
+            D, S = dsbev(T.view())                 # :187
+            D, S = sort_eig_abs(D, S, k)           # :188
+            info.eig_ms += (time.perf_counter() - t0) * 1e3
+            if check_convergence(Bi, S, b, k, tol):   # :189
+                info.converged = True
+                break
+        T.insert_B(Bi, i)                          # :193
+    info.iters = i
+    info.nblocks = i                               # Q_1..Q_i (length(Q))
+    D = D[::-1].copy()
+    S = S[:, ::-1].copy()
+    info.status = _lib.RBL_OK if info.converged else _lib.RBL_WARN_NOT_CONVERGED
+    V = None
+    if ritz and S.size:
+        V = ctx.ritz(S.shape[0] // b, min(k, S.shape[1]), S)   # RBL_gpu.jl:219
+    return D, V, info
+
+
+def RBL_gpu(A, k: int, b: int, *, device: int = 0, kryl_sz: int = KRYL_SZ_GPU, omega=None,
+            seed: int = 0, reorth_order: int = 0, return_info: bool = False):
+    """Drop-in for ``RBL_gpu(A::SparseMatrixCSC{Float64}, k, b)`` (RBL_gpu.jl:205):
+    returns (D, V) — D the k largest-|lambda| eigenvalues (descending |lambda|), V n x k."""
+    with Context(device) as ctx:
+        ctx.set_matrix(A)
+        ctx.set_option(_lib.RBL_OPT_REORTH_ORDER, reorth_order)
+        D, V, info = lanczos(ctx, k, b, kryl_sz=kryl_sz, omega=omega, seed=seed)
+    return (D, V, info) if return_info else (D, V)

@@ -1,0 +1,139 @@
+/*
+ * rbl_hip.h — C-ABI of librbl_hip.so, the MI355X (gfx950) Randomized Block Lanczos
+ * inner loop.  Plain pointers and sizes only; no torch / HIP types cross this boundary.
+ *
+ * The reference (Iasonaspg/GPU-Randomized-Block-Lanczos) has no FFI layer: its "API" is
+ * the Julia function pair RBL(A,k,b) (Julia/RBL.jl:119) / RBL_gpu(A,k,b)
+ * (Julia/RBL_gpu.jl:205).  Its only native-call convention is the ccall into LAPACK at
+ * Julia/common.jl:32-34 (ILP64 Ref{Int64} scalars, Ptr{Float64} column-major buffers).
+ * This header follows that convention: int64 sizes, column-major dense buffers at the
+ * boundary, caller-allocated outputs, every pointer borrowed only for the call.
+ *
+ * Each entry point below names the reference code it replaces.  The host loop that
+ * replaces Julia/RBL_gpu.jl:162-194 (T_j assembly, dsbev, sort, convergence test —
+ * Julia/common.jl:9-65) stays on the CPU and calls rbl_step() once per block step.
+ *
+ * Status codes: 0 ok, <0 error (rbl_last_error() has text), >0 warning.
+ * Threading: one context per caller, not re-entrant; every entry point re-binds its
+ * device, so callers may migrate between OS threads (Julia tasks).
+ */
+#ifndef RBL_HIP_H
+#define RBL_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RBL_ABI_VERSION 1
+
+#define RBL_OK                  0
+#define RBL_WARN_NOT_CONVERGED  1   /* host-side status for the P6 case */
+#define RBL_WARN_QR_SHIFTED     2   /* rank-deficient block: shifted CholQR3 was used      */
+#define RBL_ERR_INVALID        -1   /* bad argument / unsupported option                   */
+#define RBL_ERR_HIP            -2   /* HIP runtime failure                                 */
+#define RBL_ERR_OOM            -3   /* device allocation failed                            */
+#define RBL_ERR_RCCL           -4   /* RCCL failure                                        */
+#define RBL_ERR_STATE          -5   /* call out of order (e.g. step before start)          */
+#define RBL_ERR_NUMERIC        -6   /* QR breakdown that the fallback could not repair     */
+
+/* Timer stages; names match the reference's TimerOutputs labels (Julia/RBL_gpu.jl:152-187,219). */
+#define RBL_STAGE_AQ          0   /* "AQ"            RBL_gpu.jl:152,176  SpMM + fused 3-term term */
+#define RBL_STAGE_3TERM       1   /* "3-term"        RBL_gpu.jl:153-154,177-179                  */
+#define RBL_STAGE_QR          2   /* "qr"            RBL_gpu.jl:155,180-184                      */
+#define RBL_STAGE_PART_REORTH 3   /* "part reorth"   RBL_gpu.jl:165                               */
+#define RBL_STAGE_LOC_REORTH  4   /* "loc reorth"    RBL_gpu.jl:167                               */
+#define RBL_STAGE_RITZ        5   /* "Ritz vectors"  RBL_gpu.jl:219                               */
+#define RBL_STAGE_COMM        6   /* halo exchange + all-reduce (no reference equivalent)         */
+#define RBL_NUM_STAGES        7
+
+/* Options for rbl_set_option(). */
+#define RBL_OPT_TIMERS        0   /* 1: record per-stage hipEvents (adds event records)         */
+#define RBL_OPT_REORTH_ORDER  1   /* 0: block-CGS (batched, default); 1: ascending-j block MGS  */
+                                  /*    exactly as RBL.jl:30-48 / RBL_gpu.jl:65-67               */
+#define RBL_OPT_SPMM_KERNEL   2   /* 0: auto; 1: global-gather CSR; 2: LDS-window CSR           */
+
+typedef struct rbl_ctx rbl_ctx;
+
+int rbl_abi_version(void);
+
+/* ---- context ------------------------------------------------------------------------
+ * Replaces the implicit CUDA.jl device state of RBL_gpu.jl:1-6. */
+int rbl_create(rbl_ctx** ctx, int device);
+/* One rank of a row-partitioned multi-GPU job (one process per GPU).  `unique_id` is the
+ * 128-byte RCCL id produced by rbl_get_unique_id() on rank 0 and broadcast by the host. */
+int rbl_get_unique_id(uint8_t unique_id[128]);
+int rbl_create_dist(rbl_ctx** ctx, int device, int nranks, int rank, const uint8_t unique_id[128]);
+int rbl_free(rbl_ctx* ctx);
+const char* rbl_last_error(const rbl_ctx* ctx);
+int rbl_set_option(rbl_ctx* ctx, int option, int64_t value);
+
+/* ---- matrix --------------------------------------------------------------------------
+ * Replaces `Ag = adapt(CuArray, A)` (RBL_gpu.jl:209).  A is symmetric, so the CSC arrays
+ * of Julia's SparseMatrixCSC{Float64,Int64} are the CSR arrays of A; `index_base` 1 accepts
+ * them unchanged.  With nranks > 1 every rank passes the whole matrix and keeps the rows
+ * [row_begin,row_end) of the nnz-balanced partition (rbl_plan_row_partition). */
+int rbl_set_matrix_csc(rbl_ctx* ctx, int64_t n, int64_t nnz, const int64_t* colptr,
+                       const int64_t* rowval, const double* nzval, int index_base);
+/* Local CSR rows [row_begin,row_end) of an n x n symmetric matrix, global column ids. */
+int rbl_set_matrix_csr_rows(rbl_ctx* ctx, int64_t n, int64_t row_begin, int64_t row_end,
+                            const int64_t* rowptr, const int64_t* colind, const double* val,
+                            int index_base);
+/* Device-side generator of the seeded symmetric "hash-window" matrix:
+ * entry (r,c), |r-c| <= halfwidth, r != c, exists iff hash(seed,min,max) < density, with a
+ * uniform(-1,1) value from the same hash; diagonal = uniform(-1,1) plus plant[l] at row
+ * l*floor(n/nplant) for l < nplant.  Each rank generates only its own rows. */
+int rbl_gen_matrix_hashwindow(rbl_ctx* ctx, int64_t n, int64_t halfwidth, double density,
+                              uint64_t seed, int nplant, const double* plant);
+int rbl_matrix_info(rbl_ctx* ctx, int64_t* n, int64_t* row_begin, int64_t* row_end,
+                    int64_t* nnz_local);
+/* Download the local CSR (0-based) — test/inspection only. */
+int rbl_get_matrix_csr(rbl_ctx* ctx, int64_t* rowptr, int32_t* colind, double* val);
+
+/* ---- Krylov run -----------------------------------------------------------------------
+ * rbl_start replaces RBL_gpu.jl:213-214 (`Qg_d = CUDA.randn(n,b); Qg_d = qr(Ag*Qg_d).Q`)
+ * and the buffer planning of RBL_gpu.jl:95-104 (the whole basis lives in HBM).
+ * `omega` is the local n_local x b column-major start block, or NULL for a device
+ * counter-based N(0,1) draw from `seed`.  basis_bits: 64 (fp64 basis). */
+int rbl_start(rbl_ctx* ctx, int b, int max_blocks, int basis_bits, const double* omega,
+              uint64_t seed);
+/* One block Lanczos step i (1-based) — RBL_gpu.jl:149-161 for i == 1 and :163-184 for
+ * i >= 2: partial reorth of Q_i, Q_{i-1} against Q_1..Q_{i-2} when `part_reorth` is set
+ * (the reference sets it for even i), local reorth, U = A Q_i - Q_{i-1} B_i^T,
+ * A_i = Q_i^T U, U -= Q_i A_i, Q_{i+1} B_{i+1} = qr(U).  A_out/B_out: b x b column-major
+ * host buffers receiving A_i and B_{i+1} (upper triangular) — the only per-step traffic. */
+int rbl_step(rbl_ctx* ctx, int i, int part_reorth, double* A_out, double* B_out);
+/* Ritz vectors — RBL_gpu.jl:106-132 / RBL.jl:61-71 in fp64:  V = [Q_1..Q_nblocks] S.
+ * S: (nblocks*b) x k column-major (host); V_out: n_local x k column-major (host). */
+int rbl_ritz(rbl_ctx* ctx, int nblocks, int k, const double* S, double* V_out);
+/* Copy basis block j (1-based) to the host (n_local x b column-major) — tests only. */
+int rbl_get_block(rbl_ctx* ctx, int j, double* Q_out);
+int rbl_num_blocks(rbl_ctx* ctx);
+
+/* ---- timers --------------------------------------------------------------------------- */
+int rbl_num_stages(void);
+const char* rbl_stage_name(int stage);
+int rbl_timers(rbl_ctx* ctx, double* ms, int nstages);
+int rbl_reset_timers(rbl_ctx* ctx);
+/* Wall-clock of the device work of the most recent call (ms), from hipEvents. */
+int rbl_synchronize(rbl_ctx* ctx);
+
+/* ---- host-only planning (callable without a GPU) -------------------------------------- */
+/* nnz-balanced contiguous row partition: bounds_out[0..nranks] (bounds_out[0]=0). */
+int rbl_plan_row_partition(int64_t n, const int64_t* rowptr, int nranks, int64_t* bounds_out);
+/* Column footprint of local rows: for each rank q, the contiguous global row range
+ * [lo[q],hi[q]) of Q that the local rows reference within q's partition (lo==hi: none). */
+int rbl_plan_halo(int64_t nrows_local, const int64_t* rowptr, const int64_t* colind,
+                  int index_base, int nranks, const int64_t* bounds, int64_t* lo, int64_t* hi);
+/* Hash-window generator on the host (same bits as the device generator): counts only
+ * (rowptr_out, n_rows+1) when colind/val are NULL.  Rows [row_begin,row_end). */
+int rbl_hashwindow_rows_host(int64_t n, int64_t halfwidth, double density, uint64_t seed,
+                             int nplant, const double* plant, int64_t row_begin,
+                             int64_t row_end, int64_t* rowptr_out, int64_t* colind_out,
+                             double* val_out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RBL_HIP_H */

@@ -1,0 +1,72 @@
+"""NumPy restatement of the seeded hash-window matrix generator — TEST INFRASTRUCTURE ONLY.
+
+The synthetic inputs of SURVEY.md §8(d) (C1/C2/C4a) are defined by this generator; the HIP
+library generates the same bits on the device (gen.hip) and on the host
+(plan.cpp: rbl_hashwindow_rows_host).  Tests assert all three agree bit for bit.
+
+Definition: entry (r, c), |r - c| <= W, r != c, exists iff u53(h(seed, min, max)) < p with
+h = mix64(mix64(seed + lo) ^ hi); its value is 2 u - 1, u = u53(mix64(h ^ K)).  The diagonal
+always exists with value 2u-1 (h(seed, r, r)) plus plant[l] at row l * floor(n / nplant).
+"""
+from __future__ import annotations
+
+import numpy as np
+import scipy.sparse as sp
+
+_M = np.uint64(0xFFFFFFFFFFFFFFFF)
+_K = np.uint64(0x5851F42D4C957F2D)
+
+
+def mix64(z):
+    z = np.asarray(z, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        z = z + np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return z ^ (z >> np.uint64(31))
+
+
+def pair_hash(seed, lo, hi):
+    with np.errstate(over="ignore"):
+        return mix64(mix64(np.uint64(seed) + np.asarray(lo).astype(np.uint64))
+                     ^ np.asarray(hi).astype(np.uint64))
+
+
+def u53(h):
+    return (h >> np.uint64(11)).astype(np.float64) * 2.0 ** -53
+
+
+def hashwindow_csr(n: int, W: int, p: float, seed: int, plant=None, row_begin=0, row_end=None):
+    """Rows [row_begin, row_end) of the symmetric hash-window matrix as SciPy CSR (shape m x n)."""
+    row_end = n if row_end is None else row_end
+    rows = np.arange(row_begin, row_end, dtype=np.int64)
+    d = np.arange(-W, W + 1, dtype=np.int64)
+    R = np.repeat(rows, d.size)
+    Cc = (rows[:, None] + d[None, :]).ravel()
+    ok = (Cc >= 0) & (Cc < n)
+    R, Cc = R[ok], Cc[ok]
+    lo = np.minimum(R, Cc)
+    hi = np.maximum(R, Cc)
+    h = pair_hash(seed, lo, hi)
+    diag = R == Cc
+    keep = diag | (u53(h) < p)
+    R, Cc, h, diag = R[keep], Cc[keep], h[keep], diag[keep]
+    u = u53(mix64(h ^ _K))
+    val = (u + u) - 1.0
+    if plant is not None and len(plant):
+        plant = np.asarray(plant, dtype=np.float64)
+        stride = n // len(plant)
+        pr = R[diag]
+        add = np.zeros(pr.size)
+        sel = (pr % stride == 0) & (pr // stride < len(plant))
+        add[sel] = plant[pr[sel] // stride]
+        val[np.flatnonzero(diag)] += add
+    m = row_end - row_begin
+    A = sp.csr_matrix((val, (R - row_begin, Cc)), shape=(m, n))
+    A.sort_indices()
+    return A
+
+
+def planted_spectrum(k: int, scale: float = 100.0):
+    """Planted diagonal of SURVEY §8(d) C1: 2k entries at scale*(2k+1-l), l = 1..2k."""
+    return np.array([scale * (2 * k + 1 - l) for l in range(1, 2 * k + 1)], dtype=np.float64)

@@ -1,0 +1,252 @@
+"""CPU restatement of the reference Randomized Block Lanczos (RBL) — TEST INFRASTRUCTURE ONLY.
+
+This module is the parity *oracle* for the MI355X HIP path.  It is imported only by
+``tests/``, ``__graft_entry__.smoke()`` and the ``cpu_baseline`` leg of ``bench.py``;
+the product path (``gpu-randomized-block-lanczos_amd/rbl``) never imports it and fails
+loudly if the HIP library is missing.
+
+It restates, in NumPy/SciPy, the *effective* semantics of
+
+* ``Julia/RBL.jl:74-142``   (``lanczos_iteration`` / ``RBL`` / ``recover_eigvec``), and
+* ``Julia/common.jl:9-65``  (``insertA!``, ``insertB!``, ``dsbev``, ``sort_eig_abs``,
+  ``check_convergence``),
+
+with the GPU driver's loop bound (``Julia/RBL_gpu.jl:211``: 1200) available through
+``kryl_sz``.  Parity traps from SURVEY.md Appendix A are honoured:
+
+* P1 — ``loc_reorth!`` (``RBL.jl:4-13``) is ONE projection without renormalisation:
+  only the first iteration's in-place ``gemm!`` reaches the caller's block.
+* P3 — Ritz coefficients are fp64 (``RBL.jl:61-71``), not the fp32 ``cu()`` path.
+* P4 — ``qr_mode="posdiag"`` flips Householder signs so that ``R`` has a non-negative
+  diagonal (the CholQR convention of the HIP path); ``"householder"`` keeps LAPACK's.
+* P5 — the starting block ``Omega`` is an input (the reference draws it unseeded).
+* P6 — non-convergence returns ``converged=False`` and best-effort Ritz pairs instead
+  of the reference's BoundsError.
+* P8 — partial reorth at even ``i`` touches ``Q_i`` and ``Q_{i-1}`` against
+  ``Q_1..Q_{i-2}`` in ascending ``j`` (block MGS, ``RBL.jl:30-48``), before local reorth.
+
+Pinning: ``tests/test_oracle_known_answer.py`` runs the reference's own known-answer
+suites (``Julia/Unit Testing/test.jl:16-50`` via ``mod_dec.jl``/``slow_dec.jl``/
+``step_dec.jl``: relative eigenvalue-error norm < 1e-13).  Julia is absent from the
+image, so no reference output can be generated; those suites are the pin.
+"""
+from __future__ import annotations
+
+import numpy as np
+import scipy.linalg
+import scipy.sparse as sp
+from scipy.linalg import lapack
+
+RESIDUAL_TOL = 1e-7          # RBL.jl:109, RBL_gpu.jl:189 (absolute)
+KRYL_SZ_CPU = 1400           # RBL.jl:133
+KRYL_SZ_GPU = 1200           # RBL_gpu.jl:211
+
+
+# ----------------------------------------------------------------------------------------
+# common.jl restatement
+# ----------------------------------------------------------------------------------------
+def insertA(Ai: np.ndarray, b: int) -> np.ndarray:
+    """common.jl:9-17 — a (b+1) x b lower-band slab holding tril(A_i)."""
+    T = np.zeros((b + 1, b))
+    nA = Ai.shape[1]
+    for j in range(nA):
+        T[: nA - j, j] = Ai[j:nA, j]
+    return T
+
+
+def insertB(Bi: np.ndarray, T: np.ndarray, b: int, it: int) -> None:
+    """common.jl:20-26 — write triu(B_{it+1}) into the last rows of columns (it-1)b+1..it*b."""
+    nB = Bi.shape[1]
+    start = (it - 1) * b
+    for j in range(1, nB + 1):
+        T[T.shape[0] - j:, start + j - 1] = Bi[:j, j - 1]
+
+
+def dsbev(T: np.ndarray):
+    """common.jl:36-48 — LAPACK dsbev(jobz='V', uplo='L', kd=b) on the lower band T."""
+    w, z, info = lapack.dsbev(T, compute_v=1, lower=1)
+    if info != 0:  # the reference ignores info (common.jl:43-46); we surface it
+        raise np.linalg.LinAlgError(f"dsbev info={info}")
+    return w, z
+
+
+def sort_eig_abs(D: np.ndarray, V: np.ndarray, k: int):
+    """common.jl:50-54 — stable sort by |lambda| ascending, keep the top k (ascending)."""
+    perm = np.argsort(np.abs(D), kind="stable")
+    perm_k = perm[len(perm) - k:]
+    return D[perm_k], V[:, perm_k]
+
+
+def check_convergence(B: np.ndarray, V: np.ndarray, b: int, k: int, tol: float) -> bool:
+    """common.jl:56-65 — ||B_{i+1} S[end-b+1:end, l]||_2 <= tol for every l."""
+    Y = B @ V[V.shape[0] - b:, :]
+    return bool(np.all(np.linalg.norm(Y[:, :k], axis=0) <= tol))
+
+
+# ----------------------------------------------------------------------------------------
+# RBL.jl restatement
+# ----------------------------------------------------------------------------------------
+def _qr(U: np.ndarray, mode: str):
+    Q, R = np.linalg.qr(U, mode="reduced")     # LAPACK dgeqrf + dorgqr, as Julia's qr()
+    if mode == "posdiag":
+        s = np.sign(np.diag(R))
+        s[s == 0] = 1.0
+        Q = Q * s[None, :]
+        R = R * s[:, None]
+    return Q, R
+
+
+def loc_reorth(U1: np.ndarray, U2: np.ndarray) -> None:
+    """RBL.jl:4-13, effective semantics (P1): U1 -= U2 (U2^T U1), in place, once."""
+    U1 -= U2 @ (U2.T @ U1)
+
+
+def part_reorth(Q: list, mode: str = "mgs") -> None:
+    """RBL.jl:30-48: reorthogonalise Q[i] and Q[i-1] against Q[1..i-2] (1-based).
+
+    ``mode="mgs"`` is the reference's ascending-j block MGS; ``"cgs"`` is one block-CGS
+    projection against all j at once (the HIP path's batched form).
+    """
+    i = len(Q)
+    if i < 3:
+        return
+    if mode == "mgs":
+        for j in range(i - 2):
+            Qj = Q[j]
+            Q[i - 1] -= Qj @ (Qj.T @ Q[i - 1])
+            Q[i - 2] -= Qj @ (Qj.T @ Q[i - 2])
+    else:
+        W = np.hstack(Q[: i - 2])
+        X = np.hstack([Q[i - 1], Q[i - 2]])
+        X -= W @ (W.T @ X)
+        b = Q[0].shape[1]
+        Q[i - 1][:] = X[:, :b]
+        Q[i - 2][:] = X[:, b:]
+
+
+def recover_eigvec(Q: list, S: np.ndarray, k: int) -> np.ndarray:
+    """RBL.jl:61-71 — V = sum_j Q_j S[(j-1)b+1:jb, :] in fp64."""
+    n, b = Q[0].shape
+    V = np.zeros((n, k))
+    nblk = S.shape[0] // b
+    for j in range(nblk):
+        V += Q[j] @ S[j * b:(j + 1) * b, :k]
+    return V
+
+
+class OracleResult:
+    def __init__(self, D, V, iters, nblocks, converged, trace):
+        self.D, self.V, self.iters, self.nblocks = D, V, iters, nblocks
+        self.converged, self.trace = converged, trace
+
+    def __iter__(self):               # allow  D, V = RBL(...)
+        return iter((self.D, self.V))
+
+
+def lanczos_iteration(A, k: int, b: int, kryl_sz: int, Qi: np.ndarray, *, qr_mode="householder",
+                      reorth_mode="mgs", check=True, max_steps=None, trace=False):
+    """RBL.jl:74-117 (CPU ``lanczos_iteration``), effective semantics.
+
+    Returns (D descending |lambda|, S columns aligned, Q list, iters, converged, trace).
+    """
+    Q = [Qi]
+    tr = {"A": [], "B": []} if trace else None
+    U = A @ Qi                                            # :80
+    Ai = Qi.T @ U                                         # :81
+    U -= Qi @ Ai                                          # :82
+    Qi, Bi = _qr(U, qr_mode)                              # :84-86
+    if tr is not None:
+        tr["A"].append(Ai.copy()); tr["B"].append(Bi.copy())
+    T = insertA(Ai, b)                                    # :87
+    insertB(Bi, T, b, 1)                                  # :88
+    D = np.zeros(0); S = np.zeros((0, 0))
+    converged = False
+    i = 1
+    while i * b < kryl_sz:                                # :90
+        if max_steps is not None and i >= max_steps:
+            break
+        i += 1
+        Q.append(Qi)                                      # :92
+        if i % 2 == 0:                                    # :93-95
+            part_reorth(Q, reorth_mode)
+        loc_reorth(Q[i - 1], Q[i - 2])                    # :96
+        U = A @ Q[i - 1]                                  # :97
+        U -= Q[i - 2] @ Bi.T                              # :98
+        Ai = Q[i - 1].T @ U                               # :99
+        U -= Q[i - 1] @ Ai                                # :101
+        Qi, Bi = _qr(U, qr_mode)                          # :102-104
+        if tr is not None:
+            tr["A"].append(Ai.copy()); tr["B"].append(Bi.copy())
+        T = np.hstack([T, insertA(Ai, b)])                # :105
+        if check and (i * b > k) and (i % 4 == 0):       # :106
+            D, S = dsbev(T)                               # :107
+            D, S = sort_eig_abs(D, S, k)                  # :108
+            if check_convergence(Bi, S, b, k, RESIDUAL_TOL):   # :109
+                converged = True
+                break
+        insertB(Bi, T, b, i)                              # :113
+    if tr is not None:
+        tr["T"] = T
+    return D[::-1].copy(), S[:, ::-1].copy(), Q, i, converged, tr
+
+
+def RBL(A, k: int, b: int, *, omega=None, seed=None, kryl_sz=KRYL_SZ_CPU, qr_mode="householder",
+        reorth_mode="mgs", check=True, max_steps=None, trace=False) -> OracleResult:
+    """RBL.jl:119-142 — k largest-|lambda| eigenpairs of symmetric A with block size b."""
+    n = A.shape[1]
+    if omega is None:
+        omega = np.random.default_rng(seed).standard_normal((n, b))
+    Qi, _ = _qr(A @ np.asarray(omega, dtype=np.float64), qr_mode)   # :136-137
+    D, S, Q, iters, conv, tr = lanczos_iteration(A, k, b, kryl_sz, Qi, qr_mode=qr_mode,
+                                                 reorth_mode=reorth_mode, check=check,
+                                                 max_steps=max_steps, trace=trace)
+    V = recover_eigvec(Q, S, k) if S.size else np.zeros((n, 0))    # :140
+    if tr is not None:
+        tr["S"] = S
+        tr["Q"] = Q
+    return OracleResult(D, V, iters, len(Q), conv, tr)
+
+
+def RBL_gpu_semantics(A, k, b, **kw) -> OracleResult:
+    """RBL_gpu.jl:205-221 semantics: the same loop with max Krylov size 1200."""
+    kw.setdefault("kryl_sz", KRYL_SZ_GPU)
+    return RBL(A, k, b, **kw)
+
+
+# ----------------------------------------------------------------------------------------
+# Known-answer generators — Julia/Unit Testing/test.jl:16-50
+# ----------------------------------------------------------------------------------------
+def moderate_decay_matrix(n: int, k: int):
+    """test.jl:17-28 — a_i = i(i+1)/2; expected a[n], a[n-1], ..."""
+    a = np.cumsum(np.arange(1, n + 1, dtype=np.float64))
+    return sp.diags(a).tocsr(), a[::-1][:k].copy()
+
+
+def slow_decay_matrix(n: int, k: int):
+    """test.jl:31-37 — a_i = i."""
+    a = np.arange(1, n + 1, dtype=np.float64)
+    return sp.diags(a).tocsr(), a[::-1][:k].copy()
+
+
+def step_decay_matrix(n: int, k: int):
+    """test.jl:40-50 — ones(n) except a[2k+1-i] = i*n for i=1..2k; expected a[1:k]."""
+    a = np.ones(n)
+    sz = 2 * k
+    for i in range(1, sz + 1):
+        a[sz - i] = i * n
+    return sp.diags(a).tocsr(), a[:k].copy()
+
+
+def rbl_residual(A, eig, k, b, **kw):
+    """test.jl:10-14 — relative error vector (d - eig) ./ eig."""
+    r = RBL(A, k, b, **kw)
+    return (r.D - eig) / eig
+
+
+KNOWN_ANSWER_SUITES = {
+    # name: (generator, n values, k, b)  — mod_dec.jl/slow_dec.jl/step_dec.jl:3-7
+    "moderate": (moderate_decay_matrix, list(range(100, 1000, 200)), 5, 5),
+    "slow": (slow_decay_matrix, list(range(100, 1000, 200)), 5, 5),
+    "step": (step_decay_matrix, list(range(100000, 1000000, 200000)), 5, 5),
+}
+KNOWN_ANSWER_TOL = 1e-13

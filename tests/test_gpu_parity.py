@@ -1,0 +1,162 @@
+"""GPU parity: the HIP path (through the C-ABI) against the CPU oracle on the same inputs.
+
+Tolerances (north star / SURVEY §8(c)):
+  * eigenvalues  |lambda_gpu - lambda_oracle| / |lambda| < 1e-10;
+  * reference known-answer suites (test.jl): relative error norm < 1e-13;
+  * eigenvectors 1 - |v_gpu^T v_oracle| < 1e-8 and ||A v - lambda v|| / |lambda| < 1e-7;
+  * per-step A_i, B_{i+1} (CholQR R has a non-negative diagonal, so the oracle runs with
+    qr_mode="posdiag"): relative 1e-9 over the first steps.
+"""
+import numpy as np
+import pytest
+
+from oracle import matgen
+from oracle import rbl_oracle as o
+
+pytestmark = pytest.mark.gpu
+
+EIG_TOL = 1e-10
+VEC_TOL = 1e-8
+RES_TOL = 1e-7
+
+
+@pytest.fixture(scope="module")
+def rbl():
+    import rbl as _r
+    return _r
+
+
+def c1_matrix(n=10000, k=10, W=64, seed=20261015):
+    """symmetric hash-window + planted top spectrum."""
+    p = min(1.0, 0.01 * n / (2 * W)) if n <= 2 * W * 100 else 0.7734
+    return matgen.hashwindow_csr(n, W, p, seed, matgen.planted_spectrum(k))
+
+
+def test_device_generator_bit_exact(rbl):
+    n, W, p, seed = 20000, 64, 0.7734, 99
+    plant = matgen.planted_spectrum(10)
+    with rbl.Context(0) as ctx:
+        ctx.gen_hashwindow(n, W, p, seed, plant)
+        rp, col, val = ctx.get_matrix_csr()
+    A = matgen.hashwindow_csr(n, W, p, seed, plant)
+    assert np.array_equal(rp, A.indptr)
+    assert np.array_equal(col.astype(np.int64), A.indices)
+    assert np.array_equal(val, A.data)
+
+
+@pytest.mark.parametrize("b", [1, 5, 8, 16, 32])
+def test_first_steps_trace(rbl, b):
+    A = c1_matrix(4000, 10)
+    n = A.shape[0]
+    omega = np.random.default_rng(b).standard_normal((n, b))
+    steps = 6
+    ref = o.RBL_gpu_semantics(A, 10, b, omega=omega, qr_mode="posdiag", reorth_mode="cgs",
+                              check=False, max_steps=steps, trace=True)
+    with rbl.Context(0) as ctx:
+        ctx.set_matrix(A)
+        _, _, info = rbl.lanczos(ctx, 10, b, omega=omega, check=False, max_steps=steps,
+                                 trace=True, ritz=False)
+    assert len(info.trace_A) == len(ref.trace["A"]) == steps
+    for i in range(steps):
+        Ar, Br = ref.trace["A"][i], ref.trace["B"][i]
+        Ag, Bg = info.trace_A[i], info.trace_B[i]
+        sa = np.abs(Ar).max()
+        sb = np.abs(Br).max()
+        assert np.abs(Ag - Ar).max() <= 1e-9 * sa, (i, np.abs(Ag - Ar).max(), sa)
+        assert np.abs(Bg - Br).max() <= 1e-9 * sb, (i, np.abs(Bg - Br).max(), sb)
+
+
+@pytest.mark.parametrize("order", [0, 1])
+def test_eigenpairs_c1(rbl, order):
+    """C1 (n = 10,000, b = 8, k = 10): eigenvalues vs the oracle < 1e-10."""
+    k, b = 10, 8
+    A = c1_matrix(10000, k)
+    n = A.shape[0]
+    omega = np.random.default_rng(7).standard_normal((n, b))
+    ref = o.RBL_gpu_semantics(A, k, b, omega=omega, qr_mode="posdiag",
+                              reorth_mode="cgs" if order == 0 else "mgs")
+    D, V, info = rbl.RBL_gpu(A, k, b, omega=omega, reorth_order=order, return_info=True)
+    assert ref.converged and info.converged
+    assert info.iters == ref.iters
+    rel = np.abs(D - ref.D) / np.abs(ref.D)
+    assert rel.max() < EIG_TOL, rel
+    ov = np.abs(np.sum(V * ref.V, axis=0)) / (np.linalg.norm(V, axis=0) * np.linalg.norm(ref.V, axis=0))
+    assert (1 - ov).max() < VEC_TOL, 1 - ov
+    res = np.linalg.norm(A @ V - V * D, axis=0) / np.abs(D)
+    assert res.max() < RES_TOL, res
+
+
+@pytest.mark.parametrize("suite", ["moderate", "slow", "step"])
+def test_reference_known_answer_suites_on_gpu(rbl, suite):
+    """Julia/Unit Testing/*_dec.jl run through the HIP path (the reference only runs them on
+    its CPU RBL): relative error norm < 1e-13."""
+    gen, ns, k, b = o.KNOWN_ANSWER_SUITES[suite]
+    for n in ns:
+        A, eig = gen(n, k)
+        D, V, info = rbl.RBL_gpu(A, k, b, seed=1000 + n, return_info=True)
+        assert info.converged, (suite, n)
+        err = np.linalg.norm((D - eig) / eig)
+        assert err < o.KNOWN_ANSWER_TOL, (suite, n, err)
+
+
+def test_known_answer_with_oracle_omega(rbl):
+    """Same Omega on both sides: eigenvalues agree with the oracle to 1e-10 on a suite case
+    that runs through Krylov exhaustion (n = 100 spans R^n after 20 blocks)."""
+    A, eig = o.slow_decay_matrix(100, 5)
+    omega = np.random.default_rng(0).standard_normal((100, 5))
+    ref = o.RBL_gpu_semantics(A, 5, 5, omega=omega, qr_mode="posdiag", reorth_mode="cgs")
+    D, V, info = rbl.RBL_gpu(A, 5, 5, omega=omega, return_info=True)
+    assert np.abs(D - ref.D).max() / np.abs(ref.D).max() < EIG_TOL
+
+
+def test_basis_orthonormal(rbl):
+    A = c1_matrix(6000, 10)
+    b = 16
+    with rbl.Context(0) as ctx:
+        ctx.set_matrix(A)
+        rbl.lanczos(ctx, 10, b, seed=3, check=False, max_steps=10, ritz=False)
+        Q = np.hstack([ctx.get_block(j) for j in range(1, ctx.num_blocks() + 1)])
+    G = Q.T @ Q
+    assert np.abs(G - np.eye(G.shape[0])).max() < 1e-8
+
+
+def test_nonconvergence_warning(rbl):
+    A, _ = o.slow_decay_matrix(3000, 5)
+    D, V, info = rbl.RBL_gpu(A, 5, 5, kryl_sz=60, seed=1, return_info=True)
+    assert not info.converged and info.status == 1
+    assert V is not None and V.shape == (3000, 5)
+
+
+def test_zero_and_tiny_matrices(rbl):
+    """Edge cases: an all-zero matrix (U == 0: R = 0, Krylov breakdown) and n < b."""
+    import scipy.sparse as sp
+    Z = sp.csr_matrix((50, 50))
+    D, V, info = rbl.RBL_gpu(Z, 2, 4, seed=1, return_info=True)
+    assert info.converged and np.all(D == 0)
+    A = sp.diags(np.arange(1.0, 13.0)).tocsr()  # n = 12, b = 4: R^n exhausted after 3 blocks
+    D, V, info = rbl.RBL_gpu(A, 2, 4, seed=2, return_info=True)
+    assert info.converged
+    assert np.allclose(D, [12.0, 11.0], rtol=1e-12)
+
+
+def test_invalid_arguments_fail_loudly(rbl):
+    with rbl.Context(0) as ctx:
+        with pytest.raises(rbl.RBLError):
+            ctx.start(8, 10)                      # no matrix
+        ctx.set_matrix(c1_matrix(1000, 2))
+        with pytest.raises(rbl.RBLError):
+            ctx.start(65, 10)                     # b > 64
+        ctx.start(8, 4, seed=1)
+        with pytest.raises(rbl.RBLError):
+            ctx.step(3, False)                    # out of order
+
+
+def test_stage_timers(rbl):
+    A = c1_matrix(5000, 4)
+    with rbl.Context(0) as ctx:
+        ctx.set_matrix(A)
+        ctx.set_option(0, 1)
+        rbl.lanczos(ctx, 4, 8, seed=1, check=False, max_steps=8, ritz=True)
+        t = ctx.timers()
+    for s in ("AQ", "3-term", "qr", "part reorth", "loc reorth"):
+        assert t[s] > 0.0, (s, t)

@@ -1,0 +1,90 @@
+"""CPU: the C-ABI library loads, exports every symbol include/rbl_hip.h declares, and its
+host-only entry points (planning, host generator) agree with the oracle side."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+import scipy.sparse as sp
+
+from oracle import matgen
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "rbl_hip.h")
+
+
+def header_functions():
+    txt = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(rbl_\w+)\s*\(", txt, re.M)))
+
+
+def test_library_exports_every_header_symbol():
+    from rbl import _lib
+    names = header_functions()
+    assert len(names) >= 25
+    raw = ctypes.CDLL(_lib.LIB_PATH)
+    missing = [n for n in names if not hasattr(raw, n)]
+    assert not missing, missing
+    # and the Python binding declares a signature for each
+    assert set(names) == set(_lib.SIGNATURES), set(names) ^ set(_lib.SIGNATURES)
+
+
+def test_abi_version_and_stage_names():
+    from rbl import _lib
+    assert _lib.lib.rbl_abi_version() == 1
+    assert _lib.stage_names() == ["AQ", "3-term", "qr", "part reorth", "loc reorth",
+                                  "Ritz vectors", "comm"]
+
+
+@pytest.mark.parametrize("W,p,seed", [(0, 0.5, 1), (3, 0.9, 2), (64, 0.7734, 20261015)])
+def test_host_generator_matches_numpy(W, p, seed):
+    from rbl import _lib
+    n = 3000
+    plant = matgen.planted_spectrum(10)
+    rp, col, val = _lib.hashwindow_rows_host(n, W, p, seed, plant, 0, n)
+    A = matgen.hashwindow_csr(n, W, p, seed, plant)
+    assert np.array_equal(rp, A.indptr)
+    assert np.array_equal(col, A.indices)
+    assert np.array_equal(val, A.data)          # bit-exact
+    assert abs(A - A.T).max() == 0.0            # symmetric by construction
+
+
+def test_host_generator_row_slices_tile():
+    from rbl import _lib
+    n, W, p, seed = 2000, 16, 0.6, 5
+    full = matgen.hashwindow_csr(n, W, p, seed)
+    parts = [matgen.hashwindow_csr(n, W, p, seed, None, a, b) for a, b in [(0, 700), (700, 2000)]]
+    assert (sp.vstack(parts) != full).nnz == 0
+    rp, col, val = _lib.hashwindow_rows_host(n, W, p, seed, None, 700, 2000)
+    assert np.array_equal(col, parts[1].indices) and np.array_equal(val, parts[1].data)
+
+
+def test_row_partition_balanced_and_monotone():
+    from rbl import _lib
+    A = matgen.hashwindow_csr(10000, 32, 0.8, 3)
+    for P in (1, 2, 3, 8):
+        bnd = _lib.plan_row_partition(A.indptr, P)
+        assert bnd[0] == 0 and bnd[-1] == 10000 and np.all(np.diff(bnd) >= 0)
+        w = np.diff(A.indptr[bnd]) + np.diff(bnd)
+        assert w.max() <= w.mean() * 1.05 + 200
+
+
+def test_row_partition_ragged_rows():
+    from rbl import _lib
+    rowptr = np.array([0, 0, 0, 50, 50, 51, 51, 51, 100], dtype=np.int64)  # empty + heavy rows
+    bnd = _lib.plan_row_partition(rowptr, 3)
+    assert bnd[0] == 0 and bnd[-1] == 8 and np.all(np.diff(bnd) >= 0)
+
+
+def test_plan_halo_window():
+    from rbl import _lib
+    n, W = 1000, 10
+    A = matgen.hashwindow_csr(n, W, 1.0, 1)
+    bounds = np.array([0, 250, 500, 750, 1000], dtype=np.int64)
+    sl = A[250:500]
+    lo, hi = _lib.plan_halo(sl.indptr, sl.indices, bounds)
+    assert (lo[0], hi[0]) == (240, 250)
+    assert (lo[1], hi[1]) == (250, 500)
+    assert (lo[2], hi[2]) == (500, 510)
+    assert hi[3] == lo[3] == 0

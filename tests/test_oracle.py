@@ -1,0 +1,81 @@
+"""CPU: pin the oracle against the reference's own known-answer suites and check its helpers.
+
+Julia/Unit Testing/test.jl:16-50 with mod_dec.jl / slow_dec.jl / step_dec.jl:3-7 —
+norm of the relative eigenvalue error < 1e-13 for k = 5, b = 5.
+"""
+import numpy as np
+import pytest
+
+from oracle import rbl_oracle as o
+
+
+@pytest.mark.parametrize("suite", ["moderate", "slow", "step"])
+def test_known_answer_suites(suite):
+    gen, ns, k, b = o.KNOWN_ANSWER_SUITES[suite]
+    for n in ns:
+        A, eig = gen(n, k)
+        r = o.RBL(A, k, b, seed=1000 + n)
+        assert r.converged
+        err = np.linalg.norm((r.D - eig) / eig)
+        assert err < o.KNOWN_ANSWER_TOL, (suite, n, err)
+
+
+def test_insert_band_matches_dense_T():
+    rng = np.random.default_rng(0)
+    b, m = 3, 4
+    As = [rng.standard_normal((b, b)) for _ in range(m)]
+    As = [a + a.T for a in As]
+    Bs = [np.triu(rng.standard_normal((b, b))) for _ in range(m)]
+    T = o.insertA(As[0], b)
+    o.insertB(Bs[0], T, b, 1)
+    for i in range(1, m):
+        T = np.hstack([T, o.insertA(As[i], b)])
+        if i < m - 1:
+            o.insertB(Bs[i], T, b, i + 1)
+    N = m * b
+    dense = np.zeros((N, N))
+    for i in range(m):
+        dense[i * b:(i + 1) * b, i * b:(i + 1) * b] = As[i]
+        if i < m - 1:
+            dense[(i + 1) * b:(i + 2) * b, i * b:(i + 1) * b] = Bs[i]
+            dense[i * b:(i + 1) * b, (i + 1) * b:(i + 2) * b] = Bs[i].T
+    w, _ = o.dsbev(T)
+    assert np.allclose(np.sort(w), np.linalg.eigvalsh(dense), atol=1e-12)
+
+
+def test_sort_eig_abs_stable_and_magnitude():
+    D = np.array([-5.0, 1.0, 5.0, -2.0, 3.0])
+    V = np.eye(5)
+    d, v = o.sort_eig_abs(D, V, 3)
+    assert list(d) == [3.0, -5.0, 5.0]      # stable: -5 (index 0) before 5 (index 2)
+    assert v.shape == (5, 3)
+
+
+def test_mgs_and_cgs_reorth_agree():
+    rng = np.random.default_rng(1)
+    n, b = 200, 4
+    # orthonormal earlier blocks (as in Lanczos) + targets with a small loss of orthogonality
+    Qa = np.linalg.qr(rng.standard_normal((n, 5 * b)))[0]
+    Q = [Qa[:, j * b:(j + 1) * b].copy() for j in range(5)]
+    for t in (3, 4):
+        Q[t] += 1e-6 * (Q[0] @ rng.standard_normal((b, b)) + Q[1] @ rng.standard_normal((b, b)))
+    Q1 = [q.copy() for q in Q]
+    Q2 = [q.copy() for q in Q]
+    o.part_reorth(Q1, "mgs")
+    o.part_reorth(Q2, "cgs")
+    for a, c in zip(Q1, Q2):
+        assert np.allclose(a, c, atol=1e-12)
+
+
+def test_nonconvergence_is_reported():
+    A, _ = o.slow_decay_matrix(2000, 5)
+    r = o.RBL(A, 5, 5, seed=3, kryl_sz=60)
+    assert not r.converged
+    assert r.V.shape[0] == 2000
+
+
+def test_posdiag_qr_gives_same_eigenvalues():
+    A, eig = o.moderate_decay_matrix(300, 5)
+    r1 = o.RBL(A, 5, 5, seed=11, qr_mode="householder")
+    r2 = o.RBL(A, 5, 5, seed=11, qr_mode="posdiag")
+    assert np.allclose(r1.D, r2.D, rtol=1e-13)
