@@ -28,11 +28,14 @@ struct CsrDev {
   const int64_t* rowptr = nullptr;
   const int32_t* col = nullptr;
   const double* val = nullptr;
-  // LDS-window metadata (per row tile): min/max column, and whether every tile fits.
+  // LDS-window metadata (16-row tiles): forward-filled min/max column per tile, and
+  // whether every tile fits the window kernel's ring for b = 16 / b = 32.
   const int64_t* tile_cmin = nullptr;
   const int64_t* tile_cmax = nullptr;
-  int tile_rows = 0;
-  bool window_ok = false;
+  int64_t ntiles = 0;
+  int64_t tiles_per_wg = 0;
+  bool window_ok16 = false;
+  bool window_ok32 = false;
 };
 
 // --- spmm.hip ----------------------------------------------------------------------------
@@ -40,6 +43,12 @@ struct CsrDev {
 // variant: 0 auto, 1 global gather, 2 LDS window.
 void spmm(const CsrDev& A, const double* Qin, int64_t col_off, int b, double* U,
           const double* Qprev, const double* Bi, int variant, hipStream_t s);
+
+// spmm_window.hip: persistent LDS-window kernel (b in {16,32}); false if not applicable.
+bool spmm_window(const CsrDev& A, const double* Qin, int64_t col_off, int b, double* U,
+                 const double* Qprev, const double* Bi, hipStream_t s);
+int window_grid();              // workgroups for the window kernel (= CUs)
+constexpr int kWindowTileRows = 16;
 
 // --- tsmm.hip ----------------------------------------------------------------------------
 // Partial Gram:  slab[s][a][c] = sum over rows of split s of W[r][a] * X[r][c]

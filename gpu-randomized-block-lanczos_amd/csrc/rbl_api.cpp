@@ -35,8 +35,8 @@ struct rbl_ctx {
   double* d_val = nullptr;
   int64_t* d_tcmin = nullptr;
   int64_t* d_tcmax = nullptr;
-  int tile_rows = 256;
-  bool window_ok = false;
+  int64_t ntiles = 0, tiles_per_wg = 0;
+  bool window_ok16 = false, window_ok32 = false;
   std::vector<int64_t> bounds;            // nranks+1
   std::vector<int64_t> need_lo, need_hi;  // rows I need from rank q
   std::vector<int64_t> give_lo, give_hi;  // rows rank q needs from me
@@ -110,9 +110,63 @@ CsrDev csr(rbl_ctx* ctx) {
   A.val = ctx->d_val;
   A.tile_cmin = ctx->d_tcmin;
   A.tile_cmax = ctx->d_tcmax;
-  A.tile_rows = ctx->tile_rows;
-  A.window_ok = ctx->window_ok;
+  A.ntiles = ctx->ntiles;
+  A.tiles_per_wg = ctx->tiles_per_wg;
+  A.window_ok16 = ctx->window_ok16;
+  A.window_ok32 = ctx->window_ok32;
   return A;
+}
+
+// Per-16-row-tile column footprint for the LDS-window SpMM and the checks that every tile
+// fits its ring (spmm_window.hip): columns sorted per row, footprints non-decreasing, a
+// tile's nonzeros <= 2048, ring rows: 256 (b=32) / 512 (b=16), new rows per tile <= 32 / 64.
+int prepare_window(rbl_ctx* ctx, const std::vector<int64_t>& rp) {
+  ctx->window_ok16 = ctx->window_ok32 = false;
+  ctx->ntiles = (ctx->nloc + kWindowTileRows - 1) / kWindowTileRows;
+  if (ctx->ntiles == 0 || ctx->nnz == 0) return RBL_OK;
+  const int64_t nt = ctx->ntiles;
+  HIPC(hipMalloc(&ctx->d_tcmin, nt * sizeof(int64_t)));
+  HIPC(hipMalloc(&ctx->d_tcmax, nt * sizeof(int64_t)));
+  CsrDev A;
+  A.nrows = ctx->nloc;
+  A.rowptr = ctx->d_rowptr;
+  A.col = ctx->d_col;
+  tile_col_range(A, kWindowTileRows, ctx->d_tcmin, ctx->d_tcmax, ctx->stream);
+  std::vector<int64_t> cmin(nt), cmax(nt);
+  HIPC(hipMemcpyAsync(cmin.data(), ctx->d_tcmin, nt * sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
+  HIPC(hipMemcpyAsync(cmax.data(), ctx->d_tcmax, nt * sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
+  HIPC(hipStreamSynchronize(ctx->stream));
+  // forward-fill empty tiles (cmax < 0), then backward-fill leading empties
+  int64_t first = -1;
+  for (int64_t t = 0; t < nt; ++t) {
+    if (cmax[t] < 0) {
+      if (t > 0) { cmin[t] = cmin[t - 1]; cmax[t] = cmax[t - 1]; }
+    } else if (first < 0) {
+      first = t;
+    }
+  }
+  if (first < 0) return RBL_OK;
+  for (int64_t t = 0; t < first; ++t) { cmin[t] = cmin[first]; cmax[t] = cmax[first]; }
+  bool ok = true;
+  int64_t max_span = 0, max_new = 0;
+  for (int64_t t = 0; t < nt && ok; ++t) {
+    const int64_t ra = t * kWindowTileRows;
+    const int64_t rb = std::min(ra + kWindowTileRows, ctx->nloc);
+    if (rp[rb] - rp[ra] > 2048) ok = false;
+    max_span = std::max(max_span, cmax[t] + 1 - cmin[t]);
+    if (t > 0) {
+      if (cmin[t] < cmin[t - 1] || cmax[t] < cmax[t - 1]) ok = false;
+      max_span = std::max(max_span, cmax[t] + 1 - cmin[t - 1]);
+      max_new = std::max(max_new, cmax[t] - std::max(cmax[t - 1], cmin[t] - 1));
+    }
+  }
+  ctx->window_ok32 = ok && max_span <= 256 && max_new <= 32;
+  ctx->window_ok16 = ok && max_span <= 512 && max_new <= 64;
+  HIPC(hipMemcpy(ctx->d_tcmin, cmin.data(), nt * sizeof(int64_t), hipMemcpyHostToDevice));
+  HIPC(hipMemcpy(ctx->d_tcmax, cmax.data(), nt * sizeof(int64_t), hipMemcpyHostToDevice));
+  const int64_t grid = window_grid();
+  ctx->tiles_per_wg = std::max<int64_t>(1, (nt + grid - 1) / grid);
+  return RBL_OK;
 }
 
 // ---- timers --------------------------------------------------------------------------
@@ -294,6 +348,8 @@ void free_matrix(rbl_ctx* ctx) {
   hipFree(ctx->d_tcmin); ctx->d_tcmin = nullptr;
   hipFree(ctx->d_tcmax); ctx->d_tcmax = nullptr;
   ctx->n = ctx->nloc = ctx->nnz = 0;
+  ctx->ntiles = ctx->tiles_per_wg = 0;
+  ctx->window_ok16 = ctx->window_ok32 = false;
 }
 
 // Exchange halo needs among ranks and size the extended buffer.
@@ -387,6 +443,7 @@ int upload_csr(rbl_ctx* ctx, int64_t n, int64_t r0, int64_t r1, const int64_t* r
       ctx->need_hi[q] = hi[q] < 0 ? 0 : hi[q];
     }
   }
+  CHK(prepare_window(ctx, rp));
   return setup_halo(ctx);
 }
 
@@ -563,6 +620,7 @@ int rbl_gen_matrix_hashwindow(rbl_ctx* ctx, int64_t n, int64_t halfwidth, double
       ctx->need_hi[q] = hi;
     }
   }
+  CHK(prepare_window(ctx, rp));
   return setup_halo(ctx);
 }
 
@@ -588,6 +646,51 @@ int rbl_get_matrix_csr(rbl_ctx* ctx, int64_t* rowptr, int32_t* colind, double* v
   return RBL_OK;
 }
 
+int rbl_spmm_kernel_for(rbl_ctx* ctx, int b) {
+  if (!ctx || !ctx->d_rowptr) return RBL_ERR_INVALID;
+  if (ctx->spmm_variant == 1) return 1;
+  const bool win = ctx->ntiles > 0 && ((b == 16 && ctx->window_ok16) || (b == 32 && ctx->window_ok32));
+  return win ? 2 : 1;
+}
+
+int rbl_apply(rbl_ctx* ctx, int b, const double* X, double* Y) {
+  if (!ctx || b < 1 || b > 64 || !X || !Y) return fail(ctx, RBL_ERR_INVALID, "rbl_apply: bad arguments");
+  if (!ctx->d_rowptr) return fail(ctx, RBL_ERR_STATE, "rbl_apply: no matrix");
+  if (ctx->b != 0 && ctx->b != b && ctx->nranks > 1)
+    return fail(ctx, RBL_ERR_STATE, "rbl_apply: b differs from the running Krylov block size");
+  HIPC(hipSetDevice(ctx->device));
+  const int64_t nl = std::max<int64_t>(ctx->nloc, 1);
+  double *d_x = nullptr, *d_xr = nullptr, *d_y = nullptr, *d_ext = nullptr;
+  HIPC(hipMalloc(&d_x, nl * b * sizeof(double)));
+  HIPC(hipMalloc(&d_xr, nl * b * sizeof(double)));
+  HIPC(hipMalloc(&d_y, nl * b * sizeof(double)));
+  HIPC(hipMemcpyAsync(d_x, X, ctx->nloc * b * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+  colmajor_to_rowmajor(d_x, ctx->nloc, b, d_xr, ctx->stream);
+  const double* Qin = d_xr;
+  int64_t off = 0;
+  if (ctx->nranks > 1) {  // halo exchange through a private extended buffer
+    HIPC(hipMalloc(&d_ext, std::max<int64_t>(ctx->ext_hi - ctx->ext_lo, 1) * b * sizeof(double)));
+    double* keep_ext = ctx->d_qext;
+    const int keep_b = ctx->b;
+    ctx->d_qext = d_ext;
+    ctx->b = b;
+    const int st = halo_exchange(ctx, d_xr, &Qin, &off);
+    ctx->d_qext = keep_ext;
+    ctx->b = keep_b;
+    if (st < 0) return st;
+  }
+  spmm(csr(ctx), Qin, off, b, d_y, nullptr, nullptr, ctx->spmm_variant, ctx->stream);
+  HIPC(hipGetLastError());
+  rowmajor_to_colmajor(d_y, ctx->nloc, b, d_x, ctx->stream);
+  HIPC(hipMemcpyAsync(Y, d_x, ctx->nloc * b * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+  HIPC(hipStreamSynchronize(ctx->stream));
+  hipFree(d_x);
+  hipFree(d_xr);
+  hipFree(d_y);
+  hipFree(d_ext);
+  return RBL_OK;
+}
+
 int rbl_start(rbl_ctx* ctx, int b, int max_blocks, int basis_bits, const double* omega,
               uint64_t seed) {
   if (!ctx) return RBL_ERR_INVALID;
@@ -597,6 +700,14 @@ int rbl_start(rbl_ctx* ctx, int b, int max_blocks, int basis_bits, const double*
   if (basis_bits != 64) return fail(ctx, RBL_ERR_INVALID, "only the fp64 basis is implemented");
   HIPC(hipSetDevice(ctx->device));
   HIPC(hipStreamSynchronize(ctx->stream));
+  // a repeated run with the same shape reuses the HBM plan (allocating ~100 GB of basis
+  // per run costs more than the run itself at n = 1e7)
+  const bool reuse = ctx->d_basis && ctx->b == b && ctx->max_blocks == max_blocks &&
+                     ctx->slot == ctx->nloc * b;
+  if (reuse) {
+    ctx->nblocks = 0;
+    HIPC(hipMemsetAsync(ctx->d_flags, 0, 4 * sizeof(int), ctx->stream));
+  } else {
   free_run(ctx);
   ctx->b = b;
   ctx->max_blocks = max_blocks;
@@ -623,6 +734,7 @@ int rbl_start(rbl_ctx* ctx, int b, int max_blocks, int basis_bits, const double*
   HIPC(hipMalloc(&ctx->d_flags, 4 * sizeof(int)));
   HIPC(hipMemset(ctx->d_flags, 0, 4 * sizeof(int)));
   HIPC(hipHostMalloc(&ctx->h_pin, 2 * b * b * sizeof(double), hipHostMallocDefault));
+  }
 
   // Omega (row-major) in d_T
   if (omega) {

@@ -49,6 +49,8 @@ SIGNATURES = {
     "rbl_gen_matrix_hashwindow": (C.c_int, [_p, _i64, _i64, C.c_double, _u64, C.c_int, _pd]),
     "rbl_matrix_info": (C.c_int, [_p, _pi64, _pi64, _pi64, _pi64]),
     "rbl_get_matrix_csr": (C.c_int, [_p, _pi64, _pi32, _pd]),
+    "rbl_apply": (C.c_int, [_p, C.c_int, _pd, _pd]),
+    "rbl_spmm_kernel_for": (C.c_int, [_p, C.c_int]),
     "rbl_start": (C.c_int, [_p, C.c_int, C.c_int, C.c_int, _pd, _u64]),
     "rbl_step": (C.c_int, [_p, C.c_int, C.c_int, _pd, _pd]),
     "rbl_ritz": (C.c_int, [_p, C.c_int, C.c_int, _pd, _pd]),

@@ -116,6 +116,19 @@ class Context:
                     "rbl_get_matrix_csr")
         return rowptr, col[:nnz], val[:nnz]
 
+    def apply(self, X: np.ndarray) -> np.ndarray:
+        """Y = A X on the device (local rows), through the same SpMM kernels as a step."""
+        n, r0, r1, _ = self.matrix_info()
+        X = np.asfortranarray(X, dtype=np.float64)
+        b = X.shape[1]
+        Y = np.zeros((r1 - r0, b), order="F")
+        self._check(lib.rbl_apply(self._h, b, dptr(X), dptr(Y)), "rbl_apply")
+        return Y
+
+    def spmm_kernel_for(self, b: int) -> int:
+        """1 = global-gather CSR kernel, 2 = LDS-window CSR kernel."""
+        return self._check(lib.rbl_spmm_kernel_for(self._h, b), "rbl_spmm_kernel_for")
+
     # -- Krylov run -------------------------------------------------------------------------
     def start(self, b: int, max_blocks: int, omega=None, seed: int = 0) -> None:
         om = None

@@ -90,6 +90,13 @@ int rbl_matrix_info(rbl_ctx* ctx, int64_t* n, int64_t* row_begin, int64_t* row_e
                     int64_t* nnz_local);
 /* Download the local CSR (0-based) — test/inspection only. */
 int rbl_get_matrix_csr(rbl_ctx* ctx, int64_t* rowptr, int32_t* colind, double* val);
+/* Y = A X for a host n_local x b column-major block (the operator of RBL_gpu.jl:176,
+ * `mul!(U, Ag, Qg_d)`), through the same SpMM kernels as rbl_step (multi-rank: with the
+ * halo exchange).  Allocates its own device buffers. */
+int rbl_apply(rbl_ctx* ctx, int b, const double* X, double* Y);
+/* Which SpMM kernel rbl_step / rbl_apply use for block size b under the current option:
+ * 1 = global-gather CSR, 2 = LDS-window CSR. */
+int rbl_spmm_kernel_for(rbl_ctx* ctx, int b);
 
 /* ---- Krylov run -----------------------------------------------------------------------
  * rbl_start replaces RBL_gpu.jl:213-214 (`Qg_d = CUDA.randn(n,b); Qg_d = qr(Ag*Qg_d).Q`)

@@ -1,0 +1,93 @@
+"""GPU: the CSR SpMM kernels (global gather and LDS window) against SciPy's A @ X.
+
+Floating-point tolerance: every output element within 1e-13 * (|A| |X|) of the fp64 SciPy
+product (the kernels only reorder the fp64 sums)."""
+import numpy as np
+import pytest
+import scipy.sparse as sp
+
+from oracle import matgen
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def rbl():
+    import rbl as _r
+    return _r
+
+
+def _check(A, Y, X):
+    ref = A @ X
+    bound = (abs(A) @ np.abs(X)) * 1e-13 + 1e-300
+    assert np.all(np.abs(Y - ref) <= bound), np.max(np.abs(Y - ref) / bound)
+
+
+def _rand_sym(n, density, seed, empty_rows=()):
+    R = sp.random(n, n, density=density, random_state=seed, format="csr")
+    A = (R + R.T).tolil()
+    for r in empty_rows:
+        A[r, :] = 0
+        A[:, r] = 0
+    return sp.csr_matrix(A)
+
+
+@pytest.mark.parametrize("b", [1, 5, 8, 16, 32, 64])
+@pytest.mark.parametrize("variant", [0, 1])
+def test_spmm_hashwindow(rbl, b, variant):
+    A = matgen.hashwindow_csr(7000, 64, 0.7734, 5, matgen.planted_spectrum(10))
+    X = np.random.default_rng(b).standard_normal((A.shape[0], b))
+    with rbl.Context(0) as ctx:
+        ctx.set_matrix(A)
+        ctx.set_option(2, variant)
+        if variant == 0 and b in (16, 32):
+            assert ctx.spmm_kernel_for(b) == 2      # the LDS-window kernel is the one tested
+        Y = ctx.apply(X)
+    _check(A, Y, X)
+
+
+@pytest.mark.parametrize("b", [16, 32])
+def test_spmm_window_ragged_and_partial_tiles(rbl, b):
+    """n not a multiple of the 16-row tile, narrow and wide windows, rows of very different
+    lengths and a band that grows then shrinks."""
+    for n, W, p in [(1001, 3, 0.9), (333, 100, 0.3), (4099, 64, 1.0), (17, 8, 0.5)]:
+        A = matgen.hashwindow_csr(n, W, p, n)
+        X = np.random.default_rng(n).standard_normal((n, b))
+        with rbl.Context(0) as ctx:
+            ctx.set_matrix(A)
+            Y = ctx.apply(X)
+            k = ctx.spmm_kernel_for(b)
+        _check(A, Y, X)
+        tile_nnz = np.diff(A.indptr[np.r_[np.arange(0, n, 16), n]]).max()
+        if W <= 64 and tile_nnz <= 2048:     # the window kernel's metadata cap per tile
+            assert k == 2, (n, W)
+        if tile_nnz > 2048:
+            assert k == 1, (n, W)
+
+
+@pytest.mark.parametrize("b", [8, 16, 32])
+def test_spmm_general_pattern_and_empty_rows(rbl, b):
+    """Random (R-MAT-like, unbanded) pattern: the gather kernel; empty rows give zero rows."""
+    A = _rand_sym(3000, 0.01, 3, empty_rows=(0, 5, 2999))
+    X = np.random.default_rng(1).standard_normal((3000, b))
+    with rbl.Context(0) as ctx:
+        ctx.set_matrix(A)
+        assert ctx.spmm_kernel_for(b) == 1
+        Y = ctx.apply(X)
+    _check(A, Y, X)
+    assert np.all(Y[[0, 5, 2999]] == 0)
+
+
+def test_spmm_window_and_gather_agree_in_lanczos(rbl):
+    """The whole block step is insensitive to the SpMM kernel choice (1e-12 on A_i)."""
+    A = matgen.hashwindow_csr(6000, 64, 0.7734, 9, matgen.planted_spectrum(10))
+    out = []
+    for variant in (1, 0):
+        with rbl.Context(0) as ctx:
+            ctx.set_matrix(A)
+            ctx.set_option(2, variant)
+            _, _, info = rbl.lanczos(ctx, 10, 32, seed=4, check=False, max_steps=6, trace=True,
+                                     ritz=False)
+            out.append(info)
+    for a1, a2 in zip(out[0].trace_A, out[1].trace_A):
+        assert np.abs(a1 - a2).max() <= 1e-12 * np.abs(a1).max()

@@ -1,15 +1,15 @@
+# GPU round check: parity tests, then the bench, then a rocprofv3 kernel trace of the bench.
 set -u
 mkdir -p gpurun_out
-rocminfo 2>/dev/null | grep -m3 -E "gfx|Marketing" > gpurun_out/rocminfo.txt
-timeout -k 10 600 python -m pytest tests -m gpu -q --timeout 300 > gpurun_out/t1.log 2>&1; rc=$?
-echo "pytest rc=$rc"
-if [ $rc -gt 1 ]; then exit $rc; fi
-timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1; rc=$?
-echo "smoke rc=$rc"
-if [ $rc -gt 1 ]; then exit $rc; fi
-timeout -k 10 300 python bench.py --n 1000000 --b 16 --k 20 --steps 2 --no-cpu-baseline > gpurun_out/b1.log 2>&1; rc=$?
-echo "bench small rc=$rc"
+export TMPDIR=/tmp
+timeout -k 10 900 python -m pytest tests -m gpu -q --timeout 300 -x > gpurun_out/t1.log 2>&1; rc=$?
+echo "pytest rc=$rc"; tail -3 gpurun_out/t1.log
 if [ $rc -ne 0 ]; then exit $rc; fi
-timeout -k 10 600 python bench.py --steps 2 > gpurun_out/b2.log 2>&1; rc=$?
-echo "bench full rc=$rc"
+timeout -k 10 900 python bench.py --steps 2 > gpurun_out/b2.log 2>&1; rc=$?
+echo "bench rc=$rc"; tail -c 3000 gpurun_out/b2.log
+if [ $rc -ne 0 ]; then exit $rc; fi
+if [ "${PROFILE:-1}" = "1" ]; then
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-ttk > gpurun_out/prof.log 2>&1; rc=$?
+echo "rocprof rc=$rc"
+fi
 exit $rc
