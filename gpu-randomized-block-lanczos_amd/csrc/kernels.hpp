@@ -65,6 +65,16 @@ void reduce_slab(const double* slab, int splits, int64_t len, double* out, const
 void tsmm(int64_t nrows, const PanelRun& X, const double* C, int ldc, const Panels& Y,
           double alpha, double beta, const int* skip, hipStream_t s);
 
+// --- reorth.hip: v_mfma_f64_4x4x4f64 fast paths (panel widths 16 / 32), selected by
+// gram_splits / gram_partial / tsmm above when applicable.
+bool gram44_ok(int nW, int w, int xcount, int xw);
+int gram44_splits(int64_t nrows, int nW);
+void gram44_partial(int64_t nrows, const PanelRun& W, const Panels& X, double* slab, int splits,
+                    const int* skip, hipStream_t s);
+bool tsmm44_ok(int xw, int ky);
+void tsmm44(int64_t nrows, const PanelRun& X, const double* C, int ldc, const Panels& Y,
+            double alpha, double beta, const int* skip, hipStream_t s);
+
 // --- smallmat.hip ------------------------------------------------------------------------
 // Cholesky step of (shifted) CholQR on the b x b Gram G (row-major, symmetric):
 //   mode 0: first pass — try unshifted; on breakdown or estimated cond > 3e7 use the

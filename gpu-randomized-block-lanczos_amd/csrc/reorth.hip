@@ -1,0 +1,312 @@
+// reorth.hip — fp64 tall-skinny GEMMs on v_mfma_f64_4x4x4f64 (gfx950).
+//
+// Measured on MI355X (tools/mfma_probe.hip): the 4-block 4x4x4 fp64 MFMA sustains ~71 TF/s,
+// the 16x16x4 shape ~46 TF/s, so the compute-heavy GEMMs of the block step use 4x4x4:
+//   * k_gram44:  C = W^T X  with W the Krylov basis (m panels) and X = [Q_i, Q_{i-1}] —
+//                the partial-reorth coefficients of RBL_gpu.jl:33,39 (part_reorth_gpu_async!)
+//                batched over every j (block CGS, one launch instead of 2(i-2) gemms);
+//   * k_tsmm44:  Y = beta Y + alpha X C  with X a run of panels — the partial-reorth update
+//                (RBL_gpu.jl:34,40), the 3-term / local-reorth updates, CholQR apply and the
+//                Ritz projection V = [Q_1..Q_m] S (RBL_gpu.jl:121, RBL.jl:68).
+//
+// v_mfma_f64_4x4x4f64 lane layout (tools/mfma_layout_probe.hip), block g = (lane>>2)&3:
+//   A[i = lane&3][k = lane>>4], B[k = lane>>4][j = lane&3], D[i = lane>>4][j = lane&3].
+// With the 4 blocks on 4 consecutive row-quads, the A operand of a wave is
+//   M[r0 + (lane&15)][k0 + (lane>>4)]  (Gram: W^T -> W[r0+(lane>>4)][a0+(lane&15)]),
+// i.e. 16 consecutive doubles per k — coalesced 128-B segments.
+#include "kernels.hpp"
+
+namespace rbl {
+
+__device__ __forceinline__ double mfma4(double a, double b, double c) {
+  return __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, c, 0, 0, 0);
+}
+
+// ----------------------------------------------------------------------------------------
+// Gram C = W^T X: one Krylov panel per wave (8 panels per workgroup), X rows staged in LDS
+// in 32-row chunks shared by the 8 waves, A operands prefetched one chunk ahead.
+// ----------------------------------------------------------------------------------------
+constexpr int kG44Waves = 8;
+constexpr int kG44Rows = 32;
+
+template <int B, int NX>
+__global__ __launch_bounds__(512) void k_gram44(int64_t nrows, PanelRun W, Panels X, double* slab,
+                                                int npg, int64_t rows_per, const int* skip) {
+  if (skip && *skip) return;
+  constexpr int KC = NX * B;
+  constexpr int AG = B / 16;
+  constexpr int CG = KC / 4;
+  constexpr int LD = KC + 4;  // +8 dwords: the 2 rows a half-wave reads sit in different banks
+  constexpr int EPT = kG44Rows * KC / 512;
+  __shared__ __attribute__((aligned(16))) double xs[2][kG44Rows * LD];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int q = lane >> 4;
+  // XCD-aware mapping: the npg workgroups of one row split share blockIdx % 8 (one XCD under
+  // round-robin dispatch) and are consecutive there, so X is fetched once per XCD L2.
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, t = bid >> 3;
+  const int pg = t % npg;
+  const int64_t s = (int64_t)(t / npg) * 8 + xcd;
+  const int64_t r_begin = s * rows_per;
+  const int64_t r_end = r_begin + rows_per < nrows ? r_begin + rows_per : nrows;
+  const int j = pg * kG44Waves + wave;
+  const bool active = j < W.count;
+  const double* wp = W.base + (int64_t)(active ? j : 0) * W.stride + (lane & 15);
+
+  double acc[AG][CG];
+#pragma unroll
+  for (int ag = 0; ag < AG; ++ag)
+#pragma unroll
+    for (int cg = 0; cg < CG; ++cg) acc[ag][cg] = 0.0;
+
+  const int xe0 = tid * EPT;
+  const int xrow = xe0 / KC, xcol = xe0 % KC;
+  const double* xsrc = X.ptr[xcol / B] + (xcol % B);
+  auto load_x = [&](int64_t rc0, double (&xr)[EPT]) {
+    const int64_t r = rc0 + xrow;
+#pragma unroll
+    for (int v = 0; v < EPT; ++v) xr[v] = r < r_end ? xsrc[r * B + v] : 0.0;
+  };
+  auto store_x = [&](int buf, const double (&xr)[EPT]) {
+#pragma unroll
+    for (int v = 0; v < EPT; ++v) xs[buf][xrow * LD + xcol + v] = xr[v];
+  };
+  auto load_a = [&](int64_t rc0, double (&ar)[8][AG]) {
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+      const int64_t r = rc0 + 4 * ks + q;
+      const bool ok = active && r < r_end;
+#pragma unroll
+      for (int ag = 0; ag < AG; ++ag) ar[ks][ag] = ok ? wp[r * B + 16 * ag] : 0.0;
+    }
+  };
+
+  const int64_t nchunks = r_end > r_begin ? (r_end - r_begin + kG44Rows - 1) / kG44Rows : 0;
+  double xr[EPT];
+  double acur[8][AG], anext[8][AG];
+  if (nchunks > 0) {
+    load_x(r_begin, xr);
+    store_x(0, xr);
+    load_a(r_begin, acur);
+  }
+  __syncthreads();
+  for (int64_t c = 0; c < nchunks; ++c) {
+    const int64_t rc0 = r_begin + c * kG44Rows;
+    const bool more = c + 1 < nchunks;
+    if (more) {
+      load_x(rc0 + kG44Rows, xr);
+      load_a(rc0 + kG44Rows, anext);
+    }
+    const double* xb = xs[c & 1];
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+#pragma unroll
+      for (int cg = 0; cg < CG; ++cg) {
+        const double bf = xb[(4 * ks + q) * LD + 4 * cg + (lane & 3)];
+#pragma unroll
+        for (int ag = 0; ag < AG; ++ag) acc[ag][cg] = mfma4(acur[ks][ag], bf, acc[ag][cg]);
+      }
+    }
+    if (more) {
+      store_x((int)((c + 1) & 1), xr);
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks)
+#pragma unroll
+        for (int ag = 0; ag < AG; ++ag) acur[ks][ag] = anext[ks][ag];
+    }
+    __syncthreads();
+  }
+  if (!active) return;
+  const int KW = W.count * B;
+  double* out = slab + (s * KW + (int64_t)j * B) * KC;
+  const int g = (lane >> 2) & 3;
+#pragma unroll
+  for (int ag = 0; ag < AG; ++ag)
+#pragma unroll
+    for (int cg = 0; cg < CG; ++cg) {
+      const int a = 16 * ag + 4 * g + (lane >> 4);
+      const int cc = 4 * cg + (lane & 3);
+      out[(int64_t)a * KC + cc] = acc[ag][cg];
+    }
+}
+
+bool gram44_ok(int nW, int w, int xcount, int xw) {
+  return nW >= 2 && (w == 16 || w == 32) && xw == w && (xcount == 1 || xcount == 2);
+}
+
+int gram44_splits(int64_t nrows, int nW) {
+  const int npg = (nW + kG44Waves - 1) / kG44Waves;
+  // ~2 workgroups per CU of 8 waves; splits a multiple of 8 (XCD mapping), >= 256 rows each
+  int64_t s8 = (512 + 8 * npg - 1) / (8 * npg);
+  const int64_t max_s8 = (nrows + 8 * 256 - 1) / (8 * 256);
+  if (s8 > max_s8) s8 = max_s8;
+  if (s8 < 1) s8 = 1;
+  return (int)(s8 * 8);
+}
+
+template <int B, int NX>
+static void launch_gram44(int64_t nrows, const PanelRun& W, const Panels& X, double* slab,
+                          int splits, const int* skip, hipStream_t st) {
+  const int npg = (W.count + kG44Waves - 1) / kG44Waves;
+  int64_t rows_per = (nrows + splits - 1) / splits;
+  rows_per = (rows_per + kG44Rows - 1) / kG44Rows * kG44Rows;
+  hipLaunchKernelGGL((k_gram44<B, NX>), dim3(npg * splits), dim3(512), 0, st, nrows, W, X, slab,
+                     npg, rows_per, skip);
+}
+
+void gram44_partial(int64_t nrows, const PanelRun& W, const Panels& X, double* slab, int splits,
+                    const int* skip, hipStream_t st) {
+  if (W.w == 32) {
+    if (X.count == 2) return launch_gram44<32, 2>(nrows, W, X, slab, splits, skip, st);
+    return launch_gram44<32, 1>(nrows, W, X, slab, splits, skip, st);
+  }
+  if (X.count == 2) return launch_gram44<16, 2>(nrows, W, X, slab, splits, skip, st);
+  return launch_gram44<16, 1>(nrows, W, X, slab, splits, skip, st);
+}
+
+// ----------------------------------------------------------------------------------------
+// Y = beta Y + alpha X C: 4 waves x 32 rows per workgroup, C staged in LDS 32 k at a time,
+// A operands read 2 k per 16-B load (k permuted consistently in A and B), next chunk's A
+// prefetched while the current one computes.
+// ----------------------------------------------------------------------------------------
+constexpr int kT44Rows = 32;   // rows per wave
+constexpr int kT44K = 32;      // k per chunk
+
+template <int B, int KYP>
+__global__ __launch_bounds__(256) void k_tsmm44(int64_t nrows, PanelRun X, const double* __restrict__ C,
+                                                int ldc, int KY, Panels Y, double alpha, double beta,
+                                                const int* skip) {
+  if (skip && *skip) return;
+  constexpr int CG = KYP / 4;
+  constexpr int LDC = KYP + 4;
+  __shared__ __attribute__((aligned(16))) double cs[2][kT44K * LDC];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int q = lane >> 4;
+  const int64_t r0 = ((int64_t)blockIdx.x * 4 + wave) * kT44Rows;
+  const int K = X.count * B;
+  const int nch = (K + kT44K - 1) / kT44K;
+
+  double acc[2][CG];
+#pragma unroll
+  for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+    for (int cg = 0; cg < CG; ++cg) acc[rt][cg] = 0.0;
+
+  // A: rows r0 + 16 rt + (lane&15); k = k0 + 8 h + 2 q + v, h in [0,4), v in {0,1}
+  int64_t arow[2];
+  bool aok[2];
+#pragma unroll
+  for (int rt = 0; rt < 2; ++rt) {
+    arow[rt] = r0 + 16 * rt + (lane & 15);
+    aok[rt] = arow[rt] < nrows;
+  }
+  typedef double d2v __attribute__((ext_vector_type(2)));
+  auto load_a = [&](int ch, d2v (&ar)[2][4]) {
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+      const int k = ch * kT44K + 8 * h + 2 * q;
+      const bool kv = k < K;
+      const int pan = kv ? k / B : 0;
+      const int col = k - pan * B;
+      const double* xp = X.base + (int64_t)pan * X.stride + col;
+#pragma unroll
+      for (int rt = 0; rt < 2; ++rt) {
+        if (kv && aok[rt]) {
+          ar[rt][h] = *reinterpret_cast<const d2v*>(xp + arow[rt] * B);
+        } else {
+          ar[rt][h] = d2v{0.0, 0.0};
+        }
+      }
+    }
+  };
+  // C chunk: 32 x KYP, 256 threads; element e -> (k = e / KYP, c = e % KYP)
+  constexpr int CEPT = kT44K * KYP / 256;
+  auto load_c = [&](int ch, double (&cr)[CEPT]) {
+#pragma unroll
+    for (int v = 0; v < CEPT; ++v) {
+      const int e = tid + v * 256;
+      const int k = ch * kT44K + e / KYP, c = e % KYP;
+      cr[v] = (k < K && c < KY) ? C[(int64_t)k * ldc + c] : 0.0;
+    }
+  };
+  auto store_c = [&](int buf, const double (&cr)[CEPT]) {
+#pragma unroll
+    for (int v = 0; v < CEPT; ++v) {
+      const int e = tid + v * 256;
+      cs[buf][(e / KYP) * LDC + (e % KYP)] = cr[v];
+    }
+  };
+
+  d2v acur[2][4], anext[2][4];
+  double cr[CEPT];
+  load_c(0, cr);
+  store_c(0, cr);
+  load_a(0, acur);
+  __syncthreads();
+  for (int ch = 0; ch < nch; ++ch) {
+    const bool more = ch + 1 < nch;
+    if (more) {
+      load_c(ch + 1, cr);
+      load_a(ch + 1, anext);
+    }
+    const double* cb = cs[ch & 1];
+#pragma unroll
+    for (int h = 0; h < 4; ++h)
+#pragma unroll
+      for (int v = 0; v < 2; ++v)
+#pragma unroll
+        for (int cg = 0; cg < CG; ++cg) {
+          const double bf = cb[(8 * h + 2 * q + v) * LDC + 4 * cg + (lane & 3)];
+#pragma unroll
+          for (int rt = 0; rt < 2; ++rt) acc[rt][cg] = mfma4(acur[rt][h][v], bf, acc[rt][cg]);
+        }
+    if (more) {
+      store_c((ch + 1) & 1, cr);
+#pragma unroll
+      for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+        for (int h = 0; h < 4; ++h) acur[rt][h] = anext[rt][h];
+    }
+    __syncthreads();
+  }
+  const int g = (lane >> 2) & 3;
+#pragma unroll
+  for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+    for (int cg = 0; cg < CG; ++cg) {
+      const int64_t r = r0 + 16 * rt + 4 * g + (lane >> 4);
+      const int c = 4 * cg + (lane & 3);
+      if (r < nrows && c < KY) {
+        const int t = c / Y.w;
+        double* yp = const_cast<double*>(Y.ptr[t]) + r * Y.w + (c - t * Y.w);
+        const double v = alpha * acc[rt][cg];
+        *yp = beta == 0.0 ? v : beta * (*yp) + v;
+      }
+    }
+}
+
+bool tsmm44_ok(int xw, int ky) { return (xw == 16 || xw == 32) && ky >= 1 && ky <= 64; }
+
+template <int B, int KYP>
+static void launch_tsmm44(int64_t nrows, const PanelRun& X, const double* C, int ldc, int KY,
+                          const Panels& Y, double alpha, double beta, const int* skip,
+                          hipStream_t st) {
+  const int64_t wgs = (nrows + 4 * kT44Rows - 1) / (4 * kT44Rows);
+  hipLaunchKernelGGL((k_tsmm44<B, KYP>), dim3((unsigned)wgs), dim3(256), 0, st, nrows, X, C, ldc,
+                     KY, Y, alpha, beta, skip);
+}
+
+void tsmm44(int64_t nrows, const PanelRun& X, const double* C, int ldc, const Panels& Y,
+            double alpha, double beta, const int* skip, hipStream_t st) {
+  const int KY = Y.count * Y.w;
+  if (X.w == 32) {
+    if (KY <= 16) return launch_tsmm44<32, 16>(nrows, X, C, ldc, KY, Y, alpha, beta, skip, st);
+    if (KY <= 32) return launch_tsmm44<32, 32>(nrows, X, C, ldc, KY, Y, alpha, beta, skip, st);
+    return launch_tsmm44<32, 64>(nrows, X, C, ldc, KY, Y, alpha, beta, skip, st);
+  }
+  if (KY <= 16) return launch_tsmm44<16, 16>(nrows, X, C, ldc, KY, Y, alpha, beta, skip, st);
+  if (KY <= 32) return launch_tsmm44<16, 32>(nrows, X, C, ldc, KY, Y, alpha, beta, skip, st);
+  return launch_tsmm44<16, 64>(nrows, X, C, ldc, KY, Y, alpha, beta, skip, st);
+}
+
+}  // namespace rbl

@@ -113,6 +113,7 @@ static int tiles16(int x) { return (x + 15) / 16; }
 static int pick_at(int w) { int t = tiles16(w); return t <= 1 ? 1 : (t <= 2 ? 2 : 4); }
 
 int gram_splits(int64_t nrows, int nW, int w, int xcols) {
+  if (xcols % w == 0 && gram44_ok(nW, w, xcols / w, w)) return gram44_splits(nrows, nW);
   const int ctt = tiles16(xcols);
   const int ct = ctt <= 1 ? 1 : (ctt <= 2 ? 2 : 4);
   const int ncg = (ctt + ct - 1) / ct;
@@ -141,6 +142,7 @@ static void launch_gram_t(int64_t nrows, const PanelRun& W, const Panels& X, dou
 
 void gram_partial(int64_t nrows, const PanelRun& W, const Panels& X, double* slab, int splits,
                   const int* skip, hipStream_t s) {
+  if (gram44_ok(W.count, W.w, X.count, X.w)) return gram44_partial(nrows, W, X, slab, splits, skip, s);
   const int at = pick_at(W.w);
   const int ctt = tiles16(X.count * X.w);
   const int ct = ctt <= 1 ? 1 : (ctt <= 2 ? 2 : 4);
@@ -156,19 +158,39 @@ void gram_partial(int64_t nrows, const PanelRun& W, const Panels& X, double* sla
 // ----------------------------------------------------------------------------------------
 // Deterministic slab reduction
 // ----------------------------------------------------------------------------------------
-__global__ void k_reduce(const double* __restrict__ slab, int splits, int64_t len,
-                         double* __restrict__ out, const int* skip) {
+// 256 threads = 16 elements x 16 split lanes; split lane j sums splits j, j+16, ... (4
+// independent chains to keep loads in flight), then a fixed LDS tree over the 16 lanes.
+__global__ __launch_bounds__(256) void k_reduce(const double* __restrict__ slab, int splits,
+                                                int64_t len, double* __restrict__ out,
+                                                const int* skip) {
   if (skip && *skip) return;
-  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= len) return;
-  double acc = 0.0;
-  for (int s = 0; s < splits; ++s) acc += slab[(int64_t)s * len + e];
-  out[e] = acc;
+  __shared__ double part[16][17];
+  const int el = threadIdx.x & 15, j = threadIdx.x >> 4;
+  const int64_t e = (int64_t)blockIdx.x * 16 + el;
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+  if (e < len) {
+    int s = j;
+    for (; s + 48 < splits; s += 64) {
+      a0 += slab[(int64_t)s * len + e];
+      a1 += slab[(int64_t)(s + 16) * len + e];
+      a2 += slab[(int64_t)(s + 32) * len + e];
+      a3 += slab[(int64_t)(s + 48) * len + e];
+    }
+    for (; s < splits; s += 16) a0 += slab[(int64_t)s * len + e];
+  }
+  part[j][el] = (a0 + a1) + (a2 + a3);
+  __syncthreads();
+  if (j == 0 && e < len) {
+    double acc = 0.0;
+#pragma unroll
+    for (int t = 0; t < 16; ++t) acc += part[t][el];
+    out[e] = acc;
+  }
 }
 
 void reduce_slab(const double* slab, int splits, int64_t len, double* out, const int* skip,
                  hipStream_t s) {
-  const int blocks = (int)((len + 255) / 256);
+  const int blocks = (int)((len + 15) / 16);
   hipLaunchKernelGGL(k_reduce, dim3(blocks), dim3(256), 0, s, slab, splits, len, out, skip);
 }
 
@@ -261,6 +283,7 @@ static void launch_tsmm_t(int64_t nrows, const PanelRun& X, const double* C, int
 
 void tsmm(int64_t nrows, const PanelRun& X, const double* C, int ldc, const Panels& Y,
           double alpha, double beta, const int* skip, hipStream_t s) {
+  if (tsmm44_ok(X.w, Y.count * Y.w)) return tsmm44(nrows, X, C, ldc, Y, alpha, beta, skip, s);
   const int ctt = tiles16(Y.count * Y.w);
   const int ct = ctt <= 1 ? 1 : (ctt <= 2 ? 2 : 4);
   const int ncg = (ctt + ct - 1) / ct;

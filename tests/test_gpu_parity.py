@@ -66,10 +66,11 @@ def test_first_steps_trace(rbl, b):
         assert np.abs(Bg - Br).max() <= 1e-9 * sb, (i, np.abs(Bg - Br).max(), sb)
 
 
-@pytest.mark.parametrize("order", [0, 1])
-def test_eigenpairs_c1(rbl, order):
-    """C1 (n = 10,000, b = 8, k = 10): eigenvalues vs the oracle < 1e-10."""
-    k, b = 10, 8
+@pytest.mark.parametrize("order,b", [(0, 8), (1, 8), (0, 16), (1, 16), (0, 32)])
+def test_eigenpairs_c1(rbl, order, b):
+    """C1 (n = 10,000, k = 10; b = 8 as configured, plus the 16/32 fast paths): eigenvalues
+    vs the oracle < 1e-10."""
+    k = 10
     A = c1_matrix(10000, k)
     n = A.shape[0]
     omega = np.random.default_rng(7).standard_normal((n, b))
