@@ -108,6 +108,7 @@ def main():
     ctx.set_option(_lib.RBL_OPT_TIMERS, 1)
     ctx.set_option(_lib.RBL_OPT_SPMM_KERNEL, args.spmm_kernel)
     m_max = rbl.rbl_gpu.max_steps_for(args.kryl, b)
+    spmm_kernel = {1: "gather", 2: "lds-window", 3: "lds-band-mfma"}[ctx.spmm_kernel_for(b)]
 
     def one_run():
         rbl.lanczos(ctx, k, b, kryl_sz=args.kryl, seed=args.seed + 1, check=False, ritz=False)
@@ -150,7 +151,7 @@ def main():
             traffic = tj.get("spmm_hbm_bytes_per_launch")
     except (OSError, ValueError):
         pass
-    roof_spmm = {"kernel": "spmm (AQ stage)", "bound": "hbm", "achieved": round(spmm_gbs, 1),
+    roof_spmm = {"kernel": f"spmm {spmm_kernel} (AQ stage)", "bound": "hbm", "achieved": round(spmm_gbs, 1),
                  "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(spmm_gbs / HBM_PEAK_GBS, 4),
                  "traffic": traffic, "algorithmic_bytes_per_launch": int(spmm_bytes),
                  "ms_per_launch": round(spmm_ms, 4)}

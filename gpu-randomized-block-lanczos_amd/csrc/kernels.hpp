@@ -32,10 +32,14 @@ struct CsrDev {
   // whether every tile fits the window kernel's ring for b = 16 / b = 32.
   const int64_t* tile_cmin = nullptr;
   const int64_t* tile_cmax = nullptr;
+  // per tile: e0, nnz, lo, hi (ring rows the tile adds), cmin, cmax, 0, 0
+  const int64_t* tile_info = nullptr;
   int64_t ntiles = 0;
   int64_t tiles_per_wg = 0;
   bool window_ok16 = false;
   bool window_ok32 = false;
+  bool band_ok16 = false;   // spmm_band.hip applicable (and dense enough to pay)
+  bool band_ok32 = false;
 };
 
 // --- spmm.hip ----------------------------------------------------------------------------
@@ -48,6 +52,9 @@ void spmm(const CsrDev& A, const double* Qin, int64_t col_off, int b, double* U,
 bool spmm_window(const CsrDev& A, const double* Qin, int64_t col_off, int b, double* U,
                  const double* Qprev, const double* Bi, hipStream_t s);
 int window_grid();              // workgroups for the window kernel (= CUs)
+// spmm_band.hip: LDS-densified band tiles on fp64 MFMA (b in {16,32}); false if not applicable.
+bool spmm_band(const CsrDev& A, const double* Qin, int64_t col_off, int b, double* U,
+               const double* Qprev, const double* Bi, hipStream_t s);
 constexpr int kWindowTileRows = 16;
 
 // --- tsmm.hip ----------------------------------------------------------------------------

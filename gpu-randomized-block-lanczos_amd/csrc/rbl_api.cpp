@@ -35,8 +35,10 @@ struct rbl_ctx {
   double* d_val = nullptr;
   int64_t* d_tcmin = nullptr;
   int64_t* d_tcmax = nullptr;
+  int64_t* d_tinfo = nullptr;
   int64_t ntiles = 0, tiles_per_wg = 0;
   bool window_ok16 = false, window_ok32 = false;
+  bool band_ok16 = false, band_ok32 = false;
   std::vector<int64_t> bounds;            // nranks+1
   std::vector<int64_t> need_lo, need_hi;  // rows I need from rank q
   std::vector<int64_t> give_lo, give_hi;  // rows rank q needs from me
@@ -110,10 +112,13 @@ CsrDev csr(rbl_ctx* ctx) {
   A.val = ctx->d_val;
   A.tile_cmin = ctx->d_tcmin;
   A.tile_cmax = ctx->d_tcmax;
+  A.tile_info = ctx->d_tinfo;
   A.ntiles = ctx->ntiles;
   A.tiles_per_wg = ctx->tiles_per_wg;
   A.window_ok16 = ctx->window_ok16;
   A.window_ok32 = ctx->window_ok32;
+  A.band_ok16 = ctx->band_ok16;
+  A.band_ok32 = ctx->band_ok32;
   return A;
 }
 
@@ -122,6 +127,7 @@ CsrDev csr(rbl_ctx* ctx) {
 // tile's nonzeros <= 2048, ring rows: 256 (b=32) / 512 (b=16), new rows per tile <= 32 / 64.
 int prepare_window(rbl_ctx* ctx, const std::vector<int64_t>& rp) {
   ctx->window_ok16 = ctx->window_ok32 = false;
+  ctx->band_ok16 = ctx->band_ok32 = false;
   ctx->ntiles = (ctx->nloc + kWindowTileRows - 1) / kWindowTileRows;
   if (ctx->ntiles == 0 || ctx->nnz == 0) return RBL_OK;
   const int64_t nt = ctx->ntiles;
@@ -162,8 +168,40 @@ int prepare_window(rbl_ctx* ctx, const std::vector<int64_t>& rp) {
   }
   ctx->window_ok32 = ok && max_span <= 256 && max_new <= 32;
   ctx->window_ok16 = ok && max_span <= 512 && max_new <= 64;
+  // band (MFMA) kernel: 256-row ring, tile band <= 160 columns, rows <= 192 nonzeros, and the
+  // dense tiles at least 25 % filled (else the zero padding costs more than it saves)
+  {
+    int64_t max_row = 0, dense = 0, max_k = 0;
+    for (int64_t i = 0; i < ctx->nloc; ++i) max_row = std::max(max_row, rp[i + 1] - rp[i]);
+    for (int64_t t = 0; t < nt; ++t) {
+      const int64_t k = cmax[t] + 1 - cmin[t];
+      max_k = std::max(max_k, k);
+      dense += kWindowTileRows * ((k + 3) / 4 * 4);
+    }
+    const bool bok = ok && max_span <= 256 && max_k <= 160 && max_row <= 192 &&
+                     4 * ctx->nnz >= dense;
+    ctx->band_ok32 = bok && max_new <= 32;
+    ctx->band_ok16 = bok && max_new <= 64;
+  }
   HIPC(hipMemcpy(ctx->d_tcmin, cmin.data(), nt * sizeof(int64_t), hipMemcpyHostToDevice));
   HIPC(hipMemcpy(ctx->d_tcmax, cmax.data(), nt * sizeof(int64_t), hipMemcpyHostToDevice));
+  std::vector<int64_t> info(8 * nt, 0);
+  for (int64_t t = 0; t < nt; ++t) {
+    const int64_t ra = t * kWindowTileRows;
+    const int64_t rb = std::min(ra + kWindowTileRows, ctx->nloc);
+    int64_t lo = cmin[t];
+    if (t > 0) lo = std::max(lo, cmax[t - 1] + 1);
+    const int64_t hi = std::max(lo, cmax[t] + 1);
+    int64_t* f = &info[8 * t];
+    f[0] = rp[ra];
+    f[1] = rp[rb] - rp[ra];
+    f[2] = lo;
+    f[3] = hi;
+    f[4] = cmin[t];
+    f[5] = cmax[t];
+  }
+  HIPC(hipMalloc(&ctx->d_tinfo, 8 * nt * sizeof(int64_t)));
+  HIPC(hipMemcpy(ctx->d_tinfo, info.data(), 8 * nt * sizeof(int64_t), hipMemcpyHostToDevice));
   const int64_t grid = window_grid();
   ctx->tiles_per_wg = std::max<int64_t>(1, (nt + grid - 1) / grid);
   return RBL_OK;
@@ -347,9 +385,11 @@ void free_matrix(rbl_ctx* ctx) {
   hipFree(ctx->d_val); ctx->d_val = nullptr;
   hipFree(ctx->d_tcmin); ctx->d_tcmin = nullptr;
   hipFree(ctx->d_tcmax); ctx->d_tcmax = nullptr;
+  hipFree(ctx->d_tinfo); ctx->d_tinfo = nullptr;
   ctx->n = ctx->nloc = ctx->nnz = 0;
   ctx->ntiles = ctx->tiles_per_wg = 0;
   ctx->window_ok16 = ctx->window_ok32 = false;
+  ctx->band_ok16 = ctx->band_ok32 = false;
 }
 
 // Exchange halo needs among ranks and size the extended buffer.
@@ -512,7 +552,7 @@ int rbl_set_option(rbl_ctx* ctx, int option, int64_t value) {
       ctx->reorth_order = (int)value;
       return RBL_OK;
     case RBL_OPT_SPMM_KERNEL:
-      if (value < 0 || value > 2) return fail(ctx, RBL_ERR_INVALID, "spmm kernel must be 0|1|2");
+      if (value < 0 || value > 3) return fail(ctx, RBL_ERR_INVALID, "spmm kernel must be 0..3");
       ctx->spmm_variant = (int)value;
       return RBL_OK;
     default: return fail(ctx, RBL_ERR_INVALID, "unknown option");
@@ -649,8 +689,12 @@ int rbl_get_matrix_csr(rbl_ctx* ctx, int64_t* rowptr, int32_t* colind, double* v
 int rbl_spmm_kernel_for(rbl_ctx* ctx, int b) {
   if (!ctx || !ctx->d_rowptr) return RBL_ERR_INVALID;
   if (ctx->spmm_variant == 1) return 1;
+  const int v = ctx->spmm_variant;
+  const bool band = ctx->ntiles > 0 && ((b == 16 && ctx->band_ok16) || (b == 32 && ctx->band_ok32));
   const bool win = ctx->ntiles > 0 && ((b == 16 && ctx->window_ok16) || (b == 32 && ctx->window_ok32));
-  return win ? 2 : 1;
+  if ((v == 0 || v == 3) && band) return 3;
+  if ((v == 0 || v == 2 || v == 3) && win) return 2;
+  return 1;
 }
 
 int rbl_apply(rbl_ctx* ctx, int b, const double* X, double* Y) {

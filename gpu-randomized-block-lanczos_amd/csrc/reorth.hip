@@ -59,25 +59,31 @@ __global__ __launch_bounds__(512) void k_gram44(int64_t nrows, PanelRun W, Panel
 #pragma unroll
     for (int cg = 0; cg < CG; ++cg) acc[ag][cg] = 0.0;
 
+  // Prefetch loads are unconditional (clamped rows) so every chunk issues the same VMEM ops
+  // and the compiler's vmcnt waits count just the chunk being consumed; rows past r_end are
+  // zeroed on the X side (at the LDS store), so the clamped W rows contribute nothing.
   const int xe0 = tid * EPT;
   const int xrow = xe0 / KC, xcol = xe0 % KC;
   const double* xsrc = X.ptr[xcol / B] + (xcol % B);
+  const int64_t rlast = r_end > 0 ? r_end - 1 : 0;
   auto load_x = [&](int64_t rc0, double (&xr)[EPT]) {
     const int64_t r = rc0 + xrow;
+    const int64_t rc = r < rlast ? r : rlast;
 #pragma unroll
-    for (int v = 0; v < EPT; ++v) xr[v] = r < r_end ? xsrc[r * B + v] : 0.0;
+    for (int v = 0; v < EPT; ++v) xr[v] = xsrc[rc * B + v];
   };
-  auto store_x = [&](int buf, const double (&xr)[EPT]) {
+  auto store_x = [&](int buf, int64_t rc0, const double (&xr)[EPT]) {
+    const bool ok = rc0 + xrow < r_end;
 #pragma unroll
-    for (int v = 0; v < EPT; ++v) xs[buf][xrow * LD + xcol + v] = xr[v];
+    for (int v = 0; v < EPT; ++v) xs[buf][xrow * LD + xcol + v] = ok ? xr[v] : 0.0;
   };
   auto load_a = [&](int64_t rc0, double (&ar)[8][AG]) {
 #pragma unroll
     for (int ks = 0; ks < 8; ++ks) {
       const int64_t r = rc0 + 4 * ks + q;
-      const bool ok = active && r < r_end;
+      const int64_t rc = r < rlast ? r : rlast;
 #pragma unroll
-      for (int ag = 0; ag < AG; ++ag) ar[ks][ag] = ok ? wp[r * B + 16 * ag] : 0.0;
+      for (int ag = 0; ag < AG; ++ag) ar[ks][ag] = wp[rc * B + 16 * ag];
     }
   };
 
@@ -86,17 +92,16 @@ __global__ __launch_bounds__(512) void k_gram44(int64_t nrows, PanelRun W, Panel
   double acur[8][AG], anext[8][AG];
   if (nchunks > 0) {
     load_x(r_begin, xr);
-    store_x(0, xr);
+    store_x(0, r_begin, xr);
     load_a(r_begin, acur);
   }
   __syncthreads();
   for (int64_t c = 0; c < nchunks; ++c) {
     const int64_t rc0 = r_begin + c * kG44Rows;
-    const bool more = c + 1 < nchunks;
-    if (more) {
-      load_x(rc0 + kG44Rows, xr);
-      load_a(rc0 + kG44Rows, anext);
-    }
+    // unconditional (clamped on the last chunk): a uniform branch here would make the
+    // waitcnt pass merge a no-load path and drain the prefetch before the MFMAs
+    load_x(rc0 + kG44Rows, xr);
+    load_a(rc0 + kG44Rows, anext);
     const double* xb = xs[c & 1];
 #pragma unroll
     for (int ks = 0; ks < 8; ++ks) {
@@ -107,13 +112,13 @@ __global__ __launch_bounds__(512) void k_gram44(int64_t nrows, PanelRun W, Panel
         for (int ag = 0; ag < AG; ++ag) acc[ag][cg] = mfma4(acur[ks][ag], bf, acc[ag][cg]);
       }
     }
-    if (more) {
-      store_x((int)((c + 1) & 1), xr);
+    // unconditional as well: a consumer under `if (more)` lets LLVM sink the loads into it
+    // (after the MFMAs); on the last chunk this writes the dead spare buffer
+    store_x((int)((c + 1) & 1), rc0 + kG44Rows, xr);
 #pragma unroll
-      for (int ks = 0; ks < 8; ++ks)
+    for (int ks = 0; ks < 8; ++ks)
 #pragma unroll
-        for (int ag = 0; ag < AG; ++ag) acur[ks][ag] = anext[ks][ag];
-    }
+      for (int ag = 0; ag < AG; ++ag) acur[ks][ag] = anext[ks][ag];
     __syncthreads();
   }
   if (!active) return;
@@ -135,9 +140,11 @@ bool gram44_ok(int nW, int w, int xcount, int xw) {
 }
 
 int gram44_splits(int64_t nrows, int nW) {
-  const int npg = (nW + kG44Waves - 1) / kG44Waves;
-  // ~2 workgroups per CU of 8 waves; splits a multiple of 8 (XCD mapping), >= 256 rows each
-  int64_t s8 = (512 + 8 * npg - 1) / (8 * npg);
+  (void)nW;
+  // One 8-wave workgroup fits per CU (~184 VGPRs): with one split per CU the grid is
+  // exactly npg full rounds of 256 workgroups (no partially filled last round).
+  // Splits stay a multiple of 8 (XCD mapping) and >= 256 rows each.
+  int64_t s8 = window_grid() / 8;
   const int64_t max_s8 = (nrows + 8 * 256 - 1) / (8 * 256);
   if (s8 > max_s8) s8 = max_s8;
   if (s8 < 1) s8 = 1;
@@ -193,30 +200,27 @@ __global__ __launch_bounds__(256) void k_tsmm44(int64_t nrows, PanelRun X, const
     for (int cg = 0; cg < CG; ++cg) acc[rt][cg] = 0.0;
 
   // A: rows r0 + 16 rt + (lane&15); k = k0 + 8 h + 2 q + v, h in [0,4), v in {0,1}
+  // Prefetch loads are unconditional (clamped addresses) so each chunk issues the same VMEM
+  // ops and the vmcnt waits count only the chunk consumed.  Rows past nrows compute garbage
+  // that is never stored; k past K reads a valid panel but meets zeroed C rows (zeroed at
+  // the LDS store).
   int64_t arow[2];
-  bool aok[2];
 #pragma unroll
   for (int rt = 0; rt < 2; ++rt) {
-    arow[rt] = r0 + 16 * rt + (lane & 15);
-    aok[rt] = arow[rt] < nrows;
+    const int64_t r = r0 + 16 * rt + (lane & 15);
+    arow[rt] = r < nrows ? r : nrows - 1;
   }
   typedef double d2v __attribute__((ext_vector_type(2)));
   auto load_a = [&](int ch, d2v (&ar)[2][4]) {
 #pragma unroll
     for (int h = 0; h < 4; ++h) {
-      const int k = ch * kT44K + 8 * h + 2 * q;
-      const bool kv = k < K;
-      const int pan = kv ? k / B : 0;
+      const int k0 = ch * kT44K + 8 * h + 2 * q;
+      const int k = k0 < K ? k0 : K - 2;
+      const int pan = k / B;
       const int col = k - pan * B;
       const double* xp = X.base + (int64_t)pan * X.stride + col;
 #pragma unroll
-      for (int rt = 0; rt < 2; ++rt) {
-        if (kv && aok[rt]) {
-          ar[rt][h] = *reinterpret_cast<const d2v*>(xp + arow[rt] * B);
-        } else {
-          ar[rt][h] = d2v{0.0, 0.0};
-        }
-      }
+      for (int rt = 0; rt < 2; ++rt) ar[rt][h] = *reinterpret_cast<const d2v*>(xp + arow[rt] * B);
     }
   };
   // C chunk: 32 x KYP, 256 threads; element e -> (k = e / KYP, c = e % KYP)
@@ -226,29 +230,28 @@ __global__ __launch_bounds__(256) void k_tsmm44(int64_t nrows, PanelRun X, const
     for (int v = 0; v < CEPT; ++v) {
       const int e = tid + v * 256;
       const int k = ch * kT44K + e / KYP, c = e % KYP;
-      cr[v] = (k < K && c < KY) ? C[(int64_t)k * ldc + c] : 0.0;
+      const int kc = k < K ? k : K - 1, cc = c < KY ? c : KY - 1;
+      cr[v] = C[(int64_t)kc * ldc + cc];
     }
   };
-  auto store_c = [&](int buf, const double (&cr)[CEPT]) {
+  auto store_c = [&](int buf, int ch, const double (&cr)[CEPT]) {
 #pragma unroll
     for (int v = 0; v < CEPT; ++v) {
       const int e = tid + v * 256;
-      cs[buf][(e / KYP) * LDC + (e % KYP)] = cr[v];
+      const int k = ch * kT44K + e / KYP, c = e % KYP;
+      cs[buf][(e / KYP) * LDC + (e % KYP)] = (k < K && c < KY) ? cr[v] : 0.0;
     }
   };
 
   d2v acur[2][4], anext[2][4];
   double cr[CEPT];
   load_c(0, cr);
-  store_c(0, cr);
+  store_c(0, 0, cr);
   load_a(0, acur);
   __syncthreads();
   for (int ch = 0; ch < nch; ++ch) {
-    const bool more = ch + 1 < nch;
-    if (more) {
-      load_c(ch + 1, cr);
-      load_a(ch + 1, anext);
-    }
+    load_c(ch + 1, cr);  // unconditional, clamped (see k_gram44)
+    load_a(ch + 1, anext);
     const double* cb = cs[ch & 1];
 #pragma unroll
     for (int h = 0; h < 4; ++h)
@@ -260,13 +263,11 @@ __global__ __launch_bounds__(256) void k_tsmm44(int64_t nrows, PanelRun X, const
 #pragma unroll
           for (int rt = 0; rt < 2; ++rt) acc[rt][cg] = mfma4(acur[rt][h][v], bf, acc[rt][cg]);
         }
-    if (more) {
-      store_c((ch + 1) & 1, cr);
+    store_c((ch + 1) & 1, ch + 1, cr);  // unconditional (see k_gram44)
 #pragma unroll
-      for (int rt = 0; rt < 2; ++rt)
+    for (int rt = 0; rt < 2; ++rt)
 #pragma unroll
-        for (int h = 0; h < 4; ++h) acur[rt][h] = anext[rt][h];
-    }
+      for (int h = 0; h < 4; ++h) acur[rt][h] = anext[rt][h];
     __syncthreads();
   }
   const int g = (lane >> 2) & 3;

@@ -69,7 +69,11 @@ static void launch_gather(const CsrDev& A, const double* Q, int64_t off, int b, 
 void spmm(const CsrDev& A, const double* Qin, int64_t col_off, int b, double* U,
           const double* Qprev, const double* Bi, int variant, hipStream_t s) {
   if (A.nrows <= 0) return;
-  if (variant != 1 && spmm_window(A, Qin, col_off, b, U, Qprev, Bi, s)) return;
+  // 0 auto: band (MFMA) > window (DPP) > gather;  1 gather;  2 window;  3 band
+  if ((variant == 0 || variant == 3) && spmm_band(A, Qin, col_off, b, U, Qprev, Bi, s)) return;
+  if ((variant == 0 || variant == 2 || variant == 3) &&
+      spmm_window(A, Qin, col_off, b, U, Qprev, Bi, s))
+    return;
   if (b <= 1) return launch_gather<1>(A, Qin, col_off, b, U, Qprev, Bi, s);
   if (b <= 2) return launch_gather<2>(A, Qin, col_off, b, U, Qprev, Bi, s);
   if (b <= 4) return launch_gather<4>(A, Qin, col_off, b, U, Qprev, Bi, s);

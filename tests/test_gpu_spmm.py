@@ -33,15 +33,19 @@ def _rand_sym(n, density, seed, empty_rows=()):
 
 
 @pytest.mark.parametrize("b", [1, 5, 8, 16, 32, 64])
-@pytest.mark.parametrize("variant", [0, 1])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3])
 def test_spmm_hashwindow(rbl, b, variant):
+    """variant 1 = gather, 2 = LDS window (DPP), 3 = LDS band tiles on MFMA, 0 = auto."""
     A = matgen.hashwindow_csr(7000, 64, 0.7734, 5, matgen.planted_spectrum(10))
     X = np.random.default_rng(b).standard_normal((A.shape[0], b))
     with rbl.Context(0) as ctx:
         ctx.set_matrix(A)
         ctx.set_option(2, variant)
-        if variant == 0 and b in (16, 32):
-            assert ctx.spmm_kernel_for(b) == 2      # the LDS-window kernel is the one tested
+        k = ctx.spmm_kernel_for(b)
+        if b in (16, 32):
+            assert k == {0: 3, 1: 1, 2: 2, 3: 3}[variant]   # the kernel under test really runs
+        else:
+            assert k == 1
         Y = ctx.apply(X)
     _check(A, Y, X)
 
@@ -60,9 +64,23 @@ def test_spmm_window_ragged_and_partial_tiles(rbl, b):
         _check(A, Y, X)
         tile_nnz = np.diff(A.indptr[np.r_[np.arange(0, n, 16), n]]).max()
         if W <= 64 and tile_nnz <= 2048:     # the window kernel's metadata cap per tile
-            assert k == 2, (n, W)
+            assert k in (2, 3), (n, W)
         if tile_nnz > 2048:
-            assert k == 1, (n, W)
+            assert k in (1, 3), (n, W)
+
+
+@pytest.mark.parametrize("b", [16, 32])
+@pytest.mark.parametrize("variant", [2, 3])
+def test_spmm_window_kernels_ragged(rbl, b, variant):
+    """Both LDS kernels forced, on ragged tiles / narrow and wide bands / dense bands."""
+    for n, W, p in [(1001, 3, 0.9), (333, 60, 0.5), (4099, 64, 1.0), (17, 8, 0.5), (2000, 30, 0.2)]:
+        A = matgen.hashwindow_csr(n, W, p, n + 7)
+        X = np.random.default_rng(n).standard_normal((n, b))
+        with rbl.Context(0) as ctx:
+            ctx.set_matrix(A)
+            ctx.set_option(2, variant)
+            Y = ctx.apply(X)
+        _check(A, Y, X)
 
 
 @pytest.mark.parametrize("b", [8, 16, 32])
@@ -82,7 +100,7 @@ def test_spmm_window_and_gather_agree_in_lanczos(rbl):
     """The whole block step is insensitive to the SpMM kernel choice (1e-12 on A_i)."""
     A = matgen.hashwindow_csr(6000, 64, 0.7734, 9, matgen.planted_spectrum(10))
     out = []
-    for variant in (1, 0):
+    for variant in (1, 2, 3):
         with rbl.Context(0) as ctx:
             ctx.set_matrix(A)
             ctx.set_option(2, variant)
