@@ -8,7 +8,6 @@
 // (max_blocks+1 slots of n_local x b, row-major), U, one scratch block, the Gram slab and
 // b x b scalars.  Nothing but b x b blocks crosses PCIe per step.
 #include <hip/hip_runtime.h>
-#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <cstdio>
@@ -17,6 +16,7 @@
 #include <vector>
 
 #include "../../include/rbl_hip.h"
+#include "comm.hpp"
 #include "kernels.hpp"
 
 using namespace rbl;
@@ -25,7 +25,7 @@ struct rbl_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   int nranks = 1, rank = 0;
-  ncclComm_t comm = nullptr;
+  Comm* comm = nullptr;  // RCCL or in-process transport (comm.hpp); null for one rank
   std::string err;
 
   // matrix (local rows [r0,r1) of an n x n symmetric matrix)
@@ -89,11 +89,10 @@ int fail(rbl_ctx* c, int code, const std::string& msg) {
       return fail(ctx, _e == hipErrorOutOfMemory ? RBL_ERR_OOM : RBL_ERR_HIP,          \
                   std::string(#expr) + ": " + hipGetErrorString(_e));                 \
   } while (0)
-#define NCCLC(expr)                                                                   \
-  do {                                                                                \
-    ncclResult_t _r = (expr);                                                         \
-    if (_r != ncclSuccess)                                                            \
-      return fail(ctx, RBL_ERR_RCCL, std::string(#expr) + ": " + ncclGetErrorString(_r)); \
+#define COMMC(expr)               \
+  do {                            \
+    int _s = (expr);              \
+    if (_s < 0) return _s;        \
   } while (0)
 #define CHK(expr)             \
   do {                        \
@@ -249,7 +248,7 @@ void harvest_timers(rbl_ctx* ctx) {  // after a stream sync
 int allreduce(rbl_ctx* ctx, double* buf, size_t count) {
   if (ctx->nranks == 1) return RBL_OK;
   StageScope t(ctx, RBL_STAGE_COMM);
-  NCCLC(ncclAllReduce(buf, buf, count, ncclDouble, ncclSum, ctx->comm, ctx->stream));
+  COMMC(ctx->comm->allreduce_sum(buf, count, ctx->stream, &ctx->err));
   return RBL_OK;
 }
 
@@ -345,19 +344,21 @@ int halo_exchange(rbl_ctx* ctx, const double* Q, const double** Qin, int64_t* of
   double* ext = ctx->d_qext;
   HIPC(hipMemcpyAsync(ext + (ctx->r0 - ctx->ext_lo) * b, Q, ctx->nloc * b * sizeof(double),
                       hipMemcpyDeviceToDevice, ctx->stream));
-  NCCLC(ncclGroupStart());
+  std::vector<Comm::Xfer> x(ctx->nranks);
   for (int q = 0; q < ctx->nranks; ++q) {
     if (q == ctx->rank) continue;
     const int64_t gl = ctx->give_lo[q], gh = ctx->give_hi[q];
-    if (gh > gl)
-      NCCLC(ncclSend(Q + (gl - ctx->r0) * b, (size_t)(gh - gl) * b, ncclDouble, q, ctx->comm,
-                     ctx->stream));
+    if (gh > gl) {
+      x[q].send = Q + (gl - ctx->r0) * b;
+      x[q].nsend = (size_t)(gh - gl) * b;
+    }
     const int64_t nl = ctx->need_lo[q], nh = ctx->need_hi[q];
-    if (nh > nl)
-      NCCLC(ncclRecv(ext + (nl - ctx->ext_lo) * b, (size_t)(nh - nl) * b, ncclDouble, q, ctx->comm,
-                     ctx->stream));
+    if (nh > nl) {
+      x[q].recv = ext + (nl - ctx->ext_lo) * b;
+      x[q].nrecv = (size_t)(nh - nl) * b;
+    }
   }
-  NCCLC(ncclGroupEnd());
+  COMMC(ctx->comm->exchange(x, ctx->stream, &ctx->err));
   *Qin = ext;
   *off = ctx->ext_lo;
   return RBL_OK;
@@ -411,17 +412,8 @@ int setup_halo(rbl_ctx* ctx) {
     mine[2 * q] = ctx->need_lo[q];
     mine[2 * q + 1] = ctx->need_hi[q];
   }
-  int64_t *d_in = nullptr, *d_out = nullptr;
-  HIPC(hipMalloc(&d_in, 2 * P * sizeof(int64_t)));
-  HIPC(hipMalloc(&d_out, 2 * P * P * sizeof(int64_t)));
-  HIPC(hipMemcpy(d_in, mine.data(), 2 * P * sizeof(int64_t), hipMemcpyHostToDevice));
-  NCCLC(ncclAllGather(d_in, d_out, 2 * P, ncclInt64, ctx->comm, ctx->stream));
   std::vector<int64_t> all(2 * P * P);
-  HIPC(hipMemcpyAsync(all.data(), d_out, all.size() * sizeof(int64_t), hipMemcpyDeviceToHost,
-                      ctx->stream));
-  HIPC(hipStreamSynchronize(ctx->stream));
-  hipFree(d_in);
-  hipFree(d_out);
+  COMMC(ctx->comm->allgather_host(mine.data(), all.data(), 2 * P, ctx->stream, &ctx->err));
   for (int p = 0; p < P; ++p) {
     if (p == ctx->rank) continue;
     ctx->give_lo[p] = all[(size_t)p * 2 * P + 2 * ctx->rank];
@@ -506,11 +498,8 @@ int rbl_create(rbl_ctx** out, int device) {
 }
 
 int rbl_get_unique_id(uint8_t unique_id[128]) {
-  ncclUniqueId id;
-  if (ncclGetUniqueId(&id) != ncclSuccess) return RBL_ERR_RCCL;
-  static_assert(sizeof(id) == 128, "ncclUniqueId size");
-  memcpy(unique_id, &id, 128);
-  return RBL_OK;
+  if (!unique_id) return RBL_ERR_INVALID;
+  return rccl_unique_id(unique_id) == 0 ? RBL_OK : RBL_ERR_RCCL;
 }
 
 int rbl_create_dist(rbl_ctx** out, int device, int nranks, int rank, const uint8_t unique_id[128]) {
@@ -521,10 +510,33 @@ int rbl_create_dist(rbl_ctx** out, int device, int nranks, int rank, const uint8
   ctx->nranks = nranks;
   ctx->rank = rank;
   if (nranks > 1) {
-    ncclUniqueId id;
-    memcpy(&id, unique_id, 128);
-    NCCLC(ncclCommInitRank(&ctx->comm, nranks, id, rank));
+    if (!unique_id) return fail(ctx, RBL_ERR_INVALID, "rbl_create_dist: null unique_id");
+    ctx->comm = make_rccl_comm(nranks, rank, unique_id, &ctx->err);
+    if (!ctx->comm) return RBL_ERR_RCCL;
   }
+  return RBL_OK;
+}
+
+int rbl_local_group_create(rbl_group** group, int nranks) {
+  if (!group || nranks < 1) return RBL_ERR_INVALID;
+  *group = reinterpret_cast<rbl_group*>(local_group_create(nranks));
+  return RBL_OK;
+}
+
+int rbl_local_group_free(rbl_group* group) {
+  local_group_release(reinterpret_cast<LocalGroup*>(group));
+  return RBL_OK;
+}
+
+int rbl_create_local(rbl_ctx** out, int device, rbl_group* group, int rank) {
+  if (!out || !group) return RBL_ERR_INVALID;
+  int s = rbl_create(out, device);
+  if (s != RBL_OK) return s;
+  rbl_ctx* ctx = *out;
+  ctx->comm = make_local_comm(reinterpret_cast<LocalGroup*>(group), rank, &ctx->err);
+  if (!ctx->comm) return RBL_ERR_INVALID;
+  ctx->nranks = ctx->comm->nranks;
+  ctx->rank = rank;
   return RBL_OK;
 }
 
@@ -535,7 +547,7 @@ int rbl_free(rbl_ctx* ctx) {
   free_run(ctx);
   free_matrix(ctx);
   for (auto e : ctx->ev_pool) hipEventDestroy(e);
-  if (ctx->comm) ncclCommDestroy(ctx->comm);
+  delete ctx->comm;
   if (ctx->stream) hipStreamDestroy(ctx->stream);
   delete ctx;
   return RBL_OK;
@@ -584,18 +596,9 @@ int rbl_set_matrix_csr_rows(rbl_ctx* ctx, int64_t n, int64_t row_begin, int64_t 
   HIPC(hipSetDevice(ctx->device));
   // the partition is the callers' (every rank's [row_begin,row_end) must tile [0,n))
   if (ctx->nranks > 1) {
-    int64_t *d = nullptr, *d_all = nullptr;
     int64_t mine[2] = {row_begin, row_end};
-    HIPC(hipMalloc(&d, 2 * sizeof(int64_t)));
-    HIPC(hipMalloc(&d_all, 2 * ctx->nranks * sizeof(int64_t)));
-    HIPC(hipMemcpy(d, mine, sizeof(mine), hipMemcpyHostToDevice));
-    NCCLC(ncclAllGather(d, d_all, 2, ncclInt64, ctx->comm, ctx->stream));
     std::vector<int64_t> all(2 * ctx->nranks);
-    HIPC(hipMemcpyAsync(all.data(), d_all, all.size() * sizeof(int64_t), hipMemcpyDeviceToHost,
-                        ctx->stream));
-    HIPC(hipStreamSynchronize(ctx->stream));
-    hipFree(d);
-    hipFree(d_all);
+    COMMC(ctx->comm->allgather_host(mine, all.data(), 2, ctx->stream, &ctx->err));
     ctx->bounds.assign(ctx->nranks + 1, 0);
     for (int p = 0; p < ctx->nranks; ++p) {
       if (all[2 * p] != (p == 0 ? 0 : all[2 * p - 1]))

@@ -36,7 +36,6 @@ constexpr int kThreads = 1024;
 constexpr int kMaxK = 160;            // band width per tile (columns)
 constexpr int kAdLd = kMaxK + 2;      // 324 dwords == 4 mod 64: conflict-free A reads
 constexpr int kRing = 256;            // ring rows
-constexpr int kRowEntries = 192;      // CSR entries per row staged (3 per lane)
 }  // namespace band
 
 __device__ __forceinline__ double mfma4b(double a, double b, double c) {

@@ -41,6 +41,9 @@ SIGNATURES = {
     "rbl_create": (C.c_int, [C.POINTER(_p), C.c_int]),
     "rbl_get_unique_id": (C.c_int, [_pu8]),
     "rbl_create_dist": (C.c_int, [C.POINTER(_p), C.c_int, C.c_int, C.c_int, _pu8]),
+    "rbl_local_group_create": (C.c_int, [C.POINTER(_p), C.c_int]),
+    "rbl_local_group_free": (C.c_int, [_p]),
+    "rbl_create_local": (C.c_int, [C.POINTER(_p), C.c_int, _p, C.c_int]),
     "rbl_free": (C.c_int, [_p]),
     "rbl_last_error": (C.c_char_p, [_p]),
     "rbl_set_option": (C.c_int, [_p, C.c_int, _i64]),

@@ -30,14 +30,44 @@ KRYL_SZ_GPU = 1200          # RBL_gpu.jl:211
 RESIDUAL_TOL = 1e-7         # RBL_gpu.jl:189
 
 
+class LocalGroup:
+    """In-process rank group (rbl_local_group_create): the multi-rank code path with a
+    host-staged transport instead of RCCL, so it runs with several ranks on one GPU."""
+
+    def __init__(self, nranks: int):
+        import ctypes as C
+        self._h = C.c_void_p()
+        st = lib.rbl_local_group_create(C.byref(self._h), nranks)
+        if st < 0:
+            raise RBLError(st, "rbl_local_group_create")
+        self.nranks = nranks
+
+    def close(self) -> None:
+        if self._h:
+            lib.rbl_local_group_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class Context:
     """One librbl_hip context: one GPU, or one rank of a row-partitioned job."""
 
     def __init__(self, device: int = 0, nranks: int = 1, rank: int = 0,
-                 unique_id: bytes | None = None):
+                 unique_id: bytes | None = None, group: "LocalGroup | None" = None):
+        """nranks == 1: a single-GPU context.  nranks > 1 with `unique_id`: one rank of an RCCL
+        job (one process per GPU).  `group`: one rank of an in-process LocalGroup (each rank
+        driven by its own thread; ranks may share a GPU)."""
         import ctypes as C
         self._h = C.c_void_p()
-        if nranks == 1:
+        if group is not None:
+            nranks = group.nranks
+            st = lib.rbl_create_local(C.byref(self._h), device, group._h, rank)
+        elif nranks == 1:
             st = lib.rbl_create(C.byref(self._h), device)
         else:
             uid = np.frombuffer(unique_id, dtype=np.uint8).copy()

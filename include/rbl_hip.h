@@ -52,7 +52,9 @@ extern "C" {
 #define RBL_OPT_TIMERS        0   /* 1: record per-stage hipEvents (adds event records)         */
 #define RBL_OPT_REORTH_ORDER  1   /* 0: block-CGS (batched, default); 1: ascending-j block MGS  */
                                   /*    exactly as RBL.jl:30-48 / RBL_gpu.jl:65-67               */
-#define RBL_OPT_SPMM_KERNEL   2   /* 0: auto; 1: global-gather CSR; 2: LDS-window CSR           */
+#define RBL_OPT_SPMM_KERNEL   2   /* 0: auto; 1: global-gather CSR; 2: LDS-window CSR (DPP);
+                                   * 3: LDS band tiles on fp64 MFMA (falls back 3 -> 2 -> 1
+                                   * when the matrix does not fit the kernel's limits)         */
 
 typedef struct rbl_ctx rbl_ctx;
 
@@ -65,6 +67,15 @@ int rbl_create(rbl_ctx** ctx, int device);
  * 128-byte RCCL id produced by rbl_get_unique_id() on rank 0 and broadcast by the host. */
 int rbl_get_unique_id(uint8_t unique_id[128]);
 int rbl_create_dist(rbl_ctx** ctx, int device, int nranks, int rank, const uint8_t unique_id[128]);
+/* In-process rank group: `nranks` contexts in ONE process, each driven by its own host thread
+ * (several may share a GPU).  Same multi-rank code path as rbl_create_dist with the RCCL
+ * transport replaced by host-staged copies; used to exercise partitioning, halos and the
+ * distributed Grams on a single-GPU machine.  The group is reference-counted: release it
+ * with rbl_local_group_free whenever convenient (contexts keep it alive). */
+typedef struct rbl_group rbl_group;
+int rbl_local_group_create(rbl_group** group, int nranks);
+int rbl_local_group_free(rbl_group* group);
+int rbl_create_local(rbl_ctx** ctx, int device, rbl_group* group, int rank);
 int rbl_free(rbl_ctx* ctx);
 const char* rbl_last_error(const rbl_ctx* ctx);
 int rbl_set_option(rbl_ctx* ctx, int option, int64_t value);
@@ -95,7 +106,7 @@ int rbl_get_matrix_csr(rbl_ctx* ctx, int64_t* rowptr, int32_t* colind, double* v
  * halo exchange).  Allocates its own device buffers. */
 int rbl_apply(rbl_ctx* ctx, int b, const double* X, double* Y);
 /* Which SpMM kernel rbl_step / rbl_apply use for block size b under the current option:
- * 1 = global-gather CSR, 2 = LDS-window CSR. */
+ * 1 = global-gather CSR, 2 = LDS-window CSR (DPP), 3 = LDS band tiles on fp64 MFMA. */
 int rbl_spmm_kernel_for(rbl_ctx* ctx, int b);
 
 /* ---- Krylov run -----------------------------------------------------------------------

@@ -1,0 +1,151 @@
+"""GPU: the row-partitioned multi-rank path on one GPU.
+
+Ranks are contexts of one in-process LocalGroup, each driven by its own thread; the library
+code they run (nnz-balanced partition, halo tables, halo exchange before every SpMM,
+distributed Grams + sums, distributed CholQR, Ritz rows) is the code the RCCL transport runs,
+only the transport differs (comm.hpp).  RCCL itself cannot be exercised here: it rejects two
+ranks on one device.
+
+Tolerances: eigenvalues |dλ|/|λ| < 1e-10 against the single-rank run and the oracle (the
+partitioned sums only reorder fp64 additions); per-step A_i within 1e-9 relative; Ritz
+vectors 1 - |v·v'| < 1e-8.
+"""
+import threading
+
+import numpy as np
+import pytest
+
+from oracle import matgen
+from oracle import rbl_oracle as o
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def rbl():
+    import rbl as _r
+    return _r
+
+
+def run_ranks(rbl, P, fn, timeout=240):
+    """Run fn(ctx, rank) on P in-process ranks (one thread each); return the per-rank results."""
+    group = rbl.LocalGroup(P)
+    out = [None] * P
+    errs = []
+
+    def worker(r):
+        try:
+            with rbl.Context(0, group=group, rank=r) as ctx:
+                out[r] = fn(ctx, r)
+        except BaseException as e:  # noqa: BLE001 - reported below
+            errs.append((r, repr(e)))
+
+    ths = [threading.Thread(target=worker, args=(r,)) for r in range(P)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join(timeout)
+    group.close()
+    assert not any(t.is_alive() for t in ths), "a rank hung"
+    assert not errs, errs
+    return out
+
+
+def _single(rbl, A, k, b, omega, steps=None, check=True):
+    with rbl.Context(0) as ctx:
+        ctx.set_matrix(A)
+        return rbl.lanczos(ctx, k, b, omega=omega, check=check, max_steps=steps, trace=True)
+
+
+@pytest.mark.parametrize("P", [2, 3, 4])
+def test_multirank_apply_matches_scipy(rbl, P):
+    A = matgen.hashwindow_csr(5000, 40, 0.6, 3, matgen.planted_spectrum(5))
+    X = np.random.default_rng(P).standard_normal((A.shape[0], 16))
+
+    def fn(ctx, r):
+        ctx.set_matrix(A)
+        n, r0, r1, _ = ctx.matrix_info()
+        return r0, r1, ctx.apply(X[r0:r1])
+
+    parts = run_ranks(rbl, P, fn)
+    assert parts[0][0] == 0 and parts[-1][1] == A.shape[0]
+    for (a0, a1, _), (b0, _, _) in zip(parts, parts[1:]):
+        assert a1 == b0
+    Y = np.vstack([y for _, _, y in parts])
+    ref = A @ X
+    assert np.abs(Y - ref).max() <= 1e-12 * np.abs(ref).max()
+
+
+@pytest.mark.parametrize("P,b", [(2, 8), (3, 16), (4, 32)])
+def test_multirank_lanczos_matches_single_rank(rbl, P, b):
+    """Full RBL run (convergence checks on, Ritz vectors) on P ranks == 1 rank == oracle."""
+    k = 10
+    A = matgen.hashwindow_csr(6000, 48, 0.5, 11, matgen.planted_spectrum(k))
+    omega = np.random.default_rng(7).standard_normal((A.shape[0], b))
+    D1, V1, info1 = _single(rbl, A, k, b, omega)
+    assert info1.converged
+
+    def fn(ctx, r):
+        ctx.set_matrix(A)
+        n, r0, r1, _ = ctx.matrix_info()
+        D, V, info = rbl.lanczos(ctx, k, b, omega=omega[r0:r1], check=True, trace=True)
+        return r0, r1, D, V, info
+
+    parts = run_ranks(rbl, P, fn)
+    for r0, r1, D, V, info in parts:
+        assert info.converged and info.iters == info1.iters
+        assert np.max(np.abs(D - D1) / np.abs(D1)) < 1e-10
+        for a, a1 in zip(info.trace_A, info1.trace_A):
+            assert np.abs(a - a1).max() <= 1e-9 * np.abs(a1).max()
+    V = np.vstack([p[3] for p in parts])
+    dots = np.abs(np.sum(V * V1, axis=0))
+    assert np.all(1 - dots < 1e-8), dots
+    ref = o.RBL_gpu_semantics(A, k, b, omega=omega, qr_mode="posdiag")
+    assert np.max(np.abs(parts[0][2] - ref.D) / np.abs(ref.D)) < 1e-10
+
+
+@pytest.mark.parametrize("P", [2, 4])
+def test_multirank_device_generator_and_fixed_steps(rbl, P):
+    """Each rank generates only its rows on the device; the fixed-step run (bench mode, block
+    CGS partial reorth through the distributed Gram) matches the single-rank run."""
+    n, W, p, seed, k, b = 8000, 64, 0.7734, 99, 10, 32
+    plant = matgen.planted_spectrum(k)
+
+    def fn(ctx, r):
+        ctx.gen_hashwindow(n, W, p, seed, plant)
+        _, _, info = rbl.lanczos(ctx, k, b, seed=5, check=False, max_steps=12, trace=True,
+                                 ritz=False)
+        return info
+
+    with rbl.Context(0) as ctx:
+        ctx.gen_hashwindow(n, W, p, seed, plant)
+        _, _, info1 = rbl.lanczos(ctx, k, b, seed=5, check=False, max_steps=12, trace=True,
+                                  ritz=False)
+    infos = run_ranks(rbl, P, fn)
+    for info in infos:
+        assert len(info.trace_A) == len(info1.trace_A) == 12
+        for a, a1 in zip(info.trace_A, info1.trace_A):
+            assert np.abs(a - a1).max() <= 1e-9 * np.abs(a1).max()
+        for bb, bb1 in zip(info.trace_B, info1.trace_B):
+            assert np.abs(bb - bb1).max() <= 1e-9 * np.abs(bb1).max()
+
+
+def test_multirank_tiny_slices(rbl):
+    """More ranks than comfortable: 4 ranks on n = 12 (3 rows each), b = 4."""
+    import scipy.sparse as sp
+    rng = np.random.default_rng(3)
+    M = rng.standard_normal((12, 12))
+    A = sp.csr_matrix(M + M.T)
+    omega = rng.standard_normal((12, 4))
+    D1, V1, info1 = _single(rbl, A, 2, 4, omega, check=False, steps=2)
+
+    def fn(ctx, r):
+        ctx.set_matrix(A)
+        _, r0, r1, _ = ctx.matrix_info()
+        _, _, info = rbl.lanczos(ctx, 2, 4, omega=omega[r0:r1], check=False, max_steps=2,
+                                 trace=True, ritz=False)
+        return info
+
+    for info in run_ranks(rbl, 4, fn):
+        for a, a1 in zip(info.trace_A, info1.trace_A):
+            assert np.abs(a - a1).max() <= 1e-10 * np.abs(a1).max()
