@@ -143,21 +143,28 @@ def main():
     reorth_flops = sum(8.0 * nloc * b * b * (i - 2) for i in range(4, m_max + 1, 2))
     reorth_ms = stage_per_run["part reorth"]
     reorth_tf = reorth_flops / (reorth_ms * 1e-3) / 1e12 if reorth_ms > 0 else 0.0
-    traffic = None
+    # HBM bytes from PMC counters (tools/pmc_traffic.sh -> tools/pmc_summarize.py; separate
+    # FETCH_SIZE / WRITE_SIZE passes, gfx950 per-width calibration): a committed measurement of
+    # the same kernels on the same config, used only when the config matches
+    traffic = traffic_reorth = None
     try:
         with open(args.traffic_json) as f:
             tj = json.load(f)
-        if tj.get("config", {}).get("n") == n and tj.get("config", {}).get("b") == b:
+        if tj.get("config", {}).get("n") == n and tj.get("config", {}).get("b") == b and world == 1:
             traffic = tj.get("spmm_hbm_bytes_per_launch")
+            traffic_reorth = tj.get("part_reorth_hbm_bytes_per_run")
     except (OSError, ValueError):
         pass
     roof_spmm = {"kernel": f"spmm {spmm_kernel} (AQ stage)", "bound": "hbm", "achieved": round(spmm_gbs, 1),
                  "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(spmm_gbs / HBM_PEAK_GBS, 4),
-                 "traffic": traffic, "algorithmic_bytes_per_launch": int(spmm_bytes),
+                 "traffic": None if traffic is None else int(traffic),
+                 "algorithmic_bytes_per_launch": int(spmm_bytes),
                  "ms_per_launch": round(spmm_ms, 4)}
     roof_reorth = {"kernel": "partial reorth (gram+update)", "bound": "mfma",
                    "achieved": round(reorth_tf, 2), "peak": FP64_MFMA_PEAK_TF, "unit": "TFLOP/s",
-                   "frac": round(reorth_tf / FP64_MFMA_PEAK_TF, 4), "traffic": None,
+                   "frac": round(reorth_tf / FP64_MFMA_PEAK_TF, 4),
+                   "traffic": None if traffic_reorth is None else int(traffic_reorth),
+                   "traffic_unit": "HBM bytes per run (gram + update, 18 launches each)",
                    "algorithmic_flops_per_run": reorth_flops, "ms_per_run": round(reorth_ms, 3)}
     if stage["part reorth"] > stage["AQ"]:
         roofline, roofline2 = roof_reorth, roof_spmm

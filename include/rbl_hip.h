@@ -134,7 +134,10 @@ int rbl_num_stages(void);
 const char* rbl_stage_name(int stage);
 int rbl_timers(rbl_ctx* ctx, double* ms, int nstages);
 int rbl_reset_timers(rbl_ctx* ctx);
-/* Wall-clock of the device work of the most recent call (ms), from hipEvents. */
+/* Stage times accumulate (ms, hipEvents on the context stream) while RBL_OPT_TIMERS is
+ * set; names are the reference's TimerOutputs labels (RBL_gpu.jl:153-186: "AQ", "3-term",
+ * "qr", "part reorth", "loc reorth", "Ritz vectors") plus "comm" (halo + all-reduce).
+ * rbl_synchronize waits for the context's stream and folds finished events into them. */
 int rbl_synchronize(rbl_ctx* ctx);
 
 /* ---- host-only planning (callable without a GPU) -------------------------------------- */
