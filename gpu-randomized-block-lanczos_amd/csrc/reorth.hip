@@ -36,7 +36,9 @@ __global__ __launch_bounds__(512) void k_gram44(int64_t nrows, PanelRun W, Panel
   constexpr int KC = NX * B;
   constexpr int AG = B / 16;
   constexpr int CG = KC / 4;
-  constexpr int LD = KC + 4;  // +8 dwords: the 2 rows a half-wave reads sit in different banks
+  // rows of a ds_read_b128 lane group differ by one: LD/2 = 4 mod 16 puts their 16-B slots
+  // in disjoint banks (LD = KC + 8)
+  constexpr int LD = KC + 8;
   constexpr int EPT = kG44Rows * KC / 512;
   __shared__ __attribute__((aligned(16))) double xs[2][kG44Rows * LD];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -75,7 +77,7 @@ __global__ __launch_bounds__(512) void k_gram44(int64_t nrows, PanelRun W, Panel
   auto store_x = [&](int buf, int64_t rc0, const double (&xr)[EPT]) {
     const bool ok = rc0 + xrow < r_end;
 #pragma unroll
-    for (int v = 0; v < EPT; ++v) xs[buf][xrow * LD + xcol + v] = ok ? xr[v] : 0.0;
+    for (int v = 0; v < EPT; ++v) xs[buf][xrow * LD + perm8(xcol + v)] = ok ? xr[v] : 0.0;
   };
   auto load_a = [&](int64_t rc0, double (&ar)[8][AG]) {
 #pragma unroll
@@ -103,13 +105,18 @@ __global__ __launch_bounds__(512) void k_gram44(int64_t nrows, PanelRun W, Panel
     load_x(rc0 + kG44Rows, xr);
     load_a(rc0 + kG44Rows, anext);
     const double* xb = xs[c & 1];
+    if (active) {  // idle waves (j >= nW) only help stage X: leave the MFMA pipe to the rest
 #pragma unroll
-    for (int ks = 0; ks < 8; ++ks) {
+      for (int ks = 0; ks < 8; ++ks) {
 #pragma unroll
-      for (int cg = 0; cg < CG; ++cg) {
-        const double bf = xb[(4 * ks + q) * LD + 4 * cg + (lane & 3)];
+        for (int cp = 0; cp < CG / 2; ++cp) {  // column groups 2cp, 2cp+1 in one 16-B read
+          const d2v bf = *reinterpret_cast<const d2v*>(xb + (4 * ks + q) * LD + 8 * cp + 2 * (lane & 3));
 #pragma unroll
-        for (int ag = 0; ag < AG; ++ag) acc[ag][cg] = mfma4(acur[ks][ag], bf, acc[ag][cg]);
+          for (int ag = 0; ag < AG; ++ag) {
+            acc[ag][2 * cp] = mfma4(acur[ks][ag], bf.x, acc[ag][2 * cp]);
+            acc[ag][2 * cp + 1] = mfma4(acur[ks][ag], bf.y, acc[ag][2 * cp + 1]);
+          }
+        }
       }
     }
     // unconditional as well: a consumer under `if (more)` lets LLVM sink the loads into it
@@ -185,7 +192,7 @@ __global__ __launch_bounds__(256) void k_tsmm44(int64_t nrows, PanelRun X, const
                                                 const int* skip) {
   if (skip && *skip) return;
   constexpr int CG = KYP / 4;
-  constexpr int LDC = KYP + 4;
+  constexpr int LDC = KYP + 8;  // lane-group rows differ by 2: LDC = 8 mod 16 (see k_gram44)
   __shared__ __attribute__((aligned(16))) double cs[2][kT44K * LDC];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int q = lane >> 4;
@@ -210,7 +217,6 @@ __global__ __launch_bounds__(256) void k_tsmm44(int64_t nrows, PanelRun X, const
     const int64_t r = r0 + 16 * rt + (lane & 15);
     arow[rt] = r < nrows ? r : nrows - 1;
   }
-  typedef double d2v __attribute__((ext_vector_type(2)));
   auto load_a = [&](int ch, d2v (&ar)[2][4]) {
 #pragma unroll
     for (int h = 0; h < 4; ++h) {
@@ -239,7 +245,7 @@ __global__ __launch_bounds__(256) void k_tsmm44(int64_t nrows, PanelRun X, const
     for (int v = 0; v < CEPT; ++v) {
       const int e = tid + v * 256;
       const int k = ch * kT44K + e / KYP, c = e % KYP;
-      cs[buf][(e / KYP) * LDC + (e % KYP)] = (k < K && c < KY) ? cr[v] : 0.0;
+      cs[buf][(e / KYP) * LDC + perm8(e % KYP)] = (k < K && c < KY) ? cr[v] : 0.0;
     }
   };
 
@@ -258,10 +264,13 @@ __global__ __launch_bounds__(256) void k_tsmm44(int64_t nrows, PanelRun X, const
 #pragma unroll
       for (int v = 0; v < 2; ++v)
 #pragma unroll
-        for (int cg = 0; cg < CG; ++cg) {
-          const double bf = cb[(8 * h + 2 * q + v) * LDC + 4 * cg + (lane & 3)];
+        for (int cp = 0; cp < CG / 2; ++cp) {  // column groups 2cp, 2cp+1 in one 16-B read
+          const d2v bf = *reinterpret_cast<const d2v*>(cb + (8 * h + 2 * q + v) * LDC + 8 * cp + 2 * (lane & 3));
 #pragma unroll
-          for (int rt = 0; rt < 2; ++rt) acc[rt][cg] = mfma4(acur[rt][h][v], bf, acc[rt][cg]);
+          for (int rt = 0; rt < 2; ++rt) {
+            acc[rt][2 * cp] = mfma4(acur[rt][h][v], bf.x, acc[rt][2 * cp]);
+            acc[rt][2 * cp + 1] = mfma4(acur[rt][h][v], bf.y, acc[rt][2 * cp + 1]);
+          }
         }
     store_c((ch + 1) & 1, ch + 1, cr);  // unconditional (see k_gram44)
 #pragma unroll

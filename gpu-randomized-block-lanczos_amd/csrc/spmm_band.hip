@@ -34,7 +34,10 @@ namespace band {
 constexpr int kTileRows = 16;
 constexpr int kThreads = 1024;
 constexpr int kMaxK = 160;            // band width per tile (columns)
-constexpr int kAdLd = kMaxK + 2;      // 324 dwords == 4 mod 64: conflict-free A reads
+// dense tile rows: columns stored at perm8(k) so a lane's k-steps u, u+1 (columns k, k+4)
+// come in one ds_read_b128; the 16 rows of a lane group land on distinct 16-B bank slots
+// when kAdLd = 4 mod 32 (slot(r, q) = 2r + q mod 16 over each group's (r, q) set)
+constexpr int kAdLd = kMaxK + 4;
 constexpr int kRing = 256;            // ring rows
 }  // namespace band
 
@@ -64,7 +67,7 @@ struct BandLayout {
   static constexpr int NCG = B / 4;            // column groups of 4
   static constexpr int KSPLIT = 16 / NCG;      // waves per column group
   static constexpr int RLD = B + (B == 32 ? 4 : 4);  // ring row stride (doubles): 36 / 20
-  static constexpr int QPLD = B + 2;           // Q_{i-1} tile stride: == 4 mod 64 dwords at b=32
+  static constexpr int QPLD = 36;              // Q_{i-1} tile stride, = 4 mod 32 (as kAdLd)
   static constexpr int kRingOff = 0;
   static constexpr int kRingBytes = band::kRing * RLD * 8;
   static constexpr int kAdOff = kRingBytes;
@@ -156,12 +159,12 @@ __global__ __launch_bounds__(band::kThreads) void k_spmm_band(BandArgs a) {
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
       const int64_t e = S.rs + lane + 64 * j;
-      if (e < S.re) ad[S.c[j] - cmin] = S.v[j];
+      if (e < S.re) ad[perm8(S.c[j] - cmin)] = S.v[j];
     }
     const int64_t row = S.lo + tid / B;
     if (row < S.hi) ring[(row & (band::kRing - 1)) * RLD + (tid % B)] = S.q;
     if constexpr (EPI) {
-      if (tid < band::kTileRows * B) qpb(buf)[(tid / B) * QPLD + (tid % B)] = S.qp;
+      if (tid < band::kTileRows * B) qpb(buf)[(tid / B) * QPLD + perm8(tid % B)] = S.qp;
     }
     if (tid == 0) {
       dsb(buf)[0] = cmin;
@@ -185,32 +188,44 @@ __global__ __launch_bounds__(band::kThreads) void k_spmm_band(BandArgs a) {
     const int buf = (int)(t & 1);
     const int cmin = dsb(buf)[0], K = dsb(buf)[1];
     const int ks = (K + 3) >> 2;
-    const int half = (ks + KSPLIT - 1) / KSPLIT;
+    const int half = ((ks + 2 * KSPLIT - 1) / (2 * KSPLIT)) * 2;  // even: k-step pairs align
     const int kb = h * half;
     const int ke = kb + half < ks ? kb + half : ks;
-    const double* ad = adb(buf) + (lane & 15) * band::kAdLd + (lane >> 4);
+    // lane (row r, q): column 4 k' + q sits at perm8(4 k' + q) = 8 (k'/2) + 2q + (k'&1)
+    const double* ad = adb(buf) + (lane & 15) * band::kAdLd + 2 * (lane >> 4);
     const int bcol = 4 * cg + (lane & 3);
     double acc = 0.0;
     int kk = kb;
-    for (; kk + 4 <= ke; kk += 4) {  // 4 k-steps: 8 LDS reads in flight, 4 MFMAs
-      double av[4], bv[4];
+    for (; kk + 4 <= ke; kk += 4) {  // 4 k-steps: 2 x 16-B A reads + 4 B reads, 4 MFMAs
+      d2v av[2];
+      double bv[4];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int k = 4 * (kk + u);
-        av[u] = ad[k];
-        bv[u] = ring[((cmin + k + (lane >> 4)) & (band::kRing - 1)) * RLD + bcol];
-      }
+      for (int u = 0; u < 2; ++u) av[u] = *reinterpret_cast<const d2v*>(ad + 8 * ((kk >> 1) + u));
 #pragma unroll
-      for (int u = 0; u < 4; ++u) acc = mfma4b(av[u], bv[u], acc);
+      for (int u = 0; u < 4; ++u)
+        bv[u] = ring[((cmin + 4 * (kk + u) + (lane >> 4)) & (band::kRing - 1)) * RLD + bcol];
+      acc = mfma4b(av[0].x, bv[0], acc);
+      acc = mfma4b(av[0].y, bv[1], acc);
+      acc = mfma4b(av[1].x, bv[2], acc);
+      acc = mfma4b(av[1].y, bv[3], acc);
     }
     for (; kk < ke; ++kk) {
       const int k = 4 * kk;
-      acc = mfma4b(ad[k], ring[((cmin + k + (lane >> 4)) & (band::kRing - 1)) * RLD + bcol], acc);
+      acc = mfma4b(ad[perm8(k)], ring[((cmin + k + (lane >> 4)) & (band::kRing - 1)) * RLD + bcol], acc);
     }
     if constexpr (EPI) {
-      const double* qp = qpb(buf) + (lane & 15) * QPLD + (lane >> 4);
+      const double* qp = qpb(buf) + (lane & 15) * QPLD + 2 * (lane >> 4);
+      if constexpr (EKS % 2 == 0) {
 #pragma unroll
-      for (int e = 0; e < EKS; ++e) acc = mfma4b(qp[4 * (h * EKS + e)], bt[e], acc);
+        for (int e = 0; e < EKS; e += 2) {
+          const d2v qv = *reinterpret_cast<const d2v*>(qp + 8 * ((h * EKS + e) >> 1));
+          acc = mfma4b(qv.x, bt[e], acc);
+          acc = mfma4b(qv.y, bt[e + 1], acc);
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < EKS; ++e) acc = mfma4b(qp[perm8(4 * (h * EKS + e))], bt[e], acc);
+      }
     }
     if (h > 0) {
       xcb(buf)[((h - 1) * NCG + cg) * 64 + lane] = acc;
