@@ -22,6 +22,11 @@ struct PanelRun {
 
 // CSR rows [0,nrows) of the local slice; columns are global ids; Q row c lives at
 // Qin + (c - col_off) * b.
+// Device CSR arrays carry kCsrPad zero entries past nnz, and every n x b buffer an SpMM
+// writes carries kRowPad spare rows: the band kernel's loads and stores run unguarded.
+constexpr int64_t kCsrPad = 256;
+constexpr int64_t kRowPad = 16;
+
 struct CsrDev {
   int64_t nrows = 0;
   int64_t nnz = 0;

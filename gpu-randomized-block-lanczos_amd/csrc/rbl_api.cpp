@@ -177,7 +177,12 @@ int prepare_window(rbl_ctx* ctx, const std::vector<int64_t>& rp) {
       max_k = std::max(max_k, k);
       dense += kWindowTileRows * ((k + 3) / 4 * 4);
     }
-    const bool bok = ok && max_span <= 256 && max_k <= 160 && max_row <= 192 &&
+    // producers write tile t+2's new ring rows while tile t is multiplied: the 256-row ring
+    // must hold [cmin(t), cmax(t+2)]
+    int64_t max_span2 = 0;
+    for (int64_t t = 0; t < nt; ++t)
+      max_span2 = std::max(max_span2, cmax[std::min(t + 2, nt - 1)] + 1 - cmin[t]);
+    const bool bok = ok && max_span2 <= 256 && max_k <= 160 && max_row <= 192 &&
                      4 * ctx->nnz >= dense;
     ctx->band_ok32 = bok && max_new <= 32;
     ctx->band_ok16 = bok && max_new <= 64;
@@ -449,8 +454,10 @@ int upload_csr(rbl_ctx* ctx, int64_t n, int64_t r0, int64_t r1, const int64_t* r
   ctx->nloc = m;
   ctx->nnz = nnz;
   HIPC(hipMalloc(&ctx->d_rowptr, (m + 1) * sizeof(int64_t)));
-  HIPC(hipMalloc(&ctx->d_col, std::max<int64_t>(nnz, 1) * sizeof(int32_t)));
-  HIPC(hipMalloc(&ctx->d_val, std::max<int64_t>(nnz, 1) * sizeof(double)));
+  HIPC(hipMalloc(&ctx->d_col, (nnz + kCsrPad) * sizeof(int32_t)));
+  HIPC(hipMalloc(&ctx->d_val, (nnz + kCsrPad) * sizeof(double)));
+  HIPC(hipMemset(ctx->d_col + nnz, 0, kCsrPad * sizeof(int32_t)));
+  HIPC(hipMemset(ctx->d_val + nnz, 0, kCsrPad * sizeof(double)));
   HIPC(hipMemcpy(ctx->d_rowptr, rp.data(), (m + 1) * sizeof(int64_t), hipMemcpyHostToDevice));
   if (nnz) {
     HIPC(hipMemcpy(ctx->d_col, ci.data(), nnz * sizeof(int32_t), hipMemcpyHostToDevice));
@@ -640,8 +647,10 @@ int rbl_gen_matrix_hashwindow(rbl_ctx* ctx, int64_t n, int64_t halfwidth, double
   for (int64_t i = 0; i < m; ++i) rp[i + 1] = rp[i] + cnt[i];
   ctx->nnz = rp[m];
   HIPC(hipMalloc(&ctx->d_rowptr, (m + 1) * sizeof(int64_t)));
-  HIPC(hipMalloc(&ctx->d_col, std::max<int64_t>(ctx->nnz, 1) * sizeof(int32_t)));
-  HIPC(hipMalloc(&ctx->d_val, std::max<int64_t>(ctx->nnz, 1) * sizeof(double)));
+  HIPC(hipMalloc(&ctx->d_col, (ctx->nnz + kCsrPad) * sizeof(int32_t)));
+  HIPC(hipMalloc(&ctx->d_val, (ctx->nnz + kCsrPad) * sizeof(double)));
+  HIPC(hipMemset(ctx->d_col + ctx->nnz, 0, kCsrPad * sizeof(int32_t)));
+  HIPC(hipMemset(ctx->d_val + ctx->nnz, 0, kCsrPad * sizeof(double)));
   HIPC(hipMemcpy(ctx->d_rowptr, rp.data(), (m + 1) * sizeof(int64_t), hipMemcpyHostToDevice));
   double* d_plant = nullptr;
   if (nplant > 0) {
@@ -710,7 +719,7 @@ int rbl_apply(rbl_ctx* ctx, int b, const double* X, double* Y) {
   double *d_x = nullptr, *d_xr = nullptr, *d_y = nullptr, *d_ext = nullptr;
   HIPC(hipMalloc(&d_x, nl * b * sizeof(double)));
   HIPC(hipMalloc(&d_xr, nl * b * sizeof(double)));
-  HIPC(hipMalloc(&d_y, nl * b * sizeof(double)));
+  HIPC(hipMalloc(&d_y, (nl + kRowPad) * b * sizeof(double)));
   HIPC(hipMemcpyAsync(d_x, X, ctx->nloc * b * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
   colmajor_to_rowmajor(d_x, ctx->nloc, b, d_xr, ctx->stream);
   const double* Qin = d_xr;
@@ -761,7 +770,7 @@ int rbl_start(rbl_ctx* ctx, int b, int max_blocks, int basis_bits, const double*
   ctx->slot = ctx->nloc * b;
   const int64_t nl = std::max<int64_t>(ctx->nloc, 1);
   HIPC(hipMalloc(&ctx->d_basis, (size_t)(max_blocks + 1) * nl * b * sizeof(double)));
-  HIPC(hipMalloc(&ctx->d_U, nl * b * sizeof(double)));
+  HIPC(hipMalloc(&ctx->d_U, (nl + kRowPad) * b * sizeof(double)));
   ctx->T_cols = b;
   HIPC(hipMalloc(&ctx->d_T, nl * b * sizeof(double)));
   if (ctx->nranks > 1)
