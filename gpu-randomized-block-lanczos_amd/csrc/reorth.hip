@@ -106,16 +106,30 @@ __global__ __launch_bounds__(512) void k_gram44(int64_t nrows, PanelRun W, Panel
     load_a(rc0 + kG44Rows, anext);
     const double* xb = xs[c & 1];
     if (active) {  // idle waves (j >= nW) only help stage X: leave the MFMA pipe to the rest
+      // B operands of one ks slice (CG/2 16-B reads) are read one slice ahead: with two
+      // waves per SIMD, in-wave lookahead is what covers the LDS latency
+      const double* xl = xb + q * LD + 2 * (lane & 3);
+      d2v bcur[CG / 2], bnxt[CG / 2];
+#pragma unroll
+      for (int cp = 0; cp < CG / 2; ++cp) bcur[cp] = *reinterpret_cast<const d2v*>(xl + 8 * cp);
 #pragma unroll
       for (int ks = 0; ks < 8; ++ks) {
+        if (ks + 1 < 8) {
+#pragma unroll
+          for (int cp = 0; cp < CG / 2; ++cp)
+            bnxt[cp] = *reinterpret_cast<const d2v*>(xl + 4 * (ks + 1) * LD + 8 * cp);
+        }
 #pragma unroll
         for (int cp = 0; cp < CG / 2; ++cp) {  // column groups 2cp, 2cp+1 in one 16-B read
-          const d2v bf = *reinterpret_cast<const d2v*>(xb + (4 * ks + q) * LD + 8 * cp + 2 * (lane & 3));
 #pragma unroll
           for (int ag = 0; ag < AG; ++ag) {
-            acc[ag][2 * cp] = mfma4(acur[ks][ag], bf.x, acc[ag][2 * cp]);
-            acc[ag][2 * cp + 1] = mfma4(acur[ks][ag], bf.y, acc[ag][2 * cp + 1]);
+            acc[ag][2 * cp] = mfma4(acur[ks][ag], bcur[cp].x, acc[ag][2 * cp]);
+            acc[ag][2 * cp + 1] = mfma4(acur[ks][ag], bcur[cp].y, acc[ag][2 * cp + 1]);
           }
+        }
+        if (ks + 1 < 8) {
+#pragma unroll
+          for (int cp = 0; cp < CG / 2; ++cp) bcur[cp] = bnxt[cp];
         }
       }
     }
@@ -206,6 +220,26 @@ __global__ __launch_bounds__(256) void k_tsmm44(int64_t nrows, PanelRun X, const
 #pragma unroll
     for (int cg = 0; cg < CG; ++cg) acc[rt][cg] = 0.0;
 
+  // Y rows for beta != 0, row-major 16 B per lane (element e = 2 lane + 128 m of each
+  // 16-row tile), loaded before the k-loop so their latency hides behind it
+  constexpr int kYPer = 16 * KYP / 128;
+  constexpr bool kPrefY = KYP <= 32;  // b x b updates (one k-chunk); long-K runs load Y late
+  d2v yold[2][kYPer];
+  auto load_y = [&](int rt, int m) -> d2v {
+    const int e = 2 * lane + 128 * m, row = e / KYP, c = e % KYP;
+    int64_t r = r0 + 16 * rt + row;
+    r = r < nrows ? r : nrows - 1;
+    const int cc = c < KY ? c : 0;
+    const int t = cc / Y.w;
+    return *reinterpret_cast<const d2v*>(Y.ptr[t] + r * Y.w + (cc - t * Y.w));
+  };
+  if (kPrefY && beta != 0.0) {
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+      for (int m = 0; m < kYPer; ++m) yold[rt][m] = load_y(rt, m);
+  }
+
   // A: rows r0 + 16 rt + (lane&15); k = k0 + 8 h + 2 q + v, h in [0,4), v in {0,1}
   // Prefetch loads are unconditional (clamped addresses) so each chunk issues the same VMEM
   // ops and the vmcnt waits count only the chunk consumed.  Rows past nrows compute garbage
@@ -258,20 +292,33 @@ __global__ __launch_bounds__(256) void k_tsmm44(int64_t nrows, PanelRun X, const
   for (int ch = 0; ch < nch; ++ch) {
     load_c(ch + 1, cr);  // unconditional, clamped (see k_gram44)
     load_a(ch + 1, anext);
-    const double* cb = cs[ch & 1];
+    const double* cb = cs[ch & 1] + 2 * q * LDC + 2 * (lane & 3);
+    // C operands of one (h, v) slice (CG/2 16-B reads) are read one slice ahead
+    d2v bcur[CG / 2], bnxt[CG / 2];
 #pragma unroll
-    for (int h = 0; h < 4; ++h)
+    for (int cp = 0; cp < CG / 2; ++cp) bcur[cp] = *reinterpret_cast<const d2v*>(cb + 8 * cp);
 #pragma unroll
-      for (int v = 0; v < 2; ++v)
+    for (int hv = 0; hv < 8; ++hv) {
+      const int h = hv >> 1, v = hv & 1;
+      if (hv + 1 < 8) {
+        const int row = 8 * ((hv + 1) >> 1) + ((hv + 1) & 1);
 #pragma unroll
-        for (int cp = 0; cp < CG / 2; ++cp) {  // column groups 2cp, 2cp+1 in one 16-B read
-          const d2v bf = *reinterpret_cast<const d2v*>(cb + (8 * h + 2 * q + v) * LDC + 8 * cp + 2 * (lane & 3));
+        for (int cp = 0; cp < CG / 2; ++cp)
+          bnxt[cp] = *reinterpret_cast<const d2v*>(cb + row * LDC + 8 * cp);
+      }
 #pragma unroll
-          for (int rt = 0; rt < 2; ++rt) {
-            acc[rt][2 * cp] = mfma4(acur[rt][h][v], bf.x, acc[rt][2 * cp]);
-            acc[rt][2 * cp + 1] = mfma4(acur[rt][h][v], bf.y, acc[rt][2 * cp + 1]);
-          }
+      for (int cp = 0; cp < CG / 2; ++cp) {  // column groups 2cp, 2cp+1 in one 16-B read
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt) {
+          acc[rt][2 * cp] = mfma4(acur[rt][h][v], bcur[cp].x, acc[rt][2 * cp]);
+          acc[rt][2 * cp + 1] = mfma4(acur[rt][h][v], bcur[cp].y, acc[rt][2 * cp + 1]);
         }
+      }
+      if (hv + 1 < 8) {
+#pragma unroll
+        for (int cp = 0; cp < CG / 2; ++cp) bcur[cp] = bnxt[cp];
+      }
+    }
     store_c((ch + 1) & 1, ch + 1, cr);  // unconditional (see k_gram44)
 #pragma unroll
     for (int rt = 0; rt < 2; ++rt)
@@ -279,20 +326,30 @@ __global__ __launch_bounds__(256) void k_tsmm44(int64_t nrows, PanelRun X, const
       for (int h = 0; h < 4; ++h) acur[rt][h] = anext[rt][h];
     __syncthreads();
   }
+  // epilogue: the D-layout tile goes through LDS (the C buffers are free after the loop's
+  // last barrier) so Y is read and written row-major, 16 B per lane, fully coalesced; Y was
+  // prefetched before the k-loop.  Column c of staged row r sits at c ^ (4 ((r >> 2) & 3)):
+  // the four row quads a ds_write_b64 lane group covers land 8 banks apart.
+  double* ot = &cs[0][0] + wave * 16 * KYP;
   const int g = (lane >> 2) & 3;
 #pragma unroll
-  for (int rt = 0; rt < 2; ++rt)
+  for (int rt = 0; rt < 2; ++rt) {
 #pragma unroll
-    for (int cg = 0; cg < CG; ++cg) {
-      const int64_t r = r0 + 16 * rt + 4 * g + (lane >> 4);
-      const int c = 4 * cg + (lane & 3);
+    for (int cg = 0; cg < CG; ++cg)
+      ot[(4 * g + q) * KYP + ((4 * cg + (lane & 3)) ^ (4 * g))] = alpha * acc[rt][cg];
+#pragma unroll
+    for (int m = 0; m < kYPer; ++m) {
+      const int e = 2 * lane + 128 * m, row = e / KYP, c = e % KYP;
+      const int64_t r = r0 + 16 * rt + row;
+      d2v v = *reinterpret_cast<const d2v*>(ot + row * KYP + (c ^ (4 * ((row >> 2) & 3))));
       if (r < nrows && c < KY) {
         const int t = c / Y.w;
-        double* yp = const_cast<double*>(Y.ptr[t]) + r * Y.w + (c - t * Y.w);
-        const double v = alpha * acc[rt][cg];
-        *yp = beta == 0.0 ? v : beta * (*yp) + v;
+        d2v* yp = reinterpret_cast<d2v*>(const_cast<double*>(Y.ptr[t]) + r * Y.w + (c - t * Y.w));
+        if (beta != 0.0) v += beta * (kPrefY ? yold[rt][m] : load_y(rt, m));
+        *yp = v;
       }
     }
+  }
 }
 
 bool tsmm44_ok(int xw, int ky) { return (xw == 16 || xw == 32) && ky >= 1 && ky <= 64; }
