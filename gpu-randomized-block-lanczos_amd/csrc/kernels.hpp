@@ -47,6 +47,15 @@ struct CsrDev {
   bool band_ok32 = false;
 };
 
+// --- rowop.hip ---------------------------------------------------------------------------
+// Y' = beta Y + alpha X C (X, Y: n x b panels, C: b x b row-major, ldc) in one pass, and if
+// slab != null the Gram Y'^T Y' as grid partials slab[grid][b][b] (reduce with reduce_slab).
+// X may equal Y (in place).  b in {16, 32}.
+bool rowgram_ok(int b);
+int rowgram_grid(int64_t nrows);
+void rowgram(int64_t nrows, int b, const double* X, const double* C, int ldc, double* Y,
+             double alpha, double beta, double* slab, int grid, const int* skip, hipStream_t s);
+
 // --- spmm.hip ----------------------------------------------------------------------------
 // U = A * Qin  (+ epilogue U -= Qprev * Bt^T with Bt = B_i row-major b x b, if Qprev).
 // variant: 0 auto, 1 global gather, 2 LDS window.

@@ -310,29 +310,61 @@ int tsmm_checked(rbl_ctx* ctx, const PanelRun& X, const double* C, int ldc, cons
   return RBL_OK;
 }
 
+// Fused one-pass row operation (rowop.hip): Y = beta Y + alpha X C and, if G, the Gram
+// G = Y^T Y over all ranks.  b in {16, 32}.
+int rowop(rbl_ctx* ctx, const double* X, const double* C, double* Y, double alpha, double beta,
+          double* G, const int* skip) {
+  const int b = ctx->b;
+  const int grid = rowgram_grid(ctx->nloc);
+  if (G && (size_t)grid * b * b > ctx->slab_elems)
+    return fail(ctx, RBL_ERR_INVALID, "internal: row-op slab too small");
+  rowgram(ctx->nloc, b, X, C, b, Y, alpha, beta, G ? ctx->d_slab : nullptr, grid, skip, ctx->stream);
+  HIPC(hipGetLastError());
+  if (!G) return RBL_OK;
+  reduce_slab(ctx->d_slab, grid, (int64_t)b * b, G, skip, ctx->stream);
+  HIPC(hipGetLastError());
+  return allreduce(ctx, G, (size_t)b * b);
+}
+
 // Tall-skinny QR of U (n_local x b) into Qout; B = R (b x b, upper, row-major) in S_RTOT.
-int tsqr(rbl_ctx* ctx, const double* U, double* Qout) {
+// Shifted CholQR2 (+ a third pass after a shifted first pass).  `g1_ready`: S_G already holds
+// U^T U (the fused 3-term update computed it); each apply computes the next pass's Gram in the
+// same pass over the rows when b allows (rowop).
+int tsqr(rbl_ctx* ctx, const double* U, double* Qout, bool g1_ready = false) {
   StageScope t(ctx, RBL_STAGE_QR);
   const int b = ctx->b;
   int* need3 = ctx->d_flags;      // [need3, skip3]
   int* status = ctx->d_flags + 2; // [breakdown, shifted count]
   double* G = smallp(ctx, S_G);
+  const int* skip3 = need3 + 1;
+  const bool fused = rowgram_ok(b);
   // pass 1 (shift decided on device)
-  CHK(gram(ctx, run1(U, b), pan1(U, b), G, nullptr));
+  if (!g1_ready) CHK(gram(ctx, run1(U, b), pan1(U, b), G, nullptr));
   chol_step(G, b, ctx->n, 0, smallp(ctx, S_R), smallp(ctx, S_RINV), smallp(ctx, S_RTOT), need3,
             status, nullptr, ctx->stream);
-  CHK(tsmm_checked(ctx, run1(U, b), smallp(ctx, S_RINV), b, pan1(Qout, b), 1.0, 0.0, nullptr));
+  if (fused) {
+    CHK(rowop(ctx, U, smallp(ctx, S_RINV), Qout, 1.0, 0.0, G, nullptr));
+  } else {
+    CHK(tsmm_checked(ctx, run1(U, b), smallp(ctx, S_RINV), b, pan1(Qout, b), 1.0, 0.0, nullptr));
+    CHK(gram(ctx, run1(Qout, b), pan1(Qout, b), G, nullptr));
+  }
   // pass 2
-  CHK(gram(ctx, run1(Qout, b), pan1(Qout, b), G, nullptr));
   chol_step(G, b, ctx->n, 1, smallp(ctx, S_R), smallp(ctx, S_RINV), smallp(ctx, S_RTOT), need3,
             status, nullptr, ctx->stream);
-  CHK(tsmm_checked(ctx, run1(Qout, b), smallp(ctx, S_RINV), b, pan1(Qout, b), 1.0, 0.0, nullptr));
+  if (fused) {  // in place; the Gram feeds pass 3 when a shifted first pass asked for it
+    CHK(rowop(ctx, Qout, smallp(ctx, S_RINV), Qout, 1.0, 0.0, G, nullptr));
+  } else {
+    CHK(tsmm_checked(ctx, run1(Qout, b), smallp(ctx, S_RINV), b, pan1(Qout, b), 1.0, 0.0, nullptr));
+    CHK(gram(ctx, run1(Qout, b), pan1(Qout, b), G, skip3));
+  }
   // pass 3 only after a shifted first pass (device flag; kernels early-exit otherwise)
-  const int* skip3 = need3 + 1;
-  CHK(gram(ctx, run1(Qout, b), pan1(Qout, b), G, skip3));
   chol_step(G, b, ctx->n, 1, smallp(ctx, S_R), smallp(ctx, S_RINV), smallp(ctx, S_RTOT), need3,
             status, skip3, ctx->stream);
-  CHK(tsmm_checked(ctx, run1(Qout, b), smallp(ctx, S_RINV), b, pan1(Qout, b), 1.0, 0.0, skip3));
+  if (fused) {
+    CHK(rowop(ctx, Qout, smallp(ctx, S_RINV), Qout, 1.0, 0.0, nullptr, skip3));
+  } else {
+    CHK(tsmm_checked(ctx, run1(Qout, b), smallp(ctx, S_RINV), b, pan1(Qout, b), 1.0, 0.0, skip3));
+  }
   HIPC(hipGetLastError());
   return RBL_OK;
 }
@@ -782,6 +814,7 @@ int rbl_start(rbl_ctx* ctx, int b, int max_blocks, int basis_bits, const double*
       const size_t sp = (size_t)gram_splits(ctx->nloc, nW, b, xc);
       slab = std::max(slab, sp * nW * b * xc);
     }
+  slab = std::max(slab, (size_t)rowgram_grid(ctx->nloc) * b * b);  // rowop partials
   ctx->slab_elems = slab;
   HIPC(hipMalloc(&ctx->d_slab, slab * sizeof(double)));
   ctx->C_elems = (size_t)std::max(1, max_blocks) * b * 2 * b;
@@ -852,10 +885,14 @@ int rbl_step(rbl_ctx* ctx, int i, int part_reorth, double* A_out, double* B_out)
     }
   }
   // local reorth: Q_i -= Q_{i-1} (Q_{i-1}^T Q_i), one projection (RBL_gpu.jl:83-93, P1)
+  const bool fused = rowgram_ok(b);
   if (i >= 2) {
     StageScope t(ctx, RBL_STAGE_LOC_REORTH);
     CHK(gram(ctx, run1(Qm, b), pan1(Qi, b), ctx->d_C, nullptr));
-    CHK(tsmm_checked(ctx, run1(Qm, b), ctx->d_C, b, pan1(Qi, b), -1.0, 1.0, nullptr));
+    if (fused)
+      CHK(rowop(ctx, Qm, ctx->d_C, Qi, -1.0, 1.0, nullptr, nullptr));
+    else
+      CHK(tsmm_checked(ctx, run1(Qm, b), ctx->d_C, b, pan1(Qi, b), -1.0, 1.0, nullptr));
   }
   // U = A Q_i - Q_{i-1} B_i^T   (RBL_gpu.jl:176-177)
   {
@@ -868,14 +905,18 @@ int rbl_step(rbl_ctx* ctx, int i, int part_reorth, double* A_out, double* B_out)
            ctx->spmm_variant, ctx->stream);
     HIPC(hipGetLastError());
   }
-  // A_i = Q_i^T U ; U -= Q_i A_i   (RBL_gpu.jl:178-179)
+  // A_i = Q_i^T U ; U -= Q_i A_i   (RBL_gpu.jl:178-179); fused: the update pass also forms
+  // U^T U, CholQR's first Gram
   {
     StageScope t(ctx, RBL_STAGE_3TERM);
     CHK(gram(ctx, run1(Qi, b), pan1(ctx->d_U, b), smallp(ctx, S_AI), nullptr));
-    CHK(tsmm_checked(ctx, run1(Qi, b), smallp(ctx, S_AI), b, pan1(ctx->d_U, b), -1.0, 1.0, nullptr));
+    if (fused)
+      CHK(rowop(ctx, Qi, smallp(ctx, S_AI), ctx->d_U, -1.0, 1.0, smallp(ctx, S_G), nullptr));
+    else
+      CHK(tsmm_checked(ctx, run1(Qi, b), smallp(ctx, S_AI), b, pan1(ctx->d_U, b), -1.0, 1.0, nullptr));
   }
   // Q_{i+1} B_{i+1} = qr(U)   (RBL_gpu.jl:180-184)
-  CHK(tsqr(ctx, ctx->d_U, slotp(ctx, i)));
+  CHK(tsqr(ctx, ctx->d_U, slotp(ctx, i), fused));
   copy_small(smallp(ctx, S_RTOT), smallp(ctx, S_BPREV), (int64_t)b * b, ctx->stream);
   HIPC(hipMemcpyAsync(ctx->h_pin, smallp(ctx, S_AI), (size_t)b * b * sizeof(double),
                       hipMemcpyDeviceToHost, ctx->stream));

@@ -1,0 +1,226 @@
+// rowop.hip — fused b x b row operations of the block step on v_mfma_f64_4x4x4f64 (gfx950):
+//
+//   Y' = beta Y + alpha X C          (X, Y: n x B panels, C: B x B)
+//   G  = Y'^T Y'   (optional)        (per-workgroup partials, reduced by reduce_slab)
+//
+// One pass over X and Y instead of two: the 3-term update U -= Q_i A_i (RBL_gpu.jl:179)
+// hands CholQR its first Gram U^T U, and each CholQR apply Q = U R^-1 (RBL_gpu.jl:180) the
+// Gram of the next pass (tsqr in rbl_api.cpp).
+//
+// The Gram needs no data movement: in the MFMA D layout a lane holds
+// Y'[4g + (lane>>4)][4cg + (lane&3)] for row quad g = (lane>>2)&3 and column group cg, which
+// is exactly the A operand (A[i = lane&3][k = lane>>4] = Y'[k][4icg + i]) and the B operand
+// (B[k = lane>>4][j = lane&3] = Y'[k][4jcg + j]) of the 4x4x4 MFMA whose block g yields
+// sum_{k in quad g} Y'[k][4icg + i] Y'[k][4jcg + j]; the four blocks are summed once at the end.
+//
+// Persistent grid: each wave walks 16-row tiles grid-stride (register budget), with the next
+// block's X (A layout, 16 B per lane) and Y (row-major, 16 B per lane) prefetched.  Y enters
+// and leaves the D layout through a per-wave LDS tile (column c of row r stored at
+// c ^ 4((r >> 2) & 3): the four row quads of a ds_write_b64 lane group land 8 banks apart).
+#include "kernels.hpp"
+
+namespace rbl {
+
+namespace {
+
+constexpr int kRowThreads = 256;  // 4 waves
+constexpr int kBlockRows = 16;    // rows per wave per iteration (one MFMA row tile)
+
+__device__ __forceinline__ double mfma4r(double a, double b, double c) {
+  return __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, c, 0, 0, 0);
+}
+
+template <int B, bool GRAM>
+__global__ __launch_bounds__(kRowThreads) __attribute__((amdgpu_waves_per_eu(GRAM ? 2 : 3))) void k_rowgram(int64_t nrows, const double* X,  // X may alias Y (in-place apply)
+                                                         const double* __restrict__ C, int ldc,
+                                                         double* Y, double alpha, double beta,
+                                                         double* __restrict__ slab, const int* skip) {
+  if (skip && *skip) return;
+  constexpr int CG = B / 4;
+  constexpr int NH = B / 8;                 // A-operand loads per row tile (2 k each)
+  constexpr int LDC = B + 8;                // C rows: lane-group rows differ by 2 (see reorth.hip)
+  constexpr int kYPer = 16 * B / 128;       // row-major d2v per lane per 16-row tile
+  constexpr int NG = CG * (CG + 1) / 2;     // Gram accumulators (upper triangle of quads)
+  __shared__ __attribute__((aligned(16))) double cs[B * LDC];
+  __shared__ __attribute__((aligned(16))) double ys[4][16 * B];
+  __shared__ double gs[GRAM ? 4 * B * B : 1];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int q = lane >> 4, g = (lane >> 2) & 3, j = lane & 3;
+
+  // alpha C into LDS, columns in perm8 order (column groups 2cp, 2cp+1 in one 16-B read)
+  for (int e = tid; e < B * B; e += kRowThreads) {
+    const int k = e / B, c = e % B;
+    cs[k * LDC + perm8(c)] = alpha * C[(int64_t)k * ldc + c];
+  }
+  __syncthreads();
+
+  double* ot = ys[wave];
+  auto swz = [](int row, int c) { return row * B + (c ^ (4 * ((row >> 2) & 3))); };
+
+  const int64_t nblk = (nrows + kBlockRows - 1) / kBlockRows;
+  const int64_t stride = (int64_t)gridDim.x * 4;
+  int64_t blk = (int64_t)blockIdx.x * 4 + wave;
+
+  // loads (clamped rows: always issued)
+  auto load_x = [&](int64_t b0, d2v (&xa)[1][NH]) {
+#pragma unroll
+    for (int rt = 0; rt < 1; ++rt) {
+      int64_t r = b0 * kBlockRows + 16 * rt + (lane & 15);
+      r = r < nrows ? r : nrows - 1;
+#pragma unroll
+      for (int h = 0; h < NH; ++h)
+        xa[rt][h] = *reinterpret_cast<const d2v*>(X + r * B + 8 * h + 2 * q);
+    }
+  };
+  auto load_y = [&](int64_t b0, d2v (&yr)[1][kYPer]) {
+#pragma unroll
+    for (int rt = 0; rt < 1; ++rt)
+#pragma unroll
+      for (int m = 0; m < kYPer; ++m) {
+        const int e = 2 * lane + 128 * m;
+        int64_t r = b0 * kBlockRows + 16 * rt + e / B;
+        r = r < nrows ? r : nrows - 1;
+        yr[rt][m] = *reinterpret_cast<const d2v*>(Y + r * B + (e % B));
+      }
+  };
+
+  double gacc[GRAM ? NG : 1];
+#pragma unroll
+  for (int p = 0; p < (GRAM ? NG : 1); ++p) gacc[p] = 0.0;
+
+  d2v xa[1][NH], ya[1][kYPer];
+  const bool by = beta != 0.0;
+  const int64_t blk_c = blk < nblk ? blk : nblk - 1;
+  load_x(blk_c, xa);
+  if (by) load_y(blk_c, ya);
+  for (; blk < nblk; blk += stride) {
+    // keep the C operands in LDS: without this compiler barrier LLVM hoists their reads out
+    // of the loop and holds 32 x 16 B per lane in registers (occupancy 1, spills)
+    asm volatile("" ::: "memory");
+    d2v xn[1][NH], yn[1][kYPer];
+    {
+      const int64_t bn = blk + stride < nblk ? blk + stride : nblk - 1;  // clamped prefetch
+      load_x(bn, xn);
+      if (by) load_y(bn, yn);
+    }
+    double acc[1][CG];
+#pragma unroll
+    for (int rt = 0; rt < 1; ++rt) {
+      if (by) {  // beta Y into the D layout through the wave's LDS tile
+#pragma unroll
+        for (int m = 0; m < kYPer; ++m) {
+          const int e = 2 * lane + 128 * m;
+          *reinterpret_cast<d2v*>(ot + swz(e / B, e % B)) = beta * ya[rt][m];
+        }
+#pragma unroll
+        for (int cg = 0; cg < CG; ++cg) acc[rt][cg] = ot[swz(4 * g + q, 4 * cg + j)];
+      } else {
+#pragma unroll
+        for (int cg = 0; cg < CG; ++cg) acc[rt][cg] = 0.0;
+      }
+      // acc += X (alpha C): k = 8h + 2q + v
+#pragma unroll
+      for (int h = 0; h < NH; ++h)
+#pragma unroll
+        for (int v = 0; v < 2; ++v) {
+          const double a = v ? xa[rt][h].y : xa[rt][h].x;
+          const double* cb = cs + (8 * h + 2 * q + v) * LDC + 2 * j;
+#pragma unroll
+          for (int cp = 0; cp < CG / 2; ++cp) {
+            const d2v bf = *reinterpret_cast<const d2v*>(cb + 8 * cp);
+            acc[rt][2 * cp] = mfma4r(a, bf.x, acc[rt][2 * cp]);
+            acc[rt][2 * cp + 1] = mfma4r(a, bf.y, acc[rt][2 * cp + 1]);
+          }
+          if constexpr (CG % 2) {
+            acc[rt][CG - 1] = mfma4r(a, cb[8 * (CG / 2)], acc[rt][CG - 1]);
+          }
+        }
+      const int64_t rbase = blk * kBlockRows + 16 * rt;
+      if constexpr (GRAM) {
+        // rows past the end (clamped loads) must not enter the Gram
+        const bool live = rbase + 4 * g + q < nrows;
+        double am[CG];
+#pragma unroll
+        for (int cg = 0; cg < CG; ++cg) am[cg] = live ? acc[rt][cg] : 0.0;
+        int p = 0;
+#pragma unroll
+        for (int ic = 0; ic < CG; ++ic)
+#pragma unroll
+          for (int jc = ic; jc < CG; ++jc, ++p) gacc[p] = mfma4r(am[ic], am[jc], gacc[p]);
+      }
+      // Y' out: D layout -> LDS -> row-major 16-B stores
+#pragma unroll
+      for (int cg = 0; cg < CG; ++cg) ot[swz(4 * g + q, 4 * cg + j)] = acc[rt][cg];
+#pragma unroll
+      for (int m = 0; m < kYPer; ++m) {
+        const int e = 2 * lane + 128 * m;
+        const int64_t r = rbase + e / B;
+        const d2v v = *reinterpret_cast<const d2v*>(ot + swz(e / B, e % B));
+        if (r < nrows) *reinterpret_cast<d2v*>(Y + r * B + (e % B)) = v;
+      }
+    }
+#pragma unroll
+    for (int rt = 0; rt < 1; ++rt) {
+#pragma unroll
+      for (int h = 0; h < NH; ++h) xa[rt][h] = xn[rt][h];
+#pragma unroll
+      for (int m = 0; m < kYPer; ++m) ya[rt][m] = yn[rt][m];
+    }
+  }
+  if constexpr (GRAM) {
+    // sum the four row-quad blocks (lane bits 2, 3), then the four waves, into slab[block]
+    double* gw = gs + wave * B * B;
+    int p = 0;
+#pragma unroll
+    for (int ic = 0; ic < CG; ++ic)
+#pragma unroll
+      for (int jc = ic; jc < CG; ++jc, ++p) {
+        double v = gacc[p];
+        v += __shfl_xor(v, 4, 64);
+        v += __shfl_xor(v, 8, 64);
+        if (g == 0) {
+          const int r = 4 * ic + q, c = 4 * jc + j;
+          gw[r * B + c] = v;
+          if (ic != jc) gw[c * B + r] = v;  // lower triangle of the off-diagonal quads
+        }
+      }
+    __syncthreads();
+    double* out = slab + (int64_t)blockIdx.x * B * B;
+    for (int e = tid; e < B * B; e += kRowThreads)
+      out[e] = (gs[e] + gs[B * B + e]) + (gs[2 * B * B + e] + gs[3 * B * B + e]);
+  }
+}
+
+template <int B, bool GRAM>
+void launch_rowgram(int64_t nrows, const double* X, const double* C, int ldc, double* Y,
+                    double alpha, double beta, double* slab, int grid, const int* skip,
+                    hipStream_t s) {
+  hipLaunchKernelGGL((k_rowgram<B, GRAM>), dim3(grid), dim3(kRowThreads), 0, s, nrows, X, C, ldc,
+                     Y, alpha, beta, slab, skip);
+}
+
+}  // namespace
+
+bool rowgram_ok(int b) { return b == 16 || b == 32; }
+
+int rowgram_grid(int64_t nrows) {
+  // two workgroups per CU at b = 32 (register-bound); never more blocks than rows need
+  int64_t g = 2 * window_grid();
+  const int64_t need = (nrows + 4 * kBlockRows - 1) / (4 * kBlockRows);
+  if (g > need) g = need;
+  return (int)(g < 1 ? 1 : g);
+}
+
+void rowgram(int64_t nrows, int b, const double* X, const double* C, int ldc, double* Y,
+             double alpha, double beta, double* slab, int grid, const int* skip, hipStream_t s) {
+  const bool gram = slab != nullptr;
+  if (b == 32) {
+    if (gram) launch_rowgram<32, true>(nrows, X, C, ldc, Y, alpha, beta, slab, grid, skip, s);
+    else launch_rowgram<32, false>(nrows, X, C, ldc, Y, alpha, beta, slab, grid, skip, s);
+  } else {
+    if (gram) launch_rowgram<16, true>(nrows, X, C, ldc, Y, alpha, beta, slab, grid, skip, s);
+    else launch_rowgram<16, false>(nrows, X, C, ldc, Y, alpha, beta, slab, grid, skip, s);
+  }
+}
+
+}  // namespace rbl
