@@ -45,6 +45,8 @@ struct CsrDev {
   bool window_ok32 = false;
   bool band_ok16 = false;   // spmm_band.hip applicable (and dense enough to pay)
   bool band_ok32 = false;
+  bool band_gram = false;   // every tile's own rows lie in its band window (ring-resident)
+  int64_t row0 = 0;         // global index of local row 0 (row-partitioned runs)
 };
 
 // --- rowop.hip ---------------------------------------------------------------------------
@@ -58,17 +60,22 @@ void rowgram(int64_t nrows, int b, const double* X, const double* C, int ldc, do
 
 // --- spmm.hip ----------------------------------------------------------------------------
 // U = A * Qin  (+ epilogue U -= Qprev * Bt^T with Bt = B_i row-major b x b, if Qprev).
-// variant: 0 auto, 1 global gather, 2 LDS window.
-void spmm(const CsrDev& A, const double* Qin, int64_t col_off, int b, double* U,
-          const double* Qprev, const double* Bi, int variant, hipStream_t s);
+// variant: 0 auto, 1 global gather, 2 LDS window, 3 LDS band (MFMA).
+// ai_slab: if non-null and the band kernel runs with band_gram, it also forms the partials
+// of A_i = Qin[own rows]^T U (b x b per workgroup) there; returns how many (0: not formed).
+int spmm(const CsrDev& A, const double* Qin, int64_t col_off, int b, double* U,
+         const double* Qprev, const double* Bi, int variant, hipStream_t s,
+         double* ai_slab = nullptr);
 
 // spmm_window.hip: persistent LDS-window kernel (b in {16,32}); false if not applicable.
 bool spmm_window(const CsrDev& A, const double* Qin, int64_t col_off, int b, double* U,
                  const double* Qprev, const double* Bi, hipStream_t s);
 int window_grid();              // workgroups for the window kernel (= CUs)
 // spmm_band.hip: LDS-densified band tiles on fp64 MFMA (b in {16,32}); false if not applicable.
+// ai_slab / ai_parts: see spmm().
 bool spmm_band(const CsrDev& A, const double* Qin, int64_t col_off, int b, double* U,
-               const double* Qprev, const double* Bi, hipStream_t s);
+               const double* Qprev, const double* Bi, hipStream_t s, double* ai_slab = nullptr,
+               int* ai_parts = nullptr);
 constexpr int kWindowTileRows = 16;
 
 // --- tsmm.hip ----------------------------------------------------------------------------

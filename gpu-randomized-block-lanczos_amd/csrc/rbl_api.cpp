@@ -39,6 +39,7 @@ struct rbl_ctx {
   int64_t ntiles = 0, tiles_per_wg = 0;
   bool window_ok16 = false, window_ok32 = false;
   bool band_ok16 = false, band_ok32 = false;
+  bool band_gram = false;                 // band kernel may form A_i (tile rows ring-resident)
   std::vector<int64_t> bounds;            // nranks+1
   std::vector<int64_t> need_lo, need_hi;  // rows I need from rank q
   std::vector<int64_t> give_lo, give_hi;  // rows rank q needs from me
@@ -118,6 +119,8 @@ CsrDev csr(rbl_ctx* ctx) {
   A.window_ok32 = ctx->window_ok32;
   A.band_ok16 = ctx->band_ok16;
   A.band_ok32 = ctx->band_ok32;
+  A.band_gram = ctx->band_gram;
+  A.row0 = ctx->r0;
   return A;
 }
 
@@ -127,6 +130,7 @@ CsrDev csr(rbl_ctx* ctx) {
 int prepare_window(rbl_ctx* ctx, const std::vector<int64_t>& rp) {
   ctx->window_ok16 = ctx->window_ok32 = false;
   ctx->band_ok16 = ctx->band_ok32 = false;
+  ctx->band_gram = false;
   ctx->ntiles = (ctx->nloc + kWindowTileRows - 1) / kWindowTileRows;
   if (ctx->ntiles == 0 || ctx->nnz == 0) return RBL_OK;
   const int64_t nt = ctx->ntiles;
@@ -186,6 +190,17 @@ int prepare_window(rbl_ctx* ctx, const std::vector<int64_t>& rp) {
                      4 * ctx->nnz >= dense;
     ctx->band_ok32 = bok && max_new <= 32;
     ctx->band_ok16 = bok && max_new <= 64;
+    // A_i = Q^T U inside the band kernel reads Q's tile rows from the ring: each tile's own
+    // (global) rows must lie in its band, and stay resident until the tile's U is final (one
+    // phase late at b=16): rows [r(t), r(t)+16) vs the ring's [cmin(t), cmax(t+3)]
+    bool gok = bok;
+    for (int64_t t = 0; t < nt && gok; ++t) {
+      const int64_t ra = ctx->r0 + t * kWindowTileRows;
+      const int64_t rb = ctx->r0 + std::min((t + 1) * kWindowTileRows, ctx->nloc) - 1;
+      if (ra < cmin[t] || rb > cmax[t]) gok = false;
+      if (cmax[std::min(t + 3, nt - 1)] + 1 - ra > 256) gok = false;
+    }
+    ctx->band_gram = gok;
   }
   HIPC(hipMemcpy(ctx->d_tcmin, cmin.data(), nt * sizeof(int64_t), hipMemcpyHostToDevice));
   HIPC(hipMemcpy(ctx->d_tcmax, cmax.data(), nt * sizeof(int64_t), hipMemcpyHostToDevice));
@@ -895,21 +910,29 @@ int rbl_step(rbl_ctx* ctx, int i, int part_reorth, double* A_out, double* B_out)
       CHK(tsmm_checked(ctx, run1(Qm, b), ctx->d_C, b, pan1(Qi, b), -1.0, 1.0, nullptr));
   }
   // U = A Q_i - Q_{i-1} B_i^T   (RBL_gpu.jl:176-177)
+  int ai_parts = 0;
   {
     const double* Qin = nullptr;
     int64_t off = 0;
     CHK(halo_exchange(ctx, Qi, &Qin, &off));
     StageScope t(ctx, RBL_STAGE_AQ);
+    // the band kernel can also form the partials of A_i = Q_i^T U while U is in registers
     if (ctx->nloc > 0)
-      spmm(csr(ctx), Qin, off, b, ctx->d_U, Qm, i >= 2 ? smallp(ctx, S_BPREV) : nullptr,
-           ctx->spmm_variant, ctx->stream);
+      ai_parts = spmm(csr(ctx), Qin, off, b, ctx->d_U, Qm, i >= 2 ? smallp(ctx, S_BPREV) : nullptr,
+                      ctx->spmm_variant, ctx->stream, ctx->d_slab);
     HIPC(hipGetLastError());
   }
   // A_i = Q_i^T U ; U -= Q_i A_i   (RBL_gpu.jl:178-179); fused: the update pass also forms
   // U^T U, CholQR's first Gram
   {
     StageScope t(ctx, RBL_STAGE_3TERM);
-    CHK(gram(ctx, run1(Qi, b), pan1(ctx->d_U, b), smallp(ctx, S_AI), nullptr));
+    if (ai_parts > 0) {
+      reduce_slab(ctx->d_slab, ai_parts, (int64_t)b * b, smallp(ctx, S_AI), nullptr, ctx->stream);
+      HIPC(hipGetLastError());
+      CHK(allreduce(ctx, smallp(ctx, S_AI), (size_t)b * b));
+    } else {
+      CHK(gram(ctx, run1(Qi, b), pan1(ctx->d_U, b), smallp(ctx, S_AI), nullptr));
+    }
     if (fused)
       CHK(rowop(ctx, Qi, smallp(ctx, S_AI), ctx->d_U, -1.0, 1.0, smallp(ctx, S_G), nullptr));
     else

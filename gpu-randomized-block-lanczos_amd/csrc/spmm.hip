@@ -66,21 +66,25 @@ static void launch_gather(const CsrDev& A, const double* Q, int64_t off, int b, 
                      A.rowptr, A.col, A.val, Q, off, b, U, Qprev, Bi);
 }
 
-void spmm(const CsrDev& A, const double* Qin, int64_t col_off, int b, double* U,
-          const double* Qprev, const double* Bi, int variant, hipStream_t s) {
-  if (A.nrows <= 0) return;
+int spmm(const CsrDev& A, const double* Qin, int64_t col_off, int b, double* U,
+         const double* Qprev, const double* Bi, int variant, hipStream_t s, double* ai_slab) {
+  if (A.nrows <= 0) return 0;
   // 0 auto: band (MFMA) > window (DPP) > gather;  1 gather;  2 window;  3 band
-  if ((variant == 0 || variant == 3) && spmm_band(A, Qin, col_off, b, U, Qprev, Bi, s)) return;
+  int parts = 0;
+  if ((variant == 0 || variant == 3) &&
+      spmm_band(A, Qin, col_off, b, U, Qprev, Bi, s, ai_slab, &parts))
+    return parts;
   if ((variant == 0 || variant == 2 || variant == 3) &&
       spmm_window(A, Qin, col_off, b, U, Qprev, Bi, s))
-    return;
-  if (b <= 1) return launch_gather<1>(A, Qin, col_off, b, U, Qprev, Bi, s);
-  if (b <= 2) return launch_gather<2>(A, Qin, col_off, b, U, Qprev, Bi, s);
-  if (b <= 4) return launch_gather<4>(A, Qin, col_off, b, U, Qprev, Bi, s);
-  if (b <= 8) return launch_gather<8>(A, Qin, col_off, b, U, Qprev, Bi, s);
-  if (b <= 16) return launch_gather<16>(A, Qin, col_off, b, U, Qprev, Bi, s);
-  if (b <= 32) return launch_gather<32>(A, Qin, col_off, b, U, Qprev, Bi, s);
-  return launch_gather<64>(A, Qin, col_off, b, U, Qprev, Bi, s);
+    return 0;
+  if (b <= 1) launch_gather<1>(A, Qin, col_off, b, U, Qprev, Bi, s);
+  else if (b <= 2) launch_gather<2>(A, Qin, col_off, b, U, Qprev, Bi, s);
+  else if (b <= 4) launch_gather<4>(A, Qin, col_off, b, U, Qprev, Bi, s);
+  else if (b <= 8) launch_gather<8>(A, Qin, col_off, b, U, Qprev, Bi, s);
+  else if (b <= 16) launch_gather<16>(A, Qin, col_off, b, U, Qprev, Bi, s);
+  else if (b <= 32) launch_gather<32>(A, Qin, col_off, b, U, Qprev, Bi, s);
+  else launch_gather<64>(A, Qin, col_off, b, U, Qprev, Bi, s);
+  return 0;
 }
 
 }  // namespace rbl

@@ -76,6 +76,8 @@ struct BandArgs {
   double* U;             // padded to a multiple of 16 rows
   const double* Qprev;
   const double* Bi;
+  double* ai_slab;           // AIG: per-workgroup partials of A_i = Q[own rows]^T U (b x b)
+  int64_t row0;              // global index of local row 0 (ring rows are global)
   int ablate;                // diagnostics only (RBL_SPMM_ABLATE=1: skip compute)
   unsigned long long* prof;  // diagnostics only (PROF instantiation)
 };
@@ -123,7 +125,12 @@ __device__ __forceinline__ int lane32(int64_t v, int l) {
 
 // PROF (diagnostic instantiation, RBL_SPMM_PROF=1): per-wave shader-clock cycles of work
 // and of barrier wait, summed into a.prof[wave * 4 + {0,1,3}] (3 = tiles).
-template <int B, bool EPI, bool PROF = false>
+// AIG: the consumers also form A_i = Q^T U over the tile rows (RBL_gpu.jl:178) while U is
+// in registers: in the MFMA D layout a lane holds U[4g + (lane>>4)][4cg + (lane&3)], which
+// is the B operand (B[k][j] = U[4g+k][4cg+j]) of the 4x4x4 MFMA whose A operand is the
+// ring element Q[4g + (lane>>4)][4qc + (lane&3)] (A[i][k] = Q[4g+k][4qc+i]); block g yields
+// the row quad's share of (Q^T U)[4qc+i][4cg+j], summed over blocks at the end.
+template <int B, bool EPI, bool PROF = false, bool AIG = false>
 __global__ __launch_bounds__(band::kThreads) void k_spmm_band(BandArgs a) {
   using L = BandLayout<B>;
   constexpr int NCG = L::NCG, KSPLIT = L::KSPLIT, QPLD = L::QPLD;
@@ -310,9 +317,22 @@ __global__ __launch_bounds__(band::kThreads) void k_spmm_band(BandArgs a) {
       }
     }
     double pend = 0.0;  // KSPLIT > 1, h == 0: accumulator awaiting its partner's half
+    double ai[AIG ? NCG : 1];
+#pragma unroll
+    for (int c = 0; c < (AIG ? NCG : 1); ++c) ai[c] = 0.0;
     auto store_u = [&](int64_t t, double acc) {  // U rows padded to a multiple of 16
       const int g = (lane >> 2) & 3;
       (a.U + t * band::kTileRows * B)[(4 * g + (lane >> 4)) * B + bcol] = acc;
+      if constexpr (AIG) {
+        const int64_t rl = t * band::kTileRows + 4 * g + (lane >> 4);
+        const double um = rl < a.nrows ? acc : 0.0;  // rows past the end: no share
+        const int grow = (int)(a.row0 + rl);
+#pragma unroll
+        for (int qc = 0; qc < NCG; ++qc) {
+          const double qv = *reinterpret_cast<const double*>(smem + ring_addr(grow, 4 * qc + (lane & 3)));
+          ai[qc] = mfma4b(qv, um, ai[qc]);
+        }
+      }
     };
     auto compute = [&](int64_t t, int buf) {
       if (a.ablate == 1) return;  // diagnostics: pipeline only
@@ -409,6 +429,19 @@ __global__ __launch_bounds__(band::kThreads) void k_spmm_band(BandArgs a) {
       if (t + 2 < t1) phase(t + 2, 2);
     }
     finalize(t1 - 1);
+    if constexpr (AIG) {
+      if (KSPLIT == 1 || h == 0) {  // the waves that stored U own its column groups
+        const int g = (lane >> 2) & 3;
+        double* out = a.ai_slab + (int64_t)blockIdx.x * B * B;
+#pragma unroll
+        for (int qc = 0; qc < NCG; ++qc) {
+          double v = ai[qc];
+          v += __shfl_xor(v, 4, 64);
+          v += __shfl_xor(v, 8, 64);
+          if (g == 0) out[(4 * qc + (lane >> 4)) * B + bcol] = v;
+        }
+      }
+    }
   }
   if constexpr (PROF) {
     if (lane == 0) {
@@ -420,7 +453,7 @@ __global__ __launch_bounds__(band::kThreads) void k_spmm_band(BandArgs a) {
   }
 }
 
-template <int B, bool EPI>
+template <int B, bool EPI, bool AIG>
 static void launch_band_t(const BandArgs& a0, int grid, hipStream_t s) {
   static bool attr = false;
   static const bool prof = [] {
@@ -428,15 +461,15 @@ static void launch_band_t(const BandArgs& a0, int grid, hipStream_t s) {
     return e && atoi(e) != 0;
   }();
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_spmm_band<B, EPI>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_spmm_band<B, EPI, false, AIG>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, BandLayout<B>::kLds);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_spmm_band<B, EPI, true>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_spmm_band<B, EPI, true, AIG>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, BandLayout<B>::kLds);
     attr = true;
   }
   if (!prof) {
-    hipLaunchKernelGGL((k_spmm_band<B, EPI>), dim3(grid), dim3(band::kThreads), BandLayout<B>::kLds,
-                       s, a0);
+    hipLaunchKernelGGL((k_spmm_band<B, EPI, false, AIG>), dim3(grid), dim3(band::kThreads),
+                       BandLayout<B>::kLds, s, a0);
     return;
   }
   // diagnostics: work / barrier cycles per wave and tile, printed to stderr
@@ -445,7 +478,7 @@ static void launch_band_t(const BandArgs& a0, int grid, hipStream_t s) {
   if (!d) (void)hipMalloc(&d, 64 * sizeof(unsigned long long));
   (void)hipMemsetAsync(d, 0, 64 * sizeof(unsigned long long), s);
   a.prof = d;
-  hipLaunchKernelGGL((k_spmm_band<B, EPI, true>), dim3(grid), dim3(band::kThreads),
+  hipLaunchKernelGGL((k_spmm_band<B, EPI, true, AIG>), dim3(grid), dim3(band::kThreads),
                      BandLayout<B>::kLds, s, a);
   unsigned long long hbuf[64];
   (void)hipMemcpyAsync(hbuf, d, sizeof(hbuf), hipMemcpyDeviceToHost, s);
@@ -459,7 +492,8 @@ static void launch_band_t(const BandArgs& a0, int grid, hipStream_t s) {
 }
 
 bool spmm_band(const CsrDev& A, const double* Qin, int64_t col_off, int b, double* U,
-               const double* Qprev, const double* Bi, hipStream_t s) {
+               const double* Qprev, const double* Bi, hipStream_t s, double* ai_slab,
+               int* ai_parts) {
   if (A.ntiles <= 0 || !((b == 16 && A.band_ok16) || (b == 32 && A.band_ok32))) return false;
   BandArgs a;
   a.nrows = A.nrows;
@@ -480,12 +514,24 @@ bool spmm_band(const CsrDev& A, const double* Qin, int64_t col_off, int b, doubl
   }();
   a.ablate = ablate;
   a.prof = nullptr;
+  a.row0 = A.row0;
   const int grid = (int)((A.ntiles + A.tiles_per_wg - 1) / A.tiles_per_wg);
   const bool epi = Qprev != nullptr;
+  const bool aig = ai_slab != nullptr && A.band_gram;
+  a.ai_slab = aig ? ai_slab : nullptr;
+  if (ai_parts) *ai_parts = aig ? grid : 0;
   if (b == 32) {
-    if (epi) launch_band_t<32, true>(a, grid, s); else launch_band_t<32, false>(a, grid, s);
+    if (epi) {
+      if (aig) launch_band_t<32, true, true>(a, grid, s); else launch_band_t<32, true, false>(a, grid, s);
+    } else {
+      if (aig) launch_band_t<32, false, true>(a, grid, s); else launch_band_t<32, false, false>(a, grid, s);
+    }
   } else {
-    if (epi) launch_band_t<16, true>(a, grid, s); else launch_band_t<16, false>(a, grid, s);
+    if (epi) {
+      if (aig) launch_band_t<16, true, true>(a, grid, s); else launch_band_t<16, true, false>(a, grid, s);
+    } else {
+      if (aig) launch_band_t<16, false, true>(a, grid, s); else launch_band_t<16, false, false>(a, grid, s);
+    }
   }
   return true;
 }
