@@ -106,30 +106,16 @@ __global__ __launch_bounds__(512) void k_gram44(int64_t nrows, PanelRun W, Panel
     load_a(rc0 + kG44Rows, anext);
     const double* xb = xs[c & 1];
     if (active) {  // idle waves (j >= nW) only help stage X: leave the MFMA pipe to the rest
-      // B operands of one ks slice (CG/2 16-B reads) are read one slice ahead: with two
-      // waves per SIMD, in-wave lookahead is what covers the LDS latency
-      const double* xl = xb + q * LD + 2 * (lane & 3);
-      d2v bcur[CG / 2], bnxt[CG / 2];
-#pragma unroll
-      for (int cp = 0; cp < CG / 2; ++cp) bcur[cp] = *reinterpret_cast<const d2v*>(xl + 8 * cp);
 #pragma unroll
       for (int ks = 0; ks < 8; ++ks) {
-        if (ks + 1 < 8) {
-#pragma unroll
-          for (int cp = 0; cp < CG / 2; ++cp)
-            bnxt[cp] = *reinterpret_cast<const d2v*>(xl + 4 * (ks + 1) * LD + 8 * cp);
-        }
 #pragma unroll
         for (int cp = 0; cp < CG / 2; ++cp) {  // column groups 2cp, 2cp+1 in one 16-B read
+          const d2v bf = *reinterpret_cast<const d2v*>(xb + (4 * ks + q) * LD + 8 * cp + 2 * (lane & 3));
 #pragma unroll
           for (int ag = 0; ag < AG; ++ag) {
-            acc[ag][2 * cp] = mfma4(acur[ks][ag], bcur[cp].x, acc[ag][2 * cp]);
-            acc[ag][2 * cp + 1] = mfma4(acur[ks][ag], bcur[cp].y, acc[ag][2 * cp + 1]);
+            acc[ag][2 * cp] = mfma4(acur[ks][ag], bf.x, acc[ag][2 * cp]);
+            acc[ag][2 * cp + 1] = mfma4(acur[ks][ag], bf.y, acc[ag][2 * cp + 1]);
           }
-        }
-        if (ks + 1 < 8) {
-#pragma unroll
-          for (int cp = 0; cp < CG / 2; ++cp) bcur[cp] = bnxt[cp];
         }
       }
     }
@@ -201,7 +187,7 @@ constexpr int kT44Rows = 32;   // rows per wave
 constexpr int kT44K = 32;      // k per chunk
 
 template <int B, int KYP>
-__global__ __launch_bounds__(256) void k_tsmm44(int64_t nrows, PanelRun X, const double* __restrict__ C,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k_tsmm44(int64_t nrows, PanelRun X, const double* __restrict__ C,
                                                 int ldc, int KY, Panels Y, double alpha, double beta,
                                                 const int* skip) {
   if (skip && *skip) return;
@@ -293,30 +279,18 @@ __global__ __launch_bounds__(256) void k_tsmm44(int64_t nrows, PanelRun X, const
     load_c(ch + 1, cr);  // unconditional, clamped (see k_gram44)
     load_a(ch + 1, anext);
     const double* cb = cs[ch & 1] + 2 * q * LDC + 2 * (lane & 3);
-    // C operands of one (h, v) slice (CG/2 16-B reads) are read one slice ahead
-    d2v bcur[CG / 2], bnxt[CG / 2];
-#pragma unroll
-    for (int cp = 0; cp < CG / 2; ++cp) bcur[cp] = *reinterpret_cast<const d2v*>(cb + 8 * cp);
 #pragma unroll
     for (int hv = 0; hv < 8; ++hv) {
       const int h = hv >> 1, v = hv & 1;
-      if (hv + 1 < 8) {
-        const int row = 8 * ((hv + 1) >> 1) + ((hv + 1) & 1);
-#pragma unroll
-        for (int cp = 0; cp < CG / 2; ++cp)
-          bnxt[cp] = *reinterpret_cast<const d2v*>(cb + row * LDC + 8 * cp);
-      }
+      const double* cr0 = cb + (8 * h + v) * LDC;
 #pragma unroll
       for (int cp = 0; cp < CG / 2; ++cp) {  // column groups 2cp, 2cp+1 in one 16-B read
+        const d2v bf = *reinterpret_cast<const d2v*>(cr0 + 8 * cp);
 #pragma unroll
         for (int rt = 0; rt < 2; ++rt) {
-          acc[rt][2 * cp] = mfma4(acur[rt][h][v], bcur[cp].x, acc[rt][2 * cp]);
-          acc[rt][2 * cp + 1] = mfma4(acur[rt][h][v], bcur[cp].y, acc[rt][2 * cp + 1]);
+          acc[rt][2 * cp] = mfma4(acur[rt][h][v], bf.x, acc[rt][2 * cp]);
+          acc[rt][2 * cp + 1] = mfma4(acur[rt][h][v], bf.y, acc[rt][2 * cp + 1]);
         }
-      }
-      if (hv + 1 < 8) {
-#pragma unroll
-        for (int cp = 0; cp < CG / 2; ++cp) bcur[cp] = bnxt[cp];
       }
     }
     store_c((ch + 1) & 1, ch + 1, cr);  // unconditional (see k_gram44)
