@@ -46,6 +46,7 @@ struct CsrDev {
   bool band_ok16 = false;   // spmm_band.hip applicable (and dense enough to pay)
   bool band_ok32 = false;
   bool band_gram = false;   // every tile's own rows lie in its band window (ring-resident)
+  bool band_pair = false;   // every tile-row pair (2p, 2p+1) has <= 253 nonzeros
   int64_t row0 = 0;         // global index of local row 0 (row-partitioned runs)
 };
 

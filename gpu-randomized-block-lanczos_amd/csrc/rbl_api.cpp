@@ -40,6 +40,7 @@ struct rbl_ctx {
   bool window_ok16 = false, window_ok32 = false;
   bool band_ok16 = false, band_ok32 = false;
   bool band_gram = false;                 // band kernel may form A_i (tile rows ring-resident)
+  bool band_pair = false;                 // band kernel may stage row pairs with one load set
   std::vector<int64_t> bounds;            // nranks+1
   std::vector<int64_t> need_lo, need_hi;  // rows I need from rank q
   std::vector<int64_t> give_lo, give_hi;  // rows rank q needs from me
@@ -120,6 +121,7 @@ CsrDev csr(rbl_ctx* ctx) {
   A.band_ok16 = ctx->band_ok16;
   A.band_ok32 = ctx->band_ok32;
   A.band_gram = ctx->band_gram;
+  A.band_pair = ctx->band_pair;
   A.row0 = ctx->r0;
   return A;
 }
@@ -131,6 +133,7 @@ int prepare_window(rbl_ctx* ctx, const std::vector<int64_t>& rp) {
   ctx->window_ok16 = ctx->window_ok32 = false;
   ctx->band_ok16 = ctx->band_ok32 = false;
   ctx->band_gram = false;
+  ctx->band_pair = false;
   ctx->ntiles = (ctx->nloc + kWindowTileRows - 1) / kWindowTileRows;
   if (ctx->ntiles == 0 || ctx->nnz == 0) return RBL_OK;
   const int64_t nt = ctx->ntiles;
@@ -201,6 +204,11 @@ int prepare_window(rbl_ctx* ctx, const std::vector<int64_t>& rp) {
       if (cmax[std::min(t + 3, nt - 1)] + 1 - ra > 256) gok = false;
     }
     ctx->band_gram = gok;
+    // rows (2p, 2p+1) of every 16-row tile: nonzeros + up to 3 of alignment shift <= 256
+    int64_t max_pair = 0;
+    for (int64_t r = 0; r < ctx->nloc; r += 2)
+      max_pair = std::max(max_pair, rp[std::min(r + 2, ctx->nloc)] - rp[r]);
+    ctx->band_pair = bok && max_pair + 3 <= 256;
   }
   HIPC(hipMemcpy(ctx->d_tcmin, cmin.data(), nt * sizeof(int64_t), hipMemcpyHostToDevice));
   HIPC(hipMemcpy(ctx->d_tcmax, cmax.data(), nt * sizeof(int64_t), hipMemcpyHostToDevice));

@@ -111,9 +111,13 @@ struct BandRow {
   d2v v0, v1;
 };
 
+// PAIR staging: the two rows of a producer wave are contiguous in CSR, so one set of 16-B
+// lane loads (64 lanes x 4 entries) covers both when their nonzeros + alignment shift fit 256
+// (checked on the host: CsrDev::band_pair); r0 then holds the pair and r1 is unused.
 struct BandStage {
   int64_t desc_next;  // lane l <= 16: rowptr[16T'+l]; 17..20: lo, hi, cmin, cmax of the next tile
   int nnew, lo, cmin, K;  // of the tile the registers below hold (wave-uniform)
+  int cnt0;               // PAIR: entries of the first row of the pair
   BandRow r0, r1;
   double q0, q1;      // new ring rows, two elements per producer thread
   double qp;          // Q_{i-1} tile, one element per producer thread
@@ -130,7 +134,7 @@ __device__ __forceinline__ int lane32(int64_t v, int l) {
 // is the B operand (B[k][j] = U[4g+k][4cg+j]) of the 4x4x4 MFMA whose A operand is the
 // ring element Q[4g + (lane>>4)][4qc + (lane&3)] (A[i][k] = Q[4g+k][4qc+i]); block g yields
 // the row quad's share of (Q^T U)[4qc+i][4cg+j], summed over blocks at the end.
-template <int B, bool EPI, bool PROF = false, bool AIG = false>
+template <int B, bool EPI, bool PROF = false, bool AIG = false, bool PAIR = false>
 __global__ __launch_bounds__(band::kThreads) void k_spmm_band(BandArgs a) {
   using L = BandLayout<B>;
   constexpr int NCG = L::NCG, KSPLIT = L::KSPLIT, QPLD = L::QPLD;
@@ -213,8 +217,13 @@ __global__ __launch_bounds__(band::kThreads) void k_spmm_band(BandArgs a) {
       S.lo = lo;
       S.nnew = hi - lo;
       S.desc_next = load_desc(t + kRegStages);
-      load_row(rs, m_lo - rs_lo, S.r0);
-      load_row(rs + (m_lo - rs_lo), e_lo - m_lo, S.r1);
+      if constexpr (PAIR) {
+        S.cnt0 = m_lo - rs_lo;
+        load_row(rs, e_lo - rs_lo, S.r0);  // both rows: one load set
+      } else {
+        load_row(rs, m_lo - rs_lo, S.r0);
+        load_row(rs + (m_lo - rs_lo), e_lo - m_lo, S.r1);
+      }
       // new ring rows lo + qr and lo + qr + kQStep, clamped to the last new row (threads
       // past it re-read and later re-store that row's data)
       const int nq = S.nnew > 0 ? S.nnew : 1;
@@ -247,11 +256,32 @@ __global__ __launch_bounds__(band::kThreads) void k_spmm_band(BandArgs a) {
         ad[perm8(x)] = vv[k];
       }
     };
+    auto store_pair = [&](double* ad, const BandRow& R, int cnt0, int cmin) {
+      constexpr int kTail = band::kAdLd / 2 - 64;
+      d2v* ad2 = reinterpret_cast<d2v*>(ad);
+      ad2[lane] = d2v{0.0, 0.0};
+      ad2[64 + (lane < kTail ? lane : kTail - 1)] = d2v{0.0, 0.0};
+      ad2[band::kAdLd / 2 + lane] = d2v{0.0, 0.0};
+      ad2[band::kAdLd / 2 + 64 + (lane < kTail ? lane : kTail - 1)] = d2v{0.0, 0.0};
+      const int er = 4 * lane - R.shift;
+      const int cc[4] = {R.c.x, R.c.y, R.c.z, R.c.w};
+      const double vv[4] = {R.v0.x, R.v0.y, R.v1.x, R.v1.y};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int x = (unsigned)(er + k) < (unsigned)R.cnt ? cc[k] - cmin : band::kTrash;
+        const int row = er + k >= cnt0 ? band::kAdLd : 0;
+        ad[row + perm8(x)] = vv[k];
+      }
+    };
     auto store_stage = [&](int64_t t, const BandStage& S, int buf) {
       if (t >= t1) return;
       double* ad = adb(buf) + 2 * p * band::kAdLd;
-      store_row(ad, S.r0, S.cmin);
-      store_row(ad + band::kAdLd, S.r1, S.cmin);
+      if constexpr (PAIR) {
+        store_pair(ad, S.r0, S.cnt0, S.cmin);
+      } else {
+        store_row(ad, S.r0, S.cmin);
+        store_row(ad + band::kAdLd, S.r1, S.cmin);
+      }
       if (p * (64 / B) < S.nnew) {  // wave-uniform: some new row among this wave's first
         const int l0 = qr < S.nnew ? qr : S.nnew - 1;
         *reinterpret_cast<double*>(smem + ring_addr(S.lo + l0, qc)) = S.q0;
@@ -453,7 +483,7 @@ __global__ __launch_bounds__(band::kThreads) void k_spmm_band(BandArgs a) {
   }
 }
 
-template <int B, bool EPI, bool AIG>
+template <int B, bool EPI, bool AIG, bool PAIR>
 static void launch_band_t(const BandArgs& a0, int grid, hipStream_t s) {
   static bool attr = false;
   static const bool prof = [] {
@@ -461,14 +491,14 @@ static void launch_band_t(const BandArgs& a0, int grid, hipStream_t s) {
     return e && atoi(e) != 0;
   }();
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_spmm_band<B, EPI, false, AIG>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_spmm_band<B, EPI, false, AIG, PAIR>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, BandLayout<B>::kLds);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_spmm_band<B, EPI, true, AIG>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_spmm_band<B, EPI, true, AIG, PAIR>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, BandLayout<B>::kLds);
     attr = true;
   }
   if (!prof) {
-    hipLaunchKernelGGL((k_spmm_band<B, EPI, false, AIG>), dim3(grid), dim3(band::kThreads),
+    hipLaunchKernelGGL((k_spmm_band<B, EPI, false, AIG, PAIR>), dim3(grid), dim3(band::kThreads),
                        BandLayout<B>::kLds, s, a0);
     return;
   }
@@ -478,7 +508,7 @@ static void launch_band_t(const BandArgs& a0, int grid, hipStream_t s) {
   if (!d) (void)hipMalloc(&d, 64 * sizeof(unsigned long long));
   (void)hipMemsetAsync(d, 0, 64 * sizeof(unsigned long long), s);
   a.prof = d;
-  hipLaunchKernelGGL((k_spmm_band<B, EPI, true, AIG>), dim3(grid), dim3(band::kThreads),
+  hipLaunchKernelGGL((k_spmm_band<B, EPI, true, AIG, PAIR>), dim3(grid), dim3(band::kThreads),
                      BandLayout<B>::kLds, s, a);
   unsigned long long hbuf[64];
   (void)hipMemcpyAsync(hbuf, d, sizeof(hbuf), hipMemcpyDeviceToHost, s);
@@ -520,18 +550,20 @@ bool spmm_band(const CsrDev& A, const double* Qin, int64_t col_off, int b, doubl
   const bool aig = ai_slab != nullptr && A.band_gram;
   a.ai_slab = aig ? ai_slab : nullptr;
   if (ai_parts) *ai_parts = aig ? grid : 0;
-  if (b == 32) {
-    if (epi) {
-      if (aig) launch_band_t<32, true, true>(a, grid, s); else launch_band_t<32, true, false>(a, grid, s);
-    } else {
-      if (aig) launch_band_t<32, false, true>(a, grid, s); else launch_band_t<32, false, false>(a, grid, s);
-    }
-  } else {
-    if (epi) {
-      if (aig) launch_band_t<16, true, true>(a, grid, s); else launch_band_t<16, true, false>(a, grid, s);
-    } else {
-      if (aig) launch_band_t<16, false, true>(a, grid, s); else launch_band_t<16, false, false>(a, grid, s);
-    }
+  // every combination is its own kernel (template flags): pick by (b, epilogue, A_i, pair)
+  const int key = (b == 32 ? 8 : 0) | (epi ? 4 : 0) | (aig ? 2 : 0) | (A.band_pair ? 1 : 0);
+  switch (key) {
+#define RBL_BAND_CASE(K, BB, E, G, P) \
+    case K: launch_band_t<BB, E, G, P>(a, grid, s); break;
+    RBL_BAND_CASE(0, 16, false, false, false) RBL_BAND_CASE(1, 16, false, false, true)
+    RBL_BAND_CASE(2, 16, false, true, false)  RBL_BAND_CASE(3, 16, false, true, true)
+    RBL_BAND_CASE(4, 16, true, false, false)  RBL_BAND_CASE(5, 16, true, false, true)
+    RBL_BAND_CASE(6, 16, true, true, false)   RBL_BAND_CASE(7, 16, true, true, true)
+    RBL_BAND_CASE(8, 32, false, false, false) RBL_BAND_CASE(9, 32, false, false, true)
+    RBL_BAND_CASE(10, 32, false, true, false) RBL_BAND_CASE(11, 32, false, true, true)
+    RBL_BAND_CASE(12, 32, true, false, false) RBL_BAND_CASE(13, 32, true, false, true)
+    RBL_BAND_CASE(14, 32, true, true, false)  RBL_BAND_CASE(15, 32, true, true, true)
+#undef RBL_BAND_CASE
   }
   return true;
 }
