@@ -23,43 +23,42 @@ __device__ __forceinline__ double mfma4(double a, double b, double c) {
 }
 
 // ----------------------------------------------------------------------------------------
-// Gram C = W^T X: one Krylov panel per wave (8 panels per workgroup), X rows staged in LDS
-// in 32-row chunks shared by the 8 waves, A operands prefetched one chunk ahead.
+// Gram C = W^T X: one Krylov panel per wave, 4 waves per workgroup (three workgroups per CU:
+// while one waits at its per-chunk barrier the others keep the MFMA pipe busy), X rows
+// staged in LDS in 16-row chunks shared by the 4 waves, A operands prefetched one chunk ahead.
+// A last panel group with r < 4 panels splits the X columns over 4 / r waves per panel, so
+// the even panel counts partial reorth produces leave no wave idle (tools/gram_probe.hip:
+// idle waves cost ~25% at 18 panels with 8-wave groups).
 // ----------------------------------------------------------------------------------------
-constexpr int kG44Waves = 8;
-constexpr int kG44Rows = 32;
+constexpr int kG44Waves = 4;
+constexpr int kG44Rows = 16;
 
-template <int B, int NX>
-__global__ __launch_bounds__(512) void k_gram44(int64_t nrows, PanelRun W, Panels X, double* slab,
-                                                int npg, int64_t rows_per, const int* skip) {
-  if (skip && *skip) return;
+template <int B, int NX, int NPH>
+__device__ __forceinline__ void gram44_body(int64_t r_begin, int64_t r_end, int64_t s, int pg,
+                                            int r, const PanelRun& W, const Panels& X,
+                                            double* slab, double* xs_base) {
   constexpr int KC = NX * B;
   constexpr int AG = B / 16;
   constexpr int CG = KC / 4;
-  // rows of a ds_read_b128 lane group differ by one: LD/2 = 4 mod 16 puts their 16-B slots
-  // in disjoint banks (LD = KC + 8)
-  constexpr int LD = KC + 8;
-  constexpr int EPT = kG44Rows * KC / 512;
-  __shared__ __attribute__((aligned(16))) double xs[2][kG44Rows * LD];
+  constexpr int CGP = CG / NPH;  // column groups of this wave (even: read in pairs)
+  constexpr int LD = KC + 8;     // rows of a ds_read_b128 lane group differ by one: disjoint banks
+  constexpr int EPT = kG44Rows * KC / (kG44Waves * 64);
+  constexpr int KS = kG44Rows / 4;
+  static_assert(CGP >= 2 && CGP % 2 == 0, "column split");
+  double(*xs)[kG44Rows * LD] = reinterpret_cast<double(*)[kG44Rows * LD]>(xs_base);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int q = lane >> 4;
-  // XCD-aware mapping: the npg workgroups of one row split share blockIdx % 8 (one XCD under
-  // round-robin dispatch) and are consecutive there, so X is fetched once per XCD L2.
-  const int bid = blockIdx.x;
-  const int xcd = bid & 7, t = bid >> 3;
-  const int pg = t % npg;
-  const int64_t s = (int64_t)(t / npg) * 8 + xcd;
-  const int64_t r_begin = s * rows_per;
-  const int64_t r_end = r_begin + rows_per < nrows ? r_begin + rows_per : nrows;
-  const int j = pg * kG44Waves + wave;
-  const bool active = j < W.count;
-  const double* wp = W.base + (int64_t)(active ? j : 0) * W.stride + (lane & 15);
+  const int j = pg * kG44Waves + wave % r;  // panel
+  const int ph = wave / r;                  // column phase
+  const bool active = ph < NPH;
+  const int cp0 = ph < NPH ? ph * (CGP / 2) : 0;
+  const double* wp = W.base + (int64_t)j * W.stride + (lane & 15);
 
-  double acc[AG][CG];
+  double acc[AG][CGP];
 #pragma unroll
   for (int ag = 0; ag < AG; ++ag)
 #pragma unroll
-    for (int cg = 0; cg < CG; ++cg) acc[ag][cg] = 0.0;
+    for (int cg = 0; cg < CGP; ++cg) acc[ag][cg] = 0.0;
 
   // Prefetch loads are unconditional (clamped rows) so every chunk issues the same VMEM ops
   // and the compiler's vmcnt waits count just the chunk being consumed; rows past r_end are
@@ -69,8 +68,8 @@ __global__ __launch_bounds__(512) void k_gram44(int64_t nrows, PanelRun W, Panel
   const double* xsrc = X.ptr[xcol / B] + (xcol % B);
   const int64_t rlast = r_end > 0 ? r_end - 1 : 0;
   auto load_x = [&](int64_t rc0, double (&xr)[EPT]) {
-    const int64_t r = rc0 + xrow;
-    const int64_t rc = r < rlast ? r : rlast;
+    const int64_t rr = rc0 + xrow;
+    const int64_t rc = rr < rlast ? rr : rlast;
 #pragma unroll
     for (int v = 0; v < EPT; ++v) xr[v] = xsrc[rc * B + v];
   };
@@ -79,11 +78,11 @@ __global__ __launch_bounds__(512) void k_gram44(int64_t nrows, PanelRun W, Panel
 #pragma unroll
     for (int v = 0; v < EPT; ++v) xs[buf][xrow * LD + perm8(xcol + v)] = ok ? xr[v] : 0.0;
   };
-  auto load_a = [&](int64_t rc0, double (&ar)[8][AG]) {
+  auto load_a = [&](int64_t rc0, double (&ar)[KS][AG]) {
 #pragma unroll
-    for (int ks = 0; ks < 8; ++ks) {
-      const int64_t r = rc0 + 4 * ks + q;
-      const int64_t rc = r < rlast ? r : rlast;
+    for (int ks = 0; ks < KS; ++ks) {
+      const int64_t rr = rc0 + 4 * ks + q;
+      const int64_t rc = rr < rlast ? rr : rlast;
 #pragma unroll
       for (int ag = 0; ag < AG; ++ag) ar[ks][ag] = wp[rc * B + 16 * ag];
     }
@@ -91,7 +90,7 @@ __global__ __launch_bounds__(512) void k_gram44(int64_t nrows, PanelRun W, Panel
 
   const int64_t nchunks = r_end > r_begin ? (r_end - r_begin + kG44Rows - 1) / kG44Rows : 0;
   double xr[EPT];
-  double acur[8][AG], anext[8][AG];
+  double acur[KS][AG], anext[KS][AG];
   if (nchunks > 0) {
     load_x(r_begin, xr);
     store_x(0, r_begin, xr);
@@ -104,12 +103,12 @@ __global__ __launch_bounds__(512) void k_gram44(int64_t nrows, PanelRun W, Panel
     // waitcnt pass merge a no-load path and drain the prefetch before the MFMAs
     load_x(rc0 + kG44Rows, xr);
     load_a(rc0 + kG44Rows, anext);
-    const double* xb = xs[c & 1];
-    if (active) {  // idle waves (j >= nW) only help stage X: leave the MFMA pipe to the rest
+    const double* xb = xs[c & 1] + 8 * cp0;
+    if (active) {  // idle waves (a 3-panel group) only help stage X
 #pragma unroll
-      for (int ks = 0; ks < 8; ++ks) {
+      for (int ks = 0; ks < KS; ++ks) {
 #pragma unroll
-        for (int cp = 0; cp < CG / 2; ++cp) {  // column groups 2cp, 2cp+1 in one 16-B read
+        for (int cp = 0; cp < CGP / 2; ++cp) {  // column groups 2cp, 2cp+1 in one 16-B read
           const d2v bf = *reinterpret_cast<const d2v*>(xb + (4 * ks + q) * LD + 8 * cp + 2 * (lane & 3));
 #pragma unroll
           for (int ag = 0; ag < AG; ++ag) {
@@ -123,23 +122,47 @@ __global__ __launch_bounds__(512) void k_gram44(int64_t nrows, PanelRun W, Panel
     // (after the MFMAs); on the last chunk this writes the dead spare buffer
     store_x((int)((c + 1) & 1), rc0 + kG44Rows, xr);
 #pragma unroll
-    for (int ks = 0; ks < 8; ++ks)
+    for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
       for (int ag = 0; ag < AG; ++ag) acur[ks][ag] = anext[ks][ag];
     __syncthreads();
   }
   if (!active) return;
   const int KW = W.count * B;
-  double* out = slab + (s * KW + (int64_t)j * B) * KC;
+  double* out = slab + (s * KW + (int64_t)j * B) * KC + 4 * (2 * cp0);
   const int g = (lane >> 2) & 3;
 #pragma unroll
   for (int ag = 0; ag < AG; ++ag)
 #pragma unroll
-    for (int cg = 0; cg < CG; ++cg) {
+    for (int cg = 0; cg < CGP; ++cg) {
       const int a = 16 * ag + 4 * g + (lane >> 4);
       const int cc = 4 * cg + (lane & 3);
       out[(int64_t)a * KC + cc] = acc[ag][cg];
     }
+}
+
+template <int B, int NX>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k_gram44(
+    int64_t nrows, PanelRun W, Panels X, double* slab, int npg, int64_t rows_per, const int* skip) {
+  if (skip && *skip) return;
+  constexpr int KC = NX * B;
+  constexpr int CG = KC / 4;
+  constexpr int NPH2 = CG / 2 >= 2 ? 2 : 1;
+  constexpr int NPH4 = CG / 2 >= 4 ? 4 : NPH2;
+  __shared__ __attribute__((aligned(16))) double xs[2 * kG44Rows * (KC + 8)];
+  // XCD-aware mapping: the npg workgroups of one row split share blockIdx % 8 (one XCD under
+  // round-robin dispatch) and are consecutive there, so X is fetched once per XCD L2.
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, t = bid >> 3;
+  const int pg = t % npg;
+  const int64_t s = (int64_t)(t / npg) * 8 + xcd;
+  const int64_t r_begin = s * rows_per;
+  const int64_t r_end = r_begin + rows_per < nrows ? r_begin + rows_per : nrows;
+  const int rem = W.count - pg * kG44Waves;
+  const int r = rem < kG44Waves ? rem : kG44Waves;  // panels in this group (workgroup-uniform)
+  if (r >= 3) gram44_body<B, NX, 1>(r_begin, r_end, s, pg, r, W, X, slab, xs);
+  else if (r == 2) gram44_body<B, NX, NPH2>(r_begin, r_end, s, pg, r, W, X, slab, xs);
+  else gram44_body<B, NX, NPH4>(r_begin, r_end, s, pg, r, W, X, slab, xs);
 }
 
 bool gram44_ok(int nW, int w, int xcount, int xw) {
@@ -148,11 +171,10 @@ bool gram44_ok(int nW, int w, int xcount, int xw) {
 
 int gram44_splits(int64_t nrows, int nW) {
   (void)nW;
-  // One 8-wave workgroup fits per CU (~184 VGPRs): with one split per CU the grid is
-  // exactly npg full rounds of 256 workgroups (no partially filled last round).
-  // Splits stay a multiple of 8 (XCD mapping) and >= 256 rows each.
-  int64_t s8 = window_grid() / 8;
-  const int64_t max_s8 = (nrows + 8 * 256 - 1) / (8 * 256);
+  // three 4-wave workgroups per CU: 3 x CUs splits, a multiple of 8 (XCD mapping), each
+  // split >= 128 rows
+  int64_t s8 = 3 * window_grid() / 8;
+  const int64_t max_s8 = (nrows + 8 * 128 - 1) / (8 * 128);
   if (s8 > max_s8) s8 = max_s8;
   if (s8 < 1) s8 = 1;
   return (int)(s8 * 8);
@@ -164,7 +186,7 @@ static void launch_gram44(int64_t nrows, const PanelRun& W, const Panels& X, dou
   const int npg = (W.count + kG44Waves - 1) / kG44Waves;
   int64_t rows_per = (nrows + splits - 1) / splits;
   rows_per = (rows_per + kG44Rows - 1) / kG44Rows * kG44Rows;
-  hipLaunchKernelGGL((k_gram44<B, NX>), dim3(npg * splits), dim3(512), 0, st, nrows, W, X, slab,
+  hipLaunchKernelGGL((k_gram44<B, NX>), dim3(npg * splits), dim3(256), 0, st, nrows, W, X, slab,
                      npg, rows_per, skip);
 }
 

@@ -1,0 +1,83 @@
+// reorth_probe.cpp — time the shipped partial-reorth kernels (gram44_partial + reduce_slab,
+// tsmm44) at n = 1e7, b = 32, X = [Q_i, Q_{i-1}] for a range of basis sizes (diagnostic).
+// Build: tools/build_probe.sh (links the library's objects).
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <vector>
+
+#include "../gpu-randomized-block-lanczos_amd/csrc/kernels.hpp"
+
+__global__ void k_fill(double* p, int64_t n, uint64_t seed) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    uint64_t z = (uint64_t)i * 0x9E3779B97F4A7C15ull + seed;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    p[i] = ((double)(z >> 11) * 0x1.0p-53 - 0.5) * 1e-2;
+  }
+}
+static void fill(double* p, int64_t n, uint64_t seed) {
+  hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, 0, p, n, seed);
+}
+
+int main(int argc, char** argv) {
+  const int64_t n = argc > 1 ? atoll(argv[1]) : 10000000;
+  const int b = 32, nWmax = 36;
+  double *W, *X0, *X1, *slab, *C, *Cg;
+  if (hipMalloc(&W, (size_t)n * b * nWmax * 8) != hipSuccess) return 1;
+  (void)hipMalloc(&X0, (size_t)n * b * 8);
+  (void)hipMalloc(&X1, (size_t)n * b * 8);
+  fill(W, n * b * nWmax, 1);
+  fill(X0, n * b, 2);
+  fill(X1, n * b, 3);
+  const int smax = rbl::gram44_splits(n, nWmax);
+  (void)hipMalloc(&slab, (size_t)smax * nWmax * b * 64 * 8);
+  (void)hipMalloc(&C, (size_t)nWmax * b * 64 * 8);
+  fill(C, nWmax * b * 64, 4);
+  (void)hipMalloc(&Cg, (size_t)nWmax * b * 64 * 8);
+  hipEvent_t e0, e1, e2;
+  (void)hipEventCreate(&e0);
+  (void)hipEventCreate(&e1);
+  (void)hipEventCreate(&e2);
+  double tg = 0, tt = 0, fl = 0;
+  for (int nW = 2; nW <= nWmax; nW += 2) {
+    rbl::PanelRun Wr;
+    Wr.base = W;
+    Wr.stride = n * b;
+    Wr.count = nW;
+    Wr.w = b;
+    rbl::Panels X;
+    X.ptr[0] = X0;
+    X.ptr[1] = X1;
+    X.count = 2;
+    X.w = b;
+    const int splits = rbl::gram44_splits(n, nW);
+    float bg = 1e30f, bt = 1e30f;
+    for (int rep = 0; rep < 3; ++rep) {
+      (void)hipEventRecord(e0);
+      rbl::gram44_partial(n, Wr, X, slab, splits, nullptr, 0);
+      rbl::reduce_slab(slab, splits, (int64_t)nW * b * 64, Cg, nullptr, 0);  // C stays fixed: X must not blow up
+      (void)hipEventRecord(e1);
+      rbl::tsmm44(n, Wr, C, 64, X, -1.0, 1.0, nullptr, 0);
+      (void)hipEventRecord(e2);
+      (void)hipEventSynchronize(e2);
+      float g, t;
+      (void)hipEventElapsedTime(&g, e0, e1);
+      (void)hipEventElapsedTime(&t, e1, e2);
+      if (rep) {
+        bg = g < bg ? g : bg;
+        bt = t < bt ? t : bt;
+      }
+    }
+    const double f = 2.0 * n * nW * b * 64;
+    printf("nW=%2d  gram %7.3f ms %5.1f TF   tsmm %7.3f ms %5.1f TF\n", nW, bg, f / bg / 1e9, bt,
+           f / bt / 1e9);
+    tg += bg;
+    tt += bt;
+    fl += f;
+  }
+  printf("sum over nW=2..36 step 2: gram %.1f ms (%.1f TF)  tsmm %.1f ms (%.1f TF)\n", tg,
+         fl / tg / 1e9, tt, fl / tt / 1e9);
+  return 0;
+}
