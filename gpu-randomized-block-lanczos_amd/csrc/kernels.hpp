@@ -48,6 +48,9 @@ struct CsrDev {
   bool band_gram = false;   // every tile's own rows lie in its band window (ring-resident)
   bool band_pair = false;   // every tile-row pair (2p, 2p+1) has <= 253 nonzeros
   int64_t row0 = 0;         // global index of local row 0 (row-partitioned runs)
+  // band kernel: per nonzero, its byte offset in the tile's dense LDS band
+  // ((row % 16) * kBandLd + perm8(col - c16(tile))) * 8 (band_positions; kCsrPad entries past nnz)
+  const uint16_t* band_pos = nullptr;
 };
 
 // --- rowop.hip ---------------------------------------------------------------------------
@@ -78,6 +81,14 @@ bool spmm_band(const CsrDev& A, const double* Qin, int64_t col_off, int b, doubl
                const double* Qprev, const double* Bi, hipStream_t s, double* ai_slab = nullptr,
                int* ai_parts = nullptr);
 constexpr int kWindowTileRows = 16;
+// Band kernel geometry (host checks in rbl_api.cpp): a tile's band [c16, cmax] with
+// c16 = cmin & ~15 spans <= kBandMaxK columns; the Q ring holds kBandRing rows; per tile a
+// producer pass stores ring rows in whole sets of 512 / b (one element per producer thread).
+constexpr int kBandMaxK = 176;
+constexpr int kBandLd = 196;
+constexpr int kBandRing = 256;
+// positions of every nonzero in its tile's dense band (CsrDev::band_pos), from tile_info
+void band_positions(const CsrDev& A, uint16_t* pos, hipStream_t s);
 
 // --- tsmm.hip ----------------------------------------------------------------------------
 // Partial Gram:  slab[s][a][c] = sum over rows of split s of W[r][a] * X[r][c]

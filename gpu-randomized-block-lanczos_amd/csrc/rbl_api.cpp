@@ -36,6 +36,7 @@ struct rbl_ctx {
   int64_t* d_tcmin = nullptr;
   int64_t* d_tcmax = nullptr;
   int64_t* d_tinfo = nullptr;
+  uint16_t* d_bpos = nullptr;  // band kernel: per-nonzero dense-tile positions
   int64_t ntiles = 0, tiles_per_wg = 0;
   bool window_ok16 = false, window_ok32 = false;
   bool band_ok16 = false, band_ok32 = false;
@@ -123,6 +124,7 @@ CsrDev csr(rbl_ctx* ctx) {
   A.band_gram = ctx->band_gram;
   A.band_pair = ctx->band_pair;
   A.row0 = ctx->r0;
+  A.band_pos = ctx->d_bpos;
   return A;
 }
 
@@ -174,22 +176,23 @@ int prepare_window(rbl_ctx* ctx, const std::vector<int64_t>& rp) {
   }
   ctx->window_ok32 = ok && max_span <= 256 && max_new <= 32;
   ctx->window_ok16 = ok && max_span <= 512 && max_new <= 64;
-  // band (MFMA) kernel: 256-row ring, tile band <= 160 columns, rows <= 192 nonzeros, and the
-  // dense tiles at least 25 % filled (else the zero padding costs more than it saves)
+  // band (MFMA) kernel (spmm_band.hip): tile band [c16, cmax] (c16 = cmin & ~15) at most
+  // kBandMaxK columns, rows <= 192 nonzeros, and the dense tiles at least 25 % filled (else
+  // the zero padding costs more than it saves)
   {
     int64_t max_row = 0, dense = 0, max_k = 0;
     for (int64_t i = 0; i < ctx->nloc; ++i) max_row = std::max(max_row, rp[i + 1] - rp[i]);
     for (int64_t t = 0; t < nt; ++t) {
-      const int64_t k = cmax[t] + 1 - cmin[t];
+      const int64_t k = cmax[t] + 1 - (cmin[t] & ~int64_t(15));
       max_k = std::max(max_k, k);
-      dense += kWindowTileRows * ((k + 3) / 4 * 4);
+      dense += kWindowTileRows * ((k + 15) / 16 * 16);
     }
-    // producers write tile t+2's new ring rows while tile t is multiplied: the 256-row ring
-    // must hold [cmin(t), cmax(t+2)]
+    // producers write tile t+2's new ring rows while tile t is multiplied: the ring must hold
+    // [cmin(t), cmax(t+2)]
     int64_t max_span2 = 0;
     for (int64_t t = 0; t < nt; ++t)
       max_span2 = std::max(max_span2, cmax[std::min(t + 2, nt - 1)] + 1 - cmin[t]);
-    const bool bok = ok && max_span2 <= 256 && max_k <= 160 && max_row <= 192 &&
+    const bool bok = ok && max_span2 <= kBandRing && max_k <= kBandMaxK && max_row <= 192 &&
                      4 * ctx->nnz >= dense;
     ctx->band_ok32 = bok && max_new <= 32;
     ctx->band_ok16 = bok && max_new <= 64;
@@ -201,7 +204,7 @@ int prepare_window(rbl_ctx* ctx, const std::vector<int64_t>& rp) {
       const int64_t ra = ctx->r0 + t * kWindowTileRows;
       const int64_t rb = ctx->r0 + std::min((t + 1) * kWindowTileRows, ctx->nloc) - 1;
       if (ra < cmin[t] || rb > cmax[t]) gok = false;
-      if (cmax[std::min(t + 3, nt - 1)] + 1 - ra > 256) gok = false;
+      if (cmax[std::min(t + 3, nt - 1)] + 1 - ra > kBandRing) gok = false;
     }
     ctx->band_gram = gok;
     // rows (2p, 2p+1) of every 16-row tile: nonzeros + up to 3 of alignment shift <= 256
@@ -229,6 +232,14 @@ int prepare_window(rbl_ctx* ctx, const std::vector<int64_t>& rp) {
   }
   HIPC(hipMalloc(&ctx->d_tinfo, 8 * nt * sizeof(int64_t)));
   HIPC(hipMemcpy(ctx->d_tinfo, info.data(), 8 * nt * sizeof(int64_t), hipMemcpyHostToDevice));
+  if (ctx->band_ok16 || ctx->band_ok32) {  // dense-tile positions for the band kernel
+    HIPC(hipMalloc(&ctx->d_bpos, (ctx->nnz + kCsrPad) * sizeof(uint16_t)));
+    HIPC(hipMemsetAsync(ctx->d_bpos + ctx->nnz, 0, kCsrPad * sizeof(uint16_t), ctx->stream));
+    CsrDev A2 = csr(ctx);
+    band_positions(A2, ctx->d_bpos, ctx->stream);
+    HIPC(hipGetLastError());
+    HIPC(hipStreamSynchronize(ctx->stream));
+  }
   const int64_t grid = window_grid();
   ctx->tiles_per_wg = std::max<int64_t>(1, (nt + grid - 1) / grid);
   return RBL_OK;
@@ -447,6 +458,7 @@ void free_matrix(rbl_ctx* ctx) {
   hipFree(ctx->d_tcmin); ctx->d_tcmin = nullptr;
   hipFree(ctx->d_tcmax); ctx->d_tcmax = nullptr;
   hipFree(ctx->d_tinfo); ctx->d_tinfo = nullptr;
+  hipFree(ctx->d_bpos); ctx->d_bpos = nullptr;
   ctx->n = ctx->nloc = ctx->nnz = 0;
   ctx->ntiles = ctx->tiles_per_wg = 0;
   ctx->window_ok16 = ctx->window_ok32 = false;

@@ -11,7 +11,8 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "librbl_hip.so")
+# RBL_LIB: a diagnostics build of the same library (tools/build_variant.sh)
+LIB_PATH = os.environ.get("RBL_LIB") or os.path.join(_HERE, "librbl_hip.so")
 
 RBL_OK = 0
 RBL_WARN_NOT_CONVERGED = 1

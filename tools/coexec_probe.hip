@@ -5,14 +5,26 @@
 
 #include <cstdio>
 
-template <int MODE>  // 0: all waves MFMA, 1: all waves VALU, 2: even waves MFMA / odd VALU
+template <int MODE>  // 0: all waves MFMA, 1: all waves VALU, 2: even waves MFMA / odd VALU,
+                     // 3: all waves int VALU, 4: even waves MFMA / odd int VALU
 __global__ __launch_bounds__(512) void k_mix(double* out, int iters, double a0) {
   const int wave = threadIdx.x >> 6;
-  const bool mfma = MODE == 0 || (MODE == 2 && (wave & 1) == 0);
+  const bool mfma = MODE == 0 || ((MODE == 2 || MODE == 4) && (wave & 1) == 0);
+  const bool ivalu = MODE == 3 || (MODE == 4 && (wave & 1));
   double acc[8];
   for (int i = 0; i < 8; ++i) acc[i] = i * 1e-3;
   const double a = a0 + threadIdx.x * 1e-6, b = 1.0 - threadIdx.x * 1e-7;
-  if (mfma) {
+  if (ivalu) {
+    unsigned u[8];
+    for (int i = 0; i < 8; ++i) u[i] = threadIdx.x * 2654435761u + i;
+    for (int it = 0; it < iters; ++it) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int i = 0; i < 8; ++i) u[i] = (u[i] ^ (u[i] >> 7)) + 0x9E3779B9u;
+    }
+    for (int i = 0; i < 8; ++i) acc[i] = u[i];
+  } else if (mfma) {
     for (int it = 0; it < iters; ++it) {
 #pragma unroll
       for (int i = 0; i < 8; ++i) acc[i] = __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, acc[i], 0, 0, 0);
@@ -37,12 +49,14 @@ int main() {
   (void)hipEventCreate(&e0);
   (void)hipEventCreate(&e1);
   const int wgs = 256 * 4, iters = 4000;
-  for (int mode = 0; mode < 3; ++mode) {
+  for (int mode = 0; mode < 5; ++mode) {
     for (int rep = 0; rep < 2; ++rep) {
       (void)hipEventRecord(e0);
       if (mode == 0) hipLaunchKernelGGL(k_mix<0>, dim3(wgs), dim3(512), 0, 0, out, iters, 0.5);
       if (mode == 1) hipLaunchKernelGGL(k_mix<1>, dim3(wgs), dim3(512), 0, 0, out, iters, 0.5);
       if (mode == 2) hipLaunchKernelGGL(k_mix<2>, dim3(wgs), dim3(512), 0, 0, out, iters, 0.5);
+      if (mode == 3) hipLaunchKernelGGL(k_mix<3>, dim3(wgs), dim3(512), 0, 0, out, iters, 0.5);
+      if (mode == 4) hipLaunchKernelGGL(k_mix<4>, dim3(wgs), dim3(512), 0, 0, out, iters, 0.5);
       (void)hipEventRecord(e1);
       (void)hipEventSynchronize(e1);
       float ms;
@@ -54,8 +68,11 @@ int main() {
       if (mode == 0) flops = waves * fm;
       if (mode == 1) flops = waves * fv;
       if (mode == 2) flops = waves / 2 * (fm + fv);
-      if (rep) printf("mode %d (%s): %.3f ms  %.1f TFLOP/s\n", mode,
-                      mode == 0 ? "MFMA only" : mode == 1 ? "VALU only" : "half/half", ms, flops / ms / 1e9);
+      // int VALU: 2 ops (xor-shift, add) x 32 per iteration, counted as "flops" for the rate
+      if (mode == 3) flops = waves * fv;
+      if (mode == 4) flops = waves / 2 * (fm + fv);
+      static const char* nm[] = {"MFMA only", "fp64 VALU only", "MFMA / fp64 VALU", "int VALU only", "MFMA / int VALU"};
+      if (rep) printf("mode %d (%s): %.3f ms  %.1f T(FL)OP/s\n", mode, nm[mode], ms, flops / ms / 1e9);
     }
   }
   return 0;
