@@ -32,6 +32,7 @@ import numpy as np  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP64_MFMA_PEAK_TF = 78.6     # MI355X dense fp64 matrix spec
+FP32_MFMA_PEAK_TF = 157.3    # MI355X dense fp32 matrix spec (v_mfma_f32_16x16x4_f32)
 
 
 def parse():
@@ -51,6 +52,9 @@ def parse():
     ap.add_argument("--no-ttk", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     ap.add_argument("--spmm-kernel", type=int, default=0)
+    ap.add_argument("--basis-bits", type=int, default=64, choices=(64, 32),
+                    help="32: the mixed mode (fp32 Krylov basis + reorth on fp32 MFMA, fp64 A*Q / "
+                         "3-term / QR) of BASELINE config 5, on this workload")
     return ap.parse_args()
 
 
@@ -111,7 +115,8 @@ def main():
     spmm_kernel = {1: "gather", 2: "lds-window", 3: "lds-band-mfma"}[ctx.spmm_kernel_for(b)]
 
     def one_run():
-        rbl.lanczos(ctx, k, b, kryl_sz=args.kryl, seed=args.seed + 1, check=False, ritz=False)
+        rbl.lanczos(ctx, k, b, kryl_sz=args.kryl, seed=args.seed + 1, check=False, ritz=False,
+                    basis_bits=args.basis_bits)
 
     for _ in range(args.warmup):
         one_run()
@@ -150,7 +155,8 @@ def main():
     try:
         with open(args.traffic_json) as f:
             tj = json.load(f)
-        if tj.get("config", {}).get("n") == n and tj.get("config", {}).get("b") == b and world == 1:
+        if (tj.get("config", {}).get("n") == n and tj.get("config", {}).get("b") == b and world == 1
+                and args.basis_bits == 64):
             traffic = tj.get("spmm_hbm_bytes_per_launch")
             traffic_reorth = tj.get("part_reorth_hbm_bytes_per_run")
     except (OSError, ValueError):
@@ -160,9 +166,11 @@ def main():
                  "traffic": None if traffic is None else int(traffic),
                  "algorithmic_bytes_per_launch": int(spmm_bytes),
                  "ms_per_launch": round(spmm_ms, 4)}
-    roof_reorth = {"kernel": "partial reorth (gram+update)", "bound": "mfma",
-                   "achieved": round(reorth_tf, 2), "peak": FP64_MFMA_PEAK_TF, "unit": "TFLOP/s",
-                   "frac": round(reorth_tf / FP64_MFMA_PEAK_TF, 4),
+    mfma_peak = FP64_MFMA_PEAK_TF if args.basis_bits == 64 else FP32_MFMA_PEAK_TF
+    roof_reorth = {"kernel": "partial reorth (gram+update)" + ("" if args.basis_bits == 64 else ", fp32"),
+                   "bound": "mfma",
+                   "achieved": round(reorth_tf, 2), "peak": mfma_peak, "unit": "TFLOP/s",
+                   "frac": round(reorth_tf / mfma_peak, 4),
                    "traffic": None if traffic_reorth is None else int(traffic_reorth),
                    "traffic_unit": "HBM bytes per run (gram + update, 18 launches each)",
                    "algorithmic_flops_per_run": reorth_flops, "ms_per_run": round(reorth_ms, 3)}
@@ -178,7 +186,7 @@ def main():
         ctx.synchronize()
         t0 = time.perf_counter()
         D, V, info = rbl.lanczos(ctx, k, b, kryl_sz=args.kryl, seed=args.seed + 2, check=True,
-                                 ritz=True)
+                                 ritz=True, basis_bits=args.basis_bits)
         ctx.synchronize()
         barrier()
         ttk_s = allmax(time.perf_counter() - t0)
@@ -202,9 +210,11 @@ def main():
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
-            "dtype": "f64",
+            "dtype": "f64" if args.basis_bits == 64 else "f64 (A*Q, 3-term, QR) + f32 (basis, reorth)",
             "data": "synthetic (seeded hash-window symmetric matrix generated on device)",
-            "config": {"workload": "C4a hash-window SpMM-Lanczos", "n": n, "nnz": nnz, "b": b,
+            "config": {"workload": "C4a hash-window SpMM-Lanczos" +
+                       ("" if args.basis_bits == 64 else ", mixed precision (fp32 basis, config 5 mode)"),
+                       "n": n, "nnz": nnz, "b": b,
                        "k": k, "halfwidth": args.halfwidth, "density": args.density,
                        "block_steps_per_run": m_max, "parallelism": f"rows{world}"},
             "roofline": roofline,

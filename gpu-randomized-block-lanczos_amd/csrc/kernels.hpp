@@ -115,6 +115,19 @@ bool tsmm44_ok(int xw, int ky);
 void tsmm44(int64_t nrows, const PanelRun& X, const double* C, int ldc, const Panels& Y,
             double alpha, double beta, const int* skip, hipStream_t s);
 
+// --- reorth32.hip: the fp32 Krylov basis (mixed precision, b in {16, 32}) ---------------
+// Gram partials slab[s][a][c] = sum over split s of W[r][a] X[r][c] (W: nW fp32 panels of
+// width w at Wb + j*wstride, X: xcount fp32 panels of width w), fp32 MFMA per split.
+int gram32_splits(int64_t nrows);
+void gram32_partial(int64_t nrows, const float* Wb, int64_t wstride, int nW, int w, const float* X0,
+                    const float* X1, int xcount, double* slab, int splits, hipStream_t s);
+// Y = beta Y + alpha X C: X nX fp32 panels (k = nX*w), C fp64 row-major (rounded to f32),
+// Y ycount fp32 panels of width w (Y may alias X's panels row-for-row).
+void tsmm32(int64_t nrows, const float* Xb, int64_t xstride, int nX, int w, const double* C, int ldc,
+            float* Y0, float* Y1, int ycount, float alpha, float beta, hipStream_t s);
+void cvt_f32_to_f64(const float* src, double* dst, int64_t n, hipStream_t s);
+void cvt_f64_to_f32(const double* src, float* dst, int64_t n, hipStream_t s);
+
 // --- smallmat.hip ------------------------------------------------------------------------
 // Cholesky step of (shifted) CholQR on the b x b Gram G (row-major, symmetric):
 //   mode 0: first pass — try unshifted; on breakdown or estimated cond > 3e7 use the

@@ -49,8 +49,14 @@ struct rbl_ctx {
 
   // Krylov run
   int b = 0, max_blocks = 0, nblocks = 0;
-  double* d_basis = nullptr;  // (max_blocks+1) slots
+  double* d_basis = nullptr;  // (max_blocks+1) slots (fp64 basis)
   int64_t slot = 0;           // nloc * b
+  // fp32 basis (mixed precision, RBL_gpu.jl with FLOAT = Float32): slots in d_basis32, the
+  // current and previous block widened to fp64 in d_Qi64 / d_Qm64 for A Q, 3-term and QR
+  int basis_bits = 64;
+  float* d_basis32 = nullptr;
+  double* d_Qi64 = nullptr;
+  double* d_Qm64 = nullptr;
   double* d_U = nullptr;
   double* d_T = nullptr;      // scratch n_local x max(b,k)
   int64_t T_cols = 0;
@@ -104,6 +110,7 @@ int fail(rbl_ctx* c, int code, const std::string& msg) {
   } while (0)
 
 double* slotp(rbl_ctx* ctx, int j) { return ctx->d_basis + (int64_t)j * ctx->slot; }
+float* slotp32(rbl_ctx* ctx, int j) { return ctx->d_basis32 + (int64_t)j * ctx->slot; }
 
 CsrDev csr(rbl_ctx* ctx) {
   CsrDev A;
@@ -360,6 +367,33 @@ int rowop(rbl_ctx* ctx, const double* X, const double* C, double* Y, double alph
   return allreduce(ctx, G, (size_t)b * b);
 }
 
+// fp32 basis: Gram C = W^T [X0, X1] over all ranks (fp32 MFMA per split, fp64 sum), C fp64
+// [nW*b][xcount*b] — the FLOAT `temp` of RBL_gpu.jl:33,39,87 (rounded to f32 where applied).
+int gram32(rbl_ctx* ctx, const float* Wb, int nW, const float* X0, const float* X1, int xcount,
+           double* C) {
+  const int b = ctx->b;
+  const int splits = gram32_splits(ctx->nloc);
+  const int64_t len = (int64_t)nW * b * xcount * b;
+  if ((size_t)splits * len > ctx->slab_elems)
+    return fail(ctx, RBL_ERR_INVALID, "internal: Gram slab too small (fp32)");
+  if (ctx->nloc > 0) {
+    gram32_partial(ctx->nloc, Wb, ctx->slot, nW, b, X0, X1, xcount, ctx->d_slab, splits, ctx->stream);
+    reduce_slab(ctx->d_slab, splits, len, C, nullptr, ctx->stream);
+  } else {
+    HIPC(hipMemsetAsync(C, 0, len * sizeof(double), ctx->stream));
+  }
+  HIPC(hipGetLastError());
+  return allreduce(ctx, C, (size_t)len);
+}
+// fp32 basis: [Y0, Y1] -= X C (X: nX fp32 slots from Xb), RBL_gpu.jl:34,40,88 in FLOAT.
+int upd32(rbl_ctx* ctx, const float* Xb, int nX, const double* C, int ldc, float* Y0, float* Y1,
+          int ycount) {
+  if (ctx->nloc <= 0) return RBL_OK;
+  tsmm32(ctx->nloc, Xb, ctx->slot, nX, ctx->b, C, ldc, Y0, Y1, ycount, -1.f, 1.f, ctx->stream);
+  HIPC(hipGetLastError());
+  return RBL_OK;
+}
+
 // Tall-skinny QR of U (n_local x b) into Qout; B = R (b x b, upper, row-major) in S_RTOT.
 // Shifted CholQR2 (+ a third pass after a shifted first pass).  `g1_ready`: S_G already holds
 // U^T U (the fused 3-term update computed it); each apply computes the next pass's Gram in the
@@ -437,6 +471,10 @@ int halo_exchange(rbl_ctx* ctx, const double* Q, const double** Qin, int64_t* of
 
 void free_run(rbl_ctx* ctx) {
   hipFree(ctx->d_basis); ctx->d_basis = nullptr;
+  hipFree(ctx->d_basis32); ctx->d_basis32 = nullptr;
+  hipFree(ctx->d_Qi64); ctx->d_Qi64 = nullptr;
+  hipFree(ctx->d_Qm64); ctx->d_Qm64 = nullptr;
+  ctx->basis_bits = 64;
   hipFree(ctx->d_U); ctx->d_U = nullptr;
   hipFree(ctx->d_T); ctx->d_T = nullptr;
   hipFree(ctx->d_qext); ctx->d_qext = nullptr;
@@ -820,13 +858,17 @@ int rbl_start(rbl_ctx* ctx, int b, int max_blocks, int basis_bits, const double*
   if (!ctx->d_rowptr) return fail(ctx, RBL_ERR_STATE, "rbl_start: no matrix");
   if (b < 1 || b > 64) return fail(ctx, RBL_ERR_INVALID, "block size must be in [1,64]");
   if (max_blocks < 1) return fail(ctx, RBL_ERR_INVALID, "max_blocks must be >= 1");
-  if (basis_bits != 64) return fail(ctx, RBL_ERR_INVALID, "only the fp64 basis is implemented");
+  if (basis_bits != 64 && basis_bits != 32)
+    return fail(ctx, RBL_ERR_INVALID, "basis_bits must be 64 or 32");
+  if (basis_bits == 32 && b != 16 && b != 32)
+    return fail(ctx, RBL_ERR_INVALID, "the fp32 basis needs b in {16, 32}");
   HIPC(hipSetDevice(ctx->device));
   HIPC(hipStreamSynchronize(ctx->stream));
   // a repeated run with the same shape reuses the HBM plan (allocating ~100 GB of basis
   // per run costs more than the run itself at n = 1e7)
-  const bool reuse = ctx->d_basis && ctx->b == b && ctx->max_blocks == max_blocks &&
-                     ctx->slot == ctx->nloc * b;
+  const bool reuse = (ctx->d_basis || ctx->d_basis32) && ctx->b == b &&
+                     ctx->max_blocks == max_blocks && ctx->slot == ctx->nloc * b &&
+                     ctx->basis_bits == basis_bits;
   if (reuse) {
     ctx->nblocks = 0;
     HIPC(hipMemsetAsync(ctx->d_flags, 0, 4 * sizeof(int), ctx->stream));
@@ -836,7 +878,14 @@ int rbl_start(rbl_ctx* ctx, int b, int max_blocks, int basis_bits, const double*
   ctx->max_blocks = max_blocks;
   ctx->slot = ctx->nloc * b;
   const int64_t nl = std::max<int64_t>(ctx->nloc, 1);
-  HIPC(hipMalloc(&ctx->d_basis, (size_t)(max_blocks + 1) * nl * b * sizeof(double)));
+  ctx->basis_bits = basis_bits;
+  if (basis_bits == 64) {
+    HIPC(hipMalloc(&ctx->d_basis, (size_t)(max_blocks + 1) * nl * b * sizeof(double)));
+  } else {
+    HIPC(hipMalloc(&ctx->d_basis32, (size_t)(max_blocks + 1) * nl * b * sizeof(float)));
+    HIPC(hipMalloc(&ctx->d_Qi64, (nl + kRowPad) * b * sizeof(double)));
+    HIPC(hipMalloc(&ctx->d_Qm64, (nl + kRowPad) * b * sizeof(double)));
+  }
   HIPC(hipMalloc(&ctx->d_U, (nl + kRowPad) * b * sizeof(double)));
   ctx->T_cols = b;
   HIPC(hipMalloc(&ctx->d_T, nl * b * sizeof(double)));
@@ -850,6 +899,8 @@ int rbl_start(rbl_ctx* ctx, int b, int max_blocks, int basis_bits, const double*
       slab = std::max(slab, sp * nW * b * xc);
     }
   slab = std::max(slab, (size_t)rowgram_grid(ctx->nloc) * b * b);  // rowop partials
+  if (basis_bits == 32)  // fp32 Grams: up to (max_blocks-1) panels x 2b per split
+    slab = std::max(slab, (size_t)gram32_splits(ctx->nloc) * std::max(1, max_blocks - 1) * b * 2 * b);
   ctx->slab_elems = slab;
   HIPC(hipMalloc(&ctx->d_slab, slab * sizeof(double)));
   ctx->C_elems = (size_t)std::max(1, max_blocks) * b * 2 * b;
@@ -862,7 +913,7 @@ int rbl_start(rbl_ctx* ctx, int b, int max_blocks, int basis_bits, const double*
 
   // Omega (row-major) in d_T
   if (omega) {
-    double* d_tmp = slotp(ctx, 1 <= max_blocks ? 1 : 0);
+    double* d_tmp = basis_bits == 64 ? slotp(ctx, 1 <= max_blocks ? 1 : 0) : ctx->d_Qm64;
     HIPC(hipMemcpyAsync(d_tmp, omega, ctx->nloc * b * sizeof(double), hipMemcpyHostToDevice,
                         ctx->stream));
     colmajor_to_rowmajor(d_tmp, ctx->nloc, b, ctx->d_T, ctx->stream);
@@ -878,7 +929,12 @@ int rbl_start(rbl_ctx* ctx, int b, int max_blocks, int basis_bits, const double*
     spmm(csr(ctx), Qin, off, b, ctx->d_U, nullptr, nullptr, ctx->spmm_variant, ctx->stream);
     HIPC(hipGetLastError());
   }
-  CHK(tsqr(ctx, ctx->d_U, slotp(ctx, 0)));
+  if (basis_bits == 64) {
+    CHK(tsqr(ctx, ctx->d_U, slotp(ctx, 0)));
+  } else {  // step 1 multiplies the unrounded fp64 Q_1 (RBL_gpu.jl:142, 152); the basis holds fp32
+    CHK(tsqr(ctx, ctx->d_U, ctx->d_Qi64));
+    cvt_f64_to_f32(ctx->d_Qi64, slotp32(ctx, 0), ctx->nloc * b, ctx->stream);
+  }
   HIPC(hipStreamSynchronize(ctx->stream));
   harvest_timers(ctx);
   int flags[4];
@@ -890,17 +946,45 @@ int rbl_start(rbl_ctx* ctx, int b, int max_blocks, int basis_bits, const double*
 
 int rbl_step(rbl_ctx* ctx, int i, int part_reorth, double* A_out, double* B_out) {
   if (!ctx) return RBL_ERR_INVALID;
-  if (!ctx->d_basis || ctx->nblocks < 1) return fail(ctx, RBL_ERR_STATE, "rbl_step before rbl_start");
+  if ((!ctx->d_basis && !ctx->d_basis32) || ctx->nblocks < 1) return fail(ctx, RBL_ERR_STATE, "rbl_step before rbl_start");
   if (i != ctx->nblocks) return fail(ctx, RBL_ERR_STATE, "rbl_step: i must equal the current block count");
   if (i > ctx->max_blocks) return fail(ctx, RBL_ERR_STATE, "rbl_step: basis full (max_blocks)");
   HIPC(hipSetDevice(ctx->device));
   const int b = ctx->b;
-  double* Qi = slotp(ctx, i - 1);
-  double* Qm = i >= 2 ? slotp(ctx, i - 2) : nullptr;
+  const bool f32 = ctx->basis_bits == 32;
+  double* Qi = f32 ? ctx->d_Qi64 : slotp(ctx, i - 1);
+  double* Qm = i >= 2 ? (f32 ? ctx->d_Qm64 : slotp(ctx, i - 2)) : nullptr;
   HIPC(hipMemsetAsync(ctx->d_flags, 0, 4 * sizeof(int), ctx->stream));
+  if (f32) {
+    // FLOAT = Float32: partial and local reorth on the fp32 blocks, then the
+    // current / previous block widened to fp64 (RBL_gpu.jl:164-174)
+    float* Qi32 = slotp32(ctx, i - 1);
+    float* Qm32 = i >= 2 ? slotp32(ctx, i - 2) : nullptr;
+    if (part_reorth && i >= 3) {
+      StageScope t(ctx, RBL_STAGE_PART_REORTH);
+      const int nW = i - 2;
+      if (ctx->reorth_order == 0) {
+        CHK(gram32(ctx, slotp32(ctx, 0), nW, Qi32, Qm32, 2, ctx->d_C));
+        CHK(upd32(ctx, slotp32(ctx, 0), nW, ctx->d_C, 2 * b, Qi32, Qm32, 2));
+      } else {
+        for (int j = 0; j < nW; ++j) {
+          CHK(gram32(ctx, slotp32(ctx, j), 1, Qi32, Qm32, 2, ctx->d_C));
+          CHK(upd32(ctx, slotp32(ctx, j), 1, ctx->d_C, 2 * b, Qi32, Qm32, 2));
+        }
+      }
+    }
+    if (i >= 2) {
+      StageScope t(ctx, RBL_STAGE_LOC_REORTH);
+      CHK(gram32(ctx, Qm32, 1, Qi32, nullptr, 1, ctx->d_C));
+      CHK(upd32(ctx, Qm32, 1, ctx->d_C, b, Qi32, nullptr, 1));
+      cvt_f32_to_f64(Qi32, ctx->d_Qi64, ctx->nloc * b, ctx->stream);
+      cvt_f32_to_f64(Qm32, ctx->d_Qm64, ctx->nloc * b, ctx->stream);
+      HIPC(hipGetLastError());
+    }
+  }
 
   // partial reorth of Q_i and Q_{i-1} against Q_1..Q_{i-2}   (RBL_gpu.jl:164-166, 59-81)
-  if (part_reorth && i >= 3) {
+  if (!f32 && part_reorth && i >= 3) {
     StageScope t(ctx, RBL_STAGE_PART_REORTH);
     const int nW = i - 2;
     if (ctx->reorth_order == 0) {  // block CGS: one Gram over every j, one update
@@ -921,7 +1005,7 @@ int rbl_step(rbl_ctx* ctx, int i, int part_reorth, double* A_out, double* B_out)
   }
   // local reorth: Q_i -= Q_{i-1} (Q_{i-1}^T Q_i), one projection (RBL_gpu.jl:83-93, P1)
   const bool fused = rowgram_ok(b);
-  if (i >= 2) {
+  if (!f32 && i >= 2) {
     StageScope t(ctx, RBL_STAGE_LOC_REORTH);
     CHK(gram(ctx, run1(Qm, b), pan1(Qi, b), ctx->d_C, nullptr));
     if (fused)
@@ -959,7 +1043,13 @@ int rbl_step(rbl_ctx* ctx, int i, int part_reorth, double* A_out, double* B_out)
       CHK(tsmm_checked(ctx, run1(Qi, b), smallp(ctx, S_AI), b, pan1(ctx->d_U, b), -1.0, 1.0, nullptr));
   }
   // Q_{i+1} B_{i+1} = qr(U)   (RBL_gpu.jl:180-184)
-  CHK(tsqr(ctx, ctx->d_U, slotp(ctx, i), fused));
+  if (!f32) {
+    CHK(tsqr(ctx, ctx->d_U, slotp(ctx, i), fused));
+  } else {  // Qg = FLOAT(Qg_d) (RBL_gpu.jl:182): the new block enters the basis rounded to fp32
+    CHK(tsqr(ctx, ctx->d_U, ctx->d_Qi64, fused));
+    cvt_f64_to_f32(ctx->d_Qi64, slotp32(ctx, i), ctx->nloc * b, ctx->stream);
+    HIPC(hipGetLastError());
+  }
   copy_small(smallp(ctx, S_RTOT), smallp(ctx, S_BPREV), (int64_t)b * b, ctx->stream);
   HIPC(hipMemcpyAsync(ctx->h_pin, smallp(ctx, S_AI), (size_t)b * b * sizeof(double),
                       hipMemcpyDeviceToHost, ctx->stream));
@@ -997,12 +1087,20 @@ int rbl_ritz(rbl_ctx* ctx, int nblocks, int k, const double* S, double* V_out) {
   colmajor_to_rowmajor(d_Scm, rows, k, d_S, ctx->stream);
   {
     StageScope t(ctx, RBL_STAGE_RITZ);
-    PanelRun X;
-    X.base = slotp(ctx, 0);
-    X.stride = ctx->slot;
-    X.count = nblocks;
-    X.w = b;
-    CHK(tsmm_checked(ctx, X, d_S, k, pan1(d_V, k), 1.0, 0.0, nullptr));
+    if (ctx->basis_bits == 64) {
+      PanelRun X;
+      X.base = slotp(ctx, 0);
+      X.stride = ctx->slot;
+      X.count = nblocks;
+      X.w = b;
+      CHK(tsmm_checked(ctx, X, d_S, k, pan1(d_V, k), 1.0, 0.0, nullptr));
+    } else {  // fp32 basis: each block widened to fp64, V accumulated in fp64 (P3: fp64 Ritz)
+      for (int j = 0; j < nblocks; ++j) {
+        cvt_f32_to_f64(slotp32(ctx, j), ctx->d_Qm64, ctx->nloc * b, ctx->stream);
+        CHK(tsmm_checked(ctx, run1(ctx->d_Qm64, b), d_S + (int64_t)j * b * k, k, pan1(d_V, k), 1.0,
+                         j == 0 ? 0.0 : 1.0, nullptr));
+      }
+    }
   }
   rowmajor_to_colmajor(d_V, ctx->nloc, k, d_Vcm, ctx->stream);
   if (V_out)
@@ -1021,7 +1119,12 @@ int rbl_get_block(rbl_ctx* ctx, int j, double* Q_out) {
   if (!ctx || j < 1 || j > ctx->nblocks || !Q_out) return fail(ctx, RBL_ERR_INVALID, "rbl_get_block: bad block");
   HIPC(hipSetDevice(ctx->device));
   const int b = ctx->b;
-  rowmajor_to_colmajor(slotp(ctx, j - 1), ctx->nloc, b, ctx->d_T, ctx->stream);
+  const double* src = slotp(ctx, j - 1);
+  if (ctx->basis_bits == 32) {  // fp32 slot, returned widened
+    cvt_f32_to_f64(slotp32(ctx, j - 1), ctx->d_Qm64, ctx->nloc * b, ctx->stream);
+    src = ctx->d_Qm64;
+  }
+  rowmajor_to_colmajor(src, ctx->nloc, b, ctx->d_T, ctx->stream);
   HIPC(hipMemcpyAsync(Q_out, ctx->d_T, ctx->nloc * b * sizeof(double), hipMemcpyDeviceToHost,
                       ctx->stream));
   HIPC(hipStreamSynchronize(ctx->stream));

@@ -1,0 +1,311 @@
+// reorth32.hip — the fp32 Krylov basis (mixed-precision mode, RBL_gpu.jl with
+// FLOAT = Float32: SURVEY P9): partial and local reorthogonalisation on fp32 blocks with
+// v_mfma_f32_16x16x4_f32 (exact f32 fma chains, 64 FLOP/clk/SIMD = 2x the fp64 MFMA rate,
+// half the bytes per basis element), and the fp32 <-> fp64 conversions between the basis and
+// the fp64 SpMM / 3-term / QR path (RBL_gpu.jl:172-174, 180-182: copyto! between Qg and Qg_d).
+//
+// v_mfma_f32_16x16x4_f32 (cdna_hip_programming.md 'FP32-input MFMA'): lane l holds
+//   A[i = l&15][k = l>>4], B[k = l>>4][j = l&15], D[row 4 (l>>4) + v][col l&15], v = reg 0..3.
+#include "kernels.hpp"
+
+namespace rbl {
+
+typedef float f4v __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f4v mfma16(float a, float b, f4v c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// ----------------------------------------------------------------------------------------
+// Gram C = W^T X (fp32 in, fp32 MFMA accumulation per split; splits summed in fp64 by
+// reduce_slab): one Krylov panel per wave, 4 waves per workgroup, X rows staged in LDS in
+// 16-row chunks.  X chunk image: column c of row r at r * 64 + 4 (c & 15) + (c >> 4), so one
+// ds_read_b128 hands a lane its B operand for all four 16-column tiles.
+// ----------------------------------------------------------------------------------------
+constexpr int kG32Waves = 4;
+constexpr int kG32Rows = 16;
+
+template <int W, int NX>
+__global__ __launch_bounds__(256) void k_gram32(int64_t nrows, const float* __restrict__ Wb,
+                                                int64_t wstride, int nW, const float* __restrict__ X0,
+                                                const float* __restrict__ X1, double* __restrict__ slab,
+                                                int npg, int64_t rows_per) {
+  constexpr int KC = NX * W;        // X columns
+  constexpr int CT = KC / 16;       // 16-column tiles of X (1..4)
+  constexpr int AT = W / 16;        // 16-column tiles of the panel (1..2)
+  __shared__ __attribute__((aligned(16))) float xs[2][kG32Rows * 64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int q = lane >> 4, c16 = lane & 15;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, t = bid >> 3;  // XCD-aware: a split's panel groups share an L2
+  const int pg = t % npg;
+  const int64_t s = (int64_t)(t / npg) * 8 + xcd;
+  const int64_t r_begin = s * rows_per;
+  const int64_t r_end = r_begin + rows_per < nrows ? r_begin + rows_per : nrows;
+  const int j = pg * kG32Waves + wave;
+  const bool active = j < nW;
+  const float* wp = Wb + (int64_t)(active ? j : 0) * wstride + c16;
+  const int64_t rlast = r_end > 0 ? r_end - 1 : 0;
+
+  f4v acc[AT][CT];
+#pragma unroll
+  for (int a = 0; a < AT; ++a)
+#pragma unroll
+    for (int c = 0; c < CT; ++c) acc[a][c] = f4v{0.f, 0.f, 0.f, 0.f};
+
+  // X staging: thread (row = tid / 16, cc = tid % 16) moves X[row][cc + 16 ct] (ct < CT)
+  const int xrow = tid >> 4, xcc = tid & 15;
+  auto load_x = [&](int64_t rc0, float (&xr)[CT]) {
+    const int64_t r = rc0 + xrow;
+    const int64_t rc = r < rlast ? r : rlast;
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) {
+      const int c = xcc + 16 * ct;
+      const float* src = (NX == 2 && c >= W) ? X1 + rc * W + (c - W) : X0 + rc * W + c;
+      xr[ct] = *src;
+    }
+  };
+  auto store_x = [&](int buf, int64_t rc0, const float (&xr)[CT]) {
+    const bool ok = rc0 + xrow < r_end;  // rows past the split meet zero X (clamped W rows)
+    float* d = &xs[buf][xrow * 64 + 4 * xcc];
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) d[ct] = ok ? xr[ct] : 0.f;
+  };
+  auto load_a = [&](int64_t rc0, float (&ar)[4][AT]) {
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const int64_t r = rc0 + 4 * ks + q;
+      const int64_t rc = r < rlast ? r : rlast;
+#pragma unroll
+      for (int a = 0; a < AT; ++a) ar[ks][a] = wp[rc * W + 16 * a];
+    }
+  };
+
+  const int64_t nchunks = r_end > r_begin ? (r_end - r_begin + kG32Rows - 1) / kG32Rows : 0;
+  float xr[CT];
+  float acur[4][AT], anext[4][AT];
+  if (nchunks > 0) {
+    load_x(r_begin, xr);
+    store_x(0, r_begin, xr);
+    load_a(r_begin, acur);
+  }
+  __syncthreads();
+  for (int64_t ch = 0; ch < nchunks; ++ch) {
+    const int64_t rc0 = r_begin + ch * kG32Rows;
+    load_x(rc0 + kG32Rows, xr);  // unconditional (clamped): see reorth.hip
+    load_a(rc0 + kG32Rows, anext);
+    if (active) {
+      const float* xb = xs[ch & 1] + 4 * c16;
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const f4v bv = *reinterpret_cast<const f4v*>(xb + (4 * ks + q) * 64);
+#pragma unroll
+        for (int a = 0; a < AT; ++a)
+#pragma unroll
+          for (int c = 0; c < CT; ++c) acc[a][c] = mfma16(acur[ks][a], bv[c], acc[a][c]);
+      }
+    }
+    store_x((int)((ch + 1) & 1), rc0 + kG32Rows, xr);
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+      for (int a = 0; a < AT; ++a) acur[ks][a] = anext[ks][a];
+    __syncthreads();
+  }
+  if (!active) return;
+  // D[a][c] tile (16 x 16): lane holds rows 4q + v, column c16 of the tile
+  double* out = slab + (s * (int64_t)nW * W + (int64_t)j * W) * KC;
+#pragma unroll
+  for (int a = 0; a < AT; ++a)
+#pragma unroll
+    for (int c = 0; c < CT; ++c)
+#pragma unroll
+      for (int v = 0; v < 4; ++v)
+        out[(int64_t)(16 * a + 4 * q + v) * KC + 16 * c + c16] = (double)acc[a][c][v];
+}
+
+int gram32_splits(int64_t nrows) {
+  int64_t s8 = 3 * window_grid() / 8;
+  const int64_t max_s8 = (nrows + 8 * 128 - 1) / (8 * 128);
+  if (s8 > max_s8) s8 = max_s8;
+  if (s8 < 1) s8 = 1;
+  return (int)(s8 * 8);
+}
+
+template <int W, int NX>
+static void launch_gram32(int64_t nrows, const float* Wb, int64_t wstride, int nW, const float* X0,
+                          const float* X1, double* slab, int splits, hipStream_t st) {
+  const int npg = (nW + kG32Waves - 1) / kG32Waves;
+  int64_t rows_per = (nrows + splits - 1) / splits;
+  rows_per = (rows_per + kG32Rows - 1) / kG32Rows * kG32Rows;
+  hipLaunchKernelGGL((k_gram32<W, NX>), dim3(npg * splits), dim3(256), 0, st, nrows, Wb, wstride,
+                     nW, X0, X1, slab, npg, rows_per);
+}
+
+void gram32_partial(int64_t nrows, const float* Wb, int64_t wstride, int nW, int w, const float* X0,
+                    const float* X1, int xcount, double* slab, int splits, hipStream_t st) {
+  if (w == 32) {
+    if (xcount == 2) return launch_gram32<32, 2>(nrows, Wb, wstride, nW, X0, X1, slab, splits, st);
+    return launch_gram32<32, 1>(nrows, Wb, wstride, nW, X0, X1, slab, splits, st);
+  }
+  if (xcount == 2) return launch_gram32<16, 2>(nrows, Wb, wstride, nW, X0, X1, slab, splits, st);
+  return launch_gram32<16, 1>(nrows, Wb, wstride, nW, X0, X1, slab, splits, st);
+}
+
+// ----------------------------------------------------------------------------------------
+// Y = beta Y + alpha X C (fp32): 4 waves x 32 rows per workgroup; C (fp64 Gram, rounded to
+// f32 as the reference's FLOAT temp) staged in LDS 16 k at a time as k * 64 + 4 (c & 15) +
+// (c >> 4); A operands one float4 per lane per row tile covering 4 k-steps (k permuted:
+// lane quarter q takes k = k0 + 4q + s in step s, matched on the C side).
+// ----------------------------------------------------------------------------------------
+constexpr int kT32Rows = 32;  // rows per wave
+constexpr int kT32K = 16;     // k per chunk
+
+template <int W, int KYP>
+__global__ __launch_bounds__(256) void k_tsmm32(int64_t nrows, const float* __restrict__ Xb,
+                                                int64_t xstride, int nX, const double* __restrict__ C,
+                                                int ldc, int KY, float* Y0, float* Y1, float alpha,
+                                                float beta) {
+  constexpr int CT = KYP / 16;
+  __shared__ __attribute__((aligned(16))) float cs[2][kT32K * 64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int q = lane >> 4, c16 = lane & 15;
+  const int64_t r0 = ((int64_t)blockIdx.x * 4 + wave) * kT32Rows;
+  const int K = nX * W;
+  const int nch = (K + kT32K - 1) / kT32K;
+
+  f4v acc[2][CT];
+#pragma unroll
+  for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+    for (int c = 0; c < CT; ++c) acc[rt][c] = f4v{0.f, 0.f, 0.f, 0.f};
+
+  int64_t arow[2];
+#pragma unroll
+  for (int rt = 0; rt < 2; ++rt) {
+    const int64_t r = r0 + 16 * rt + c16;
+    arow[rt] = r < nrows ? r : nrows - 1;
+  }
+  auto load_a = [&](int ch, f4v (&ar)[2]) {
+    const int k0 = ch * kT32K + 4 * q;
+    const int k = k0 < K ? k0 : K - 4;  // clamped: k past K meets zero C rows
+    const int pan = k / W, col = k - pan * W;
+    const float* xp = Xb + (int64_t)pan * xstride + col;
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt) ar[rt] = *reinterpret_cast<const f4v*>(xp + arow[rt] * W);
+  };
+  // C chunk: 16 x KYP; thread (k = tid / 16, cc = tid % 16) moves C[k][cc + 16 ct]
+  const int ck = tid >> 4, ccc = tid & 15;
+  auto load_c = [&](int ch, float (&cr)[CT]) {
+    const int k = ch * kT32K + ck;
+    const int kc = k < K ? k : K - 1;
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) {
+      const int c = ccc + 16 * ct;
+      const int cc = c < KY ? c : KY - 1;
+      const float v = (float)C[(int64_t)kc * ldc + cc];
+      cr[ct] = (k < K && c < KY) ? alpha * v : 0.f;
+    }
+  };
+  auto store_c = [&](int buf, const float (&cr)[CT]) {
+    float* d = &cs[buf][ck * 64 + 4 * ccc];
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) d[ct] = cr[ct];
+  };
+
+  f4v acur[2], anext[2];
+  float cr[CT];
+  load_c(0, cr);
+  store_c(0, cr);
+  load_a(0, acur);
+  __syncthreads();
+  for (int ch = 0; ch < nch; ++ch) {
+    load_c(ch + 1, cr);
+    load_a(ch + 1, anext);
+    const float* cb = cs[ch & 1] + 4 * c16;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const f4v bv = *reinterpret_cast<const f4v*>(cb + (4 * q + s) * 64);
+#pragma unroll
+      for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+        for (int c = 0; c < CT; ++c) acc[rt][c] = mfma16(acur[rt][s], bv[c], acc[rt][c]);
+    }
+    store_c((ch + 1) & 1, cr);
+    acur[0] = anext[0];
+    acur[1] = anext[1];
+    __syncthreads();
+  }
+  // D: lane holds rows 4q + v, column c16 of tile (rt, c): 64-B row segments
+#pragma unroll
+  for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+    for (int c = 0; c < CT; ++c) {
+      const int col = 16 * c + c16;
+      if (col >= KY) continue;
+      float* yp = col < W ? Y0 + col : Y1 + (col - W);
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int64_t r = r0 + 16 * rt + 4 * q + v;
+        if (r < nrows) {
+          float y = acc[rt][c][v];
+          if (beta != 0.f) y += beta * yp[r * W];
+          yp[r * W] = y;
+        }
+      }
+    }
+}
+
+template <int W, int KYP>
+static void launch_tsmm32(int64_t nrows, const float* Xb, int64_t xstride, int nX, const double* C,
+                          int ldc, int KY, float* Y0, float* Y1, float alpha, float beta,
+                          hipStream_t st) {
+  const int64_t wgs = (nrows + 4 * kT32Rows - 1) / (4 * kT32Rows);
+  hipLaunchKernelGGL((k_tsmm32<W, KYP>), dim3((unsigned)wgs), dim3(256), 0, st, nrows, Xb, xstride,
+                     nX, C, ldc, KY, Y0, Y1, alpha, beta);
+}
+
+void tsmm32(int64_t nrows, const float* Xb, int64_t xstride, int nX, int w, const double* C, int ldc,
+            float* Y0, float* Y1, int ycount, float alpha, float beta, hipStream_t st) {
+  if (nrows <= 0) return;
+  const int KY = ycount * w;
+  if (w == 32) {
+    if (KY <= 32) return launch_tsmm32<32, 32>(nrows, Xb, xstride, nX, C, ldc, KY, Y0, Y1, alpha, beta, st);
+    return launch_tsmm32<32, 64>(nrows, Xb, xstride, nX, C, ldc, KY, Y0, Y1, alpha, beta, st);
+  }
+  if (KY <= 16) return launch_tsmm32<16, 16>(nrows, Xb, xstride, nX, C, ldc, KY, Y0, Y1, alpha, beta, st);
+  return launch_tsmm32<16, 32>(nrows, Xb, xstride, nX, C, ldc, KY, Y0, Y1, alpha, beta, st);
+}
+
+// ---- conversions -------------------------------------------------------------------------
+__global__ void k_f32_to_f64(const float* __restrict__ src, double* __restrict__ dst, int64_t n) {
+  const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (i + 3 < n) {
+    const f4v v = *reinterpret_cast<const f4v*>(src + i);
+    *reinterpret_cast<d2v*>(dst + i) = d2v{v.x, v.y};
+    *reinterpret_cast<d2v*>(dst + i + 2) = d2v{v.z, v.w};
+  } else {
+    for (int64_t e = i; e < n; ++e) dst[e] = src[e];
+  }
+}
+__global__ void k_f64_to_f32(const double* __restrict__ src, float* __restrict__ dst, int64_t n) {
+  const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (i + 3 < n) {
+    const d2v a = *reinterpret_cast<const d2v*>(src + i), b = *reinterpret_cast<const d2v*>(src + i + 2);
+    *reinterpret_cast<f4v*>(dst + i) = f4v{(float)a.x, (float)a.y, (float)b.x, (float)b.y};
+  } else {
+    for (int64_t e = i; e < n; ++e) dst[e] = (float)src[e];
+  }
+}
+void cvt_f32_to_f64(const float* src, double* dst, int64_t n, hipStream_t s) {
+  if (n <= 0) return;
+  const int64_t thr = (n + 3) / 4;
+  hipLaunchKernelGGL(k_f32_to_f64, dim3((unsigned)((thr + 255) / 256)), dim3(256), 0, s, src, dst, n);
+}
+void cvt_f64_to_f32(const double* src, float* dst, int64_t n, hipStream_t s) {
+  if (n <= 0) return;
+  const int64_t thr = (n + 3) / 4;
+  hipLaunchKernelGGL(k_f64_to_f32, dim3((unsigned)((thr + 255) / 256)), dim3(256), 0, s, src, dst, n);
+}
+
+}  // namespace rbl

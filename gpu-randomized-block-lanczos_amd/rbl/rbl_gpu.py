@@ -160,11 +160,13 @@ class Context:
         return self._check(lib.rbl_spmm_kernel_for(self._h, b), "rbl_spmm_kernel_for")
 
     # -- Krylov run -------------------------------------------------------------------------
-    def start(self, b: int, max_blocks: int, omega=None, seed: int = 0) -> None:
+    def start(self, b: int, max_blocks: int, omega=None, seed: int = 0, basis_bits: int = 64) -> None:
+        """basis_bits 32: the mixed mode of RBL_gpu.jl with FLOAT = Float32 (fp32 Krylov blocks
+        and reorth, fp64 A*Q / 3-term / QR / Ritz)."""
         om = None
         if omega is not None:
             om = np.asfortranarray(omega, dtype=np.float64)
-        self._check(lib.rbl_start(self._h, b, max_blocks, 64, dptr(om), seed), "rbl_start")
+        self._check(lib.rbl_start(self._h, b, max_blocks, basis_bits, dptr(om), seed), "rbl_start")
         self.b = b
 
     def step(self, i: int, part_reorth: bool):
@@ -223,12 +225,12 @@ def max_steps_for(kryl_sz: int, b: int) -> int:
 
 def lanczos(ctx: Context, k: int, b: int, *, kryl_sz: int = KRYL_SZ_GPU, omega=None, seed=0,
             check: bool = True, max_steps: int | None = None, tol: float = RESIDUAL_TOL,
-            trace: bool = False, ritz: bool = True):
+            trace: bool = False, ritz: bool = True, basis_bits: int = 64):
     """RBL_gpu.jl:134-203 + :219 on an already-loaded context.  Returns (D, V_local, info)."""
     steps_cap = max_steps_for(kryl_sz, b)
     if max_steps is not None:
         steps_cap = min(steps_cap, max_steps)
-    ctx.start(b, steps_cap, omega=omega, seed=seed)
+    ctx.start(b, steps_cap, omega=omega, seed=seed, basis_bits=basis_bits)
     info = RBLInfo()
     T = TBand(b, steps_cap)
     D = np.zeros(0)
@@ -272,11 +274,12 @@ def lanczos(ctx: Context, k: int, b: int, *, kryl_sz: int = KRYL_SZ_GPU, omega=N
 
 
 def RBL_gpu(A, k: int, b: int, *, device: int = 0, kryl_sz: int = KRYL_SZ_GPU, omega=None,
-            seed: int = 0, reorth_order: int = 0, return_info: bool = False):
+            seed: int = 0, reorth_order: int = 0, return_info: bool = False, basis_bits: int = 64):
     """Drop-in for ``RBL_gpu(A::SparseMatrixCSC{Float64}, k, b)`` (RBL_gpu.jl:205):
     returns (D, V) — D the k largest-|lambda| eigenvalues (descending |lambda|), V n x k."""
     with Context(device) as ctx:
         ctx.set_matrix(A)
         ctx.set_option(_lib.RBL_OPT_REORTH_ORDER, reorth_order)
-        D, V, info = lanczos(ctx, k, b, kryl_sz=kryl_sz, omega=omega, seed=seed)
+        D, V, info = lanczos(ctx, k, b, kryl_sz=kryl_sz, omega=omega, seed=seed,
+                             basis_bits=basis_bits)
     return (D, V, info) if return_info else (D, V)

@@ -113,7 +113,10 @@ int rbl_spmm_kernel_for(rbl_ctx* ctx, int b);
  * rbl_start replaces RBL_gpu.jl:213-214 (`Qg_d = CUDA.randn(n,b); Qg_d = qr(Ag*Qg_d).Q`)
  * and the buffer planning of RBL_gpu.jl:95-104 (the whole basis lives in HBM).
  * `omega` is the local n_local x b column-major start block, or NULL for a device
- * counter-based N(0,1) draw from `seed`.  basis_bits: 64 (fp64 basis). */
+ * counter-based N(0,1) draw from `seed`.  basis_bits: 64 (fp64 basis) or 32 (the mixed
+ * mode of RBL_gpu.jl with FLOAT = Float32, b in {16, 32}: Krylov blocks and their partial /
+ * local reorthogonalisation in fp32 on fp32 MFMA; A Q, the 3-term update, QR, A_i, B_i and
+ * the Ritz projection in fp64 from the widened blocks). */
 int rbl_start(rbl_ctx* ctx, int b, int max_blocks, int basis_bits, const double* omega,
               uint64_t seed);
 /* One block Lanczos step i (1-based) — RBL_gpu.jl:149-161 for i == 1 and :163-184 for

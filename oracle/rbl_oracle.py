@@ -216,6 +216,82 @@ def RBL_gpu_semantics(A, k, b, **kw) -> OracleResult:
 # ----------------------------------------------------------------------------------------
 # Known-answer generators — Julia/Unit Testing/test.jl:16-50
 # ----------------------------------------------------------------------------------------
+def RBL_gpu_mixed(A, k: int, b: int, *, omega, kryl_sz=KRYL_SZ_GPU, qr_mode="posdiag",
+                  reorth_mode="mgs", check=True, max_steps=None, trace=False) -> OracleResult:
+    """RBL_gpu.jl:134-219 with FLOAT = Float32, DOUBLE = Float64: the GPU driver's
+    mixed mode.  The Krylov blocks (Qg, Qg1, Qgpu) and their partial / local reorth are fp32
+    (NumPy float32 GEMMs, as CUBLAS sgemm); A*Q, the 3-term update, A_i, QR and T are fp64
+    on the widened blocks (copyto! Qg_d <- Qg, :172-173); each QR output enters the basis
+    rounded to fp32 (:180-182).  Ritz vectors in fp64 from the fp32 blocks (P3: fp64 Ritz).
+    """
+    f32 = np.float32
+    Qg_d, _ = _qr(A @ np.asarray(omega, dtype=np.float64), qr_mode)      # :213-214
+    Qg = Qg_d.astype(f32)                                                 # :142
+    Qgpu = [Qg.copy()]                                                    # :149-151
+    tr = {"A": [], "B": []} if trace else None
+    U = A @ Qg_d                                                          # :152
+    Ai = Qg_d.T @ U                                                       # :153
+    U -= Qg_d @ Ai                                                        # :154
+    Qn, Bi = _qr(U, qr_mode)                                              # :155, 159
+    Qg1 = Qg_d.astype(f32)                                                # :156
+    Qg_d = Qn
+    Qg = Qg_d.astype(f32)                                                 # :157-158
+    if tr is not None:
+        tr["A"].append(Ai.copy()); tr["B"].append(Bi.copy())
+    T = insertA(Ai, b)                                                    # :160
+    insertB(Bi, T, b, 1)                                                  # :161
+    D = np.zeros(0); S = np.zeros((0, 0))
+    converged = False
+    i = 1
+    while i * b < kryl_sz:                                                # :162
+        if max_steps is not None and i >= max_steps:
+            break
+        i += 1
+        if i % 2 == 0 and i >= 3:                                         # :164-166, 59-81
+            if reorth_mode == "mgs":
+                for j in range(i - 2):
+                    Wj = Qgpu[j]
+                    Qg -= Wj @ (Wj.T @ Qg)
+                    Qg1 -= Wj @ (Wj.T @ Qg1)
+            else:
+                W = np.hstack(Qgpu[: i - 2])
+                X = np.hstack([Qg, Qg1])
+                X -= W @ (W.T @ X)
+                Qg[:] = X[:, :b]
+                Qg1[:] = X[:, b:]
+            Qgpu[i - 2] = Qg1.copy()                                      # :76, 78
+        Qg -= Qg1 @ (Qg1.T @ Qg)                                          # :167, 83-93 (P1)
+        Qgpu.append(Qg.copy())                                            # :168-172
+        Qg_d = Qg.astype(np.float64)                                      # :173
+        Qg1_d = Qg1.astype(np.float64)                                    # :174
+        U = A @ Qg_d                                                      # :176
+        U -= Qg1_d @ Bi.T                                                 # :177
+        Ai = Qg_d.T @ U                                                   # :178
+        U -= Qg_d @ Ai                                                    # :179
+        Qn, Bi = _qr(U, qr_mode)                                          # :180, 184
+        Qg1 = Qg_d.astype(f32)                                            # :181
+        Qg_d = Qn
+        Qg = Qg_d.astype(f32)                                             # :182-183
+        if tr is not None:
+            tr["A"].append(Ai.copy()); tr["B"].append(Bi.copy())
+        T = np.hstack([T, insertA(Ai, b)])                                # :185
+        if check and (i * b > k) and (i % 4 == 0):                       # :186
+            D, S = dsbev(T)
+            D, S = sort_eig_abs(D, S, k)
+            if check_convergence(Bi, S, b, k, RESIDUAL_TOL):
+                converged = True
+                break
+        insertB(Bi, T, b, i)                                              # :193
+    D = D[::-1].copy()
+    S = S[:, ::-1].copy()
+    Qlist = [q.astype(np.float64) for q in Qgpu]
+    V = recover_eigvec(Qlist, S, k) if S.size else np.zeros((A.shape[0], 0))
+    if tr is not None:
+        tr["T"] = T
+        tr["S"] = S
+    return OracleResult(D, V, i, len(Qgpu), converged, tr)
+
+
 def moderate_decay_matrix(n: int, k: int):
     """test.jl:17-28 — a_i = i(i+1)/2; expected a[n], a[n-1], ..."""
     a = np.cumsum(np.arange(1, n + 1, dtype=np.float64))

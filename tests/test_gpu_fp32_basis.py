@@ -1,0 +1,109 @@
+"""GPU parity of the fp32-basis (mixed-precision) mode — RBL_gpu.jl with FLOAT = Float32,
+DOUBLE = Float64 (BASELINE config 5) — against the oracle's restatement of that
+mode (oracle.rbl_oracle.RBL_gpu_mixed) on the same inputs.
+
+Tolerances (stated here; the fp32 basis changes the arithmetic, not the algorithm):
+  * per-step A_i, B_{i+1} vs the mixed oracle: absolute 2e-6 * ||A||_1 over the first steps.
+    The fp32 reorth rounds in a different order (f32 MFMA partials summed in fp64 vs sgemm),
+    so each block carries O(eps32) = 6e-8 differences that A multiplies into U: entries of
+    A_i / B_{i+1} move by O(eps32 ||A||), whatever their own size;
+  * converged eigenvalues vs the mixed oracle: relative 1e-7; vs the fp64 oracle: 1e-6;
+  * Ritz residual ||A v - lambda v|| / |lambda| < 1e-5 (fp32 basis vectors);
+  * every stored basis block is exactly fp32-representable (the basis IS fp32).
+"""
+import numpy as np
+import pytest
+
+from oracle import matgen
+from oracle import rbl_oracle as o
+
+pytestmark = pytest.mark.gpu
+
+STEP_TOL = 2e-6  # x ||A||_1, absolute
+EIG_TOL_MIXED = 1e-7
+EIG_TOL_F64 = 1e-6
+RES_TOL = 1e-5
+
+
+@pytest.fixture(scope="module")
+def rbl():
+    import rbl as _r
+    return _r
+
+
+def c1_matrix(n, k, W=64, seed=20261015):
+    p = min(1.0, 0.01 * n / (2 * W)) if n <= 2 * W * 100 else 0.7734
+    return matgen.hashwindow_csr(n, W, p, seed, matgen.planted_spectrum(k))
+
+
+@pytest.mark.parametrize("b", [16, 32])
+def test_first_steps_trace_fp32(rbl, b):
+    A = c1_matrix(4000, 10)
+    n = A.shape[0]
+    omega = np.random.default_rng(b).standard_normal((n, b))
+    steps = 6
+    ref = o.RBL_gpu_mixed(A, 10, b, omega=omega, reorth_mode="cgs", check=False,
+                          max_steps=steps, trace=True)
+    with rbl.Context(0) as ctx:
+        ctx.set_matrix(A)
+        _, _, info = rbl.lanczos(ctx, 10, b, omega=omega, check=False, max_steps=steps,
+                                 trace=True, ritz=False, basis_bits=32)
+        blocks = [ctx.get_block(j) for j in range(1, steps + 1)]
+    anorm = abs(A).sum(axis=0).max()
+    for i in range(steps):
+        Ar, Br = ref.trace["A"][i], ref.trace["B"][i]
+        Ag, Bg = info.trace_A[i], info.trace_B[i]
+        assert np.abs(Ag - Ar).max() <= STEP_TOL * anorm, (i, np.abs(Ag - Ar).max(), anorm)
+        assert np.abs(Bg - Br).max() <= STEP_TOL * anorm, (i, np.abs(Bg - Br).max(), anorm)
+    for Q in blocks:  # the basis is fp32: widening its values is exact
+        assert np.array_equal(Q, Q.astype(np.float32).astype(np.float64))
+
+
+@pytest.mark.parametrize("order,b", [(0, 16), (1, 16), (0, 32)])
+def test_eigenpairs_fp32_basis(rbl, order, b):
+    k = 10
+    A = c1_matrix(10000, k)
+    n = A.shape[0]
+    omega = np.random.default_rng(7).standard_normal((n, b))
+    mode = "cgs" if order == 0 else "mgs"
+    ref = o.RBL_gpu_mixed(A, k, b, omega=omega, reorth_mode=mode)
+    ref64 = o.RBL_gpu_semantics(A, k, b, omega=omega, qr_mode="posdiag", reorth_mode=mode)
+    D, V, info = rbl.RBL_gpu(A, k, b, omega=omega, reorth_order=order, return_info=True,
+                             basis_bits=32)
+    assert ref.converged and info.converged
+    assert np.all(np.abs(D - ref.D) <= EIG_TOL_MIXED * np.abs(ref.D)), np.abs(D - ref.D) / np.abs(ref.D)
+    assert np.all(np.abs(D - ref64.D) <= EIG_TOL_F64 * np.abs(ref64.D))
+    R = A @ V - V * D[None, :]
+    res = np.linalg.norm(R, axis=0) / np.abs(D)
+    assert res.max() < RES_TOL, res
+
+
+def test_fp32_basis_multirank_matches_single(rbl):
+    """Three in-process ranks (row-partitioned, halo + all-reduce) give the single-rank fp32 run."""
+    from test_gpu_multirank import run_ranks
+    k, b = 10, 16
+    A = c1_matrix(8000, k)
+    n = A.shape[0]
+    omega = np.random.default_rng(3).standard_normal((n, b))
+    D1, V1, info1 = rbl.RBL_gpu(A, k, b, omega=omega, return_info=True, basis_bits=32)
+
+    def fn(ctx, r):
+        ctx.set_matrix(A)
+        _, r0, r1, _ = ctx.matrix_info()
+        D, V, info = rbl.lanczos(ctx, k, b, omega=omega[r0:r1], basis_bits=32)
+        return D, V, info
+
+    parts = run_ranks(rbl, 3, fn)
+    for D, _, info in parts:
+        assert info.converged and info.iters == info1.iters
+        assert np.all(np.abs(D - D1) <= EIG_TOL_MIXED * np.abs(D1))
+    V = np.vstack([p[1] for p in parts])
+    assert np.all(1 - np.abs(np.sum(V * V1, axis=0)) < 1e-6)
+
+
+def test_fp32_basis_rejects_other_b(rbl):
+    A = c1_matrix(2000, 4)
+    with rbl.Context(0) as ctx:
+        ctx.set_matrix(A)
+        with pytest.raises(rbl.RBLError):
+            ctx.start(8, 4, seed=1, basis_bits=32)
