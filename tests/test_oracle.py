@@ -79,3 +79,19 @@ def test_posdiag_qr_gives_same_eigenvalues():
     r1 = o.RBL(A, 5, 5, seed=11, qr_mode="householder")
     r2 = o.RBL(A, 5, 5, seed=11, qr_mode="posdiag")
     assert np.allclose(r1.D, r2.D, rtol=1e-13)
+
+
+def test_mixed_mode_oracle_tracks_fp64():
+    """RBL_gpu_mixed (FLOAT = Float32 GPU semantics) against the fp64 restatement on
+    a planted-spectrum matrix: the fp32 basis moves converged eigenvalues by ~1e-9 relative
+    here; the bound asserted is 1e-6 (the GPU fp32-basis parity tests use the same bound)."""
+    from oracle import matgen
+    k, b = 10, 16
+    A = matgen.hashwindow_csr(3000, 64, 0.3, 5, matgen.planted_spectrum(k))
+    omega = np.random.default_rng(2).standard_normal((A.shape[0], b))
+    r64 = o.RBL_gpu_semantics(A, k, b, omega=omega, qr_mode="posdiag")
+    r32 = o.RBL_gpu_mixed(A, k, b, omega=omega)
+    assert r64.converged and r32.converged
+    assert np.max(np.abs(r32.D - r64.D) / np.abs(r64.D)) < 1e-6
+    res = np.linalg.norm(A @ r32.V - r32.V * r32.D[None, :], axis=0) / np.abs(r32.D)
+    assert res.max() < 1e-5
