@@ -140,6 +140,8 @@ void chol_step(const double* G, int b, int64_t nglobal, int mode, double* R, dou
                double* Rtot, int* need3, int* status, const int* skip, hipStream_t s);
 // dst = src (b x b), used to stash B_i for the next step's epilogue.
 void copy_small(const double* src, double* dst, int64_t len, hipStream_t s);
+// dst = src^T (b x b row-major).
+void transpose_small(const double* src, double* dst, int b, hipStream_t s);
 
 // --- gen.hip ---------------------------------------------------------------------------
 // Hash-window matrix rows [r0,r1): counts per row, then fill given rowptr (0-based, local).

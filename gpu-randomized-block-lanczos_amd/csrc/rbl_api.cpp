@@ -37,6 +37,13 @@ struct rbl_ctx {
   int64_t* d_tcmax = nullptr;
   int64_t* d_tinfo = nullptr;
   uint16_t* d_bpos = nullptr;  // band kernel: per-nonzero dense-tile positions
+  // dense A (RBL_gpu(A::Matrix{Float64})): local rows in 32-column row-major panels
+  // (panel p = columns [32p, 32p+32), zero past n), multiplied by tsmm44 against d_qfull
+  // (all n rows of Q, zero-padded to 32 * dense_panels rows, b <= 64 columns)
+  bool dense = false;
+  double* d_dense = nullptr;
+  int64_t dense_panels = 0;
+  double* d_qfull = nullptr;
   int64_t ntiles = 0, tiles_per_wg = 0;
   bool window_ok16 = false, window_ok32 = false;
   bool band_ok16 = false, band_ok32 = false;
@@ -340,7 +347,7 @@ Panels pan2(const double* p0, const double* p1, int w) {
 }
 
 // small-buffer carve (b x b each)
-enum { S_R = 0, S_RINV, S_RTOT, S_BPREV, S_AI, S_G, S_NSMALL };
+enum { S_R = 0, S_RINV, S_RTOT, S_BPREV, S_AI, S_G, S_BT, S_NSMALL };
 double* smallp(rbl_ctx* ctx, int which) { return ctx->d_small + (int64_t)which * ctx->b * ctx->b; }
 
 int tsmm_checked(rbl_ctx* ctx, const PanelRun& X, const double* C, int ldc, const Panels& Y,
@@ -365,6 +372,32 @@ int rowop(rbl_ctx* ctx, const double* X, const double* C, double* Y, double alph
   reduce_slab(ctx->d_slab, grid, (int64_t)b * b, G, skip, ctx->stream);
   HIPC(hipGetLastError());
   return allreduce(ctx, G, (size_t)b * b);
+}
+
+bool has_matrix(const rbl_ctx* ctx) { return ctx->d_rowptr || ctx->dense; }
+
+// U = A Qin (+ U -= Qprev Bi^T when Qprev): the SpMM of RBL_gpu.jl:176-177, or for a dense
+// A (RBL_gpu.jl:205 with A::Matrix) the panel GEMM on fp64 MFMA (tsmm44 over the panels of
+// the local rows, Q gathered to all n rows by the halo exchange).  Returns the number of
+// A_i partials the band kernel formed in `slab` (0: none), or a negative status.
+int apply_A(rbl_ctx* ctx, const double* Qin, int64_t off, int b, double* U, const double* Qprev,
+            const double* Bi, double* slab) {
+  if (ctx->nloc <= 0) return 0;
+  if (!ctx->dense)
+    return spmm(csr(ctx), Qin, off, b, U, Qprev, Bi, ctx->spmm_variant, ctx->stream, slab);
+  HIPC(hipMemcpyAsync(ctx->d_qfull, Qin + (0 - off) * b, ctx->n * b * sizeof(double),
+                      hipMemcpyDeviceToDevice, ctx->stream));
+  PanelRun X;
+  X.base = ctx->d_dense;
+  X.stride = ctx->nloc * 32;
+  X.w = 32;
+  X.count = (int)ctx->dense_panels;
+  CHK(tsmm_checked(ctx, X, ctx->d_qfull, b, pan1(U, b), 1.0, 0.0, nullptr));
+  if (Qprev) {
+    transpose_small(Bi, smallp(ctx, S_BT), b, ctx->stream);
+    CHK(tsmm_checked(ctx, run1(Qprev, b), smallp(ctx, S_BT), b, pan1(U, b), -1.0, 1.0, nullptr));
+  }
+  return 0;
 }
 
 // fp32 basis: Gram C = W^T [X0, X1] over all ranks (fp32 MFMA per split, fp64 sum), C fp64
@@ -497,6 +530,10 @@ void free_matrix(rbl_ctx* ctx) {
   hipFree(ctx->d_tcmax); ctx->d_tcmax = nullptr;
   hipFree(ctx->d_tinfo); ctx->d_tinfo = nullptr;
   hipFree(ctx->d_bpos); ctx->d_bpos = nullptr;
+  hipFree(ctx->d_dense); ctx->d_dense = nullptr;
+  hipFree(ctx->d_qfull); ctx->d_qfull = nullptr;
+  ctx->dense = false;
+  ctx->dense_panels = 0;
   ctx->n = ctx->nloc = ctx->nnz = 0;
   ctx->ntiles = ctx->tiles_per_wg = 0;
   ctx->window_ok16 = ctx->window_ok32 = false;
@@ -726,6 +763,66 @@ int rbl_set_matrix_csr_rows(rbl_ctx* ctx, int64_t n, int64_t row_begin, int64_t 
   return upload_csr(ctx, n, row_begin, row_end, rowptr, colind, val, index_base, index_base);
 }
 
+int rbl_set_matrix_dense(rbl_ctx* ctx, int64_t n, int64_t row_begin, int64_t row_end,
+                         const double* A, int64_t lda) {
+  if (!ctx || n < 1 || row_begin < 0 || row_end < row_begin || row_end > n || !A ||
+      lda < row_end - row_begin || lda < 1)
+    return fail(ctx, RBL_ERR_INVALID, "rbl_set_matrix_dense: bad arguments");
+  HIPC(hipSetDevice(ctx->device));
+  free_run(ctx);
+  free_matrix(ctx);
+  ctx->bounds.assign(ctx->nranks + 1, 0);
+  if (ctx->nranks > 1) {  // the row slices must tile [0, n) in rank order
+    int64_t mine[2] = {row_begin, row_end};
+    std::vector<int64_t> all(2 * ctx->nranks);
+    COMMC(ctx->comm->allgather_host(mine, all.data(), 2, ctx->stream, &ctx->err));
+    for (int p = 0; p < ctx->nranks; ++p) {
+      if (all[2 * p] != (p == 0 ? 0 : all[2 * p - 1]))
+        return fail(ctx, RBL_ERR_INVALID, "row slices must tile [0,n) in rank order");
+      ctx->bounds[p + 1] = all[2 * p + 1];
+    }
+    if (ctx->bounds[ctx->nranks] != n) return fail(ctx, RBL_ERR_INVALID, "row slices != n");
+  } else {
+    if (row_begin != 0 || row_end != n) return fail(ctx, RBL_ERR_INVALID, "one rank holds all rows");
+    ctx->bounds[1] = n;
+  }
+  const int64_t m = row_end - row_begin;
+  ctx->n = n;
+  ctx->r0 = row_begin;
+  ctx->r1 = row_end;
+  ctx->nloc = m;
+  ctx->nnz = m * n;
+  ctx->dense = true;
+  ctx->dense_panels = (n + 31) / 32;
+  const int64_t P = ctx->dense_panels;
+  const int64_t ml = std::max<int64_t>(m, 1);
+  HIPC(hipMalloc(&ctx->d_dense, (size_t)P * ml * 32 * sizeof(double)));
+  HIPC(hipMalloc(&ctx->d_qfull, (size_t)P * 32 * 64 * sizeof(double)));
+  HIPC(hipMemsetAsync(ctx->d_qfull, 0, (size_t)P * 32 * 64 * sizeof(double), ctx->stream));
+  // column-major slice -> row-major 32-column panels, one panel at a time through a scratch
+  double* d_tmp = nullptr;
+  HIPC(hipMalloc(&d_tmp, (size_t)ml * 32 * sizeof(double)));
+  for (int64_t p = 0; p < P && m > 0; ++p) {
+    const int64_t c0 = 32 * p, nc = std::min<int64_t>(32, n - c0);
+    if (nc < 32) HIPC(hipMemsetAsync(d_tmp, 0, (size_t)m * 32 * sizeof(double), ctx->stream));
+    HIPC(hipMemcpy2DAsync(d_tmp, m * sizeof(double), A + c0 * lda, lda * sizeof(double),
+                          m * sizeof(double), nc, hipMemcpyHostToDevice, ctx->stream));
+    colmajor_to_rowmajor(d_tmp, m, 32, ctx->d_dense + p * m * 32, ctx->stream);
+  }
+  HIPC(hipGetLastError());
+  HIPC(hipStreamSynchronize(ctx->stream));
+  hipFree(d_tmp);
+  // every rank needs all n rows of Q
+  const int Pr = ctx->nranks;
+  ctx->need_lo.assign(Pr, 0);
+  ctx->need_hi.assign(Pr, 0);
+  for (int q = 0; q < Pr; ++q) {
+    ctx->need_lo[q] = ctx->bounds[q];
+    ctx->need_hi[q] = ctx->bounds[q + 1];
+  }
+  return setup_halo(ctx);
+}
+
 int rbl_gen_matrix_hashwindow(rbl_ctx* ctx, int64_t n, int64_t halfwidth, double density,
                               uint64_t seed, int nplant, const double* plant) {
   if (!ctx || n < 1 || halfwidth < 0 || nplant < 0 || (nplant > 0 && !plant) || n > INT32_MAX)
@@ -792,7 +889,8 @@ int rbl_matrix_info(rbl_ctx* ctx, int64_t* n, int64_t* row_begin, int64_t* row_e
 }
 
 int rbl_get_matrix_csr(rbl_ctx* ctx, int64_t* rowptr, int32_t* colind, double* val) {
-  if (!ctx || !ctx->d_rowptr) return fail(ctx, RBL_ERR_STATE, "no matrix");
+  if (!ctx || !ctx->d_rowptr)
+    return fail(ctx, RBL_ERR_STATE, ctx && ctx->dense ? "dense matrix: no CSR" : "no matrix");
   HIPC(hipSetDevice(ctx->device));
   if (rowptr)
     HIPC(hipMemcpy(rowptr, ctx->d_rowptr, (ctx->nloc + 1) * sizeof(int64_t), hipMemcpyDeviceToHost));
@@ -804,7 +902,8 @@ int rbl_get_matrix_csr(rbl_ctx* ctx, int64_t* rowptr, int32_t* colind, double* v
 }
 
 int rbl_spmm_kernel_for(rbl_ctx* ctx, int b) {
-  if (!ctx || !ctx->d_rowptr) return RBL_ERR_INVALID;
+  if (!ctx || !has_matrix(ctx)) return RBL_ERR_INVALID;
+  if (ctx->dense) return 4;
   if (ctx->spmm_variant == 1) return 1;
   const int v = ctx->spmm_variant;
   const bool band = ctx->ntiles > 0 && ((b == 16 && ctx->band_ok16) || (b == 32 && ctx->band_ok32));
@@ -816,7 +915,7 @@ int rbl_spmm_kernel_for(rbl_ctx* ctx, int b) {
 
 int rbl_apply(rbl_ctx* ctx, int b, const double* X, double* Y) {
   if (!ctx || b < 1 || b > 64 || !X || !Y) return fail(ctx, RBL_ERR_INVALID, "rbl_apply: bad arguments");
-  if (!ctx->d_rowptr) return fail(ctx, RBL_ERR_STATE, "rbl_apply: no matrix");
+  if (!has_matrix(ctx)) return fail(ctx, RBL_ERR_STATE, "rbl_apply: no matrix");
   if (ctx->b != 0 && ctx->b != b && ctx->nranks > 1)
     return fail(ctx, RBL_ERR_STATE, "rbl_apply: b differs from the running Krylov block size");
   HIPC(hipSetDevice(ctx->device));
@@ -840,7 +939,10 @@ int rbl_apply(rbl_ctx* ctx, int b, const double* X, double* Y) {
     ctx->b = keep_b;
     if (st < 0) return st;
   }
-  spmm(csr(ctx), Qin, off, b, d_y, nullptr, nullptr, ctx->spmm_variant, ctx->stream);
+  {
+    const int st = apply_A(ctx, Qin, off, b, d_y, nullptr, nullptr, nullptr);
+    if (st < 0) return st;
+  }
   HIPC(hipGetLastError());
   rowmajor_to_colmajor(d_y, ctx->nloc, b, d_x, ctx->stream);
   HIPC(hipMemcpyAsync(Y, d_x, ctx->nloc * b * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
@@ -855,7 +957,8 @@ int rbl_apply(rbl_ctx* ctx, int b, const double* X, double* Y) {
 int rbl_start(rbl_ctx* ctx, int b, int max_blocks, int basis_bits, const double* omega,
               uint64_t seed) {
   if (!ctx) return RBL_ERR_INVALID;
-  if (!ctx->d_rowptr) return fail(ctx, RBL_ERR_STATE, "rbl_start: no matrix");
+  if (!has_matrix(ctx)) return fail(ctx, RBL_ERR_STATE, "rbl_start: no matrix");
+  if (ctx->dense && b > 64) return fail(ctx, RBL_ERR_INVALID, "dense A: b <= 64");
   if (b < 1 || b > 64) return fail(ctx, RBL_ERR_INVALID, "block size must be in [1,64]");
   if (max_blocks < 1) return fail(ctx, RBL_ERR_INVALID, "max_blocks must be >= 1");
   if (basis_bits != 64 && basis_bits != 32)
@@ -926,7 +1029,7 @@ int rbl_start(rbl_ctx* ctx, int b, int max_blocks, int basis_bits, const double*
   CHK(halo_exchange(ctx, ctx->d_T, &Qin, &off));
   {
     StageScope t(ctx, RBL_STAGE_AQ);
-    spmm(csr(ctx), Qin, off, b, ctx->d_U, nullptr, nullptr, ctx->spmm_variant, ctx->stream);
+    CHK(apply_A(ctx, Qin, off, b, ctx->d_U, nullptr, nullptr, nullptr));
     HIPC(hipGetLastError());
   }
   if (basis_bits == 64) {
@@ -1021,9 +1124,9 @@ int rbl_step(rbl_ctx* ctx, int i, int part_reorth, double* A_out, double* B_out)
     CHK(halo_exchange(ctx, Qi, &Qin, &off));
     StageScope t(ctx, RBL_STAGE_AQ);
     // the band kernel can also form the partials of A_i = Q_i^T U while U is in registers
-    if (ctx->nloc > 0)
-      ai_parts = spmm(csr(ctx), Qin, off, b, ctx->d_U, Qm, i >= 2 ? smallp(ctx, S_BPREV) : nullptr,
-                      ctx->spmm_variant, ctx->stream, ctx->d_slab);
+    ai_parts = apply_A(ctx, Qin, off, b, ctx->d_U, Qm, i >= 2 ? smallp(ctx, S_BPREV) : nullptr,
+                       ctx->d_slab);
+    if (ai_parts < 0) return ai_parts;
     HIPC(hipGetLastError());
   }
   // A_i = Q_i^T U ; U -= Q_i A_i   (RBL_gpu.jl:178-179); fused: the update pass also forms

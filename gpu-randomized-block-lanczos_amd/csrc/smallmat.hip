@@ -133,4 +133,12 @@ void copy_small(const double* src, double* dst, int64_t len, hipStream_t s) {
   hipLaunchKernelGGL(k_copy, dim3((unsigned)((len + 255) / 256)), dim3(256), 0, s, src, dst, len);
 }
 
+// dst = src^T (b x b row-major): B_i^T for the dense path's 3-term epilogue
+__global__ void k_transpose_small(const double* __restrict__ src, double* __restrict__ dst, int b) {
+  for (int e = threadIdx.x; e < b * b; e += blockDim.x) dst[(e % b) * b + e / b] = src[e];
+}
+void transpose_small(const double* src, double* dst, int b, hipStream_t s) {
+  hipLaunchKernelGGL(k_transpose_small, dim3(1), dim3(256), 0, s, src, dst, b);
+}
+
 }  // namespace rbl

@@ -105,8 +105,18 @@ class Context:
 
     # -- matrix ---------------------------------------------------------------------------
     def set_matrix(self, A) -> None:
-        """Upload a symmetric sparse matrix (any SciPy format). CSC arrays are passed as-is
-        (Julia SparseMatrixCSC layout, RBL_gpu.jl:209); symmetry makes them the CSR arrays."""
+        """Upload a symmetric matrix: a SciPy sparse matrix (any format; CSC arrays passed
+        as-is — Julia SparseMatrixCSC layout, RBL_gpu.jl:209 — symmetry makes them the CSR
+        arrays), or a dense NumPy array (RBL_gpu(A::Matrix{Float64}): panel GEMM on fp64 MFMA;
+        with several ranks each keeps the rows of the even split)."""
+        if isinstance(A, np.ndarray):
+            n = A.shape[0]
+            if A.ndim != 2 or A.shape[1] != n:
+                raise ValueError("dense A must be square")
+            P, r = self.nranks, self.rank
+            r0, r1 = (n * r) // P, (n * (r + 1)) // P
+            self.set_matrix_dense_rows(n, r0, r1, A[r0:r1])
+            return
         A = sp.csc_matrix(A)
         A.sort_indices()
         n = A.shape[1]
@@ -115,6 +125,14 @@ class Context:
         nzval = A.data.astype(np.float64)
         self._check(lib.rbl_set_matrix_csc(self._h, n, A.nnz, i64ptr(colptr), i64ptr(rowval),
                                            dptr(nzval), 0), "rbl_set_matrix_csc")
+
+    def set_matrix_dense_rows(self, n, row_begin, row_end, A_rows) -> None:
+        """Rows [row_begin,row_end) of a dense symmetric n x n matrix (rbl_set_matrix_dense)."""
+        M = np.asfortranarray(A_rows, dtype=np.float64)
+        if M.shape != (row_end - row_begin, n):
+            raise ValueError("A_rows must be (row_end - row_begin) x n")
+        self._check(lib.rbl_set_matrix_dense(self._h, n, row_begin, row_end, dptr(M),
+                                             max(M.shape[0], 1)), "rbl_set_matrix_dense")
 
     def set_matrix_rows(self, n, row_begin, row_end, rowptr, colind, val, index_base=0) -> None:
         rowptr = np.ascontiguousarray(rowptr, dtype=np.int64)

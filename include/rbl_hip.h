@@ -91,6 +91,13 @@ int rbl_set_matrix_csc(rbl_ctx* ctx, int64_t n, int64_t nnz, const int64_t* colp
 int rbl_set_matrix_csr_rows(rbl_ctx* ctx, int64_t n, int64_t row_begin, int64_t row_end,
                             const int64_t* rowptr, const int64_t* colind, const double* val,
                             int index_base);
+/* Dense symmetric A (RBL_gpu(A::Matrix{Float64}, k, b), RBL_gpu.jl:205; images.jl's B^T B):
+ * the local rows [row_begin,row_end) as a column-major slice with leading dimension lda
+ * (one rank: the whole n x n matrix, lda >= n — Julia's Matrix pointer as-is).  A * Q then
+ * runs as a panel GEMM on fp64 MFMA with Q gathered to all n rows on every rank; b <= 64.
+ * rbl_spmm_kernel_for reports 4; rbl_get_matrix_csr fails (RBL_ERR_STATE). */
+int rbl_set_matrix_dense(rbl_ctx* ctx, int64_t n, int64_t row_begin, int64_t row_end,
+                         const double* A, int64_t lda);
 /* Device-side generator of the seeded symmetric "hash-window" matrix:
  * entry (r,c), |r-c| <= halfwidth, r != c, exists iff hash(seed,min,max) < density, with a
  * uniform(-1,1) value from the same hash; diagonal = uniform(-1,1) plus plant[l] at row
@@ -106,7 +113,8 @@ int rbl_get_matrix_csr(rbl_ctx* ctx, int64_t* rowptr, int32_t* colind, double* v
  * halo exchange).  Allocates its own device buffers. */
 int rbl_apply(rbl_ctx* ctx, int b, const double* X, double* Y);
 /* Which SpMM kernel rbl_step / rbl_apply use for block size b under the current option:
- * 1 = global-gather CSR, 2 = LDS-window CSR (DPP), 3 = LDS band tiles on fp64 MFMA. */
+ * 1 = global-gather CSR, 2 = LDS-window CSR (DPP), 3 = LDS band tiles on fp64 MFMA,
+ * 4 = dense panel GEMM (rbl_set_matrix_dense). */
 int rbl_spmm_kernel_for(rbl_ctx* ctx, int b);
 
 /* ---- Krylov run -----------------------------------------------------------------------
