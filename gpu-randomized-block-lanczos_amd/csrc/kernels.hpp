@@ -111,7 +111,7 @@ bool gram44_ok(int nW, int w, int xcount, int xw);
 int gram44_splits(int64_t nrows, int nW);
 void gram44_partial(int64_t nrows, const PanelRun& W, const Panels& X, double* slab, int splits,
                     const int* skip, hipStream_t s);
-bool tsmm44_ok(int xw, int ky);
+bool tsmm44_ok(int xw, int ky, int yw);
 void tsmm44(int64_t nrows, const PanelRun& X, const double* C, int ldc, const Panels& Y,
             double alpha, double beta, const int* skip, hipStream_t s);
 

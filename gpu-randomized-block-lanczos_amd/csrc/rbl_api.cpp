@@ -76,6 +76,10 @@ struct rbl_ctx {
   int* d_flags = nullptr;     // [need3, skip3, status0, status1]
   double* h_pin = nullptr;    // pinned staging: Ai, Rtot (2 b x b)
   bool have_bprev = false;
+  // locked Ritz vectors of the restarted variants (restarted.jl: Qlock / Qlock_gpu), fp64,
+  // vector j at d_lock + j * nloc (a width-1 panel)
+  double* d_lock = nullptr;
+  int nlock = 0, lock_cap = 0;
 
   // options
   bool timers = false;
@@ -400,6 +404,76 @@ int apply_A(rbl_ctx* ctx, const double* Qin, int64_t off, int b, double* U, cons
   return 0;
 }
 
+// X -= l (l^T X) for every locked vector l in lock order (restarted.jl:1-21,
+// restart_reorth_gpu!: one projection per locked vector, MGS over them).
+int lock_reorth(rbl_ctx* ctx, double* X) {
+  const int b = ctx->b;
+  for (int j = 0; j < ctx->nlock; ++j) {
+    const double* l = ctx->d_lock + (int64_t)j * ctx->nloc;
+    CHK(gram(ctx, run1(l, 1), pan1(X, b), ctx->d_C, nullptr));
+    CHK(tsmm_checked(ctx, run1(l, 1), ctx->d_C, b, pan1(X, b), -1.0, 1.0, nullptr));
+  }
+  return RBL_OK;
+}
+
+// Reorth of the pair (Q_i, Q_{i-1}) = slots (i-1, i-2) of the fp64 basis:
+//   flags bit 1: against the locked vectors, Q_{i-1} then Q_i (restarted.jl:54-55);
+//   flags bit 0: against Q_1..Q_{i-2} (RBL_gpu.jl:59-81; block CGS, or the reference's
+//                ascending-j block MGS with RBL_OPT_REORTH_ORDER = 1).
+// i == 1 with bit 1: Q_1 against the locked vectors (restarted.jl:41).
+int reorth_pair(rbl_ctx* ctx, int i, int flags) {
+  const int b = ctx->b;
+  double* Qi = slotp(ctx, i - 1);
+  double* Qm = i >= 2 ? slotp(ctx, i - 2) : nullptr;
+  if ((flags & 2) && ctx->nlock > 0) {
+    StageScope t(ctx, RBL_STAGE_PART_REORTH);
+    if (Qm) CHK(lock_reorth(ctx, Qm));
+    CHK(lock_reorth(ctx, Qi));
+  }
+  if ((flags & 1) && i >= 3) {
+    StageScope t(ctx, RBL_STAGE_PART_REORTH);
+    const int nW = i - 2;
+    if (ctx->reorth_order == 0) {  // block CGS: one Gram over every j, one update
+      PanelRun W;
+      W.base = slotp(ctx, 0);
+      W.stride = ctx->slot;
+      W.count = nW;
+      W.w = b;
+      CHK(gram(ctx, W, pan2(Qi, Qm, b), ctx->d_C, nullptr));
+      CHK(tsmm_checked(ctx, W, ctx->d_C, 2 * b, pan2(Qi, Qm, b), -1.0, 1.0, nullptr));
+    } else {  // ascending-j block MGS, exactly the reference order
+      for (int j = 0; j < nW; ++j) {
+        const PanelRun W = run1(slotp(ctx, j), b);
+        CHK(gram(ctx, W, pan2(Qi, Qm, b), ctx->d_C, nullptr));
+        CHK(tsmm_checked(ctx, W, ctx->d_C, 2 * b, pan2(Qi, Qm, b), -1.0, 1.0, nullptr));
+      }
+    }
+  }
+  return RBL_OK;
+}
+
+// Y (n_local x kcols, row-major) = [Q_1 .. Q_nblocks] S with S host (nblocks*b) x kcols
+// column-major — the Ritz combination of RBL.jl:61-71 / RBL_gpu.jl:106-132 (fp64 basis).
+int basis_combine(rbl_ctx* ctx, int nblocks, int kcols, const double* S, double* Y) {
+  const int b = ctx->b;
+  const int64_t rows = (int64_t)nblocks * b;
+  double *d_Scm = nullptr, *d_S = nullptr;
+  HIPC(hipMalloc(&d_Scm, rows * kcols * sizeof(double)));
+  HIPC(hipMalloc(&d_S, rows * kcols * sizeof(double)));
+  HIPC(hipMemcpyAsync(d_Scm, S, rows * kcols * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+  colmajor_to_rowmajor(d_Scm, rows, kcols, d_S, ctx->stream);
+  PanelRun X;
+  X.base = slotp(ctx, 0);
+  X.stride = ctx->slot;
+  X.count = nblocks;
+  X.w = b;
+  const int st = tsmm_checked(ctx, X, d_S, kcols, pan1(Y, kcols), 1.0, 0.0, nullptr);
+  HIPC(hipStreamSynchronize(ctx->stream));
+  hipFree(d_S);
+  hipFree(d_Scm);
+  return st;
+}
+
 // fp32 basis: Gram C = W^T [X0, X1] over all ranks (fp32 MFMA per split, fp64 sum), C fp64
 // [nW*b][xcount*b] — the FLOAT `temp` of RBL_gpu.jl:33,39,87 (rounded to f32 where applied).
 int gram32(rbl_ctx* ctx, const float* Wb, int nW, const float* X0, const float* X1, int xcount,
@@ -515,6 +589,8 @@ void free_run(rbl_ctx* ctx) {
   hipFree(ctx->d_C); ctx->d_C = nullptr;
   hipFree(ctx->d_small); ctx->d_small = nullptr;
   hipFree(ctx->d_flags); ctx->d_flags = nullptr;
+  hipFree(ctx->d_lock); ctx->d_lock = nullptr;
+  ctx->nlock = ctx->lock_cap = 0;
   if (ctx->h_pin) hipHostFree(ctx->h_pin);
   ctx->h_pin = nullptr;
   ctx->nblocks = 0;
@@ -972,6 +1048,7 @@ int rbl_start(rbl_ctx* ctx, int b, int max_blocks, int basis_bits, const double*
   const bool reuse = (ctx->d_basis || ctx->d_basis32) && ctx->b == b &&
                      ctx->max_blocks == max_blocks && ctx->slot == ctx->nloc * b &&
                      ctx->basis_bits == basis_bits;
+  ctx->nlock = 0;  // a new problem: no locked vectors
   if (reuse) {
     ctx->nblocks = 0;
     HIPC(hipMemsetAsync(ctx->d_flags, 0, 4 * sizeof(int), ctx->stream));
@@ -1058,12 +1135,14 @@ int rbl_step(rbl_ctx* ctx, int i, int part_reorth, double* A_out, double* B_out)
   double* Qi = f32 ? ctx->d_Qi64 : slotp(ctx, i - 1);
   double* Qm = i >= 2 ? (f32 ? ctx->d_Qm64 : slotp(ctx, i - 2)) : nullptr;
   HIPC(hipMemsetAsync(ctx->d_flags, 0, 4 * sizeof(int), ctx->stream));
+  if (f32 && (part_reorth & 2))
+    return fail(ctx, RBL_ERR_INVALID, "rbl_step: locked-vector reorth needs the fp64 basis");
   if (f32) {
     // FLOAT = Float32: partial and local reorth on the fp32 blocks, then the
     // current / previous block widened to fp64 (RBL_gpu.jl:164-174)
     float* Qi32 = slotp32(ctx, i - 1);
     float* Qm32 = i >= 2 ? slotp32(ctx, i - 2) : nullptr;
-    if (part_reorth && i >= 3) {
+    if ((part_reorth & 1) && i >= 3) {
       StageScope t(ctx, RBL_STAGE_PART_REORTH);
       const int nW = i - 2;
       if (ctx->reorth_order == 0) {
@@ -1086,26 +1165,9 @@ int rbl_step(rbl_ctx* ctx, int i, int part_reorth, double* A_out, double* B_out)
     }
   }
 
-  // partial reorth of Q_i and Q_{i-1} against Q_1..Q_{i-2}   (RBL_gpu.jl:164-166, 59-81)
-  if (!f32 && part_reorth && i >= 3) {
-    StageScope t(ctx, RBL_STAGE_PART_REORTH);
-    const int nW = i - 2;
-    if (ctx->reorth_order == 0) {  // block CGS: one Gram over every j, one update
-      PanelRun W;
-      W.base = slotp(ctx, 0);
-      W.stride = ctx->slot;
-      W.count = nW;
-      W.w = b;
-      CHK(gram(ctx, W, pan2(Qi, Qm, b), ctx->d_C, nullptr));
-      CHK(tsmm_checked(ctx, W, ctx->d_C, 2 * b, pan2(Qi, Qm, b), -1.0, 1.0, nullptr));
-    } else {  // ascending-j block MGS, exactly the reference order
-      for (int j = 0; j < nW; ++j) {
-        const PanelRun W = run1(slotp(ctx, j), b);
-        CHK(gram(ctx, W, pan2(Qi, Qm, b), ctx->d_C, nullptr));
-        CHK(tsmm_checked(ctx, W, ctx->d_C, 2 * b, pan2(Qi, Qm, b), -1.0, 1.0, nullptr));
-      }
-    }
-  }
+  // partial reorth of Q_i and Q_{i-1} against Q_1..Q_{i-2}   (RBL_gpu.jl:164-166, 59-81),
+  // preceded (flag bit 1, restarted variants) by the reorth against the locked vectors
+  if (!f32) CHK(reorth_pair(ctx, i, part_reorth));
   // local reorth: Q_i -= Q_{i-1} (Q_{i-1}^T Q_i), one projection (RBL_gpu.jl:83-93, P1)
   const bool fused = rowgram_ok(b);
   if (!f32 && i >= 2) {
@@ -1235,6 +1297,72 @@ int rbl_get_block(rbl_ctx* ctx, int j, double* Q_out) {
 }
 
 int rbl_num_blocks(rbl_ctx* ctx) { return ctx ? ctx->nblocks : 0; }
+
+// ---- restarted variants (restarted.jl) -------------------------------------------------
+int rbl_restart(rbl_ctx* ctx, int nblocks, const double* S) {
+  if (!ctx || !S || nblocks < 1 || nblocks > ctx->nblocks)
+    return fail(ctx, RBL_ERR_INVALID, "rbl_restart: bad arguments");
+  if (!ctx->d_basis) return fail(ctx, RBL_ERR_STATE, "rbl_restart: needs an fp64 run (rbl_start)");
+  HIPC(hipSetDevice(ctx->device));
+  const int b = ctx->b;
+  CHK(basis_combine(ctx, nblocks, b, S, ctx->d_T));
+  HIPC(hipMemcpyAsync(slotp(ctx, 0), ctx->d_T, ctx->nloc * b * sizeof(double),
+                      hipMemcpyDeviceToDevice, ctx->stream));
+  HIPC(hipMemsetAsync(ctx->d_flags, 0, 4 * sizeof(int), ctx->stream));
+  HIPC(hipStreamSynchronize(ctx->stream));
+  ctx->nblocks = 1;
+  return RBL_OK;
+}
+
+int rbl_lock(rbl_ctx* ctx, int nblocks, int nvec, const double* S) {
+  if (!ctx || !S || nblocks < 1 || nblocks > ctx->nblocks || nvec < 0)
+    return fail(ctx, RBL_ERR_INVALID, "rbl_lock: bad arguments");
+  if (!ctx->d_basis) return fail(ctx, RBL_ERR_STATE, "rbl_lock: needs an fp64 run (rbl_start)");
+  if (nvec == 0) return RBL_OK;
+  HIPC(hipSetDevice(ctx->device));
+  const int64_t nl = std::max<int64_t>(ctx->nloc, 1);
+  if (ctx->nlock + nvec > ctx->lock_cap) {
+    const int cap = std::max(2 * ctx->lock_cap, ctx->nlock + nvec);
+    double* d = nullptr;
+    HIPC(hipMalloc(&d, (size_t)cap * nl * sizeof(double)));
+    if (ctx->nlock)
+      HIPC(hipMemcpyAsync(d, ctx->d_lock, (size_t)ctx->nlock * nl * sizeof(double),
+                          hipMemcpyDeviceToDevice, ctx->stream));
+    HIPC(hipStreamSynchronize(ctx->stream));
+    hipFree(ctx->d_lock);
+    ctx->d_lock = d;
+    ctx->lock_cap = cap;
+  }
+  const int64_t rows = (int64_t)nblocks * ctx->b;
+  for (int v = 0; v < nvec; ++v)
+    CHK(basis_combine(ctx, nblocks, 1, S + v * rows, ctx->d_lock + (int64_t)(ctx->nlock + v) * nl));
+  ctx->nlock += nvec;
+  return RBL_OK;
+}
+
+int rbl_num_locked(rbl_ctx* ctx) { return ctx ? ctx->nlock : 0; }
+
+int rbl_get_locked(rbl_ctx* ctx, double* V_out) {
+  if (!ctx || !V_out) return fail(ctx, RBL_ERR_INVALID, "rbl_get_locked: bad arguments");
+  if (ctx->nlock == 0) return RBL_OK;
+  HIPC(hipSetDevice(ctx->device));
+  const int64_t nl = std::max<int64_t>(ctx->nloc, 1);
+  for (int j = 0; j < ctx->nlock; ++j)  // vector j is a contiguous column of length n_local
+    HIPC(hipMemcpy(V_out + (int64_t)j * ctx->nloc, ctx->d_lock + (int64_t)j * nl,
+                   ctx->nloc * sizeof(double), hipMemcpyDeviceToHost));
+  return RBL_OK;
+}
+
+int rbl_reorth_last(rbl_ctx* ctx, int nblocks, int flags) {
+  if (!ctx || nblocks < 1 || nblocks > ctx->nblocks)
+    return fail(ctx, RBL_ERR_INVALID, "rbl_reorth_last: bad arguments");
+  if (!ctx->d_basis) return fail(ctx, RBL_ERR_STATE, "rbl_reorth_last: needs an fp64 run");
+  HIPC(hipSetDevice(ctx->device));
+  CHK(reorth_pair(ctx, nblocks, flags));
+  HIPC(hipStreamSynchronize(ctx->stream));
+  harvest_timers(ctx);
+  return RBL_OK;
+}
 
 int rbl_num_stages(void) { return RBL_NUM_STAGES; }
 const char* rbl_stage_name(int stage) {

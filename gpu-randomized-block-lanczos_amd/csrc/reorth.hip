@@ -348,7 +348,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
   }
 }
 
-bool tsmm44_ok(int xw, int ky) { return (xw == 16 || xw == 32) && ky >= 1 && ky <= 64; }
+// the epilogue stores Y row-major 16 B (two columns) per lane: Y panel widths must be even
+bool tsmm44_ok(int xw, int ky, int yw) {
+  return (xw == 16 || xw == 32) && ky >= 1 && ky <= 64 && yw % 2 == 0;
+}
 
 template <int B, int KYP>
 static void launch_tsmm44(int64_t nrows, const PanelRun& X, const double* C, int ldc, int KY,

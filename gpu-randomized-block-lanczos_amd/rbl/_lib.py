@@ -61,6 +61,11 @@ SIGNATURES = {
     "rbl_ritz": (C.c_int, [_p, C.c_int, C.c_int, _pd, _pd]),
     "rbl_get_block": (C.c_int, [_p, C.c_int, _pd]),
     "rbl_num_blocks": (C.c_int, [_p]),
+    "rbl_restart": (C.c_int, [_p, C.c_int, _pd]),
+    "rbl_lock": (C.c_int, [_p, C.c_int, C.c_int, _pd]),
+    "rbl_num_locked": (C.c_int, [_p]),
+    "rbl_get_locked": (C.c_int, [_p, _pd]),
+    "rbl_reorth_last": (C.c_int, [_p, C.c_int, C.c_int]),
     "rbl_num_stages": (C.c_int, []),
     "rbl_stage_name": (C.c_char_p, [C.c_int]),
     "rbl_timers": (C.c_int, [_p, _pd, C.c_int]),

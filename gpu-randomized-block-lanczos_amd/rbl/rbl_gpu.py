@@ -187,13 +187,34 @@ class Context:
         self._check(lib.rbl_start(self._h, b, max_blocks, basis_bits, dptr(om), seed), "rbl_start")
         self.b = b
 
-    def step(self, i: int, part_reorth: bool):
+    def step(self, i: int, part_reorth):
+        """part_reorth: bool, or the flag word of rbl_step (bit 0 partial reorth, bit 1 the
+        locked-vector reorth of the restarted variants)."""
         b = self.b
         A = np.zeros((b, b), order="F")
         B = np.zeros((b, b), order="F")
-        st = self._check(lib.rbl_step(self._h, i, int(bool(part_reorth)), dptr(A), dptr(B)),
-                         "rbl_step")
+        st = self._check(lib.rbl_step(self._h, i, int(part_reorth), dptr(A), dptr(B)), "rbl_step")
         return A, B, st
+
+    # ---- restarted variants (restarted.jl) ----
+    def restart(self, nblocks: int, S: np.ndarray) -> None:
+        S = np.asfortranarray(S, dtype=np.float64)
+        self._check(lib.rbl_restart(self._h, nblocks, dptr(S)), "rbl_restart")
+
+    def lock(self, nblocks: int, S: np.ndarray) -> None:
+        S = np.asfortranarray(S, dtype=np.float64)
+        self._check(lib.rbl_lock(self._h, nblocks, S.shape[1], dptr(S)), "rbl_lock")
+
+    def locked(self) -> np.ndarray:
+        n, r0, r1, _ = self.matrix_info()
+        L = lib.rbl_num_locked(self._h)
+        V = np.zeros((r1 - r0, L), order="F")
+        if L:
+            self._check(lib.rbl_get_locked(self._h, dptr(V)), "rbl_get_locked")
+        return V
+
+    def reorth_last(self, nblocks: int, flags: int) -> None:
+        self._check(lib.rbl_reorth_last(self._h, nblocks, flags), "rbl_reorth_last")
 
     def ritz(self, nblocks: int, k: int, S: np.ndarray) -> np.ndarray:
         n, r0, r1, _ = self.matrix_info()

@@ -128,8 +128,10 @@ int rbl_spmm_kernel_for(rbl_ctx* ctx, int b);
 int rbl_start(rbl_ctx* ctx, int b, int max_blocks, int basis_bits, const double* omega,
               uint64_t seed);
 /* One block Lanczos step i (1-based) — RBL_gpu.jl:149-161 for i == 1 and :163-184 for
- * i >= 2: partial reorth of Q_i, Q_{i-1} against Q_1..Q_{i-2} when `part_reorth` is set
- * (the reference sets it for even i), local reorth, U = A Q_i - Q_{i-1} B_i^T,
+ * i >= 2: partial reorth of Q_i, Q_{i-1} against Q_1..Q_{i-2} when bit 0 of `part_reorth`
+ * is set (the reference sets it for even i; restarted.jl for i % 3 == 0), preceded by
+ * their reorth against the locked vectors when bit 1 is set (restarted.jl:54-55; at i == 1
+ * Q_1 alone, :41; fp64 basis only), local reorth, U = A Q_i - Q_{i-1} B_i^T,
  * A_i = Q_i^T U, U -= Q_i A_i, Q_{i+1} B_{i+1} = qr(U).  A_out/B_out: b x b column-major
  * host buffers receiving A_i and B_{i+1} (upper triangular) — the only per-step traffic. */
 int rbl_step(rbl_ctx* ctx, int i, int part_reorth, double* A_out, double* B_out);
@@ -139,6 +141,21 @@ int rbl_ritz(rbl_ctx* ctx, int nblocks, int k, const double* S, double* V_out);
 /* Copy basis block j (1-based) to the host (n_local x b column-major) — tests only. */
 int rbl_get_block(rbl_ctx* ctx, int j, double* Q_out);
 int rbl_num_blocks(rbl_ctx* ctx);
+
+/* ---- restarted variants (restarted.jl: RBL_gpu_restarted / RBL_restarted) ---------------
+ * Locked Ritz vectors live on the device (Qlock_gpu); fp64 basis runs only.
+ * rbl_restart: the next cycle starts from Q_1 = [Q_1..Q_nblocks] S (S: (nblocks*b) x b
+ *   column-major), no QR — restarted.jl:131-132 `Qi = recover_eigvec(...)`; the locked set
+ *   is kept, the block count resets to 1.
+ * rbl_lock: append the nvec Ritz vectors [Q_1..Q_nblocks] S (S: (nblocks*b) x nvec) to the
+ *   locked set — restarted.jl:121-126.  rbl_start empties the locked set.
+ * rbl_reorth_last: the end-of-cycle reorth of Q_nblocks, Q_{nblocks-1} (flags as rbl_step's
+ *   part_reorth) — restarted.jl:100-102. */
+int rbl_restart(rbl_ctx* ctx, int nblocks, const double* S);
+int rbl_lock(rbl_ctx* ctx, int nblocks, int nvec, const double* S);
+int rbl_num_locked(rbl_ctx* ctx);
+int rbl_get_locked(rbl_ctx* ctx, double* V_out);  /* n_local x num_locked column-major */
+int rbl_reorth_last(rbl_ctx* ctx, int nblocks, int flags);
 
 /* ---- timers --------------------------------------------------------------------------- */
 int rbl_num_stages(void);

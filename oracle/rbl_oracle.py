@@ -292,6 +292,93 @@ def RBL_gpu_mixed(A, k: int, b: int, *, omega, kryl_sz=KRYL_SZ_GPU, qr_mode="pos
     return OracleResult(D, V, i, len(Qgpu), converged, tr)
 
 
+def _restart_cycle(A, b, kryl, Qg_d, locked, qr_mode):
+    """restarted.jl:23-104 (lanczos_iteration_res), effective semantics with FLOAT = DOUBLE =
+    Float64: the cycle's first block is reorthogonalised against the locked vectors in the
+    basis copy (Qg) while Qg_d, un-reorthogonalised, is multiplied (:41, :44-48)."""
+    def lock_reorth(X):                                   # restart_reorth_gpu! (:1-21)
+        for l in locked:
+            X -= l @ (l.T @ X)
+    Qg = Qg_d.copy()
+    lock_reorth(Qg)                                       # :41
+    Qb = [Qg.copy()]                                      # :42-43
+    U = A @ Qg_d                                          # :44
+    Ai = Qg_d.T @ U                                       # :45
+    U -= Qg_d @ Ai                                        # :46
+    Qn, Bi = _qr(U, qr_mode)                              # :47, 51
+    Qg1 = Qg_d.copy()                                     # :48
+    Qg_d = Qn
+    Qg = Qn.copy()                                        # :49-50
+    cols, Bs = [Ai], [Bi]
+    i = 2
+    while i * b < kryl:                                   # :54
+        if i % 3 == 0:                                    # :55-59
+            lock_reorth(Qg1)
+            lock_reorth(Qg)
+            for j in range(i - 2):                        # hybrid_part_reorth! (RBL_gpu.jl:59-81)
+                Wj = Qb[j]
+                Qg -= Wj @ (Wj.T @ Qg)
+                Qg1 -= Wj @ (Wj.T @ Qg1)
+            Qb[i - 2] = Qg1.copy()
+        Qg -= Qg1 @ (Qg1.T @ Qg)                          # :60 (P1)
+        Qb.append(Qg.copy())                              # :61-64
+        Qg_d = Qg.copy()
+        Qg1_d = Qg1.copy()
+        U = A @ Qg_d                                      # :67
+        U -= Qg1_d @ Bi.T                                 # :68
+        Ai = Qg_d.T @ U                                   # :69
+        U -= Qg_d @ Ai                                    # :70
+        Qn, Bi = _qr(U, qr_mode)                          # :71-75
+        Qg1 = Qg_d.copy()
+        Qg_d = Qn
+        Qg = Qn.copy()
+        cols.append(Ai)
+        Bs.append(Bi)
+        i += 1
+    m = len(Qb)
+    X1, X2 = Qb[m - 2], Qb[m - 1]                          # :100-102
+    lock_reorth(X1)
+    lock_reorth(X2)
+    for j in range(m - 2):
+        Wj = Qb[j]
+        X2 -= Wj @ (Wj.T @ X2)
+        X1 -= Wj @ (Wj.T @ X1)
+    T = np.hstack([insertA(a, b) for a in cols])          # :52, :80
+    for it in range(1, m):                                # insertB! unless (i+1)b >= kryl (:81-83)
+        insertB(Bs[it - 1], T, b, it)
+    D, V = dsbev(T)                                       # :103
+    res = Bs[-1] @ V[m * b - b:, ::-1]                    # :104
+    return D[::-1].copy(), V[:, ::-1].copy(), res, Qb
+
+
+def RBL_restarted_semantics(A, k: int, *, omega, kryl0: int = 100, qr_mode="posdiag",
+                            max_cycles: int = 60, tol: float = RESIDUAL_TOL):
+    """restarted.jl:106-146 (RBL_gpu_restarted; kryl0 = 80 gives RBL_restarted, :196-245):
+    b = 1 Lanczos cycles with locking.  Returns (D, locked vectors, cycles)."""
+    b = 1
+    Qg_d, _ = _qr(A @ np.asarray(omega, dtype=np.float64), qr_mode)     # :112-113
+    locked, D = [], []
+    count, kryl, cycles = 0, kryl0, 0
+    while count < k and cycles < max_cycles:
+        d, v, conv, Qb = _restart_cycle(A, b, kryl, Qg_d, locked, qr_mode)
+        ncomp = 0
+        for i in range(d.size):                                          # :116-137
+            if count + ncomp >= k:
+                break
+            if np.linalg.norm(conv[:, i]) < tol:
+                ncomp += 1
+                locked.append(recover_eigvec(Qb, v[:, i:i + 1], 1))
+                D.append(d[i])
+            else:
+                Qg_d = recover_eigvec(Qb, v[:, i:i + 1], 1)
+                break
+        kryl += 10
+        count += ncomp
+        cycles += 1
+    V = np.hstack(locked) if locked else np.zeros((A.shape[0], 0))
+    return np.asarray(D), V, cycles
+
+
 def moderate_decay_matrix(n: int, k: int):
     """test.jl:17-28 — a_i = i(i+1)/2; expected a[n], a[n-1], ..."""
     a = np.cumsum(np.arange(1, n + 1, dtype=np.float64))

@@ -29,7 +29,7 @@ def dense_planted(n, k, seed=5):
     return A + (Qf * lam) @ Qf.T
 
 
-@pytest.mark.parametrize("n,b", [(1000, 8), (2048, 16), (3001, 32)])
+@pytest.mark.parametrize("n,b", [(1000, 1), (999, 5), (1000, 8), (2048, 16), (3001, 32)])
 def test_dense_apply(rbl, n, b):
     A = dense_planted(n, 5)
     X = np.random.default_rng(1).standard_normal((n, b))

@@ -161,3 +161,19 @@ def test_stage_timers(rbl):
         t = ctx.timers()
     for s in ("AQ", "3-term", "qr", "part reorth", "loc reorth"):
         assert t[s] > 0.0, (s, t)
+
+
+@pytest.mark.parametrize("b,k", [(16, 7), (32, 5)])
+def test_ritz_odd_k(rbl, b, k):
+    """Ritz projection with an odd number of vectors on the b = 16 / 32 MFMA paths."""
+    A = c1_matrix(6000, 10)
+    n = A.shape[0]
+    omega = np.random.default_rng(5).standard_normal((n, b))
+    ref = o.RBL_gpu_semantics(A, k, b, omega=omega, qr_mode="posdiag", reorth_mode="cgs")
+    D, V, info = rbl.RBL_gpu(A, k, b, omega=omega, return_info=True)
+    assert ref.converged and info.converged and V.shape == (n, k)
+    assert np.all(np.abs(D - ref.D) <= EIG_TOL * np.abs(ref.D))
+    dots = np.abs(np.sum(V * ref.V, axis=0)) / (np.linalg.norm(V, axis=0) * np.linalg.norm(ref.V, axis=0))
+    assert np.all(1 - dots < VEC_TOL), dots
+    res = np.linalg.norm(A @ V - V * D[None, :], axis=0) / np.abs(D)
+    assert res.max() < RES_TOL
