@@ -10,7 +10,9 @@
 # is what the parity tests run.
 #
 #   include("common.jl"); include("RBL_hip.jl")
-#   D, V = RBL_hip(A, k, b)              # A::SparseMatrixCSC{Float64,Int64}, symmetric
+#   D, V = RBL_hip(A, k, b)              # A::SparseMatrixCSC{Float64,Int64} or Matrix{Float64}
+#   D, V = RBL_hip(A, k, b; basis_bits = 32)   # FLOAT = Float32 mode (common.jl:5)
+#   D, V = RBL_hip_restarted(A, k)       # restarted.jl:106 (RBL_gpu_restarted)
 
 const librbl_hip = get(ENV, "RBL_HIP_LIB", "librbl_hip.so")
 
@@ -27,23 +29,36 @@ function rbl_check(ctx::Ptr{Cvoid}, st::Cint, what::String)
     return st
 end
 
-function RBL_hip(A::SparseMatrixCSC{Float64,Int64}, k::Int64, b::Int64;
-                 device::Int = 0, seed::UInt64 = rand(UInt64), kryl_sz::Int64 = 1200)
-    n = size(A, 2)
+# Ag = adapt(CuArray, A) (RBL_gpu.jl:209): Julia's 1-based CSC arrays as-is, or the dense
+# column-major matrix (RBL_gpu(A::Matrix{Float64})) as-is
+set_matrix!(ctx, A::SparseMatrixCSC{Float64,Int64}) =
+    rbl_check(ctx, ccall((:rbl_set_matrix_csc, librbl_hip), Cint,
+                         (Ptr{Cvoid}, Int64, Int64, Ptr{Int64}, Ptr{Int64}, Ptr{Float64}, Cint),
+                         ctx, size(A, 2), nnz(A), A.colptr, A.rowval, A.nzval, 1), "rbl_set_matrix_csc")
+set_matrix!(ctx, A::Matrix{Float64}) =
+    rbl_check(ctx, ccall((:rbl_set_matrix_dense, librbl_hip), Cint,
+                         (Ptr{Cvoid}, Int64, Int64, Int64, Ptr{Float64}, Int64),
+                         ctx, size(A, 2), 0, size(A, 1), A, size(A, 1)), "rbl_set_matrix_dense")
+
+function rbl_context(device::Int)
     hr = Ref{Ptr{Cvoid}}(C_NULL)
     st = ccall((:rbl_create, librbl_hip), Cint, (Ref{Ptr{Cvoid}}, Cint), hr, device)
-    ctx = hr[]
-    rbl_check(ctx, st, "rbl_create")
+    rbl_check(hr[], st, "rbl_create")
+    return hr[]
+end
+
+function RBL_hip(A::Union{SparseMatrixCSC{Float64,Int64},Matrix{Float64}}, k::Int64, b::Int64;
+                 device::Int = 0, seed::UInt64 = rand(UInt64), kryl_sz::Int64 = 1200,
+                 basis_bits::Int = 64)
+    n = size(A, 2)
+    ctx = rbl_context(device)
     try
-        # Ag = adapt(CuArray, A) (RBL_gpu.jl:209): Julia's 1-based CSC arrays as-is
-        rbl_check(ctx, ccall((:rbl_set_matrix_csc, librbl_hip), Cint,
-                             (Ptr{Cvoid}, Int64, Int64, Ptr{Int64}, Ptr{Int64}, Ptr{Float64}, Cint),
-                             ctx, n, nnz(A), A.colptr, A.rowval, A.nzval, 1), "rbl_set_matrix_csc")
+        set_matrix!(ctx, A)
         # Qg_d = qr(Ag * randn(n, b)).Q (RBL_gpu.jl:213-214); the basis lives in HBM
         m_max = cld(kryl_sz, b)
         rbl_check(ctx, ccall((:rbl_start, librbl_hip), Cint,
                              (Ptr{Cvoid}, Cint, Cint, Cint, Ptr{Float64}, UInt64),
-                             ctx, b, m_max, 64, C_NULL, seed), "rbl_start")
+                             ctx, b, m_max, basis_bits, C_NULL, seed), "rbl_start")
         Ai = zeros(Float64, b, b)
         Bi = zeros(Float64, b, b)
         step!(i, part) = rbl_check(ctx, ccall((:rbl_step, librbl_hip), Cint,
@@ -85,6 +100,83 @@ function RBL_hip(A::SparseMatrixCSC{Float64,Int64}, k::Int64, b::Int64;
                              (Ptr{Cvoid}, Cint, Cint, Ptr{Float64}, Ptr{Float64}),
                              ctx, nblocks, k, S, Vout), "rbl_ritz")
         return D, Vout
+    finally
+        ccall((:rbl_free, librbl_hip), Cint, (Ptr{Cvoid},), ctx)
+    end
+end
+
+# restarted.jl:106-146 (RBL_gpu_restarted): b = 1 cycles with locking.  The cycle
+# (lanczos_iteration_res, :23-104) is rbl_step with flags 3 every third step (partial +
+# locked reorth), rbl_reorth_last, then dsbev on the host; locked vectors and the restart
+# block stay on the device (rbl_lock / rbl_restart).  V: the locked Ritz vectors (the
+# reference returns zeros(n, k)).
+function RBL_hip_restarted(A::Union{SparseMatrixCSC{Float64,Int64},Matrix{Float64}}, k::Int64;
+                           device::Int = 0, seed::UInt64 = rand(UInt64), kryl0::Int64 = 100,
+                           max_cycles::Int64 = 60)
+    n = size(A, 2)
+    b = 1
+    ctx = rbl_context(device)
+    try
+        set_matrix!(ctx, A)
+        rbl_check(ctx, ccall((:rbl_start, librbl_hip), Cint,
+                             (Ptr{Cvoid}, Cint, Cint, Cint, Ptr{Float64}, UInt64),
+                             ctx, b, kryl0 + 10 * max_cycles, 64, C_NULL, seed), "rbl_start")
+        Ai = zeros(Float64, b, b)
+        Bi = zeros(Float64, b, b)
+        step!(i, flags) = rbl_check(ctx, ccall((:rbl_step, librbl_hip), Cint,
+                                               (Ptr{Cvoid}, Cint, Cint, Ptr{Float64}, Ptr{Float64}),
+                                               ctx, i, flags, Ai, Bi), "rbl_step")
+        D = Float64[]
+        count = 0
+        kryl = kryl0
+        cycles = 0
+        while count < k && cycles < max_cycles
+            step!(1, 2)                                          # :41-50
+            T = insertA!(copy(Ai), b)
+            insertB!(copy(Bi), T, b, 1)
+            i = 2
+            while i * b < kryl                                   # :52-86
+                step!(i, mod(i, 3) == 0 ? 3 : 0)
+                T = [T insertA!(copy(Ai), b)]
+                (i + 1) * b < kryl && insertB!(copy(Bi), T, b, i)
+                i += 1
+            end
+            m = i - 1
+            rbl_check(ctx, ccall((:rbl_reorth_last, librbl_hip), Cint, (Ptr{Cvoid}, Cint, Cint),
+                                 ctx, m, 3), "rbl_reorth_last")  # :100-102
+            d, v = dsbev('V', 'L', T)                            # :103
+            conv = Bi * v[end-b+1:end, end:-1:1]                 # :104
+            d = d[end:-1:1]
+            v = v[:, end:-1:1]
+            ncomp = 0
+            restart = nothing
+            for j = 1:length(d)                                  # :116-137
+                count + ncomp < k || break
+                if norm(conv[:, j]) < 1e-7
+                    ncomp += 1
+                    s = Matrix{Float64}(v[:, j:j])
+                    rbl_check(ctx, ccall((:rbl_lock, librbl_hip), Cint,
+                                         (Ptr{Cvoid}, Cint, Cint, Ptr{Float64}), ctx, m, 1, s), "rbl_lock")
+                    push!(D, d[j])
+                else
+                    restart = Matrix{Float64}(v[:, j:j])
+                    break
+                end
+            end
+            if restart === nothing
+                restart = zeros(Float64, m * b, b); restart[1, 1] = 1.0
+            end
+            rbl_check(ctx, ccall((:rbl_restart, librbl_hip), Cint, (Ptr{Cvoid}, Cint, Ptr{Float64}),
+                                 ctx, m, restart), "rbl_restart")
+            kryl += 10
+            count += ncomp
+            cycles += 1
+        end
+        L = ccall((:rbl_num_locked, librbl_hip), Cint, (Ptr{Cvoid},), ctx)
+        V = zeros(Float64, n, L)
+        L > 0 && rbl_check(ctx, ccall((:rbl_get_locked, librbl_hip), Cint, (Ptr{Cvoid}, Ptr{Float64}),
+                                      ctx, V), "rbl_get_locked")
+        return D, V
     finally
         ccall((:rbl_free, librbl_hip), Cint, (Ptr{Cvoid},), ctx)
     end
