@@ -58,6 +58,20 @@ def parse():
     return ap.parse_args()
 
 
+def streamed_bytes(kid, nloc, nnz_loc, b, halfwidth, m_max):
+    """Bytes the chosen SpMM kernel itself reads and writes per launch (step launches carry the
+    Q_{i-1} epilogue), beside SURVEY's CSR-based algorithmic bytes: the band-tile kernel (5)
+    streams 16 x (16 + 2H) dense doubles per 16-row tile instead of 12 B per nonzero; the
+    LDS-band kernel (3) 8 B value + 2 B position per nonzero plus the row pointers."""
+    vec = (m_max * 3 + 2) / (m_max + 1) * nloc * b * 8
+    if kid == 5:
+        H = 32 if halfwidth <= 32 else 64
+        return -(-nloc // 16) * 16 * (16 + 2 * H) * 8 + vec
+    if kid == 3:
+        return nnz_loc * 10 + (nloc + 1) * 8 + vec
+    return nnz_loc * 12 + (nloc + 1) * 8 + vec
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -112,7 +126,8 @@ def main():
     ctx.set_option(_lib.RBL_OPT_TIMERS, 1)
     ctx.set_option(_lib.RBL_OPT_SPMM_KERNEL, args.spmm_kernel)
     m_max = rbl.rbl_gpu.max_steps_for(args.kryl, b)
-    spmm_kernel = {1: "gather", 2: "lds-window", 3: "lds-band-mfma"}[ctx.spmm_kernel_for(b)]
+    spmm_kid = ctx.spmm_kernel_for(b)
+    spmm_kernel = {1: "gather", 2: "lds-window", 3: "lds-band-mfma", 5: "band-tile-mfma"}[spmm_kid]
 
     def one_run():
         rbl.lanczos(ctx, k, b, kryl_sz=args.kryl, seed=args.seed + 1, check=False, ritz=False,
@@ -165,6 +180,7 @@ def main():
                  "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(spmm_gbs / HBM_PEAK_GBS, 4),
                  "traffic": None if traffic is None else int(traffic),
                  "algorithmic_bytes_per_launch": int(spmm_bytes),
+                 "streamed_bytes_per_launch": int(streamed_bytes(spmm_kid, nloc, nnz_loc, b, args.halfwidth, m_max)),
                  "ms_per_launch": round(spmm_ms, 4)}
     mfma_peak = FP64_MFMA_PEAK_TF if args.basis_bits == 64 else FP32_MFMA_PEAK_TF
     roof_reorth = {"kernel": "partial reorth (gram+update)" + ("" if args.basis_bits == 64 else ", fp32"),

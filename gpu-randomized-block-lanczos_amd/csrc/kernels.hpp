@@ -51,6 +51,14 @@ struct CsrDev {
   // band kernel: per nonzero, its byte offset in the tile's dense LDS band
   // ((row % 16) * kBandLd + perm8(col - c16(tile))) * 8 (band_positions; kCsrPad entries past nnz)
   const uint16_t* band_pos = nullptr;
+  // band-tile kernel (spmm_bt.hip): the CSR densified into MFMA-ordered 16-row tiles with
+  // band groups NG = (2H+16)/16 (0: not applicable), and the Q rows the kernel may read
+  // (global [q_lo, q_hi); other band rows read zrow, 32 zeros)
+  const double* bt = nullptr;
+  int bt_ng = 0;
+  int64_t bt_tiles_per_wg = 0;
+  int64_t q_lo = 0, q_hi = 0;
+  const double* zrow = nullptr;
 };
 
 // --- rowop.hip ---------------------------------------------------------------------------
@@ -64,7 +72,7 @@ void rowgram(int64_t nrows, int b, const double* X, const double* C, int ldc, do
 
 // --- spmm.hip ----------------------------------------------------------------------------
 // U = A * Qin  (+ epilogue U -= Qprev * Bt^T with Bt = B_i row-major b x b, if Qprev).
-// variant: 0 auto, 1 global gather, 2 LDS window, 3 LDS band (MFMA).
+// variant: 0 auto, 1 global gather, 2 LDS window, 3 LDS band (MFMA), 4 band tiles (MFMA).
 // ai_slab: if non-null and the band kernel runs with band_gram, it also forms the partials
 // of A_i = Qin[own rows]^T U (b x b per workgroup) there; returns how many (0: not formed).
 int spmm(const CsrDev& A, const double* Qin, int64_t col_off, int b, double* U,
@@ -80,6 +88,15 @@ int window_grid();              // workgroups for the window kernel (= CUs)
 bool spmm_band(const CsrDev& A, const double* Qin, int64_t col_off, int b, double* U,
                const double* Qprev, const double* Bi, hipStream_t s, double* ai_slab = nullptr,
                int* ai_parts = nullptr);
+// spmm_bt.hip: band tiles in MFMA operand order streamed to VGPRs (b = 32, H in {32, 64});
+// false if not applicable.
+bool spmm_bt(const CsrDev& A, const double* Qin, int64_t col_off, int b, double* U,
+             const double* Qprev, const double* Bi, hipStream_t s, double* ai_slab = nullptr,
+             int* ai_parts = nullptr);
+// band-tile format of the local CSR: tiles in consumption order (slot (round * grid + wg) * 4
+// + wave), zero-filled `out` of bt_tile_slots(ntiles, tiles_per_wg) * NG * 256 doubles
+int64_t bt_tile_slots(int64_t ntiles, int64_t tiles_per_wg);
+void bt_fill(const CsrDev& A, int H, int NG, double* out, hipStream_t s);
 constexpr int kWindowTileRows = 16;
 // Band kernel geometry (host checks in rbl_api.cpp): a tile's band [c16, cmax] with
 // c16 = cmin & ~15 spans <= kBandMaxK columns; the Q ring holds kBandRing rows; per tile a

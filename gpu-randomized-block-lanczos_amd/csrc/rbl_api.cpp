@@ -37,6 +37,9 @@ struct rbl_ctx {
   int64_t* d_tcmax = nullptr;
   int64_t* d_tinfo = nullptr;
   uint16_t* d_bpos = nullptr;  // band kernel: per-nonzero dense-tile positions
+  double* d_bt = nullptr;      // band-tile kernel: the CSR in MFMA-ordered 16-row band tiles
+  int bt_ng = 0;               // its band groups (0: not applicable)
+  double* d_zrow = nullptr;    // 32 zeros: band rows the halo does not hold
   // dense A (RBL_gpu(A::Matrix{Float64})): local rows in 32-column row-major panels
   // (panel p = columns [32p, 32p+32), zero past n), multiplied by tsmm44 against d_qfull
   // (all n rows of Q, zero-padded to 32 * dense_panels rows, b <= 64 columns)
@@ -143,6 +146,12 @@ CsrDev csr(rbl_ctx* ctx) {
   A.band_pair = ctx->band_pair;
   A.row0 = ctx->r0;
   A.band_pos = ctx->d_bpos;
+  A.bt = ctx->d_bt;
+  A.bt_ng = ctx->bt_ng;
+  A.bt_tiles_per_wg = ctx->tiles_per_wg;
+  A.q_lo = ctx->nranks > 1 ? ctx->ext_lo : ctx->r0;
+  A.q_hi = ctx->nranks > 1 ? ctx->ext_hi : ctx->r0 + ctx->nloc;
+  A.zrow = ctx->d_zrow;
   return A;
 }
 
@@ -168,6 +177,14 @@ int prepare_window(rbl_ctx* ctx, const std::vector<int64_t>& rp) {
   HIPC(hipMemcpyAsync(cmin.data(), ctx->d_tcmin, nt * sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
   HIPC(hipMemcpyAsync(cmax.data(), ctx->d_tcmax, nt * sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
   HIPC(hipStreamSynchronize(ctx->stream));
+  // band-tile kernel (spmm_bt.hip): every nonempty tile's columns within
+  // [r0 + 16t - H, r0 + 16t + 16 + H) for H = 32 or 64
+  int64_t hneed = 0;
+  for (int64_t t = 0; t < nt; ++t) {
+    if (cmax[t] < 0) continue;
+    const int64_t ra = ctx->r0 + t * kWindowTileRows;
+    hneed = std::max(hneed, std::max(ra - cmin[t], cmax[t] - (ra + kWindowTileRows - 1)));
+  }
   // forward-fill empty tiles (cmax < 0), then backward-fill leading empties
   int64_t first = -1;
   for (int64_t t = 0; t < nt; ++t) {
@@ -260,6 +277,25 @@ int prepare_window(rbl_ctx* ctx, const std::vector<int64_t>& rp) {
   }
   const int64_t grid = window_grid();
   ctx->tiles_per_wg = std::max<int64_t>(1, (nt + grid - 1) / grid);
+  {
+    // dense tiles of 16 x (16 + 2H) doubles pay when they stream no more than ~1.25x the
+    // CSR's values + column indices (C4a: 18.4 KB vs 19.2 KB per tile)
+    const int H = hneed <= 32 ? 32 : hneed <= 64 ? 64 : 0;
+    const int NG = H ? (2 * H + 16) / 16 : 0;
+    const double dense_bytes = (double)nt * 16.0 * 16.0 * NG * 8.0;
+    if (H && dense_bytes <= 1.25 * 12.0 * (double)ctx->nnz) {
+      const size_t elems = (size_t)bt_tile_slots(nt, ctx->tiles_per_wg) * NG * 256;
+      HIPC(hipMalloc(&ctx->d_bt, elems * sizeof(double)));
+      HIPC(hipMemsetAsync(ctx->d_bt, 0, elems * sizeof(double), ctx->stream));
+      HIPC(hipMalloc(&ctx->d_zrow, 64 * sizeof(double)));
+      HIPC(hipMemsetAsync(ctx->d_zrow, 0, 64 * sizeof(double), ctx->stream));
+      CsrDev A3 = csr(ctx);
+      bt_fill(A3, H, NG, ctx->d_bt, ctx->stream);
+      HIPC(hipGetLastError());
+      HIPC(hipStreamSynchronize(ctx->stream));
+      ctx->bt_ng = NG;
+    }
+  }
   return RBL_OK;
 }
 
@@ -606,6 +642,9 @@ void free_matrix(rbl_ctx* ctx) {
   hipFree(ctx->d_tcmax); ctx->d_tcmax = nullptr;
   hipFree(ctx->d_tinfo); ctx->d_tinfo = nullptr;
   hipFree(ctx->d_bpos); ctx->d_bpos = nullptr;
+  hipFree(ctx->d_bt); ctx->d_bt = nullptr;
+  hipFree(ctx->d_zrow); ctx->d_zrow = nullptr;
+  ctx->bt_ng = 0;
   hipFree(ctx->d_dense); ctx->d_dense = nullptr;
   hipFree(ctx->d_qfull); ctx->d_qfull = nullptr;
   ctx->dense = false;
@@ -789,7 +828,7 @@ int rbl_set_option(rbl_ctx* ctx, int option, int64_t value) {
       ctx->reorth_order = (int)value;
       return RBL_OK;
     case RBL_OPT_SPMM_KERNEL:
-      if (value < 0 || value > 3) return fail(ctx, RBL_ERR_INVALID, "spmm kernel must be 0..3");
+      if (value < 0 || value > 4) return fail(ctx, RBL_ERR_INVALID, "spmm kernel must be 0..4");
       ctx->spmm_variant = (int)value;
       return RBL_OK;
     default: return fail(ctx, RBL_ERR_INVALID, "unknown option");
@@ -984,7 +1023,8 @@ int rbl_spmm_kernel_for(rbl_ctx* ctx, int b) {
   const int v = ctx->spmm_variant;
   const bool band = ctx->ntiles > 0 && ((b == 16 && ctx->band_ok16) || (b == 32 && ctx->band_ok32));
   const bool win = ctx->ntiles > 0 && ((b == 16 && ctx->window_ok16) || (b == 32 && ctx->window_ok32));
-  if ((v == 0 || v == 3) && band) return 3;
+  if ((v == 0 || v == 4) && b == 32 && (ctx->bt_ng == 5 || ctx->bt_ng == 9)) return 5;
+  if ((v == 0 || v == 3 || v == 4) && band) return 3;
   if ((v == 0 || v == 2 || v == 3) && win) return 2;
   return 1;
 }
@@ -1006,6 +1046,8 @@ int rbl_apply(rbl_ctx* ctx, int b, const double* X, double* Y) {
   int64_t off = 0;
   if (ctx->nranks > 1) {  // halo exchange through a private extended buffer
     HIPC(hipMalloc(&d_ext, std::max<int64_t>(ctx->ext_hi - ctx->ext_lo, 1) * b * sizeof(double)));
+    // rows between the received ranges stay finite (band-tile kernel multiplies them by 0)
+    HIPC(hipMemsetAsync(d_ext, 0, std::max<int64_t>(ctx->ext_hi - ctx->ext_lo, 1) * b * sizeof(double), ctx->stream));
     double* keep_ext = ctx->d_qext;
     const int keep_b = ctx->b;
     ctx->d_qext = d_ext;
@@ -1069,8 +1111,10 @@ int rbl_start(rbl_ctx* ctx, int b, int max_blocks, int basis_bits, const double*
   HIPC(hipMalloc(&ctx->d_U, (nl + kRowPad) * b * sizeof(double)));
   ctx->T_cols = b;
   HIPC(hipMalloc(&ctx->d_T, nl * b * sizeof(double)));
-  if (ctx->nranks > 1)
+  if (ctx->nranks > 1) {
     HIPC(hipMalloc(&ctx->d_qext, std::max<int64_t>(ctx->ext_hi - ctx->ext_lo, 1) * b * sizeof(double)));
+    HIPC(hipMemsetAsync(ctx->d_qext, 0, std::max<int64_t>(ctx->ext_hi - ctx->ext_lo, 1) * b * sizeof(double), ctx->stream));
+  }
   // Gram slab: the largest Gram is the partial-reorth one, (max_blocks-1) panels x 2b
   size_t slab = 0;
   for (int nW = 1; nW <= std::max(1, max_blocks - 1); ++nW)

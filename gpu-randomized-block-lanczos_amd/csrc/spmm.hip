@@ -69,9 +69,13 @@ static void launch_gather(const CsrDev& A, const double* Q, int64_t off, int b, 
 int spmm(const CsrDev& A, const double* Qin, int64_t col_off, int b, double* U,
          const double* Qprev, const double* Bi, int variant, hipStream_t s, double* ai_slab) {
   if (A.nrows <= 0) return 0;
-  // 0 auto: band (MFMA) > window (DPP) > gather;  1 gather;  2 window;  3 band
+  // 0 auto: band tiles > band (MFMA) > window (DPP) > gather;  1 gather;  2 window;  3 band;
+  // 4 band tiles
   int parts = 0;
-  if ((variant == 0 || variant == 3) &&
+  if ((variant == 0 || variant == 4) &&
+      spmm_bt(A, Qin, col_off, b, U, Qprev, Bi, s, ai_slab, &parts))
+    return parts;
+  if ((variant == 0 || variant == 3 || variant == 4) &&
       spmm_band(A, Qin, col_off, b, U, Qprev, Bi, s, ai_slab, &parts))
     return parts;
   if ((variant == 0 || variant == 2 || variant == 3) &&

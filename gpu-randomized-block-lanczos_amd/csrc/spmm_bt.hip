@@ -1,0 +1,447 @@
+// spmm_bt.hip — SpMM over band tiles: the CSR densified ONCE per matrix into 16-row tiles
+// stored in v_mfma_f64_4x4x4f64 operand order, streamed from HBM straight into VGPRs.
+//
+// U = A * Q_i (+ fused 3-term epilogue U -= Q_{i-1} B_i^T, + partials of A_i = Q_i^T U)
+//   — RBL_gpu.jl:176-178.
+//
+// Why: the LDS-densified band kernel (spmm_band.hip) spends its LDS bandwidth twice on A
+// (producer zero + scatter of every tile, then every consumer wave re-reading the dense tile)
+// and its VALU on the scatter; on gfx950 fp64 MFMA does not co-execute with VALU
+// (tools/coexec_probe.hip).  A banded matrix with |c - r| <= H (H = 64 at C4a) fills its
+// 16 x (16 + 2H) tile band to 69 % (100 of 144 columns per row), so the densified tile is
+// 16*144*8 = 18.4 KB against 16*100*12 = 19.2 KB of CSR values + column indices: storing it
+// dense costs no extra HBM and removes the scatter, the column indices and the A traffic
+// through LDS altogether.  What stays in LDS is the Q ring (each Q row read from HBM once per
+// CU) and, per tile, one ds_read_b128 per (k-step, column pair) of it.
+//
+// Format (bt_fill): tile t = local rows [16t, 16t+16), band = global columns
+// [row0 - H + 16t, row0 + H + 16t + 16) in NG = (2H+16)/16 groups of 16 columns; group g
+// holds 2 x 1 KiB: half h, lane l, element s = A[16t + (l&15)][c16 + 16g + 4(2h+s) + (l>>4)]
+// — exactly the A operand lane l feeds to the 4x4x4 MFMA of k-step u = 2h+s (layout below),
+// one coalesced global_load_dwordx4 per half.
+//
+// Workgroup: 256 threads = 4 waves, one per SIMD, one workgroup per CU, persistent over a
+// contiguous tile range [T0, T1) in rounds of 4 tiles (wave w takes tile T0 + 4r + w).
+// Each wave multiplies a whole tile (all 32 columns: 8 accumulators), so A is read once; the
+// next tile's group g is loaded into group g's registers as soon as they are consumed (one
+// tile period of latency cover, ~18 KiB in flight per wave).  The Q ring (256 rows, in ring
+// coordinates rho = global row - (row0 - H)) is filled one round ahead by all four waves
+// (register staged), one barrier per round.
+//
+// v_mfma_f64_4x4x4f64 layout (tools/mfma_layout_probe.hip), block G = (lane>>2)&3:
+//   A[row = lane&15][k = lane>>4], B[k = lane>>4][col = lane&3] (same in every block),
+//   D[row 4G + (lane>>4)][col lane&3].
+// Main product: blocks = the tile's 4 row quads, k = 4 band columns, B = Q ring values.
+// Accumulator acc[p][s] column j = lane&3 is U column 8p + 2j + s, so one ds_read_b128 of
+// ring row rho at 16-B slot 4p + j feeds acc[p][0] and acc[p][1].
+#include <cstdlib>
+
+#include "kernels.hpp"
+
+namespace rbl {
+
+namespace bt {
+constexpr int kThreads = 256;
+constexpr int kRing = 256;                       // ring rows (power of two)
+// ring row = 16 data slots of 16 B + 4 pad slots: row rho starts at bank slot 4*rho mod 16,
+// so the lanes of one ds_read_b128 lane group (rows rho, rho+1 or rho+2, rho+3 at the same
+// logical slots) land on disjoint banks
+constexpr int kRowBytes = 320;
+constexpr int kRingBytes = kRing * kRowBytes;   // 80 KiB
+constexpr int kBtOff = kRingBytes;              // epilogue B operand table: 8 x 4 x 16 d2v
+constexpr int kBtBytes = 1024 * 8;
+constexpr int kUStride = 336;                   // U stage row: 21 slots (bank shift 5 per row)
+constexpr int kUWave = 16 * kUStride;
+constexpr int kUOff = kBtOff + kBtBytes;
+constexpr int kLds = kUOff + 4 * kUWave;        // 111,104 B: one workgroup per CU
+static_assert(kLds <= 160 * 1024, "LDS budget");
+// A_i operand: lane reads ring slot pi(l & 15); pi maps the lanes {0-3, 12-15} of each
+// ds_read_b128 lane group to slot classes {0,1} mod 4 and {4-11} to {2,3} mod 4, so rows
+// rho (shift 0) and rho+1 (shift 4) never share a bank
+__device__ __forceinline__ int pi_slot(int i) {
+  const int c = (i >> 2) == 0 ? 0 : (i >> 2) == 1 ? 2 : (i >> 2) == 2 ? 3 : 1;
+  return 4 * (i & 3) + c;
+}
+}  // namespace bt
+
+__device__ __forceinline__ double mfma44(double a, double b, double c) {
+  return __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, c, 0, 0, 0);
+}
+
+struct BtArgs {
+  int64_t nrows;
+  int64_t ntiles;
+  int64_t tiles_per_wg;
+  const double* A;       // band tiles (bt_fill)
+  const double* Q;       // row c at Q + (c - col_off) * 32
+  int64_t col_off;
+  int64_t q_lo, q_hi;    // global rows present in Q; others read the zero row
+  const double* zrow;    // 32 zeros
+  int64_t row0;          // global index of local row 0
+  double* U;             // padded to a multiple of 16 rows
+  const double* Qprev;
+  const double* Bi;
+  double* ai_slab;       // AIG: per-workgroup partials of A_i (32 x 32 row-major)
+};
+
+// VAR (tuning variants, RBL_BT_VAR): bit 0 non-temporal A loads, bit 1 non-temporal U
+// stores, bit 2 ring reads software-pipelined one k-step ahead (bit 3: two k-steps ahead),
+// bit 4 A prefetched two tiles ahead, bit 5 ablation: main-loop MFMAs off (loads only)
+template <int NG, bool EPI, bool AIG, int VAR = 0>
+__global__ __launch_bounds__(bt::kThreads) __attribute__((amdgpu_waves_per_eu(1, 1)))
+void k_spmm_bt(BtArgs a) {
+  constexpr int B = 32;
+  constexpr int H = 8 * (NG - 1);
+  constexpr int kRoundRows = 64;                          // 4 tiles
+  constexpr int kRingSpan = kRoundRows + 16 + 2 * H - 16;  // rows one round reads (64 + 2H)
+  static_assert(kRingSpan + kRoundRows <= bt::kRing, "ring holds a round and the next one's rows");
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int64_t T0 = (int64_t)blockIdx.x * a.tiles_per_wg;
+  const int64_t T1 = T0 + a.tiles_per_wg < a.ntiles ? T0 + a.tiles_per_wg : a.ntiles;
+  if (T0 >= T1) return;
+  const int q = lane >> 4, j = lane & 3, G = (lane >> 2) & 3, i16 = lane & 15;
+  const int64_t gq = a.row0 - H;  // global row of ring coordinate 0
+
+  // 16-B chunk (slot s) of the Q row at ring coordinate rho; absent rows read zeros
+  auto qsrc = [&](int64_t rho, int s) -> const d2v* {
+    const int64_t c = rho + gq;
+    const double* p = (c >= a.q_lo && c < a.q_hi) ? a.Q + (c - a.col_off) * B : a.zrow;
+    return reinterpret_cast<const d2v*>(p) + s;
+  };
+  auto ring_ptr = [&](int64_t rho, int s) -> d2v* {
+    return reinterpret_cast<d2v*>(smem + (unsigned)(rho & (bt::kRing - 1)) * bt::kRowBytes + 16u * s);
+  };
+
+  // ---- prologue: epilogue table, ring rows of round 0 ----
+  if constexpr (EPI) {
+    // entry ((e*4 + p)*16 + q*4 + j) holds {-B_i[y][x] : s' = 0, 1} with x = 8(e>>1) + 2q +
+    // (e&1) (the Q_{i-1} column k-step e feeds), y = 8p + 2j + s'
+    double* bt = reinterpret_cast<double*>(smem + bt::kBtOff);
+    for (int idx = tid; idx < 1024; idx += bt::kThreads) {
+      const int sp = idx & 1, jj = (idx >> 1) & 3, qq = (idx >> 3) & 3, p = (idx >> 5) & 3, e = idx >> 7;
+      const int x = 8 * (e >> 1) + 2 * qq + (e & 1), y = 8 * p + 2 * jj + sp;
+      bt[idx] = -a.Bi[y * B + x];
+    }
+  }
+  for (int idx = tid; idx < kRingSpan * 16; idx += bt::kThreads) {
+    const int64_t rho = 16 * T0 + idx / 16;
+    *ring_ptr(rho, idx & 15) = *qsrc(rho, idx & 15);
+  }
+
+  // ---- per-wave state ----
+  // DEPTH register sets of A: set d holds tile tw + 4d; the tile a set finishes is replaced
+  // group by group with the tile 4*DEPTH further on (VAR bit 4: DEPTH 2)
+  constexpr int DEPTH = (VAR & 16) ? 2 : 1;
+  // tiles are stored in consumption order: slot ((round * grid + workgroup) * 4 + wave), so
+  // at any moment the whole chip sweeps one contiguous stretch of the format
+  const int64_t tslot0 = 4 * (int64_t)blockIdx.x;
+  const int64_t tslot_r = 4 * (int64_t)gridDim.x;
+  auto tile_a = [&](int64_t t, int g, int h) -> d2v {
+    const int64_t lt = t - T0;
+    const int64_t ts = (lt >> 2) * tslot_r + tslot0 + (lt & 3);
+    const d2v* p = reinterpret_cast<const d2v*>(a.A + ((((ts * NG + g) * 2 + h) * 64) + lane) * 2);
+    if constexpr (VAR & 1) return __builtin_nontemporal_load(p);
+    return *p;
+  };
+  auto clamp_t = [&](int64_t t) -> int64_t { return t < T1 ? t : T1 - 1; };
+  d2v av[DEPTH][NG][2];
+#pragma unroll
+  for (int d = 0; d < DEPTH; ++d)
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      av[d][g][0] = tile_a(clamp_t(T0 + wave + 4 * d), g, 0);
+      av[d][g][1] = tile_a(clamp_t(T0 + wave + 4 * d), g, 1);
+    }
+  auto qprev_row = [&](int64_t t) -> const d2v* {
+    int64_t r = 16 * t + i16;
+    r = r < a.nrows ? r : a.nrows - 1;
+    return reinterpret_cast<const d2v*>(a.Qprev + r * B + 2 * q);
+  };
+  d2v qp[4];
+  if constexpr (EPI) {
+#pragma unroll
+    for (int m = 0; m < 4; ++m) qp[m] = qprev_row(clamp_t(T0 + wave))[4 * m];
+  }
+  double ai[2][8];
+#pragma unroll
+  for (int x = 0; x < 2; ++x)
+#pragma unroll
+    for (int y = 0; y < 8; ++y) ai[x][y] = 0.0;
+
+  const unsigned lb = (unsigned)(q * bt::kRowBytes + 16 * j);                 // main-loop B
+  const unsigned lbt = (unsigned)(bt::kBtOff + 16 * (4 * q + j));             // epilogue B
+  const unsigned lus = (unsigned)(bt::kUOff + wave * bt::kUWave);             // U stage
+  const unsigned lai = (unsigned)(16 * bt::pi_slot(i16));                      // A_i A operand
+  __syncthreads();
+
+  // one round: this wave's tile tw (A in `avc`), then the ring rows of the next round
+  auto round = [&](int64_t R, int64_t tw, d2v (&avc)[NG][2]) {
+    // ring rows of the next round: 16 per wave, row 4i + q, slot i16
+    d2v st[4];
+    const int64_t rn = R + kRingSpan + 16 * wave;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) st[i] = *qsrc(rn + 4 * i + q, i16);
+
+    if (tw < T1) {  // wave-uniform
+      const int64_t tn = clamp_t(tw + 4 * DEPTH);
+      double acc[4][2];
+#pragma unroll
+      for (int p = 0; p < 4; ++p) acc[p][0] = acc[p][1] = 0.0;
+      if constexpr ((VAR & 12) == 0) {
+#pragma unroll
+        for (int g = 0; g < NG; ++g) {
+          const unsigned gb = (unsigned)((16 * (tw + g)) & (bt::kRing - 1)) * bt::kRowBytes + lb;
+          d2v bp[4][4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int p = 0; p < 4; ++p)
+              bp[u][p] = *reinterpret_cast<const d2v*>(smem + gb + u * 4 * bt::kRowBytes + 64 * p);
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const double av_u = (u & 1) ? avc[g][u >> 1].y : avc[g][u >> 1].x;
+#pragma unroll
+            for (int p = 0; p < 4; ++p) {
+              if constexpr (VAR & 32) {  // ablation: loads only
+                if (p == 0) acc[0][0] += av_u + bp[u][0].x;
+              } else {
+                acc[p][0] = mfma44(av_u, bp[u][p].x, acc[p][0]);
+                acc[p][1] = mfma44(av_u, bp[u][p].y, acc[p][1]);
+              }
+            }
+          }
+          avc[g][0] = tile_a(tn, g, 0);  // a later tile's group g into the freed registers
+          avc[g][1] = tile_a(tn, g, 1);
+        }
+      } else {
+        // k-steps flattened; the ring reads of k-step ks + D issue before the MFMAs of ks
+        constexpr int D = (VAR & 8) ? 2 : 1;
+        constexpr int KS = 4 * NG;
+        auto ldb = [&](int ks, d2v* bb) {
+          const unsigned gb = (unsigned)((16 * (tw + (ks >> 2))) & (bt::kRing - 1)) * bt::kRowBytes + lb;
+#pragma unroll
+          for (int p = 0; p < 4; ++p)
+            bb[p] = *reinterpret_cast<const d2v*>(smem + gb + (ks & 3) * 4 * bt::kRowBytes + 64 * p);
+        };
+        d2v bq[D + 1][4];
+#pragma unroll
+        for (int d = 0; d < D; ++d) ldb(d, bq[d]);
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+          if (ks + D < KS) ldb(ks + D, bq[(ks + D) % (D + 1)]);
+          const d2v* bb = bq[ks % (D + 1)];
+          const int g = ks >> 2, u = ks & 3;
+          const double av_u = (u & 1) ? avc[g][u >> 1].y : avc[g][u >> 1].x;
+#pragma unroll
+          for (int p = 0; p < 4; ++p) {
+            acc[p][0] = mfma44(av_u, bb[p].x, acc[p][0]);
+            acc[p][1] = mfma44(av_u, bb[p].y, acc[p][1]);
+          }
+          if (u == 3) {
+            avc[g][0] = tile_a(tn, g, 0);
+            avc[g][1] = tile_a(tn, g, 1);
+          }
+        }
+      }
+      if constexpr (EPI) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const double qv = (e & 1) ? qp[e >> 1].y : qp[e >> 1].x;
+#pragma unroll
+          for (int p = 0; p < 4; ++p) {
+            const d2v bv = *reinterpret_cast<const d2v*>(smem + lbt + 256 * (4 * e + p));
+            acc[p][0] = mfma44(qv, bv.x, acc[p][0]);
+            acc[p][1] = mfma44(qv, bv.y, acc[p][1]);
+          }
+        }
+#pragma unroll
+        for (int m = 0; m < 4; ++m) qp[m] = qprev_row(clamp_t(tw + 4))[4 * m];
+      }
+      const int64_t ru = 16 * tw + 4 * G + q;  // this lane's U row
+      d2v* urow = reinterpret_cast<d2v*>(a.U + ru * B + 2 * j);
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        const d2v uv = d2v{acc[p][0], acc[p][1]};
+        if constexpr (VAR & 2) __builtin_nontemporal_store(uv, urow + 4 * p);
+        else urow[4 * p] = uv;
+      }
+      if constexpr (AIG) {
+        // A_i += Q[tile rows]^T U[tile rows]: blocks = 4 x-quads, k = 4 tile rows, the
+        // B operand U[4ks + q][y] shared by the blocks — staged through LDS (D layout in)
+        const bool live = ru < a.nrows;
+#pragma unroll
+        for (int p = 0; p < 4; ++p)
+          *reinterpret_cast<d2v*>(smem + lus + (4 * G + q) * bt::kUStride + 16 * (4 * p + j)) =
+              live ? d2v{acc[p][0], acc[p][1]} : d2v{0.0, 0.0};
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) {
+          const int64_t rho = 16 * tw + H + 4 * ks + q;  // own rows, lane parity of q
+          const d2v aq = *reinterpret_cast<const d2v*>(
+              smem + (unsigned)(rho & (bt::kRing - 1)) * bt::kRowBytes + lai);
+#pragma unroll
+          for (int m = 0; m < 4; ++m) {
+            const d2v bu = *reinterpret_cast<const d2v*>(smem + lus + (4 * ks + q) * bt::kUStride + 16 * (4 * m + j));
+            ai[0][2 * m] = mfma44(aq.x, bu.x, ai[0][2 * m]);
+            ai[0][2 * m + 1] = mfma44(aq.x, bu.y, ai[0][2 * m + 1]);
+            ai[1][2 * m] = mfma44(aq.y, bu.x, ai[1][2 * m]);
+            ai[1][2 * m + 1] = mfma44(aq.y, bu.y, ai[1][2 * m + 1]);
+          }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) *ring_ptr(rn + 4 * i + q, i16) = st[i];
+    __syncthreads();
+  };
+
+  for (int64_t R = 16 * T0; R < 16 * T1; R += DEPTH * kRoundRows) {
+    const int64_t tw = R / 16 + wave;
+    round(R, tw, av[0]);
+    if constexpr (DEPTH == 2) {
+      if (R + kRoundRows < 16 * T1) round(R + kRoundRows, tw + 4, av[1]);
+    }
+  }
+
+  if constexpr (AIG) {
+    // sum the 4 waves' partials (ring area, free after the last barrier), wave 0 stores:
+    // lane holds A_i[x = 2 pi(4G + q) + xg][y = 8(yq >> 1) + 2j + (yq & 1)] in ai[xg][yq]
+    double* red = reinterpret_cast<double*>(smem);
+    if (wave > 0) {
+#pragma unroll
+      for (int x = 0; x < 2; ++x)
+#pragma unroll
+        for (int y = 0; y < 8; ++y) red[((wave - 1) * 16 + x * 8 + y) * 64 + lane] = ai[x][y];
+    }
+    __syncthreads();
+    if (wave == 0) {
+      double* out = a.ai_slab + (int64_t)blockIdx.x * B * B;
+      const int xb = 2 * bt::pi_slot(4 * G + q);
+#pragma unroll
+      for (int x = 0; x < 2; ++x)
+#pragma unroll
+        for (int y = 0; y < 8; ++y) {
+          double v = ai[x][y];
+#pragma unroll
+          for (int w = 0; w < 3; ++w) v += red[(w * 16 + x * 8 + y) * 64 + lane];
+          out[(xb + x) * B + 8 * (y >> 1) + 2 * j + (y & 1)] = v;
+        }
+    }
+  }
+}
+
+template <int NG, bool EPI, bool AIG, int VAR>
+static void launch_bt_v(const BtArgs& a, int grid, hipStream_t s) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_spmm_bt<NG, EPI, AIG, VAR>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, bt::kLds);
+    attr = true;
+  }
+  hipLaunchKernelGGL((k_spmm_bt<NG, EPI, AIG, VAR>), dim3(grid), dim3(bt::kThreads), bt::kLds, s, a);
+}
+template <int NG, bool EPI, bool AIG>
+static void launch_bt_t(const BtArgs& a, int grid, hipStream_t s) {
+  static const int var = [] {
+    const char* e = getenv("RBL_BT_VAR");
+    return e ? atoi(e) : -1;
+  }();
+  // default: non-temporal A loads and U stores (VAR 3): the format is read once per launch
+  // and U only by the next kernel — measured 7 % faster at C4a than the default policy
+  if constexpr (NG == 9 && EPI && AIG) {  // tuning variants (diagnostics)
+    switch (var) {
+      case 0: return launch_bt_v<NG, EPI, AIG, 0>(a, grid, s);
+      case 1: return launch_bt_v<NG, EPI, AIG, 1>(a, grid, s);
+      case 2: return launch_bt_v<NG, EPI, AIG, 2>(a, grid, s);
+      case 3: return launch_bt_v<NG, EPI, AIG, 3>(a, grid, s);
+      case 4: return launch_bt_v<NG, EPI, AIG, 4>(a, grid, s);
+      case 7: return launch_bt_v<NG, EPI, AIG, 7>(a, grid, s);
+      case 8: return launch_bt_v<NG, EPI, AIG, 8>(a, grid, s);
+      case 11: return launch_bt_v<NG, EPI, AIG, 11>(a, grid, s);
+      case 16: return launch_bt_v<NG, EPI, AIG, 16>(a, grid, s);
+      case 19: return launch_bt_v<NG, EPI, AIG, 19>(a, grid, s);
+      case 32: return launch_bt_v<NG, EPI, AIG, 32>(a, grid, s);
+      case 35: return launch_bt_v<NG, EPI, AIG, 35>(a, grid, s);
+      default: break;
+    }
+  }
+  launch_bt_v<NG, EPI, AIG, 3>(a, grid, s);
+}
+
+bool spmm_bt(const CsrDev& A, const double* Qin, int64_t col_off, int b, double* U,
+             const double* Qprev, const double* Bi, hipStream_t s, double* ai_slab, int* ai_parts) {
+  if (b != 32 || !A.bt || A.ntiles <= 0 || !(A.bt_ng == 5 || A.bt_ng == 9)) return false;
+  BtArgs a;
+  a.nrows = A.nrows;
+  a.ntiles = A.ntiles;
+  a.tiles_per_wg = A.bt_tiles_per_wg;
+  a.A = A.bt;
+  a.Q = Qin;
+  a.col_off = col_off;
+  a.q_lo = A.q_lo;
+  a.q_hi = A.q_hi;
+  a.zrow = A.zrow;
+  a.row0 = A.row0;
+  a.U = U;
+  a.Qprev = Qprev;
+  a.Bi = Bi;
+  const int grid = (int)((A.ntiles + A.bt_tiles_per_wg - 1) / A.bt_tiles_per_wg);
+  const bool epi = Qprev != nullptr;
+  const bool aig = ai_slab != nullptr;
+  a.ai_slab = ai_slab;
+  if (ai_parts) *ai_parts = aig ? grid : 0;
+  const int key = (A.bt_ng == 9 ? 4 : 0) | (epi ? 2 : 0) | (aig ? 1 : 0);
+  switch (key) {
+#define RBL_BT_CASE(K, NG, E, G) \
+    case K: launch_bt_t<NG, E, G>(a, grid, s); break;
+    RBL_BT_CASE(0, 5, false, false) RBL_BT_CASE(1, 5, false, true)
+    RBL_BT_CASE(2, 5, true, false)  RBL_BT_CASE(3, 5, true, true)
+    RBL_BT_CASE(4, 9, false, false) RBL_BT_CASE(5, 9, false, true)
+    RBL_BT_CASE(6, 9, true, false)  RBL_BT_CASE(7, 9, true, true)
+#undef RBL_BT_CASE
+  }
+  return true;
+}
+
+// ---- format (once per matrix) -----------------------------------------------------------
+// Scatter every nonzero (r, c) of the local CSR to its band-tile slot (zero-filled first);
+// duplicates add.  One wave per row.
+__global__ void k_bt_fill(int64_t nrows, const int64_t* __restrict__ rowptr,
+                          const int32_t* __restrict__ col, const double* __restrict__ val,
+                          int64_t row0, int H, int NG, int64_t tpw, int64_t grid,
+                          double* __restrict__ out) {
+  const int64_t r = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (r >= nrows) return;
+  const int64_t t = r >> 4;
+  const int64_t wg = t / tpw, lt = t % tpw;
+  const int64_t ts = ((lt >> 2) * grid + wg) * 4 + (lt & 3);  // consumption order
+  const int i = (int)(r & 15);
+  for (int64_t e = rowptr[r] + lane; e < rowptr[r + 1]; e += 64) {
+    const int rho = (int)((int64_t)col[e] - (row0 - H) - 16 * t);  // in [0, 16 + 2H)
+    const int g = rho >> 4, u = (rho >> 2) & 3, qq = rho & 3;
+    const int64_t idx = ((((ts * NG + g) * 2 + (u >> 1)) * 64) + 16 * qq + i) * 2 + (u & 1);
+    atomicAdd(out + idx, val[e]);
+  }
+}
+
+int64_t bt_tile_slots(int64_t ntiles, int64_t tpw) {
+  const int64_t grid = (ntiles + tpw - 1) / tpw;
+  return ((tpw + 3) / 4) * grid * 4;
+}
+
+void bt_fill(const CsrDev& A, int H, int NG, double* out, hipStream_t s) {
+  if (A.nrows <= 0) return;
+  const int64_t threads = A.nrows * 64;
+  const int64_t tpw = A.bt_tiles_per_wg, grid = (A.ntiles + tpw - 1) / tpw;
+  hipLaunchKernelGGL(k_bt_fill, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, A.nrows,
+                     A.rowptr, A.col, A.val, A.row0, H, NG, tpw, grid, out);
+}
+
+}  // namespace rbl

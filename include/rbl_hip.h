@@ -53,8 +53,10 @@ extern "C" {
 #define RBL_OPT_REORTH_ORDER  1   /* 0: block-CGS (batched, default); 1: ascending-j block MGS  */
                                   /*    exactly as RBL.jl:30-48 / RBL_gpu.jl:65-67               */
 #define RBL_OPT_SPMM_KERNEL   2   /* 0: auto; 1: global-gather CSR; 2: LDS-window CSR (DPP);
-                                   * 3: LDS band tiles on fp64 MFMA (falls back 3 -> 2 -> 1
-                                   * when the matrix does not fit the kernel's limits)         */
+                                   * 3: LDS-densified band on fp64 MFMA; 4: band-tile format
+                                   * (CSR densified once into MFMA operand order, b = 32,
+                                   * |c - r| <= 64); each falls back 4 -> 3 -> 2 -> 1 when
+                                   * the matrix does not fit the kernel's limits               */
 
 typedef struct rbl_ctx rbl_ctx;
 
@@ -113,8 +115,8 @@ int rbl_get_matrix_csr(rbl_ctx* ctx, int64_t* rowptr, int32_t* colind, double* v
  * halo exchange).  Allocates its own device buffers. */
 int rbl_apply(rbl_ctx* ctx, int b, const double* X, double* Y);
 /* Which SpMM kernel rbl_step / rbl_apply use for block size b under the current option:
- * 1 = global-gather CSR, 2 = LDS-window CSR (DPP), 3 = LDS band tiles on fp64 MFMA,
- * 4 = dense panel GEMM (rbl_set_matrix_dense). */
+ * 1 = global-gather CSR, 2 = LDS-window CSR (DPP), 3 = LDS-densified band on fp64 MFMA,
+ * 4 = dense panel GEMM (rbl_set_matrix_dense), 5 = band-tile format on fp64 MFMA. */
 int rbl_spmm_kernel_for(rbl_ctx* ctx, int b);
 
 /* ---- Krylov run -----------------------------------------------------------------------

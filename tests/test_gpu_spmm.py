@@ -33,17 +33,20 @@ def _rand_sym(n, density, seed, empty_rows=()):
 
 
 @pytest.mark.parametrize("b", [1, 5, 8, 16, 32, 64])
-@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
 def test_spmm_hashwindow(rbl, b, variant):
-    """variant 1 = gather, 2 = LDS window (DPP), 3 = LDS band tiles on MFMA, 0 = auto."""
+    """variant 1 = gather, 2 = LDS window (DPP), 3 = LDS-densified band on MFMA, 4 = band
+    tiles (MFMA operand order, spmm_bt.hip; kernel id 5), 0 = auto."""
     A = matgen.hashwindow_csr(7000, 64, 0.7734, 5, matgen.planted_spectrum(10))
     X = np.random.default_rng(b).standard_normal((A.shape[0], b))
     with rbl.Context(0) as ctx:
         ctx.set_matrix(A)
         ctx.set_option(2, variant)
         k = ctx.spmm_kernel_for(b)
-        if b in (16, 32):
-            assert k == {0: 3, 1: 1, 2: 2, 3: 3}[variant]   # the kernel under test really runs
+        if b == 32:
+            assert k == {0: 5, 1: 1, 2: 2, 3: 3, 4: 5}[variant]   # the kernel under test runs
+        elif b == 16:
+            assert k == {0: 3, 1: 1, 2: 2, 3: 3, 4: 3}[variant]
         else:
             assert k == 1
         Y = ctx.apply(X)
@@ -64,13 +67,13 @@ def test_spmm_window_ragged_and_partial_tiles(rbl, b):
         _check(A, Y, X)
         tile_nnz = np.diff(A.indptr[np.r_[np.arange(0, n, 16), n]]).max()
         if W <= 64 and tile_nnz <= 2048:     # the window kernel's metadata cap per tile
-            assert k in (2, 3), (n, W)
+            assert k in (2, 3, 5), (n, W)
         if tile_nnz > 2048:
-            assert k in (1, 3), (n, W)
+            assert k in (1, 3, 5), (n, W)
 
 
 @pytest.mark.parametrize("b", [16, 32])
-@pytest.mark.parametrize("variant", [2, 3])
+@pytest.mark.parametrize("variant", [2, 3, 4])
 def test_spmm_window_kernels_ragged(rbl, b, variant):
     """Both LDS kernels forced, on ragged tiles / narrow and wide bands / dense bands."""
     for n, W, p in [(1001, 3, 0.9), (333, 60, 0.5), (4099, 64, 1.0), (17, 8, 0.5), (2000, 30, 0.2)]:
@@ -100,7 +103,7 @@ def test_spmm_window_and_gather_agree_in_lanczos(rbl):
     """The whole block step is insensitive to the SpMM kernel choice (1e-12 on A_i)."""
     A = matgen.hashwindow_csr(6000, 64, 0.7734, 9, matgen.planted_spectrum(10))
     out = []
-    for variant in (1, 2, 3):
+    for variant in (1, 2, 3, 4):
         with rbl.Context(0) as ctx:
             ctx.set_matrix(A)
             ctx.set_option(2, variant)
@@ -109,3 +112,19 @@ def test_spmm_window_and_gather_agree_in_lanczos(rbl):
             out.append(info)
     for a1, a2 in zip(out[0].trace_A, out[1].trace_A):
         assert np.abs(a1 - a2).max() <= 1e-12 * np.abs(a1).max()
+
+
+@pytest.mark.parametrize("n,W,p,ng", [(7000, 64, 0.7734, 9), (5003, 30, 0.9, 5), (300, 60, 1.0, 9),
+                                      (100, 30, 1.0, 5), (17, 8, 0.5, 0), (4099, 64, 0.2, 0)])
+def test_spmm_band_tiles(rbl, n, W, p, ng):
+    """Band-tile kernel (spmm_bt.hip) at both band widths (H = 32: NG = 5 groups, H = 64: 9),
+    ragged last tiles and matrices smaller than one round; a sparse band (p = 0.2) must NOT
+    take it (its dense tiles would stream 3x the CSR bytes)."""
+    A = matgen.hashwindow_csr(n, W, p, n + 3)
+    X = np.random.default_rng(n).standard_normal((n, 32))
+    with rbl.Context(0) as ctx:
+        ctx.set_matrix(A)
+        k = ctx.spmm_kernel_for(32)
+        Y = ctx.apply(X)
+    assert (k == 5) == (ng > 0), (k, ng)
+    _check(A, Y, X)

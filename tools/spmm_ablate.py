@@ -9,9 +9,9 @@ n = int(sys.argv[1]) if len(sys.argv) > 1 else 10_000_000
 ctx = rbl.Context(0)
 ctx.gen_hashwindow(n, 64, 0.7734, 20261015, np.array([100.0 * (41 - l) for l in range(1, 41)]))
 ctx.set_option(0, 1)
-for rep in range(2):
+for rep in range(int(os.environ.get("REPS", "2"))):
     ctx.reset_timers()
     rbl.lanczos(ctx, 20, 32, seed=1, check=False, max_steps=8, ritz=False)
     ctx.synchronize()
 t = ctx.timers()
-print(os.environ.get("RBL_SPMM_ABLATE", "0"), "AQ ms per launch", t["AQ"] / 9)
+print(os.environ.get("RBL_SPMM_ABLATE", "0"), "AQ ms per launch", t["AQ"] / 9, flush=True)
