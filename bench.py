@@ -52,6 +52,11 @@ def parse():
     ap.add_argument("--no-ttk", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     ap.add_argument("--spmm-kernel", type=int, default=0)
+    ap.add_argument("--matrix", default="hashwindow", choices=("hashwindow", "rmat"),
+                    help="rmat: BASELINE config 4's power-law pattern (SURVEY §8(d) C4b)")
+    ap.add_argument("--rmat-scale", type=int, default=24)
+    ap.add_argument("--rmat-edges", type=int, default=0,
+                    help="R-MAT draws (0: 0.66 n x 100: ~1e9 nonzeros at n = 1e7 after merging)")
     ap.add_argument("--basis-bits", type=int, default=64, choices=(64, 32),
                     help="32: the mixed mode (fp32 Krylov basis + reorth on fp32 MFMA, fp64 A*Q / "
                          "3-term / QR) of BASELINE config 5, on this workload")
@@ -118,7 +123,12 @@ def main():
     n, b, k = args.n, args.b, args.k
     plant = np.array([100.0 * (2 * k + 1 - l) for l in range(1, 2 * k + 1)])
     t0 = time.perf_counter()
-    ctx.gen_hashwindow(n, args.halfwidth, args.density, args.seed, plant)
+    if args.matrix == "rmat":
+        if not args.rmat_edges:
+            args.rmat_edges = int(0.66 * 100 * n)
+        ctx.gen_rmat(n, args.rmat_scale, args.rmat_edges, args.seed, plant)
+    else:
+        ctx.gen_hashwindow(n, args.halfwidth, args.density, args.seed, plant)
     gen_s = time.perf_counter() - t0
     _, r0, r1, nnz_loc = ctx.matrix_info()
     nloc = r1 - r0
@@ -127,7 +137,8 @@ def main():
     ctx.set_option(_lib.RBL_OPT_SPMM_KERNEL, args.spmm_kernel)
     m_max = rbl.rbl_gpu.max_steps_for(args.kryl, b)
     spmm_kid = ctx.spmm_kernel_for(b)
-    spmm_kernel = {1: "gather", 2: "lds-window", 3: "lds-band-mfma", 5: "band-tile-mfma"}[spmm_kid]
+    spmm_kernel = {1: "gather", 2: "lds-window", 3: "lds-band-mfma", 5: "band-tile-mfma",
+                   6: "segmented-gather"}[spmm_kid]
 
     def one_run():
         rbl.lanczos(ctx, k, b, kryl_sz=args.kryl, seed=args.seed + 1, check=False, ritz=False,
@@ -171,7 +182,7 @@ def main():
         with open(args.traffic_json) as f:
             tj = json.load(f)
         if (tj.get("config", {}).get("n") == n and tj.get("config", {}).get("b") == b and world == 1
-                and args.basis_bits == 64):
+                and args.basis_bits == 64 and args.matrix == "hashwindow"):
             traffic = tj.get("spmm_hbm_bytes_per_launch")
             traffic_reorth = tj.get("part_reorth_hbm_bytes_per_run")
     except (OSError, ValueError):
@@ -227,11 +238,15 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f64" if args.basis_bits == 64 else "f64 (A*Q, 3-term, QR) + f32 (basis, reorth)",
-            "data": "synthetic (seeded hash-window symmetric matrix generated on device)",
-            "config": {"workload": "C4a hash-window SpMM-Lanczos" +
+            "data": f"synthetic (seeded {args.matrix} symmetric matrix generated on device)",
+            "config": {"workload": ("C4a hash-window SpMM-Lanczos" if args.matrix == "hashwindow"
+                                    else "C4b R-MAT SpMM-Lanczos") +
                        ("" if args.basis_bits == 64 else ", mixed precision (fp32 basis, config 5 mode)"),
-                       "n": n, "nnz": nnz, "b": b,
-                       "k": k, "halfwidth": args.halfwidth, "density": args.density,
+                       "n": n, "nnz": nnz, "b": b, "k": k, "matrix": args.matrix,
+                       **({"halfwidth": args.halfwidth, "density": args.density}
+                          if args.matrix == "hashwindow" else
+                          {"rmat_scale": args.rmat_scale, "rmat_edges": args.rmat_edges,
+                           "rmat_abcd": [0.57, 0.19, 0.19, 0.05]}),
                        "block_steps_per_run": m_max, "parallelism": f"rows{world}"},
             "roofline": roofline,
             "roofline_secondary": roofline2,
@@ -258,7 +273,11 @@ def cpu_baseline(args, m_max, plant):
     except Exception:
         threads = 1
     ns = args.cpu_sample_n
-    A = matgen.hashwindow_csr(ns, args.halfwidth, args.density, args.seed, plant)
+    if args.matrix == "rmat":  # same draw density per row, ids scaled down with n
+        sc = max(1, int(math.ceil(math.log2(ns))))
+        A = matgen.rmat_csr(ns, sc, int(args.rmat_edges * ns / args.n), args.seed, plant)
+    else:
+        A = matgen.hashwindow_csr(ns, args.halfwidth, args.density, args.seed, plant)
     omega = np.random.default_rng(0).standard_normal((ns, args.b))
     t0 = time.perf_counter()
     o.RBL_gpu_semantics(A, args.k, args.b, omega=omega, kryl_sz=args.kryl, check=False)

@@ -59,7 +59,21 @@ struct CsrDev {
   int64_t bt_tiles_per_wg = 0;
   int64_t q_lo = 0, q_hi = 0;
   const double* zrow = nullptr;
+  // segmented gather (spmm.hip variant 5): wave tasks (first row, info: > 0 rows of a packed
+  // short-row task, < 0 -(slot+1) of a long-row segment), segment slots' first nonzero
+  // (slot_k0, nslots + 1 entries), long rows with their first slot (lslot, nlong + 1), and a
+  // scratch of nslots x 32 partial rows
+  int64_t seg_ntasks = 0;
+  const int64_t* seg_trow = nullptr;
+  const int32_t* seg_tinfo = nullptr;
+  const int64_t* seg_slot_k0 = nullptr;
+  int64_t seg_nlong = 0;
+  const int64_t* seg_lrow = nullptr;
+  const int64_t* seg_lslot = nullptr;
+  double* seg_scratch = nullptr;
 };
+constexpr int64_t kSegLen = 4096;   // nonzeros per long-row segment
+constexpr int64_t kSegPack = 512;   // nonzeros per packed short-row task (<= 64 rows)
 
 // --- rowop.hip ---------------------------------------------------------------------------
 // Y' = beta Y + alpha X C (X, Y: n x b panels, C: b x b row-major, ldc) in one pass, and if
@@ -72,13 +86,15 @@ void rowgram(int64_t nrows, int b, const double* X, const double* C, int ldc, do
 
 // --- spmm.hip ----------------------------------------------------------------------------
 // U = A * Qin  (+ epilogue U -= Qprev * Bt^T with Bt = B_i row-major b x b, if Qprev).
-// variant: 0 auto, 1 global gather, 2 LDS window, 3 LDS band (MFMA), 4 band tiles (MFMA).
+// variant: 0 auto, 1 global gather, 2 LDS window, 3 LDS band (MFMA), 4 band tiles (MFMA),
+// 5 segmented gather (b in {16, 32}).
 // ai_slab: if non-null and the band kernel runs with band_gram, it also forms the partials
 // of A_i = Qin[own rows]^T U (b x b per workgroup) there; returns how many (0: not formed).
 int spmm(const CsrDev& A, const double* Qin, int64_t col_off, int b, double* U,
          const double* Qprev, const double* Bi, int variant, hipStream_t s,
          double* ai_slab = nullptr);
 
+bool spmm_seg_ok(const CsrDev& A, int b);
 // spmm_window.hip: persistent LDS-window kernel (b in {16,32}); false if not applicable.
 bool spmm_window(const CsrDev& A, const double* Qin, int64_t col_off, int b, double* U,
                  const double* Qprev, const double* Bi, hipStream_t s);
@@ -159,6 +175,26 @@ void chol_step(const double* G, int b, int64_t nglobal, int mode, double* R, dou
 void copy_small(const double* src, double* dst, int64_t len, hipStream_t s);
 // dst = src^T (b x b row-major).
 void transpose_small(const double* src, double* dst, int b, hipStream_t s);
+
+// --- gen_rmat.hip (R-MAT generator) -------------------------------------
+struct RmatParams {
+  int64_t n = 0;
+  int scale = 0;
+  int64_t edges = 0;
+  double a = 0.57, b = 0.19, c = 0.19;
+  uint64_t seed = 0;
+};
+// deg[r] += 1 per kept draw endpoint (duplicates counted; zero-filled deg of n int32)
+void rmat_degree(const RmatParams& p, int32_t* deg, hipStream_t s);
+// local CSR of rows [r0, r1): rowptr_dev (m+1, caller-allocated), col/val allocated here (with
+// kCsrPad zero entries); max_keys >= the own rows' kept draw endpoints.  0 or a negative status.
+int rmat_local_csr(const RmatParams& p, int64_t r0, int64_t r1, int64_t max_keys, int nplant,
+                   const double* plant_dev, int64_t* rowptr_dev, int32_t** col_dev,
+                   double** val_dev, int64_t* nnz_out, hipStream_t s);
+// per-rank column footprint of a local CSR: lo[q] = min, hi[q] = max + 1 (atomics; lo/hi
+// initialised to ~0 / 0), bounds_dev = the P+1 row boundaries
+void col_footprint(const int32_t* col, int64_t nnz, const int64_t* bounds_dev, int P,
+                   unsigned long long* lo, unsigned long long* hi, hipStream_t s);
 
 // --- gen.hip ---------------------------------------------------------------------------
 // Hash-window matrix rows [r0,r1): counts per row, then fill given rowptr (0-based, local).

@@ -40,6 +40,14 @@ struct rbl_ctx {
   double* d_bt = nullptr;      // band-tile kernel: the CSR in MFMA-ordered 16-row band tiles
   int bt_ng = 0;               // its band groups (0: not applicable)
   double* d_zrow = nullptr;    // 32 zeros: band rows the halo does not hold
+  // segmented-gather task table (spmm.hip variant 5; CsrDev::seg_*)
+  int64_t seg_ntasks = 0, seg_nlong = 0;
+  int64_t* d_seg_trow = nullptr;
+  int32_t* d_seg_tinfo = nullptr;
+  int64_t* d_seg_slot_k0 = nullptr;
+  int64_t* d_seg_lrow = nullptr;
+  int64_t* d_seg_lslot = nullptr;
+  double* d_seg_scratch = nullptr;
   // dense A (RBL_gpu(A::Matrix{Float64})): local rows in 32-column row-major panels
   // (panel p = columns [32p, 32p+32), zero past n), multiplied by tsmm44 against d_qfull
   // (all n rows of Q, zero-padded to 32 * dense_panels rows, b <= 64 columns)
@@ -152,13 +160,77 @@ CsrDev csr(rbl_ctx* ctx) {
   A.q_lo = ctx->nranks > 1 ? ctx->ext_lo : ctx->r0;
   A.q_hi = ctx->nranks > 1 ? ctx->ext_hi : ctx->r0 + ctx->nloc;
   A.zrow = ctx->d_zrow;
+  A.seg_ntasks = ctx->seg_ntasks;
+  A.seg_trow = ctx->d_seg_trow;
+  A.seg_tinfo = ctx->d_seg_tinfo;
+  A.seg_slot_k0 = ctx->d_seg_slot_k0;
+  A.seg_nlong = ctx->seg_nlong;
+  A.seg_lrow = ctx->d_seg_lrow;
+  A.seg_lslot = ctx->d_seg_lslot;
+  A.seg_scratch = ctx->d_seg_scratch;
   return A;
+}
+
+// Task table of the segmented gather (spmm.hip variant 5): short rows packed into tasks of
+// <= kSegPack nonzeros and <= 64 rows, rows over kSegLen nonzeros cut into segments.
+int prepare_segments(rbl_ctx* ctx, const std::vector<int64_t>& rp) {
+  const int64_t m = ctx->nloc;
+  if (m <= 0 || ctx->nnz <= 0) return RBL_OK;
+  std::vector<int64_t> trow, slot_k0, lrow, lslot;
+  std::vector<int32_t> tinfo;
+  int64_t cur_r0 = 0, cur_nnz = 0;
+  int cur_rows = 0;
+  auto flush = [&]() {
+    if (cur_rows) {
+      trow.push_back(cur_r0);
+      tinfo.push_back(cur_rows);
+    }
+    cur_rows = 0;
+    cur_nnz = 0;
+  };
+  for (int64_t r = 0; r < m; ++r) {
+    const int64_t d = rp[r + 1] - rp[r];
+    if (d > kSegLen) {
+      flush();
+      lrow.push_back(r);
+      lslot.push_back((int64_t)slot_k0.size());
+      for (int64_t k = rp[r]; k < rp[r + 1]; k += kSegLen) {
+        trow.push_back(r);
+        tinfo.push_back(-(int32_t)(slot_k0.size() + 1));
+        slot_k0.push_back(k);
+      }
+      continue;
+    }
+    if (cur_rows && (cur_nnz + d > kSegPack || cur_rows == 64)) flush();
+    if (!cur_rows) cur_r0 = r;
+    ++cur_rows;
+    cur_nnz += d;
+  }
+  flush();
+  lslot.push_back((int64_t)slot_k0.size());
+  slot_k0.push_back(INT64_MAX);
+  ctx->seg_ntasks = (int64_t)trow.size();
+  ctx->seg_nlong = (int64_t)lrow.size();
+  HIPC(hipMalloc(&ctx->d_seg_trow, trow.size() * sizeof(int64_t)));
+  HIPC(hipMalloc(&ctx->d_seg_tinfo, tinfo.size() * sizeof(int32_t)));
+  HIPC(hipMalloc(&ctx->d_seg_slot_k0, slot_k0.size() * sizeof(int64_t)));
+  HIPC(hipMalloc(&ctx->d_seg_lslot, lslot.size() * sizeof(int64_t)));
+  HIPC(hipMalloc(&ctx->d_seg_lrow, std::max<size_t>(lrow.size(), 1) * sizeof(int64_t)));
+  HIPC(hipMalloc(&ctx->d_seg_scratch, std::max<size_t>(slot_k0.size() - 1, 1) * 32 * sizeof(double)));
+  HIPC(hipMemcpy(ctx->d_seg_trow, trow.data(), trow.size() * sizeof(int64_t), hipMemcpyHostToDevice));
+  HIPC(hipMemcpy(ctx->d_seg_tinfo, tinfo.data(), tinfo.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+  HIPC(hipMemcpy(ctx->d_seg_slot_k0, slot_k0.data(), slot_k0.size() * sizeof(int64_t), hipMemcpyHostToDevice));
+  HIPC(hipMemcpy(ctx->d_seg_lslot, lslot.data(), lslot.size() * sizeof(int64_t), hipMemcpyHostToDevice));
+  if (!lrow.empty())
+    HIPC(hipMemcpy(ctx->d_seg_lrow, lrow.data(), lrow.size() * sizeof(int64_t), hipMemcpyHostToDevice));
+  return RBL_OK;
 }
 
 // Per-16-row-tile column footprint for the LDS-window SpMM and the checks that every tile
 // fits its ring (spmm_window.hip): columns sorted per row, footprints non-decreasing, a
 // tile's nonzeros <= 2048, ring rows: 256 (b=32) / 512 (b=16), new rows per tile <= 32 / 64.
 int prepare_window(rbl_ctx* ctx, const std::vector<int64_t>& rp) {
+  CHK(prepare_segments(ctx, rp));
   ctx->window_ok16 = ctx->window_ok32 = false;
   ctx->band_ok16 = ctx->band_ok32 = false;
   ctx->band_gram = false;
@@ -645,6 +717,13 @@ void free_matrix(rbl_ctx* ctx) {
   hipFree(ctx->d_bt); ctx->d_bt = nullptr;
   hipFree(ctx->d_zrow); ctx->d_zrow = nullptr;
   ctx->bt_ng = 0;
+  hipFree(ctx->d_seg_trow); ctx->d_seg_trow = nullptr;
+  hipFree(ctx->d_seg_tinfo); ctx->d_seg_tinfo = nullptr;
+  hipFree(ctx->d_seg_slot_k0); ctx->d_seg_slot_k0 = nullptr;
+  hipFree(ctx->d_seg_lrow); ctx->d_seg_lrow = nullptr;
+  hipFree(ctx->d_seg_lslot); ctx->d_seg_lslot = nullptr;
+  hipFree(ctx->d_seg_scratch); ctx->d_seg_scratch = nullptr;
+  ctx->seg_ntasks = ctx->seg_nlong = 0;
   hipFree(ctx->d_dense); ctx->d_dense = nullptr;
   hipFree(ctx->d_qfull); ctx->d_qfull = nullptr;
   ctx->dense = false;
@@ -828,7 +907,7 @@ int rbl_set_option(rbl_ctx* ctx, int option, int64_t value) {
       ctx->reorth_order = (int)value;
       return RBL_OK;
     case RBL_OPT_SPMM_KERNEL:
-      if (value < 0 || value > 4) return fail(ctx, RBL_ERR_INVALID, "spmm kernel must be 0..4");
+      if (value < 0 || value > 5) return fail(ctx, RBL_ERR_INVALID, "spmm kernel must be 0..5");
       ctx->spmm_variant = (int)value;
       return RBL_OK;
     default: return fail(ctx, RBL_ERR_INVALID, "unknown option");
@@ -993,6 +1072,94 @@ int rbl_gen_matrix_hashwindow(rbl_ctx* ctx, int64_t n, int64_t halfwidth, double
   return setup_halo(ctx);
 }
 
+int rbl_gen_matrix_rmat(rbl_ctx* ctx, int64_t n, int scale, int64_t edges, double a, double b,
+                        double c, uint64_t seed, int nplant, const double* plant) {
+  if (!ctx || n < 1 || scale < 1 || scale > 31 || ((int64_t)1 << scale) < n || edges < 0 ||
+      a < 0 || b < 0 || c < 0 || a + b + c > 1.0 || nplant < 0 || (nplant > 0 && !plant) ||
+      n > INT32_MAX)
+    return fail(ctx, RBL_ERR_INVALID, "rbl_gen_matrix_rmat: bad arguments");
+  if (ctx->nranks > 16) return fail(ctx, RBL_ERR_INVALID, "rbl_gen_matrix_rmat: at most 16 ranks");
+  HIPC(hipSetDevice(ctx->device));
+  free_run(ctx);
+  free_matrix(ctx);
+  RmatParams p;
+  p.n = n;
+  p.scale = scale;
+  p.edges = edges;
+  p.a = a;
+  p.b = b;
+  p.c = c;
+  p.seed = seed;
+  // degrees of every row (all ranks draw every edge): they size the key buffer and balance
+  // the row split by nonzeros (R-MAT's low ids are its hubs)
+  int32_t* d_deg = nullptr;
+  HIPC(hipMalloc(&d_deg, n * sizeof(int32_t)));
+  HIPC(hipMemsetAsync(d_deg, 0, n * sizeof(int32_t), ctx->stream));
+  rmat_degree(p, d_deg, ctx->stream);
+  HIPC(hipGetLastError());
+  std::vector<int32_t> deg(n);
+  HIPC(hipMemcpyAsync(deg.data(), d_deg, n * sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
+  HIPC(hipStreamSynchronize(ctx->stream));
+  hipFree(d_deg);
+  const int P = ctx->nranks;
+  std::vector<int64_t> pre(n + 1, 0);  // nonzeros (with duplicates) + diagonal, prefix
+  for (int64_t r = 0; r < n; ++r) pre[r + 1] = pre[r] + deg[r] + 1;
+  ctx->bounds.assign(P + 1, 0);
+  ctx->bounds[P] = n;
+  for (int q = 1; q < P; ++q) {
+    const int64_t target = pre[n] * q / P;
+    ctx->bounds[q] = std::lower_bound(pre.begin(), pre.end(), target) - pre.begin();
+    ctx->bounds[q] = std::max(ctx->bounds[q], ctx->bounds[q - 1]);
+  }
+  const int64_t r0 = ctx->bounds[ctx->rank], r1 = ctx->bounds[ctx->rank + 1], m = r1 - r0;
+  ctx->n = n;
+  ctx->r0 = r0;
+  ctx->r1 = r1;
+  ctx->nloc = m;
+  int64_t own = 0;
+  for (int64_t r = r0; r < r1; ++r) own += deg[r];
+  double* d_plant = nullptr;
+  if (nplant > 0) {
+    HIPC(hipMalloc(&d_plant, nplant * sizeof(double)));
+    HIPC(hipMemcpy(d_plant, plant, nplant * sizeof(double), hipMemcpyHostToDevice));
+  }
+  HIPC(hipMalloc(&ctx->d_rowptr, (m + 1) * sizeof(int64_t)));
+  int64_t nnz = 0;
+  const int st = rmat_local_csr(p, r0, r1, own, nplant, d_plant, ctx->d_rowptr, &ctx->d_col,
+                                &ctx->d_val, &nnz, ctx->stream);
+  hipFree(d_plant);
+  if (st == -1) return fail(ctx, RBL_ERR_INVALID, "rbl_gen_matrix_rmat: > 2^31 keys on one rank");
+  if (st < 0) return fail(ctx, st == -3 ? RBL_ERR_OOM : RBL_ERR_HIP, "rbl_gen_matrix_rmat: device generation failed");
+  ctx->nnz = nnz;
+  std::vector<int64_t> rp(m + 1);
+  HIPC(hipMemcpy(rp.data(), ctx->d_rowptr, (m + 1) * sizeof(int64_t), hipMemcpyDeviceToHost));
+  ctx->need_lo.assign(P, 0);
+  ctx->need_hi.assign(P, 0);
+  if (P > 1 && nnz > 0) {
+    int64_t* d_b = nullptr;
+    unsigned long long* d_lh = nullptr;
+    HIPC(hipMalloc(&d_b, (P + 1) * sizeof(int64_t)));
+    HIPC(hipMalloc(&d_lh, 2 * P * sizeof(unsigned long long)));
+    std::vector<unsigned long long> lh(2 * P);
+    for (int q = 0; q < P; ++q) { lh[q] = ~0ull; lh[P + q] = 0ull; }
+    HIPC(hipMemcpy(d_b, ctx->bounds.data(), (P + 1) * sizeof(int64_t), hipMemcpyHostToDevice));
+    HIPC(hipMemcpy(d_lh, lh.data(), 2 * P * sizeof(unsigned long long), hipMemcpyHostToDevice));
+    col_footprint(ctx->d_col, nnz, d_b, P, d_lh, d_lh + P, ctx->stream);
+    HIPC(hipGetLastError());
+    HIPC(hipMemcpyAsync(lh.data(), d_lh, 2 * P * sizeof(unsigned long long), hipMemcpyDeviceToHost, ctx->stream));
+    HIPC(hipStreamSynchronize(ctx->stream));
+    hipFree(d_b);
+    hipFree(d_lh);
+    for (int q = 0; q < P; ++q) {
+      if (q == ctx->rank || lh[P + q] == 0ull) continue;
+      ctx->need_lo[q] = (int64_t)lh[q];
+      ctx->need_hi[q] = (int64_t)lh[P + q];
+    }
+  }
+  CHK(prepare_window(ctx, rp));
+  return setup_halo(ctx);
+}
+
 int rbl_matrix_info(rbl_ctx* ctx, int64_t* n, int64_t* row_begin, int64_t* row_end,
                     int64_t* nnz_local) {
   if (!ctx) return RBL_ERR_INVALID;
@@ -1026,6 +1193,7 @@ int rbl_spmm_kernel_for(rbl_ctx* ctx, int b) {
   if ((v == 0 || v == 4) && b == 32 && (ctx->bt_ng == 5 || ctx->bt_ng == 9)) return 5;
   if ((v == 0 || v == 3 || v == 4) && band) return 3;
   if ((v == 0 || v == 2 || v == 3) && win) return 2;
+  if ((v == 0 || v == 5) && ctx->seg_ntasks > 0 && (b == 16 || b == 32)) return 6;
   return 1;
 }
 

@@ -58,6 +58,123 @@ __global__ __launch_bounds__(256) void k_spmm_gather(int64_t nrows, const int64_
   }
 }
 
+// ----------------------------------------------------------------------------------------
+// Variant 5 — segmented gather for unstructured power-law patterns (R-MAT),
+// b in {16, 32}.  A per-matrix task table (CsrDev::seg_*) packs short rows into wave tasks of
+// <= kSegPack nonzeros and cuts every row longer than kSegLen nonzeros into segments of its
+// own tasks, so one hub row (R-MAT's vertex 0 has ~1e6 neighbours at C4b) no longer holds a
+// single wave for the whole launch.  A lane group of BP lanes (one per column) owns a row:
+// lane c loads entry k + c of a BP-entry chunk (coalesced col/val), then the group walks the
+// chunk 8 entries at a time, broadcasting each (col, val) by __shfl and issuing the 8 Q-row
+// gathers back to back.  Segments write partial rows to `scratch`; k_seg_fixup sums each long
+// row's segments in order (deterministic) and applies the 3-term epilogue there.
+// ----------------------------------------------------------------------------------------
+template <int BP>
+__global__ __launch_bounds__(256) void k_spmm_seg(
+    int64_t ntasks, const int64_t* __restrict__ trow, const int32_t* __restrict__ tinfo,
+    const int64_t* __restrict__ rowptr, const int32_t* __restrict__ col,
+    const double* __restrict__ val, const double* __restrict__ Q, int64_t col_off,
+    double* __restrict__ U, double* __restrict__ scratch, const int64_t* __restrict__ slot_k0,
+    const double* __restrict__ Qprev, const double* __restrict__ Bi) {
+  constexpr int R = kWave / BP;
+  const int lane = threadIdx.x & 63;
+  const int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (t >= ntasks) return;
+  const int h = lane / BP, c = lane % BP;
+  const int64_t r0 = trow[t];
+  const int info = tinfo[t];
+  // nonzeros [k, e) of one row, lane c: column c; chunks of BP entries, k stepping by `step`
+  auto dot = [&](int64_t k, int64_t e, int64_t step) -> double {
+    double acc0 = 0.0, acc1 = 0.0;
+    for (; k < e; k += step) {
+      const int64_t kk = k + c;
+      const bool ok = kk < e;
+      const int cl = ok ? col[kk] : (int)col_off;  // padding: Q row 0 times 0
+      const double vl = ok ? val[kk] : 0.0;
+      const int cnt = e - k < BP ? (int)(e - k) : BP;
+      for (int j0 = 0; j0 < cnt; j0 += 8) {
+        double q[8], v[8];
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) {
+          const int cj = __shfl(cl, j0 + jj, BP);
+          v[jj] = __shfl(vl, j0 + jj, BP);
+          q[jj] = Q[(int64_t)(cj - col_off) * BP + c];
+        }
+#pragma unroll
+        for (int jj = 0; jj < 8; jj += 2) {
+          acc0 = fma(v[jj], q[jj], acc0);
+          acc1 = fma(v[jj + 1], q[jj + 1], acc1);
+        }
+      }
+    }
+    return acc0 + acc1;
+  };
+  if (info > 0) {
+    double bt[BP];  // epilogue operand B_i[c][t]
+    if (Qprev) {
+#pragma unroll
+      for (int u = 0; u < BP; ++u) bt[u] = Bi[c * BP + u];
+    }
+    for (int rr = h; rr < info; rr += R) {  // lane-group-uniform row loop
+      const int64_t row = r0 + rr;
+      double acc = dot(rowptr[row], rowptr[row + 1], BP);
+      if (Qprev) {
+        const double qv = Qprev[row * BP + c];
+#pragma unroll
+        for (int u = 0; u < BP; ++u) acc = fma(-__shfl(qv, u, BP), bt[u], acc);
+      }
+      U[row * BP + c] = acc;
+    }
+  } else {
+    const int64_t slot = -(int64_t)info - 1;
+    const int64_t k0 = slot_k0[slot], k1 = slot_k0[slot + 1];
+    const int64_t e = rowptr[r0 + 1] < k1 ? rowptr[r0 + 1] : k1;
+    double acc = dot(k0 + (int64_t)h * BP, e, (int64_t)R * BP);
+#pragma unroll
+    for (int m = BP; m < kWave; m <<= 1) acc += __shfl_xor(acc, m, kWave);
+    if (h == 0) scratch[slot * BP + c] = acc;
+  }
+}
+
+// long rows: the sum of their segments in slot order, then the 3-term epilogue
+template <int BP>
+__global__ __launch_bounds__(256) void k_seg_fixup(int64_t nlong, const int64_t* __restrict__ lrow,
+                                                  const int64_t* __restrict__ lslot,
+                                                  const double* __restrict__ scratch,
+                                                  double* __restrict__ U,
+                                                  const double* __restrict__ Qprev,
+                                                  const double* __restrict__ Bi) {
+  constexpr int R = kWave / BP;
+  const int lane = threadIdx.x & 63;
+  const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / BP;
+  (void)R;
+  if (i >= nlong) return;
+  const int c = lane % BP;
+  const int64_t row = lrow[i];
+  double acc = 0.0;
+  for (int64_t sl = lslot[i]; sl < lslot[i + 1]; ++sl) acc += scratch[sl * BP + c];
+  if (Qprev) {
+    for (int u = 0; u < BP; ++u) acc = fma(-Qprev[row * BP + u], Bi[c * BP + u], acc);
+  }
+  U[row * BP + c] = acc;
+}
+
+template <int BP>
+static void launch_seg(const CsrDev& A, const double* Q, int64_t off, double* U,
+                       const double* Qprev, const double* Bi, hipStream_t s) {
+  const int64_t blocks = (A.seg_ntasks + 3) / 4;
+  hipLaunchKernelGGL((k_spmm_seg<BP>), dim3((unsigned)blocks), dim3(256), 0, s, A.seg_ntasks,
+                     A.seg_trow, A.seg_tinfo, A.rowptr, A.col, A.val, Q, off, U, A.seg_scratch,
+                     A.seg_slot_k0, Qprev, Bi);
+  if (A.seg_nlong > 0) {
+    const int64_t th = A.seg_nlong * BP;
+    hipLaunchKernelGGL((k_seg_fixup<BP>), dim3((unsigned)((th + 255) / 256)), dim3(256), 0, s,
+                       A.seg_nlong, A.seg_lrow, A.seg_lslot, A.seg_scratch, U, Qprev, Bi);
+  }
+}
+
+bool spmm_seg_ok(const CsrDev& A, int b) { return A.seg_ntasks > 0 && (b == 16 || b == 32); }
+
 template <int BP>
 static void launch_gather(const CsrDev& A, const double* Q, int64_t off, int b, double* U,
                           const double* Qprev, const double* Bi, hipStream_t s) {
@@ -69,8 +186,8 @@ static void launch_gather(const CsrDev& A, const double* Q, int64_t off, int b, 
 int spmm(const CsrDev& A, const double* Qin, int64_t col_off, int b, double* U,
          const double* Qprev, const double* Bi, int variant, hipStream_t s, double* ai_slab) {
   if (A.nrows <= 0) return 0;
-  // 0 auto: band tiles > band (MFMA) > window (DPP) > gather;  1 gather;  2 window;  3 band;
-  // 4 band tiles
+  // 0 auto: band tiles > band (MFMA) > window (DPP) > segmented gather > gather;  1 gather;
+  // 2 window;  3 band;  4 band tiles;  5 segmented gather
   int parts = 0;
   if ((variant == 0 || variant == 4) &&
       spmm_bt(A, Qin, col_off, b, U, Qprev, Bi, s, ai_slab, &parts))
@@ -81,6 +198,11 @@ int spmm(const CsrDev& A, const double* Qin, int64_t col_off, int b, double* U,
   if ((variant == 0 || variant == 2 || variant == 3) &&
       spmm_window(A, Qin, col_off, b, U, Qprev, Bi, s))
     return 0;
+  if ((variant == 0 || variant == 5) && spmm_seg_ok(A, b)) {
+    if (b == 32) launch_seg<32>(A, Qin, col_off, U, Qprev, Bi, s);
+    else launch_seg<16>(A, Qin, col_off, U, Qprev, Bi, s);
+    return 0;
+  }
   if (b <= 1) launch_gather<1>(A, Qin, col_off, b, U, Qprev, Bi, s);
   else if (b <= 2) launch_gather<2>(A, Qin, col_off, b, U, Qprev, Bi, s);
   else if (b <= 4) launch_gather<4>(A, Qin, col_off, b, U, Qprev, Bi, s);

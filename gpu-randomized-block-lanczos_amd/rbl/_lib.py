@@ -52,6 +52,8 @@ SIGNATURES = {
     "rbl_set_matrix_csr_rows": (C.c_int, [_p, _i64, _i64, _i64, _pi64, _pi64, _pd, C.c_int]),
     "rbl_set_matrix_dense": (C.c_int, [_p, _i64, _i64, _i64, _pd, _i64]),
     "rbl_gen_matrix_hashwindow": (C.c_int, [_p, _i64, _i64, C.c_double, _u64, C.c_int, _pd]),
+    "rbl_gen_matrix_rmat": (C.c_int, [_p, _i64, C.c_int, _i64, C.c_double, C.c_double, C.c_double,
+                                      _u64, C.c_int, _pd]),
     "rbl_matrix_info": (C.c_int, [_p, _pi64, _pi64, _pi64, _pi64]),
     "rbl_get_matrix_csr": (C.c_int, [_p, _pi64, _pi32, _pd]),
     "rbl_apply": (C.c_int, [_p, C.c_int, _pd, _pd]),

@@ -149,6 +149,14 @@ class Context:
                                                   plant.size, dptr(plant) if plant.size else None),
                     "rbl_gen_matrix_hashwindow")
 
+    def gen_rmat(self, n: int, scale: int, edges: int, seed: int, plant=None,
+                 a: float = 0.57, b: float = 0.19, c: float = 0.19) -> None:
+        """Seeded symmetric R-MAT matrix generated on the device."""
+        plant = np.ascontiguousarray(plant if plant is not None else np.zeros(0), np.float64)
+        self._check(lib.rbl_gen_matrix_rmat(self._h, n, scale, edges, a, b, c, seed, plant.size,
+                                            dptr(plant) if plant.size else None),
+                    "rbl_gen_matrix_rmat")
+
     def matrix_info(self):
         v = [np.zeros(1, np.int64) for _ in range(4)]
         self._check(lib.rbl_matrix_info(self._h, *[i64ptr(x) for x in v]), "rbl_matrix_info")

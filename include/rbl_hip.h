@@ -56,7 +56,8 @@ extern "C" {
                                    * 3: LDS-densified band on fp64 MFMA; 4: band-tile format
                                    * (CSR densified once into MFMA operand order, b = 32,
                                    * |c - r| <= 64); each falls back 4 -> 3 -> 2 -> 1 when
-                                   * the matrix does not fit the kernel's limits               */
+                                   * the matrix does not fit the kernel's limits; 5: segmented
+                                   * gather (power-law rows split / packed, b in {16, 32})     */
 
 typedef struct rbl_ctx rbl_ctx;
 
@@ -106,6 +107,14 @@ int rbl_set_matrix_dense(rbl_ctx* ctx, int64_t n, int64_t row_begin, int64_t row
  * l*floor(n/nplant) for l < nplant.  Each rank generates only its own rows. */
 int rbl_gen_matrix_hashwindow(rbl_ctx* ctx, int64_t n, int64_t halfwidth, double density,
                               uint64_t seed, int nplant, const double* plant);
+/* Device-side generator of the seeded symmetric R-MAT matrix (BASELINE
+ * config 4): `edges` draws descend `scale` levels with quadrant probabilities (a, b, c,
+ * 1-a-b-c); draws with an id >= n or a self loop are dropped, the rest enter as (r,c) and
+ * (c,r), duplicates merged; off-diagonal values 2u-1 from the pair hash (as hash-window),
+ * every diagonal entry present (hash value + planted spectrum, as hash-window).  Rows are
+ * split over the ranks by nonzeros.  NumPy restatement: oracle/matgen.py rmat_csr. */
+int rbl_gen_matrix_rmat(rbl_ctx* ctx, int64_t n, int scale, int64_t edges, double a, double b,
+                        double c, uint64_t seed, int nplant, const double* plant);
 int rbl_matrix_info(rbl_ctx* ctx, int64_t* n, int64_t* row_begin, int64_t* row_end,
                     int64_t* nnz_local);
 /* Download the local CSR (0-based) — test/inspection only. */
@@ -116,7 +125,8 @@ int rbl_get_matrix_csr(rbl_ctx* ctx, int64_t* rowptr, int32_t* colind, double* v
 int rbl_apply(rbl_ctx* ctx, int b, const double* X, double* Y);
 /* Which SpMM kernel rbl_step / rbl_apply use for block size b under the current option:
  * 1 = global-gather CSR, 2 = LDS-window CSR (DPP), 3 = LDS-densified band on fp64 MFMA,
- * 4 = dense panel GEMM (rbl_set_matrix_dense), 5 = band-tile format on fp64 MFMA. */
+ * 4 = dense panel GEMM (rbl_set_matrix_dense), 5 = band-tile format on fp64 MFMA,
+ * 6 = segmented gather (unstructured patterns, b in {16, 32}). */
 int rbl_spmm_kernel_for(rbl_ctx* ctx, int b);
 
 /* ---- Krylov run -----------------------------------------------------------------------

@@ -67,6 +67,53 @@ def hashwindow_csr(n: int, W: int, p: float, seed: int, plant=None, row_begin=0,
     return A
 
 
+_RMAT_K = np.uint64(0xD1B54A32D192ED03)
+
+
+def rmat_draws(n: int, scale: int, edges: int, seed: int, a=0.57, b=0.19, c=0.19):
+    """Kept R-MAT draws (r, c) in draw order (gen_rmat.hip: rmat_draw)."""
+    e = np.arange(edges, dtype=np.int64)
+    s2 = np.uint64(seed) ^ _RMAT_K
+    ab, abc = a + b, a + b + c
+    r = np.zeros(edges, np.int64)
+    cc = np.zeros(edges, np.int64)
+    for lvl in range(scale):
+        u = u53(pair_hash(s2, e, np.full(edges, lvl, np.int64)))
+        bit = np.int64(1) << np.int64(scale - 1 - lvl)
+        r |= np.where(u >= ab, bit, 0)
+        cc |= np.where(((u >= a) & (u < ab)) | (u >= abc), bit, 0)
+    keep = (r < n) & (cc < n) & (r != cc)
+    return r[keep], cc[keep]
+
+
+def rmat_csr(n: int, scale: int, edges: int, seed: int, plant=None, row_begin=0, row_end=None,
+             a=0.57, b=0.19, c=0.19):
+    """Rows [row_begin, row_end) of the symmetric R-MAT matrix as SciPy CSR,
+    restating gen_rmat.hip: both orientations of every kept draw (duplicates merged), the
+    hash-window pair values off the diagonal, every diagonal entry with its hash value plus
+    the planted spectrum."""
+    row_end = n if row_end is None else row_end
+    r, cc = rmat_draws(n, scale, edges, seed, a, b, c)
+    R = np.concatenate([r, cc, np.arange(n, dtype=np.int64)])
+    C = np.concatenate([cc, r, np.arange(n, dtype=np.int64)])
+    sel = (R >= row_begin) & (R < row_end)
+    key = np.unique(R[sel] * np.int64(n) + C[sel])
+    R, C = key // n, key % n
+    lo, hi = np.minimum(R, C), np.maximum(R, C)
+    u = u53(mix64(pair_hash(seed, lo, hi) ^ _K))
+    val = (u + u) - 1.0
+    if plant is not None and len(plant):
+        plant = np.asarray(plant, dtype=np.float64)
+        stride = n // len(plant)
+        d = R == C
+        sel2 = d & (R % stride == 0) & (R // stride < len(plant))
+        val[sel2] += plant[R[sel2] // stride]
+    m = row_end - row_begin
+    A = sp.csr_matrix((val, (R - row_begin, C)), shape=(m, n))
+    A.sort_indices()
+    return A
+
+
 def planted_spectrum(k: int, scale: float = 100.0):
     """Planted diagonal of SURVEY §8(d) C1: 2k entries at scale*(2k+1-l), l = 1..2k."""
     return np.array([scale * (2 * k + 1 - l) for l in range(1, 2 * k + 1)], dtype=np.float64)

@@ -69,7 +69,7 @@ def test_spmm_window_ragged_and_partial_tiles(rbl, b):
         if W <= 64 and tile_nnz <= 2048:     # the window kernel's metadata cap per tile
             assert k in (2, 3, 5), (n, W)
         if tile_nnz > 2048:
-            assert k in (1, 3, 5), (n, W)
+            assert k in (1, 3, 5, 6), (n, W)
 
 
 @pytest.mark.parametrize("b", [16, 32])
@@ -93,7 +93,7 @@ def test_spmm_general_pattern_and_empty_rows(rbl, b):
     X = np.random.default_rng(1).standard_normal((3000, b))
     with rbl.Context(0) as ctx:
         ctx.set_matrix(A)
-        assert ctx.spmm_kernel_for(b) == 1
+        assert ctx.spmm_kernel_for(b) == (6 if b in (16, 32) else 1)  # segmented / plain gather
         Y = ctx.apply(X)
     _check(A, Y, X)
     assert np.all(Y[[0, 5, 2999]] == 0)
@@ -128,3 +128,46 @@ def test_spmm_band_tiles(rbl, n, W, p, ng):
         Y = ctx.apply(X)
     assert (k == 5) == (ng > 0), (k, ng)
     _check(A, Y, X)
+
+
+@pytest.mark.parametrize("b", [16, 32])
+@pytest.mark.parametrize("variant", [0, 5])
+def test_spmm_segmented_long_rows(rbl, b, variant):
+    """Segmented gather (variant 5, kernel id 6): an arrow matrix whose 3 hub rows/columns
+    touch every row (20,000 nonzeros each: 5 segments of 4,096 each, summed in order by the
+    fixup kernel) beside short random rows, empty rows and the fused 3-term epilogue path
+    through a short Lanczos trace."""
+    n = 20000
+    R = sp.random(n, n, density=2e-4, random_state=5, format="csr")
+    hub = sp.lil_matrix((n, n))
+    hub[[0, 7, 19999], :] = np.random.default_rng(1).standard_normal((3, n))
+    A = R + R.T + hub + hub.T
+    A = A.tolil()
+    A[123, :] = 0
+    A[:, 123] = 0
+    A = sp.csr_matrix(A)
+    X = np.random.default_rng(b).standard_normal((n, b))
+    with rbl.Context(0) as ctx:
+        ctx.set_matrix(A)
+        ctx.set_option(2, variant)
+        assert ctx.spmm_kernel_for(b) == 6
+        Y = ctx.apply(X)
+    _check(A, Y, X)
+    assert np.all(Y[123] == 0)
+
+
+def test_spmm_segmented_and_gather_agree_in_lanczos(rbl):
+    """Epilogue + long-row fixup inside a block step: kernels 6 and 1 give the same A_i."""
+    from oracle import matgen as mg
+    A = mg.rmat_csr(16000, 14, 1_200_000, 3, mg.planted_spectrum(5))
+    assert np.diff(A.indptr).max() > 4096     # long rows present
+    out = []
+    for variant in (1, 5):
+        with rbl.Context(0) as ctx:
+            ctx.set_matrix(A)
+            ctx.set_option(2, variant)
+            _, _, info = rbl.lanczos(ctx, 5, 32, seed=4, check=False, max_steps=6, trace=True,
+                                     ritz=False)
+            out.append(info)
+    for a1, a2 in zip(out[0].trace_A, out[1].trace_A):
+        assert np.abs(a1 - a2).max() <= 1e-12 * np.abs(a1).max()

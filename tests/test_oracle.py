@@ -6,6 +6,7 @@ norm of the relative eigenvalue error < 1e-13 for k = 5, b = 5.
 import numpy as np
 import pytest
 
+from oracle import matgen
 from oracle import rbl_oracle as o
 
 
@@ -95,3 +96,22 @@ def test_mixed_mode_oracle_tracks_fp64():
     assert np.max(np.abs(r32.D - r64.D) / np.abs(r64.D)) < 1e-6
     res = np.linalg.norm(A @ r32.V - r32.V * r32.D[None, :], axis=0) / np.abs(r32.D)
     assert res.max() < 1e-5
+
+
+def test_rmat_restatement_properties():
+    """R-MAT oracle (C4b): symmetric, sorted, every diagonal present with the planted spectrum,
+    power-law skew (the top 1 % of rows hold far more than 1 % of the nonzeros), and row
+    slices equal to the rows of the full matrix."""
+    n, k = 4000, 5
+    plant = matgen.planted_spectrum(k)
+    A = matgen.rmat_csr(n, 12, 60_000, 11, plant)
+    assert abs(A - A.T).max() == 0
+    assert np.all(A.diagonal() != 0)
+    stride = n // len(plant)
+    d = A.diagonal()
+    assert np.all(np.abs(d[::stride][:len(plant)] - plant) <= 1.0)
+    deg = np.diff(A.indptr)
+    top = np.sort(deg)[::-1][: n // 100].sum()
+    assert top > 0.1 * A.nnz
+    part = matgen.rmat_csr(n, 12, 60_000, 11, plant, row_begin=1000, row_end=2500)
+    assert (part != A[1000:2500]).nnz == 0
