@@ -57,6 +57,9 @@ def parse():
     ap.add_argument("--rmat-scale", type=int, default=24)
     ap.add_argument("--rmat-edges", type=int, default=0,
                     help="R-MAT draws (0: 0.66 n x 100: ~1e9 nonzeros at n = 1e7 after merging)")
+    ap.add_argument("--device-blocks", type=int, default=0,
+                    help="Krylov blocks kept in HBM (RBL_OPT_DEVICE_BLOCKS; older blocks spill to "
+                         "pinned host memory, the reference's hybrid buffer); 0 = all")
     ap.add_argument("--basis-bits", type=int, default=64, choices=(64, 32),
                     help="32: the mixed mode (fp32 Krylov basis + reorth on fp32 MFMA, fp64 A*Q / "
                          "3-term / QR) of BASELINE config 5, on this workload")
@@ -135,6 +138,7 @@ def main():
     nnz = allsum(nnz_loc)
     ctx.set_option(_lib.RBL_OPT_TIMERS, 1)
     ctx.set_option(_lib.RBL_OPT_SPMM_KERNEL, args.spmm_kernel)
+    ctx.set_option(_lib.RBL_OPT_DEVICE_BLOCKS, args.device_blocks)
     m_max = rbl.rbl_gpu.max_steps_for(args.kryl, b)
     spmm_kid = ctx.spmm_kernel_for(b)
     spmm_kernel = {1: "gather", 2: "lds-window", 3: "lds-band-mfma", 5: "band-tile-mfma",
@@ -247,7 +251,8 @@ def main():
                           if args.matrix == "hashwindow" else
                           {"rmat_scale": args.rmat_scale, "rmat_edges": args.rmat_edges,
                            "rmat_abcd": [0.57, 0.19, 0.19, 0.05]}),
-                       "block_steps_per_run": m_max, "parallelism": f"rows{world}"},
+                       "block_steps_per_run": m_max, "parallelism": f"rows{world}",
+                       **({"device_blocks": args.device_blocks} if args.device_blocks else {})},
             "roofline": roofline,
             "roofline_secondary": roofline2,
             "stage_ms_per_run": {s: round(v, 3) for s, v in stage_per_run.items()},

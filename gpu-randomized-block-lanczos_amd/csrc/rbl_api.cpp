@@ -72,6 +72,16 @@ struct rbl_ctx {
   // fp32 basis (mixed precision, RBL_gpu.jl with FLOAT = Float32): slots in d_basis32, the
   // current and previous block widened to fp64 in d_Qi64 / d_Qm64 for A Q, 3-term and QR
   int basis_bits = 64;
+  // host spill (RBL_OPT_DEVICE_BLOCKS): blocks j < resident live in d_basis slot j; blocks
+  // j >= resident in working slot resident + (j & 1) while among the two newest, and in
+  // pinned host slot j - resident once final (copied during step j + 2)
+  int dev_blocks_opt = 0;
+  int resident = INT32_MAX;
+  double* h_spill = nullptr;
+  double* d_stage = nullptr;          // one n_local x b staging block for spilled blocks
+  hipStream_t cstream = nullptr;      // D2H copies of finished spilled blocks
+  hipEvent_t ev_fin = nullptr, ev_d2h[2] = {nullptr, nullptr};
+  bool d2h_pending[2] = {false, false};
   float* d_basis32 = nullptr;
   double* d_Qi64 = nullptr;
   double* d_Qm64 = nullptr;
@@ -131,7 +141,23 @@ int fail(rbl_ctx* c, int code, const std::string& msg) {
     if (_s < 0) return _s;    \
   } while (0)
 
-double* slotp(rbl_ctx* ctx, int j) { return ctx->d_basis + (int64_t)j * ctx->slot; }
+// device location of fp64 block j: resident slot, or (spilled region) its working slot —
+// valid only while j is one of the two newest blocks
+double* slotp(rbl_ctx* ctx, int j) {
+  const int s = j < ctx->resident ? j : ctx->resident + (j & 1);
+  return ctx->d_basis + (int64_t)s * ctx->slot;
+}
+bool spilled(const rbl_ctx* ctx) { return ctx->resident != INT32_MAX; }
+// fp64 block j on the device: in place when resident or among the newest two of `nblocks`,
+// else copied from pinned host memory into the staging block (on the compute stream)
+const double* block_dev(rbl_ctx* ctx, int j, int nblocks, int* st) {
+  *st = 0;
+  if (j < ctx->resident || j >= nblocks - 2) return slotp(ctx, j);
+  const hipError_t e = hipMemcpyAsync(ctx->d_stage, ctx->h_spill + (int64_t)(j - ctx->resident) * ctx->slot,
+                                      ctx->slot * sizeof(double), hipMemcpyHostToDevice, ctx->stream);
+  if (e != hipSuccess) *st = RBL_ERR_HIP;
+  return ctx->d_stage;
+}
 float* slotp32(rbl_ctx* ctx, int j) { return ctx->d_basis32 + (int64_t)j * ctx->slot; }
 
 CsrDev csr(rbl_ctx* ctx) {
@@ -541,21 +567,53 @@ int reorth_pair(rbl_ctx* ctx, int i, int flags) {
   if ((flags & 1) && i >= 3) {
     StageScope t(ctx, RBL_STAGE_PART_REORTH);
     const int nW = i - 2;
-    if (ctx->reorth_order == 0) {  // block CGS: one Gram over every j, one update
+    const int nres = std::min(nW, ctx->resident);  // HBM-resident part of W
+    if (ctx->reorth_order == 0) {  // block CGS: one Gram over every resident j, one update
       PanelRun W;
       W.base = slotp(ctx, 0);
       W.stride = ctx->slot;
-      W.count = nW;
+      W.count = nres;
       W.w = b;
       CHK(gram(ctx, W, pan2(Qi, Qm, b), ctx->d_C, nullptr));
       CHK(tsmm_checked(ctx, W, ctx->d_C, 2 * b, pan2(Qi, Qm, b), -1.0, 1.0, nullptr));
     } else {  // ascending-j block MGS, exactly the reference order
-      for (int j = 0; j < nW; ++j) {
+      for (int j = 0; j < nres; ++j) {
         const PanelRun W = run1(slotp(ctx, j), b);
         CHK(gram(ctx, W, pan2(Qi, Qm, b), ctx->d_C, nullptr));
         CHK(tsmm_checked(ctx, W, ctx->d_C, 2 * b, pan2(Qi, Qm, b), -1.0, 1.0, nullptr));
       }
     }
+    // spilled blocks (host, final): streamed back one at a time, ascending j, each applied
+    // as soon as it lands — hybrid_part_reorth!'s `copyto!(Qgj, Q[j]); part_reorth_gpu!`
+    // (RBL_gpu.jl:65-68)
+    for (int j = nres; j < nW; ++j) {
+      int st = 0;
+      const double* Wj = block_dev(ctx, j, i, &st);
+      if (st) return fail(ctx, st, "partial reorth: H2D of a spilled block failed");
+      CHK(gram(ctx, run1(Wj, b), pan2(Qi, Qm, b), ctx->d_C, nullptr));
+      CHK(tsmm_checked(ctx, run1(Wj, b), ctx->d_C, 2 * b, pan2(Qi, Qm, b), -1.0, 1.0, nullptr));
+    }
+  }
+  return RBL_OK;
+}
+
+// Y = [Q_1 .. Q_nblocks] S_dev (S_dev device row-major (nblocks*b) x kcols): one run over the
+// HBM-resident blocks, then every other block (streamed from the host when spilled)
+int combine_blocks(rbl_ctx* ctx, int nblocks, int kcols, const double* d_S, double* Y) {
+  const int b = ctx->b;
+  const int nres = std::min(nblocks, ctx->resident);
+  PanelRun X;
+  X.base = slotp(ctx, 0);
+  X.stride = ctx->slot;
+  X.count = nres;
+  X.w = b;
+  CHK(tsmm_checked(ctx, X, d_S, kcols, pan1(Y, kcols), 1.0, 0.0, nullptr));
+  for (int j = nres; j < nblocks; ++j) {
+    int st = 0;
+    const double* Qj = block_dev(ctx, j, ctx->nblocks, &st);
+    if (st) return fail(ctx, st, "Ritz: H2D of a spilled block failed");
+    CHK(tsmm_checked(ctx, run1(Qj, b), d_S + (int64_t)j * b * kcols, kcols, pan1(Y, kcols), 1.0,
+                     1.0, nullptr));
   }
   return RBL_OK;
 }
@@ -570,12 +628,7 @@ int basis_combine(rbl_ctx* ctx, int nblocks, int kcols, const double* S, double*
   HIPC(hipMalloc(&d_S, rows * kcols * sizeof(double)));
   HIPC(hipMemcpyAsync(d_Scm, S, rows * kcols * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
   colmajor_to_rowmajor(d_Scm, rows, kcols, d_S, ctx->stream);
-  PanelRun X;
-  X.base = slotp(ctx, 0);
-  X.stride = ctx->slot;
-  X.count = nblocks;
-  X.w = b;
-  const int st = tsmm_checked(ctx, X, d_S, kcols, pan1(Y, kcols), 1.0, 0.0, nullptr);
+  const int st = combine_blocks(ctx, nblocks, kcols, d_S, Y);
   HIPC(hipStreamSynchronize(ctx->stream));
   hipFree(d_S);
   hipFree(d_Scm);
@@ -685,7 +738,12 @@ int halo_exchange(rbl_ctx* ctx, const double* Q, const double** Qin, int64_t* of
 }
 
 void free_run(rbl_ctx* ctx) {
+  if (ctx->cstream) hipStreamSynchronize(ctx->cstream);
   hipFree(ctx->d_basis); ctx->d_basis = nullptr;
+  hipHostFree(ctx->h_spill); ctx->h_spill = nullptr;
+  hipFree(ctx->d_stage); ctx->d_stage = nullptr;
+  ctx->resident = INT32_MAX;
+  ctx->d2h_pending[0] = ctx->d2h_pending[1] = false;
   hipFree(ctx->d_basis32); ctx->d_basis32 = nullptr;
   hipFree(ctx->d_Qi64); ctx->d_Qi64 = nullptr;
   hipFree(ctx->d_Qm64); ctx->d_Qm64 = nullptr;
@@ -892,6 +950,9 @@ int rbl_free(rbl_ctx* ctx) {
   for (auto e : ctx->ev_pool) hipEventDestroy(e);
   delete ctx->comm;
   if (ctx->stream) hipStreamDestroy(ctx->stream);
+  if (ctx->cstream) hipStreamDestroy(ctx->cstream);
+  for (hipEvent_t e : {ctx->ev_fin, ctx->ev_d2h[0], ctx->ev_d2h[1]})
+    if (e) hipEventDestroy(e);
   delete ctx;
   return RBL_OK;
 }
@@ -905,6 +966,11 @@ int rbl_set_option(rbl_ctx* ctx, int option, int64_t value) {
     case RBL_OPT_REORTH_ORDER:
       if (value < 0 || value > 1) return fail(ctx, RBL_ERR_INVALID, "reorth order must be 0|1");
       ctx->reorth_order = (int)value;
+      return RBL_OK;
+    case RBL_OPT_DEVICE_BLOCKS:
+      if (value < -1 || value == 1 || value == 2 || value > INT32_MAX)
+        return fail(ctx, RBL_ERR_INVALID, "device blocks: 0 (all), -1 (auto) or >= 3");
+      ctx->dev_blocks_opt = (int)value;
       return RBL_OK;
     case RBL_OPT_SPMM_KERNEL:
       if (value < 0 || value > 5) return fail(ctx, RBL_ERR_INVALID, "spmm kernel must be 0..5");
@@ -1255,12 +1321,31 @@ int rbl_start(rbl_ctx* ctx, int b, int max_blocks, int basis_bits, const double*
   HIPC(hipStreamSynchronize(ctx->stream));
   // a repeated run with the same shape reuses the HBM plan (allocating ~100 GB of basis
   // per run costs more than the run itself at n = 1e7)
+  // device slots of the basis (RBL_OPT_DEVICE_BLOCKS; RBL_gpu.jl:95-104 gpu_buffer_size)
+  int dev_slots = max_blocks + 1;
+  if (ctx->dev_blocks_opt != 0 && basis_bits == 64) {
+    int g = ctx->dev_blocks_opt;
+    if (g < 0) {
+      size_t fr = 0, tot = 0;
+      HIPC(hipMemGetInfo(&fr, &tot));
+      const double blk = (double)std::max<int64_t>(ctx->nloc, 1) * b * 8.0;
+      // what the run needs beside the basis: U, T, the halo copy, staging, ~slab
+      const double other = 6.0 * blk + (double)(max_blocks + 1) * b * 2 * b * 8.0 * 64;
+      g = (int)std::max(3.0, std::floor((0.8 * (double)fr - other) / blk));
+    }
+    dev_slots = std::min(dev_slots, std::max(3, g));
+  } else if (ctx->dev_blocks_opt != 0) {
+    return fail(ctx, RBL_ERR_INVALID, "RBL_OPT_DEVICE_BLOCKS: fp64 basis only");
+  }
   const bool reuse = (ctx->d_basis || ctx->d_basis32) && ctx->b == b &&
                      ctx->max_blocks == max_blocks && ctx->slot == ctx->nloc * b &&
-                     ctx->basis_bits == basis_bits;
+                     ctx->basis_bits == basis_bits &&
+                     (ctx->resident == INT32_MAX ? max_blocks + 1 : ctx->resident + 2) == dev_slots;
   ctx->nlock = 0;  // a new problem: no locked vectors
   if (reuse) {
     ctx->nblocks = 0;
+    if (ctx->cstream) HIPC(hipStreamSynchronize(ctx->cstream));
+    ctx->d2h_pending[0] = ctx->d2h_pending[1] = false;
     HIPC(hipMemsetAsync(ctx->d_flags, 0, 4 * sizeof(int), ctx->stream));
   } else {
   free_run(ctx);
@@ -1270,7 +1355,19 @@ int rbl_start(rbl_ctx* ctx, int b, int max_blocks, int basis_bits, const double*
   const int64_t nl = std::max<int64_t>(ctx->nloc, 1);
   ctx->basis_bits = basis_bits;
   if (basis_bits == 64) {
-    HIPC(hipMalloc(&ctx->d_basis, (size_t)(max_blocks + 1) * nl * b * sizeof(double)));
+    HIPC(hipMalloc(&ctx->d_basis, (size_t)dev_slots * nl * b * sizeof(double)));
+    if (dev_slots < max_blocks + 1) {  // host spill: pinned slots for blocks resident..max_blocks
+      ctx->resident = dev_slots - 2;
+      HIPC(hipHostMalloc(&ctx->h_spill, (size_t)(max_blocks + 1 - ctx->resident) * nl * b * sizeof(double),
+                         hipHostMallocDefault));
+      HIPC(hipMalloc(&ctx->d_stage, (size_t)nl * b * sizeof(double)));
+      if (!ctx->cstream) {
+        HIPC(hipStreamCreateWithFlags(&ctx->cstream, hipStreamNonBlocking));
+        HIPC(hipEventCreateWithFlags(&ctx->ev_fin, hipEventDisableTiming));
+        HIPC(hipEventCreateWithFlags(&ctx->ev_d2h[0], hipEventDisableTiming));
+        HIPC(hipEventCreateWithFlags(&ctx->ev_d2h[1], hipEventDisableTiming));
+      }
+    }
   } else {
     HIPC(hipMalloc(&ctx->d_basis32, (size_t)(max_blocks + 1) * nl * b * sizeof(float)));
     HIPC(hipMalloc(&ctx->d_Qi64, (nl + kRowPad) * b * sizeof(double)));
@@ -1380,6 +1477,17 @@ int rbl_step(rbl_ctx* ctx, int i, int part_reorth, double* A_out, double* B_out)
   // partial reorth of Q_i and Q_{i-1} against Q_1..Q_{i-2}   (RBL_gpu.jl:164-166, 59-81),
   // preceded (flag bit 1, restarted variants) by the reorth against the locked vectors
   if (!f32) CHK(reorth_pair(ctx, i, part_reorth));
+  // host spill: block i-2 is final now (the hybrid buffer's `copyto!(Q[i-1], Qg1)`,
+  // RBL_gpu.jl:76): copy it out on the side stream while the step goes on; its working slot
+  // is rewritten by this step's QR, which waits for the copy
+  if (!f32 && spilled(ctx) && i >= 2 && i - 2 >= ctx->resident) {
+    HIPC(hipEventRecord(ctx->ev_fin, ctx->stream));
+    HIPC(hipStreamWaitEvent(ctx->cstream, ctx->ev_fin, 0));
+    HIPC(hipMemcpyAsync(ctx->h_spill + (int64_t)(i - 2 - ctx->resident) * ctx->slot, slotp(ctx, i - 2),
+                        ctx->slot * sizeof(double), hipMemcpyDeviceToHost, ctx->cstream));
+    HIPC(hipEventRecord(ctx->ev_d2h[i & 1], ctx->cstream));
+    ctx->d2h_pending[i & 1] = true;
+  }
   // local reorth: Q_i -= Q_{i-1} (Q_{i-1}^T Q_i), one projection (RBL_gpu.jl:83-93, P1)
   const bool fused = rowgram_ok(b);
   if (!f32 && i >= 2) {
@@ -1420,6 +1528,10 @@ int rbl_step(rbl_ctx* ctx, int i, int part_reorth, double* A_out, double* B_out)
       CHK(tsmm_checked(ctx, run1(Qi, b), smallp(ctx, S_AI), b, pan1(ctx->d_U, b), -1.0, 1.0, nullptr));
   }
   // Q_{i+1} B_{i+1} = qr(U)   (RBL_gpu.jl:180-184)
+  if (!f32 && ctx->d2h_pending[i & 1]) {  // the working slot's previous block is on the host
+    HIPC(hipStreamWaitEvent(ctx->stream, ctx->ev_d2h[i & 1], 0));
+    ctx->d2h_pending[i & 1] = false;
+  }
   if (!f32) {
     CHK(tsqr(ctx, ctx->d_U, slotp(ctx, i), fused));
   } else {  // Qg = FLOAT(Qg_d) (RBL_gpu.jl:182): the new block enters the basis rounded to fp32
@@ -1465,12 +1577,7 @@ int rbl_ritz(rbl_ctx* ctx, int nblocks, int k, const double* S, double* V_out) {
   {
     StageScope t(ctx, RBL_STAGE_RITZ);
     if (ctx->basis_bits == 64) {
-      PanelRun X;
-      X.base = slotp(ctx, 0);
-      X.stride = ctx->slot;
-      X.count = nblocks;
-      X.w = b;
-      CHK(tsmm_checked(ctx, X, d_S, k, pan1(d_V, k), 1.0, 0.0, nullptr));
+      CHK(combine_blocks(ctx, nblocks, k, d_S, d_V));
     } else {  // fp32 basis: each block widened to fp64, V accumulated in fp64 (P3: fp64 Ritz)
       for (int j = 0; j < nblocks; ++j) {
         cvt_f32_to_f64(slotp32(ctx, j), ctx->d_Qm64, ctx->nloc * b, ctx->stream);
@@ -1496,7 +1603,9 @@ int rbl_get_block(rbl_ctx* ctx, int j, double* Q_out) {
   if (!ctx || j < 1 || j > ctx->nblocks || !Q_out) return fail(ctx, RBL_ERR_INVALID, "rbl_get_block: bad block");
   HIPC(hipSetDevice(ctx->device));
   const int b = ctx->b;
-  const double* src = slotp(ctx, j - 1);
+  int st = 0;
+  const double* src = ctx->basis_bits == 64 ? block_dev(ctx, j - 1, ctx->nblocks, &st) : nullptr;
+  if (st) return fail(ctx, st, "rbl_get_block: H2D of a spilled block failed");
   if (ctx->basis_bits == 32) {  // fp32 slot, returned widened
     cvt_f32_to_f64(slotp32(ctx, j - 1), ctx->d_Qm64, ctx->nloc * b, ctx->stream);
     src = ctx->d_Qm64;
@@ -1515,6 +1624,7 @@ int rbl_restart(rbl_ctx* ctx, int nblocks, const double* S) {
   if (!ctx || !S || nblocks < 1 || nblocks > ctx->nblocks)
     return fail(ctx, RBL_ERR_INVALID, "rbl_restart: bad arguments");
   if (!ctx->d_basis) return fail(ctx, RBL_ERR_STATE, "rbl_restart: needs an fp64 run (rbl_start)");
+  if (spilled(ctx)) return fail(ctx, RBL_ERR_STATE, "rbl_restart: needs an HBM-resident basis");
   HIPC(hipSetDevice(ctx->device));
   const int b = ctx->b;
   CHK(basis_combine(ctx, nblocks, b, S, ctx->d_T));
@@ -1530,6 +1640,7 @@ int rbl_lock(rbl_ctx* ctx, int nblocks, int nvec, const double* S) {
   if (!ctx || !S || nblocks < 1 || nblocks > ctx->nblocks || nvec < 0)
     return fail(ctx, RBL_ERR_INVALID, "rbl_lock: bad arguments");
   if (!ctx->d_basis) return fail(ctx, RBL_ERR_STATE, "rbl_lock: needs an fp64 run (rbl_start)");
+  if (spilled(ctx)) return fail(ctx, RBL_ERR_STATE, "rbl_lock: needs an HBM-resident basis");
   if (nvec == 0) return RBL_OK;
   HIPC(hipSetDevice(ctx->device));
   const int64_t nl = std::max<int64_t>(ctx->nloc, 1);
@@ -1569,6 +1680,7 @@ int rbl_reorth_last(rbl_ctx* ctx, int nblocks, int flags) {
   if (!ctx || nblocks < 1 || nblocks > ctx->nblocks)
     return fail(ctx, RBL_ERR_INVALID, "rbl_reorth_last: bad arguments");
   if (!ctx->d_basis) return fail(ctx, RBL_ERR_STATE, "rbl_reorth_last: needs an fp64 run");
+  if (spilled(ctx)) return fail(ctx, RBL_ERR_STATE, "rbl_reorth_last: needs an HBM-resident basis");
   HIPC(hipSetDevice(ctx->device));
   CHK(reorth_pair(ctx, nblocks, flags));
   HIPC(hipStreamSynchronize(ctx->stream));

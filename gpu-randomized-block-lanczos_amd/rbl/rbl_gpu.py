@@ -321,12 +321,16 @@ def lanczos(ctx: Context, k: int, b: int, *, kryl_sz: int = KRYL_SZ_GPU, omega=N
 
 
 def RBL_gpu(A, k: int, b: int, *, device: int = 0, kryl_sz: int = KRYL_SZ_GPU, omega=None,
-            seed: int = 0, reorth_order: int = 0, return_info: bool = False, basis_bits: int = 64):
+            seed: int = 0, reorth_order: int = 0, return_info: bool = False, basis_bits: int = 64,
+            device_blocks: int = 0):
     """Drop-in for ``RBL_gpu(A::SparseMatrixCSC{Float64}, k, b)`` (RBL_gpu.jl:205):
-    returns (D, V) — D the k largest-|lambda| eigenvalues (descending |lambda|), V n x k."""
+    returns (D, V) — D the k largest-|lambda| eigenvalues (descending |lambda|), V n x k.
+    device_blocks: Krylov blocks kept in HBM (RBL_OPT_DEVICE_BLOCKS: 0 all, -1 what fits —
+    the reference's gpu_buffer_size — or G >= 3; older blocks spill to pinned host memory)."""
     with Context(device) as ctx:
         ctx.set_matrix(A)
         ctx.set_option(_lib.RBL_OPT_REORTH_ORDER, reorth_order)
+        ctx.set_option(_lib.RBL_OPT_DEVICE_BLOCKS, device_blocks)
         D, V, info = lanczos(ctx, k, b, kryl_sz=kryl_sz, omega=omega, seed=seed,
                              basis_bits=basis_bits)
     return (D, V, info) if return_info else (D, V)

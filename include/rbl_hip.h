@@ -52,6 +52,13 @@ extern "C" {
 #define RBL_OPT_TIMERS        0   /* 1: record per-stage hipEvents (adds event records)         */
 #define RBL_OPT_REORTH_ORDER  1   /* 0: block-CGS (batched, default); 1: ascending-j block MGS  */
                                   /*    exactly as RBL.jl:30-48 / RBL_gpu.jl:65-67               */
+#define RBL_OPT_DEVICE_BLOCKS 3   /* Krylov blocks kept in HBM (the reference's hybrid buffer,
+                                   * RBL_GPU.jl:24-27, 59-81, 95-132): 0 = all (default); -1 =
+                                   * as many as fit in 80 % of free HBM (gpu_buffer_size);
+                                   * G >= 3 = G slots: blocks 0..G-3 resident, the two newest
+                                   * in two working slots, every older block in pinned host
+                                   * memory, streamed back over PCIe for partial reorth and
+                                   * Ritz.  fp64 basis only; set before rbl_start.              */
 #define RBL_OPT_SPMM_KERNEL   2   /* 0: auto; 1: global-gather CSR; 2: LDS-window CSR (DPP);
                                    * 3: LDS-densified band on fp64 MFMA; 4: band-tile format
                                    * (CSR densified once into MFMA operand order, b = 32,
