@@ -1358,8 +1358,9 @@ int rbl_start(rbl_ctx* ctx, int b, int max_blocks, int basis_bits, const double*
     HIPC(hipMalloc(&ctx->d_basis, (size_t)dev_slots * nl * b * sizeof(double)));
     if (dev_slots < max_blocks + 1) {  // host spill: pinned slots for blocks resident..max_blocks
       ctx->resident = dev_slots - 2;
+      // non-coherent pinned pages: the DMA engines stream them at PCIe rate both ways
       HIPC(hipHostMalloc(&ctx->h_spill, (size_t)(max_blocks + 1 - ctx->resident) * nl * b * sizeof(double),
-                         hipHostMallocDefault));
+                         hipHostMallocNonCoherent));
       HIPC(hipMalloc(&ctx->d_stage, (size_t)nl * b * sizeof(double)));
       if (!ctx->cstream) {
         HIPC(hipStreamCreateWithFlags(&ctx->cstream, hipStreamNonBlocking));
