@@ -21,6 +21,16 @@ namespace rbl {
 __device__ __forceinline__ double mfma4(double a, double b, double c) {
   return __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, c, 0, 0, 0);
 }
+// The Krylov basis W is read once per launch (up to 92 GB at C4a: no L2 / Infinity Cache
+// reuse); non-temporal loads measured no faster here (596 vs 600 ms per run), so off
+#ifndef RBL_REORTH_NT
+#define RBL_REORTH_NT 0
+#endif
+template <typename T>
+__device__ __forceinline__ T ldw(const T* p) {
+  if constexpr (RBL_REORTH_NT) return __builtin_nontemporal_load(p);
+  return *p;
+}
 
 // ----------------------------------------------------------------------------------------
 // Gram C = W^T X: one Krylov panel per wave, 4 waves per workgroup (three workgroups per CU:
@@ -84,7 +94,7 @@ __device__ __forceinline__ void gram44_body(int64_t r_begin, int64_t r_end, int6
       const int64_t rr = rc0 + 4 * ks + q;
       const int64_t rc = rr < rlast ? rr : rlast;
 #pragma unroll
-      for (int ag = 0; ag < AG; ++ag) ar[ks][ag] = wp[rc * B + 16 * ag];
+      for (int ag = 0; ag < AG; ++ag) ar[ks][ag] = ldw(wp + rc * B + 16 * ag);
     }
   };
 
@@ -268,7 +278,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
       const int col = k - pan * B;
       const double* xp = X.base + (int64_t)pan * X.stride + col;
 #pragma unroll
-      for (int rt = 0; rt < 2; ++rt) ar[rt][h] = *reinterpret_cast<const d2v*>(xp + arow[rt] * B);
+      for (int rt = 0; rt < 2; ++rt) ar[rt][h] = ldw(reinterpret_cast<const d2v*>(xp + arow[rt] * B));
     }
   };
   // C chunk: 32 x KYP, 256 threads; element e -> (k = e / KYP, c = e % KYP)

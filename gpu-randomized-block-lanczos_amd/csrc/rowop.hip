@@ -29,6 +29,19 @@ constexpr int kBlockRows = 16;    // rows per wave per iteration (one MFMA row t
 __device__ __forceinline__ double mfma4r(double a, double b, double c) {
   return __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, c, 0, 0, 0);
 }
+// n x b blocks are streamed once per pass (2.56 GB at C4a, far beyond L2 + Infinity Cache):
+// non-temporal loads and stores (RBL_ROWOP_NT=0 restores the default policy for A/B runs)
+#ifndef RBL_ROWOP_NT
+#define RBL_ROWOP_NT 1
+#endif
+__device__ __forceinline__ d2v ldnt(const d2v* p) {
+  if constexpr (RBL_ROWOP_NT) return __builtin_nontemporal_load(p);
+  return *p;
+}
+__device__ __forceinline__ void stnt(d2v v, d2v* p) {
+  if constexpr (RBL_ROWOP_NT) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
 
 template <int B, bool GRAM>
 __global__ __launch_bounds__(kRowThreads) __attribute__((amdgpu_waves_per_eu(GRAM ? 2 : 3))) void k_rowgram(int64_t nrows, const double* X,  // X may alias Y (in-place apply)
@@ -69,7 +82,7 @@ __global__ __launch_bounds__(kRowThreads) __attribute__((amdgpu_waves_per_eu(GRA
       r = r < nrows ? r : nrows - 1;
 #pragma unroll
       for (int h = 0; h < NH; ++h)
-        xa[rt][h] = *reinterpret_cast<const d2v*>(X + r * B + 8 * h + 2 * q);
+        xa[rt][h] = ldnt(reinterpret_cast<const d2v*>(X + r * B + 8 * h + 2 * q));
     }
   };
   auto load_y = [&](int64_t b0, d2v (&yr)[1][kYPer]) {
@@ -80,7 +93,7 @@ __global__ __launch_bounds__(kRowThreads) __attribute__((amdgpu_waves_per_eu(GRA
         const int e = 2 * lane + 128 * m;
         int64_t r = b0 * kBlockRows + 16 * rt + e / B;
         r = r < nrows ? r : nrows - 1;
-        yr[rt][m] = *reinterpret_cast<const d2v*>(Y + r * B + (e % B));
+        yr[rt][m] = ldnt(reinterpret_cast<const d2v*>(Y + r * B + (e % B)));
       }
   };
 
@@ -156,7 +169,7 @@ __global__ __launch_bounds__(kRowThreads) __attribute__((amdgpu_waves_per_eu(GRA
         const int e = 2 * lane + 128 * m;
         const int64_t r = rbase + e / B;
         const d2v v = *reinterpret_cast<const d2v*>(ot + swz(e / B, e % B));
-        if (r < nrows) *reinterpret_cast<d2v*>(Y + r * B + (e % B)) = v;
+        if (r < nrows) stnt(v, reinterpret_cast<d2v*>(Y + r * B + (e % B)));
       }
     }
 #pragma unroll
