@@ -198,13 +198,27 @@ def main():
                  "streamed_bytes_per_launch": int(streamed_bytes(spmm_kid, nloc, nnz_loc, b, args.halfwidth, m_max)),
                  "ms_per_launch": round(spmm_ms, 4)}
     mfma_peak = FP64_MFMA_PEAK_TF if args.basis_bits == 64 else FP32_MFMA_PEAK_TF
+    # the clock the chip holds under these kernels (profiles/pmc_clock.json: GRBM_GUI_ACTIVE
+    # / 8 / wall, MI355X_MICROARCH.md 'DVFS give-back'): the spec peak assumes 2.4 GHz
+    held = None
+    try:
+        with open(os.path.join(ROOT, "profiles", "pmc_clock.json")) as f:
+            kc = json.load(f)["kernels"]
+        ks = [kc[k] for k in ("k_gram44<32, 2>", "k_tsmm44<32, 64>") if k in kc]
+        if ks and args.basis_bits == 64 and b == 32:
+            held = sum(k["clock_ghz"] * k["avg_us"] for k in ks) / sum(k["avg_us"] for k in ks)
+    except (OSError, ValueError, KeyError):
+        pass
     roof_reorth = {"kernel": "partial reorth (gram+update)" + ("" if args.basis_bits == 64 else ", fp32"),
                    "bound": "mfma",
                    "achieved": round(reorth_tf, 2), "peak": mfma_peak, "unit": "TFLOP/s",
                    "frac": round(reorth_tf / mfma_peak, 4),
                    "traffic": None if traffic_reorth is None else int(traffic_reorth),
                    "traffic_unit": "HBM bytes per run (gram + update, 18 launches each)",
-                   "algorithmic_flops_per_run": reorth_flops, "ms_per_run": round(reorth_ms, 3)}
+                   "algorithmic_flops_per_run": reorth_flops, "ms_per_run": round(reorth_ms, 3),
+                   **({"held_clock_ghz": round(held, 3),
+                       "frac_of_peak_at_held_clock": round(reorth_tf / (mfma_peak * held / 2.4), 4)}
+                      if held else {})}
     if stage["part reorth"] > stage["AQ"]:
         roofline, roofline2 = roof_reorth, roof_spmm
     else:
