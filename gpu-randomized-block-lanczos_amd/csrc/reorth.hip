@@ -14,6 +14,8 @@
 // With the 4 blocks on 4 consecutive row-quads, the A operand of a wave is
 //   M[r0 + (lane&15)][k0 + (lane>>4)]  (Gram: W^T -> W[r0+(lane>>4)][a0+(lane&15)]),
 // i.e. 16 consecutive doubles per k — coalesced 128-B segments.
+#include <cstdlib>
+
 #include "kernels.hpp"
 
 namespace rbl {
@@ -70,32 +72,34 @@ __device__ __forceinline__ void gram44_body(int64_t r_begin, int64_t r_end, int6
 #pragma unroll
     for (int cg = 0; cg < CGP; ++cg) acc[ag][cg] = 0.0;
 
-  // Prefetch loads are unconditional (clamped rows) so every chunk issues the same VMEM ops
-  // and the compiler's vmcnt waits count just the chunk being consumed; rows past r_end are
-  // zeroed on the X side (at the LDS store), so the clamped W rows contribute nothing.
+  // Chunk c covers rows [rc0, rc0 + 16), rc0 = r_begin + 16c; a partial last chunk is shifted
+  // back to end at r_end (rcl = min(rc0, r_end - 16), wave-uniform; nrows >= 16 on this path)
+  // and its rows below rc0 — already counted — are zeroed on the X side, like rows past
+  // r_end of the prefetch beyond the last chunk.  So every load is a wave-uniform row base
+  // plus a lane constant: no per-lane clamps in the loop (fp64 MFMA does not co-execute
+  // with VALU on gfx950).
   const int xe0 = tid * EPT;
   const int xrow = xe0 / KC, xcol = xe0 % KC;
-  const double* xsrc = X.ptr[xcol / B] + (xcol % B);
-  const int64_t rlast = r_end > 0 ? r_end - 1 : 0;
+  const double* xsl = X.ptr[xcol / B] + (xcol % B) + (int64_t)xrow * B;
+  const double* wl = W.base + (int64_t)j * W.stride + (lane & 15) + q * B;
+  auto shift = [&](int64_t rc0) -> int64_t { return rc0 < r_end - kG44Rows ? rc0 : r_end - kG44Rows; };
   auto load_x = [&](int64_t rc0, double (&xr)[EPT]) {
-    const int64_t rr = rc0 + xrow;
-    const int64_t rc = rr < rlast ? rr : rlast;
+    const double* p = xsl + shift(rc0) * B;
 #pragma unroll
-    for (int v = 0; v < EPT; ++v) xr[v] = xsrc[rc * B + v];
+    for (int v = 0; v < EPT; ++v) xr[v] = p[v];
   };
   auto store_x = [&](int buf, int64_t rc0, const double (&xr)[EPT]) {
-    const bool ok = rc0 + xrow < r_end;
+    const int64_t row = shift(rc0) + xrow;
+    const bool ok = row >= rc0 && row < r_end;
 #pragma unroll
     for (int v = 0; v < EPT; ++v) xs[buf][xrow * LD + perm8(xcol + v)] = ok ? xr[v] : 0.0;
   };
   auto load_a = [&](int64_t rc0, double (&ar)[KS][AG]) {
+    const double* p = wl + shift(rc0) * B;
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-      const int64_t rr = rc0 + 4 * ks + q;
-      const int64_t rc = rr < rlast ? rr : rlast;
+    for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
-      for (int ag = 0; ag < AG; ++ag) ar[ks][ag] = ldw(wp + rc * B + 16 * ag);
-    }
+      for (int ag = 0; ag < AG; ++ag) ar[ks][ag] = ldw(p + 4 * ks * B + 16 * ag);
   };
 
   const int64_t nchunks = r_end > r_begin ? (r_end - r_begin + kG44Rows - 1) / kG44Rows : 0;
@@ -175,8 +179,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
   else gram44_body<B, NX, NPH4>(r_begin, r_end, s, pg, r, W, X, slab, xs);
 }
 
-bool gram44_ok(int nW, int w, int xcount, int xw) {
-  return nW >= 2 && (w == 16 || w == 32) && xw == w && (xcount == 1 || xcount == 2);
+bool gram44_ok(int64_t nrows, int nW, int w, int xcount, int xw) {
+  return nrows >= kG44Rows && nW >= 2 && (w == 16 || w == 32) && xw == w &&
+         (xcount == 1 || xcount == 2);
 }
 
 int gram44_splits(int64_t nrows, int nW) {
@@ -358,6 +363,113 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
   }
 }
 
+// Fast path of k_tsmm44 for the partial-reorth update (64 output columns, K a multiple of 32,
+// nrows >= 32): every address is a wave-uniform base plus a lane constant, so the k-loop runs
+// no per-load VALU (k_tsmm44 spent ~0.6 VALU per MFMA on clamps and 64-bit address math, and
+// on gfx950 fp64 MFMA does not co-execute with VALU).  A wave whose 32 rows pass nrows computes
+// the last 32 rows instead and stores only its own.
+template <int B>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k_tsmm44f(
+    int64_t nrows, PanelRun X, const double* __restrict__ C, int ldc, Panels Y, double alpha,
+    double beta, const int* skip) {
+  if (skip && *skip) return;
+  constexpr int KYP = 64, CG = KYP / 4, LDC = KYP + 8;
+  constexpr int CEPT = kT44K * KYP / 256;
+  __shared__ __attribute__((aligned(16))) double cs[2][kT44K * LDC];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int q = lane >> 4;
+  const int64_t r0 = ((int64_t)blockIdx.x * 4 + wave) * kT44Rows;
+  const int64_t rw = r0 + kT44Rows <= nrows ? r0 : nrows - kT44Rows;  // wave-uniform
+  const int nch = X.count * B / kT44K;
+
+  double acc[2][CG];
+#pragma unroll
+  for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+    for (int cg = 0; cg < CG; ++cg) acc[rt][cg] = 0.0;
+
+  // A: rows rw + 16 rt + (lane&15), k = 32 ch + 8 h + 2 q + v
+  const int aoff0 = (lane & 15) * B + 2 * q, aoff1 = aoff0 + 16 * B;
+  auto load_a = [&](int ch, d2v (&ar)[2][4]) {
+    const int chc = ch < nch ? ch : nch - 1;
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+      const int kk = kT44K * chc + 8 * h;
+      const double* xb = X.base + (int64_t)(kk / B) * X.stride + rw * B + (kk % B);
+      ar[0][h] = *reinterpret_cast<const d2v*>(xb + aoff0);
+      ar[1][h] = *reinterpret_cast<const d2v*>(xb + aoff1);
+    }
+  };
+  // C chunk rows 32 chc + wave + 4 v, column lane
+  auto load_c = [&](int ch, double (&cr)[CEPT]) {
+    const int chc = ch < nch ? ch : nch - 1;
+    const double* cb = C + (int64_t)(kT44K * chc + wave) * ldc;
+#pragma unroll
+    for (int v = 0; v < CEPT; ++v) cr[v] = cb[(int64_t)(4 * v) * ldc + lane];
+  };
+  const int cso = wave * LDC + perm8(lane);
+  auto store_c = [&](int buf, const double (&cr)[CEPT]) {
+#pragma unroll
+    for (int v = 0; v < CEPT; ++v) cs[buf][cso + 4 * v * LDC] = cr[v];
+  };
+
+  d2v acur[2][4], anext[2][4];
+  double cr[CEPT];
+  load_c(0, cr);
+  store_c(0, cr);
+  load_a(0, acur);
+  __syncthreads();
+  for (int ch = 0; ch < nch; ++ch) {
+    load_c(ch + 1, cr);
+    load_a(ch + 1, anext);
+    const double* cb = cs[ch & 1] + 2 * q * LDC + 2 * (lane & 3);
+#pragma unroll
+    for (int hv = 0; hv < 8; ++hv) {
+      const int h = hv >> 1, v = hv & 1;
+      const double* cr0 = cb + (8 * h + v) * LDC;
+#pragma unroll
+      for (int cp = 0; cp < CG / 2; ++cp) {
+        const d2v bf = *reinterpret_cast<const d2v*>(cr0 + 8 * cp);
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt) {
+          acc[rt][2 * cp] = mfma4(acur[rt][h][v], bf.x, acc[rt][2 * cp]);
+          acc[rt][2 * cp + 1] = mfma4(acur[rt][h][v], bf.y, acc[rt][2 * cp + 1]);
+        }
+      }
+    }
+    store_c((ch + 1) & 1, cr);
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+      for (int h = 0; h < 4; ++h) acur[rt][h] = anext[rt][h];
+    __syncthreads();
+  }
+  // epilogue as k_tsmm44 (D layout -> LDS -> row-major 16-B stores); rows below r0 belong
+  // to the previous wave (shifted last tile)
+  double* ot = &cs[0][0] + wave * 16 * KYP;
+  const int g = (lane >> 2) & 3;
+  constexpr int kYPer = 16 * KYP / 128;
+#pragma unroll
+  for (int rt = 0; rt < 2; ++rt) {
+#pragma unroll
+    for (int cg = 0; cg < CG; ++cg)
+      ot[(4 * g + q) * KYP + ((4 * cg + (lane & 3)) ^ (4 * g))] = alpha * acc[rt][cg];
+#pragma unroll
+    for (int m = 0; m < kYPer; ++m) {
+      const int e = 2 * lane + 128 * m, row = e / KYP, c = e % KYP;
+      const int64_t r = rw + 16 * rt + row;
+      d2v v = *reinterpret_cast<const d2v*>(ot + row * KYP + (c ^ (4 * ((row >> 2) & 3))));
+      if (r >= r0 && r < nrows) {
+        const int t = c / Y.w;
+        d2v* yp = reinterpret_cast<d2v*>(const_cast<double*>(Y.ptr[t]) + r * Y.w + (c - t * Y.w));
+        if (beta != 0.0) v += beta * *yp;
+        *yp = v;
+      }
+    }
+  }
+}
+
 // the epilogue stores Y row-major 16 B (two columns) per lane: Y panel widths must be even
 bool tsmm44_ok(int xw, int ky, int yw) {
   return (xw == 16 || xw == 32) && ky >= 1 && ky <= 64 && yw % 2 == 0;
@@ -375,6 +487,20 @@ static void launch_tsmm44(int64_t nrows, const PanelRun& X, const double* C, int
 void tsmm44(int64_t nrows, const PanelRun& X, const double* C, int ldc, const Panels& Y,
             double alpha, double beta, const int* skip, hipStream_t st) {
   const int KY = Y.count * Y.w;
+  static const bool fast_ok = [] {
+    const char* e = getenv("RBL_TSMM44_FAST");
+    return !e || atoi(e) != 0;
+  }();
+  if (fast_ok && KY == 64 && (X.count * X.w) % kT44K == 0 && nrows >= kT44Rows && Y.w % 2 == 0) {
+    const int64_t wgs = (nrows + 4 * kT44Rows - 1) / (4 * kT44Rows);
+    if (X.w == 32)
+      hipLaunchKernelGGL((k_tsmm44f<32>), dim3((unsigned)wgs), dim3(256), 0, st, nrows, X, C, ldc, Y,
+                         alpha, beta, skip);
+    else
+      hipLaunchKernelGGL((k_tsmm44f<16>), dim3((unsigned)wgs), dim3(256), 0, st, nrows, X, C, ldc, Y,
+                         alpha, beta, skip);
+    return;
+  }
   if (X.w == 32) {
     if (KY <= 16) return launch_tsmm44<32, 16>(nrows, X, C, ldc, KY, Y, alpha, beta, skip, st);
     if (KY <= 32) return launch_tsmm44<32, 32>(nrows, X, C, ldc, KY, Y, alpha, beta, skip, st);

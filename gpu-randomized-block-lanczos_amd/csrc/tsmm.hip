@@ -113,7 +113,7 @@ static int tiles16(int x) { return (x + 15) / 16; }
 static int pick_at(int w) { int t = tiles16(w); return t <= 1 ? 1 : (t <= 2 ? 2 : 4); }
 
 int gram_splits(int64_t nrows, int nW, int w, int xcols) {
-  if (xcols % w == 0 && gram44_ok(nW, w, xcols / w, w)) return gram44_splits(nrows, nW);
+  if (xcols % w == 0 && gram44_ok(nrows, nW, w, xcols / w, w)) return gram44_splits(nrows, nW);
   const int ctt = tiles16(xcols);
   const int ct = ctt <= 1 ? 1 : (ctt <= 2 ? 2 : 4);
   const int ncg = (ctt + ct - 1) / ct;
@@ -142,7 +142,7 @@ static void launch_gram_t(int64_t nrows, const PanelRun& W, const Panels& X, dou
 
 void gram_partial(int64_t nrows, const PanelRun& W, const Panels& X, double* slab, int splits,
                   const int* skip, hipStream_t s) {
-  if (gram44_ok(W.count, W.w, X.count, X.w)) return gram44_partial(nrows, W, X, slab, splits, skip, s);
+  if (gram44_ok(nrows, W.count, W.w, X.count, X.w)) return gram44_partial(nrows, W, X, slab, splits, skip, s);
   const int at = pick_at(W.w);
   const int ctt = tiles16(X.count * X.w);
   const int ct = ctt <= 1 ? 1 : (ctt <= 2 ? 2 : 4);
