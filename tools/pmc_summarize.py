@@ -59,7 +59,7 @@ def main():
     spmm = {k: v for k, v in kern.items() if k.startswith("k_spmm")}
     tot_l = sum(v["launches"] for v in spmm.values())
     spmm_bytes = sum(v["hbm_bytes_per_launch"] * v["launches"] for v in spmm.values()) / max(tot_l, 1)
-    reo = {k: v for k, v in kern.items() if k.startswith(("k_gram44", "k_tsmm44<32, 64>"))}
+    reo = {k: v for k, v in kern.items() if k.startswith(("k_gram44", "k_tsmm44<32, 64>", "k_tsmm44f"))}
     runs = 1  # bench.py --steps 1 --warmup 0: one 38-step run
     reorth_bytes = sum(v["hbm_bytes_per_launch"] * v["launches"] for v in reo.values()) / runs
     res = {
