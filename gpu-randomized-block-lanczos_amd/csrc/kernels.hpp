@@ -81,8 +81,11 @@ constexpr int64_t kSegPack = 512;   // nonzeros per packed short-row task (<= 64
 // X may equal Y (in place).  b in {16, 32}.
 bool rowgram_ok(int b);
 int rowgram_grid(int64_t nrows);
+// X32 (optional): X read from fp32 instead (widened exactly).  Y32 (optional): Y' written to
+// Y32 rounded to fp32 instead of Y — unless f64flag is non-null and *f64flag != 0 (device).
 void rowgram(int64_t nrows, int b, const double* X, const double* C, int ldc, double* Y,
-             double alpha, double beta, double* slab, int grid, const int* skip, hipStream_t s);
+             double alpha, double beta, double* slab, int grid, const int* skip, hipStream_t s,
+             const float* X32 = nullptr, float* Y32 = nullptr, const int* f64flag = nullptr);
 
 // --- spmm.hip ----------------------------------------------------------------------------
 // U = A * Qin  (+ epilogue U -= Qprev * Bt^T with Bt = B_i row-major b x b, if Qprev).
@@ -106,9 +109,10 @@ bool spmm_band(const CsrDev& A, const double* Qin, int64_t col_off, int b, doubl
                int* ai_parts = nullptr);
 // spmm_bt.hip: band tiles in MFMA operand order streamed to VGPRs (b = 32, H in {32, 64});
 // false if not applicable.
+// Q32 / Qprev32 (optional, the fp32 basis): read fp32 blocks instead of Qin / Qprev.
 bool spmm_bt(const CsrDev& A, const double* Qin, int64_t col_off, int b, double* U,
              const double* Qprev, const double* Bi, hipStream_t s, double* ai_slab = nullptr,
-             int* ai_parts = nullptr);
+             int* ai_parts = nullptr, const float* Q32 = nullptr, const float* Qprev32 = nullptr);
 // band-tile format of the local CSR: tiles in consumption order (slot (round * grid + wg) * 4
 // + wave), zero-filled `out` of bt_tile_slots(ntiles, tiles_per_wg) * NG * 256 doubles
 int64_t bt_tile_slots(int64_t ntiles, int64_t tiles_per_wg);

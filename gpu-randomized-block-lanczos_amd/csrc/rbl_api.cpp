@@ -499,12 +499,14 @@ int tsmm_checked(rbl_ctx* ctx, const PanelRun& X, const double* C, int ldc, cons
 // Fused one-pass row operation (rowop.hip): Y = beta Y + alpha X C and, if G, the Gram
 // G = Y^T Y over all ranks.  b in {16, 32}.
 int rowop(rbl_ctx* ctx, const double* X, const double* C, double* Y, double alpha, double beta,
-          double* G, const int* skip) {
+          double* G, const int* skip, const float* X32 = nullptr, float* Y32 = nullptr,
+          const int* f64flag = nullptr) {
   const int b = ctx->b;
   const int grid = rowgram_grid(ctx->nloc);
   if (G && (size_t)grid * b * b > ctx->slab_elems)
     return fail(ctx, RBL_ERR_INVALID, "internal: row-op slab too small");
-  rowgram(ctx->nloc, b, X, C, b, Y, alpha, beta, G ? ctx->d_slab : nullptr, grid, skip, ctx->stream);
+  rowgram(ctx->nloc, b, X, C, b, Y, alpha, beta, G ? ctx->d_slab : nullptr, grid, skip, ctx->stream,
+          X32, Y32, f64flag);
   HIPC(hipGetLastError());
   if (!G) return RBL_OK;
   reduce_slab(ctx->d_slab, grid, (int64_t)b * b, G, skip, ctx->stream);
@@ -666,7 +668,9 @@ int upd32(rbl_ctx* ctx, const float* Xb, int nX, const double* C, int ldc, float
 // Shifted CholQR2 (+ a third pass after a shifted first pass).  `g1_ready`: S_G already holds
 // U^T U (the fused 3-term update computed it); each apply computes the next pass's Gram in the
 // same pass over the rows when b allows (rowop).
-int tsqr(rbl_ctx* ctx, const double* U, double* Qout, bool g1_ready = false) {
+// Qout32 (fp32 basis): the final Q goes to Qout32 rounded to fp32 (Qout then holds only a
+// pass-2 intermediate when the shifted pass 3 runs).
+int tsqr(rbl_ctx* ctx, const double* U, double* Qout, bool g1_ready = false, float* Qout32 = nullptr) {
   StageScope t(ctx, RBL_STAGE_QR);
   const int b = ctx->b;
   int* need3 = ctx->d_flags;      // [need3, skip3]
@@ -688,7 +692,9 @@ int tsqr(rbl_ctx* ctx, const double* U, double* Qout, bool g1_ready = false) {
   chol_step(G, b, ctx->n, 1, smallp(ctx, S_R), smallp(ctx, S_RINV), smallp(ctx, S_RTOT), need3,
             status, nullptr, ctx->stream);
   if (fused) {  // in place; the Gram feeds pass 3 when a shifted first pass asked for it
-    CHK(rowop(ctx, Qout, smallp(ctx, S_RINV), Qout, 1.0, 0.0, G, nullptr));
+    // (fp32 basis: the result goes straight to Qout32 unless pass 3 follows)
+    CHK(rowop(ctx, Qout, smallp(ctx, S_RINV), Qout, 1.0, 0.0, G, nullptr, nullptr, Qout32,
+              Qout32 ? need3 : nullptr));
   } else {
     CHK(tsmm_checked(ctx, run1(Qout, b), smallp(ctx, S_RINV), b, pan1(Qout, b), 1.0, 0.0, nullptr));
     CHK(gram(ctx, run1(Qout, b), pan1(Qout, b), G, skip3));
@@ -697,9 +703,10 @@ int tsqr(rbl_ctx* ctx, const double* U, double* Qout, bool g1_ready = false) {
   chol_step(G, b, ctx->n, 1, smallp(ctx, S_R), smallp(ctx, S_RINV), smallp(ctx, S_RTOT), need3,
             status, skip3, ctx->stream);
   if (fused) {
-    CHK(rowop(ctx, Qout, smallp(ctx, S_RINV), Qout, 1.0, 0.0, nullptr, skip3));
+    CHK(rowop(ctx, Qout, smallp(ctx, S_RINV), Qout, 1.0, 0.0, nullptr, skip3, nullptr, Qout32));
   } else {
     CHK(tsmm_checked(ctx, run1(Qout, b), smallp(ctx, S_RINV), b, pan1(Qout, b), 1.0, 0.0, skip3));
+    if (Qout32) cvt_f64_to_f32(Qout, Qout32, ctx->nloc * b, ctx->stream);
   }
   HIPC(hipGetLastError());
   return RBL_OK;
@@ -1447,11 +1454,17 @@ int rbl_step(rbl_ctx* ctx, int i, int part_reorth, double* A_out, double* B_out)
   HIPC(hipMemsetAsync(ctx->d_flags, 0, 4 * sizeof(int), ctx->stream));
   if (f32 && (part_reorth & 2))
     return fail(ctx, RBL_ERR_INVALID, "rbl_step: locked-vector reorth needs the fp64 basis");
+  // fp32 basis, single rank, band-tile SpMM: A Q_i and the 3-term update read the fp32 blocks
+  // and widen them on load — bit for bit the widened copies (RBL_gpu.jl:173-174), without the
+  // two conversion passes.  Step 1 multiplies the unrounded fp64 Q_1 of rbl_start.
+  const bool direct32 = f32 && i >= 2 && ctx->nranks == 1 && !ctx->dense &&
+                        (ctx->spmm_variant == 0 || ctx->spmm_variant == 4) && b == 32 &&
+                        (ctx->bt_ng == 5 || ctx->bt_ng == 9);
+  float* Qi32 = f32 ? slotp32(ctx, i - 1) : nullptr;
+  float* Qm32 = f32 && i >= 2 ? slotp32(ctx, i - 2) : nullptr;
   if (f32) {
     // FLOAT = Float32: partial and local reorth on the fp32 blocks, then the
     // current / previous block widened to fp64 (RBL_gpu.jl:164-174)
-    float* Qi32 = slotp32(ctx, i - 1);
-    float* Qm32 = i >= 2 ? slotp32(ctx, i - 2) : nullptr;
     if ((part_reorth & 1) && i >= 3) {
       StageScope t(ctx, RBL_STAGE_PART_REORTH);
       const int nW = i - 2;
@@ -1469,8 +1482,10 @@ int rbl_step(rbl_ctx* ctx, int i, int part_reorth, double* A_out, double* B_out)
       StageScope t(ctx, RBL_STAGE_LOC_REORTH);
       CHK(gram32(ctx, Qm32, 1, Qi32, nullptr, 1, ctx->d_C));
       CHK(upd32(ctx, Qm32, 1, ctx->d_C, b, Qi32, nullptr, 1));
-      cvt_f32_to_f64(Qi32, ctx->d_Qi64, ctx->nloc * b, ctx->stream);
-      cvt_f32_to_f64(Qm32, ctx->d_Qm64, ctx->nloc * b, ctx->stream);
+      if (!direct32) {
+        cvt_f32_to_f64(Qi32, ctx->d_Qi64, ctx->nloc * b, ctx->stream);
+        cvt_f32_to_f64(Qm32, ctx->d_Qm64, ctx->nloc * b, ctx->stream);
+      }
       HIPC(hipGetLastError());
     }
   }
@@ -1507,8 +1522,14 @@ int rbl_step(rbl_ctx* ctx, int i, int part_reorth, double* A_out, double* B_out)
     CHK(halo_exchange(ctx, Qi, &Qin, &off));
     StageScope t(ctx, RBL_STAGE_AQ);
     // the band kernel can also form the partials of A_i = Q_i^T U while U is in registers
-    ai_parts = apply_A(ctx, Qin, off, b, ctx->d_U, Qm, i >= 2 ? smallp(ctx, S_BPREV) : nullptr,
-                       ctx->d_slab);
+    if (direct32) {
+      if (!spmm_bt(csr(ctx), nullptr, 0, b, ctx->d_U, nullptr, smallp(ctx, S_BPREV), ctx->stream,
+                   ctx->d_slab, &ai_parts, Qi32, Qm32))
+        return fail(ctx, RBL_ERR_INVALID, "internal: fp32 band-tile SpMM not applicable");
+    } else {
+      ai_parts = apply_A(ctx, Qin, off, b, ctx->d_U, Qm, i >= 2 ? smallp(ctx, S_BPREV) : nullptr,
+                         ctx->d_slab);
+    }
     if (ai_parts < 0) return ai_parts;
     HIPC(hipGetLastError());
   }
@@ -1524,7 +1545,8 @@ int rbl_step(rbl_ctx* ctx, int i, int part_reorth, double* A_out, double* B_out)
       CHK(gram(ctx, run1(Qi, b), pan1(ctx->d_U, b), smallp(ctx, S_AI), nullptr));
     }
     if (fused)
-      CHK(rowop(ctx, Qi, smallp(ctx, S_AI), ctx->d_U, -1.0, 1.0, smallp(ctx, S_G), nullptr));
+      CHK(rowop(ctx, Qi, smallp(ctx, S_AI), ctx->d_U, -1.0, 1.0, smallp(ctx, S_G), nullptr,
+                direct32 ? Qi32 : nullptr));
     else
       CHK(tsmm_checked(ctx, run1(Qi, b), smallp(ctx, S_AI), b, pan1(ctx->d_U, b), -1.0, 1.0, nullptr));
   }
@@ -1536,9 +1558,7 @@ int rbl_step(rbl_ctx* ctx, int i, int part_reorth, double* A_out, double* B_out)
   if (!f32) {
     CHK(tsqr(ctx, ctx->d_U, slotp(ctx, i), fused));
   } else {  // Qg = FLOAT(Qg_d) (RBL_gpu.jl:182): the new block enters the basis rounded to fp32
-    CHK(tsqr(ctx, ctx->d_U, ctx->d_Qi64, fused));
-    cvt_f64_to_f32(ctx->d_Qi64, slotp32(ctx, i), ctx->nloc * b, ctx->stream);
-    HIPC(hipGetLastError());
+    CHK(tsqr(ctx, ctx->d_U, ctx->d_Qi64, fused, slotp32(ctx, i)));
   }
   copy_small(smallp(ctx, S_RTOT), smallp(ctx, S_BPREV), (int64_t)b * b, ctx->stream);
   HIPC(hipMemcpyAsync(ctx->h_pin, smallp(ctx, S_AI), (size_t)b * b * sizeof(double),

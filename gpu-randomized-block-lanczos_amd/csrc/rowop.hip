@@ -43,12 +43,18 @@ __device__ __forceinline__ void stnt(d2v v, d2v* p) {
   else *p = v;
 }
 
-template <int B, bool GRAM>
+// XF: X is read from X32 (fp32, widened exactly); YF: Y' goes to Y32 rounded to fp32 (as
+// cvt_f64_to_f32) unless *f64flag is set, then to Y in fp64 — the fp32-basis step's QR
+// (RBL_gpu.jl:182 `Qg = FLOAT(Qg_d)`) without a separate narrowing pass.
+template <int B, bool GRAM, bool XF = false, bool YF = false>
 __global__ __launch_bounds__(kRowThreads) __attribute__((amdgpu_waves_per_eu(GRAM ? 2 : 3))) void k_rowgram(int64_t nrows, const double* X,  // X may alias Y (in-place apply)
                                                          const double* __restrict__ C, int ldc,
                                                          double* Y, double alpha, double beta,
-                                                         double* __restrict__ slab, const int* skip) {
+                                                         double* __restrict__ slab, const int* skip,
+                                                         const float* X32, float* Y32,
+                                                         const int* f64flag) {
   if (skip && *skip) return;
+  const bool w64 = !YF || (f64flag && *f64flag);
   constexpr int CG = B / 4;
   constexpr int NH = B / 8;                 // A-operand loads per row tile (2 k each)
   constexpr int LDC = B + 8;                // C rows: lane-group rows differ by 2 (see reorth.hip)
@@ -82,7 +88,12 @@ __global__ __launch_bounds__(kRowThreads) __attribute__((amdgpu_waves_per_eu(GRA
       r = r < nrows ? r : nrows - 1;
 #pragma unroll
       for (int h = 0; h < NH; ++h)
-        xa[rt][h] = ldnt(reinterpret_cast<const d2v*>(X + r * B + 8 * h + 2 * q));
+        if constexpr (XF) {
+          const float2 f = *reinterpret_cast<const float2*>(X32 + r * B + 8 * h + 2 * q);
+          xa[rt][h] = d2v{(double)f.x, (double)f.y};
+        } else {
+          xa[rt][h] = ldnt(reinterpret_cast<const d2v*>(X + r * B + 8 * h + 2 * q));
+        }
     }
   };
   auto load_y = [&](int64_t b0, d2v (&yr)[1][kYPer]) {
@@ -169,7 +180,10 @@ __global__ __launch_bounds__(kRowThreads) __attribute__((amdgpu_waves_per_eu(GRA
         const int e = 2 * lane + 128 * m;
         const int64_t r = rbase + e / B;
         const d2v v = *reinterpret_cast<const d2v*>(ot + swz(e / B, e % B));
-        if (r < nrows) stnt(v, reinterpret_cast<d2v*>(Y + r * B + (e % B)));
+        if (r < nrows) {
+          if (w64) stnt(v, reinterpret_cast<d2v*>(Y + r * B + (e % B)));
+          else *reinterpret_cast<float2*>(Y32 + r * B + (e % B)) = make_float2((float)v.x, (float)v.y);
+        }
       }
     }
 #pragma unroll
@@ -207,9 +221,19 @@ __global__ __launch_bounds__(kRowThreads) __attribute__((amdgpu_waves_per_eu(GRA
 template <int B, bool GRAM>
 void launch_rowgram(int64_t nrows, const double* X, const double* C, int ldc, double* Y,
                     double alpha, double beta, double* slab, int grid, const int* skip,
-                    hipStream_t s) {
-  hipLaunchKernelGGL((k_rowgram<B, GRAM>), dim3(grid), dim3(kRowThreads), 0, s, nrows, X, C, ldc,
-                     Y, alpha, beta, slab, skip);
+                    hipStream_t s, const float* X32, float* Y32, const int* f64flag) {
+  if (X32 && Y32)
+    hipLaunchKernelGGL((k_rowgram<B, GRAM, true, true>), dim3(grid), dim3(kRowThreads), 0, s, nrows, X, C, ldc,
+                       Y, alpha, beta, slab, skip, X32, Y32, f64flag);
+  else if (X32)
+    hipLaunchKernelGGL((k_rowgram<B, GRAM, true, false>), dim3(grid), dim3(kRowThreads), 0, s, nrows, X, C, ldc,
+                       Y, alpha, beta, slab, skip, X32, Y32, f64flag);
+  else if (Y32)
+    hipLaunchKernelGGL((k_rowgram<B, GRAM, false, true>), dim3(grid), dim3(kRowThreads), 0, s, nrows, X, C, ldc,
+                       Y, alpha, beta, slab, skip, X32, Y32, f64flag);
+  else
+    hipLaunchKernelGGL((k_rowgram<B, GRAM>), dim3(grid), dim3(kRowThreads), 0, s, nrows, X, C, ldc,
+                       Y, alpha, beta, slab, skip, X32, Y32, f64flag);
 }
 
 }  // namespace
@@ -225,14 +249,15 @@ int rowgram_grid(int64_t nrows) {
 }
 
 void rowgram(int64_t nrows, int b, const double* X, const double* C, int ldc, double* Y,
-             double alpha, double beta, double* slab, int grid, const int* skip, hipStream_t s) {
+             double alpha, double beta, double* slab, int grid, const int* skip, hipStream_t s,
+             const float* X32, float* Y32, const int* f64flag) {
   const bool gram = slab != nullptr;
   if (b == 32) {
-    if (gram) launch_rowgram<32, true>(nrows, X, C, ldc, Y, alpha, beta, slab, grid, skip, s);
-    else launch_rowgram<32, false>(nrows, X, C, ldc, Y, alpha, beta, slab, grid, skip, s);
+    if (gram) launch_rowgram<32, true>(nrows, X, C, ldc, Y, alpha, beta, slab, grid, skip, s, X32, Y32, f64flag);
+    else launch_rowgram<32, false>(nrows, X, C, ldc, Y, alpha, beta, slab, grid, skip, s, X32, Y32, f64flag);
   } else {
-    if (gram) launch_rowgram<16, true>(nrows, X, C, ldc, Y, alpha, beta, slab, grid, skip, s);
-    else launch_rowgram<16, false>(nrows, X, C, ldc, Y, alpha, beta, slab, grid, skip, s);
+    if (gram) launch_rowgram<16, true>(nrows, X, C, ldc, Y, alpha, beta, slab, grid, skip, s, X32, Y32, f64flag);
+    else launch_rowgram<16, false>(nrows, X, C, ldc, Y, alpha, beta, slab, grid, skip, s, X32, Y32, f64flag);
   }
 }
 

@@ -80,13 +80,16 @@ struct BtArgs {
   int64_t row0;          // global index of local row 0
   double* U;             // padded to a multiple of 16 rows
   const double* Qprev;
+  const float* Q32;      // VAR bit 6: Q and Q_{i-1} are fp32 blocks (the fp32 basis), widened
+  const float* Qprev32;  //   exactly on load (RBL_gpu.jl:173-174 copyto!(Qg_d, Qg))
   const double* Bi;
   double* ai_slab;       // AIG: per-workgroup partials of A_i (32 x 32 row-major)
 };
 
 // VAR (tuning variants, RBL_BT_VAR): bit 0 non-temporal A loads, bit 1 non-temporal U
 // stores, bit 2 ring reads software-pipelined one k-step ahead (bit 3: two k-steps ahead),
-// bit 4 A prefetched two tiles ahead, bit 5 ablation: main-loop MFMAs off (loads only)
+// bit 4 A prefetched two tiles ahead, bit 5 ablation: main-loop MFMAs off (loads only),
+// bit 6 fp32 Q / Q_{i-1} inputs
 template <int NG, bool EPI, bool AIG, int VAR = 0>
 __global__ __launch_bounds__(bt::kThreads) __attribute__((amdgpu_waves_per_eu(1, 1)))
 void k_spmm_bt(BtArgs a) {
@@ -106,10 +109,17 @@ void k_spmm_bt(BtArgs a) {
   const int64_t gq = a.row0 - H;  // global row of ring coordinate 0
 
   // 16-B chunk (slot s) of the Q row at ring coordinate rho; absent rows read zeros
-  auto qsrc = [&](int64_t rho, int s) -> const d2v* {
+  auto qload = [&](int64_t rho, int s) -> d2v {
     const int64_t c = rho + gq;
-    const double* p = (c >= a.q_lo && c < a.q_hi) ? a.Q + (c - a.col_off) * B : a.zrow;
-    return reinterpret_cast<const d2v*>(p) + s;
+    const bool in = c >= a.q_lo && c < a.q_hi;
+    if constexpr (VAR & 64) {
+      const float* p = in ? a.Q32 + (c - a.col_off) * B : reinterpret_cast<const float*>(a.zrow);
+      const float2 f = reinterpret_cast<const float2*>(p)[s];
+      return d2v{(double)f.x, (double)f.y};
+    } else {
+      const double* p = in ? a.Q + (c - a.col_off) * B : a.zrow;
+      return reinterpret_cast<const d2v*>(p)[s];
+    }
   };
   auto ring_ptr = [&](int64_t rho, int s) -> d2v* {
     return reinterpret_cast<d2v*>(smem + (unsigned)(rho & (bt::kRing - 1)) * bt::kRowBytes + 16u * s);
@@ -128,7 +138,7 @@ void k_spmm_bt(BtArgs a) {
   }
   for (int idx = tid; idx < kRingSpan * 16; idx += bt::kThreads) {
     const int64_t rho = 16 * T0 + idx / 16;
-    *ring_ptr(rho, idx & 15) = *qsrc(rho, idx & 15);
+    *ring_ptr(rho, idx & 15) = qload(rho, idx & 15);
   }
 
   // ---- per-wave state ----
@@ -155,15 +165,22 @@ void k_spmm_bt(BtArgs a) {
       av[d][g][0] = tile_a(clamp_t(T0 + wave + 4 * d), g, 0);
       av[d][g][1] = tile_a(clamp_t(T0 + wave + 4 * d), g, 1);
     }
-  auto qprev_row = [&](int64_t t) -> const d2v* {
+  auto qprev_load = [&](int64_t t, d2v (&qv)[4]) {
     int64_t r = 16 * t + i16;
     r = r < a.nrows ? r : a.nrows - 1;
-    return reinterpret_cast<const d2v*>(a.Qprev + r * B + 2 * q);
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      if constexpr (VAR & 64) {
+        const float2 f = *reinterpret_cast<const float2*>(a.Qprev32 + r * B + 2 * q + 8 * m);
+        qv[m] = d2v{(double)f.x, (double)f.y};
+      } else {
+        qv[m] = reinterpret_cast<const d2v*>(a.Qprev + r * B + 2 * q)[4 * m];
+      }
+    }
   };
   d2v qp[4];
   if constexpr (EPI) {
-#pragma unroll
-    for (int m = 0; m < 4; ++m) qp[m] = qprev_row(clamp_t(T0 + wave))[4 * m];
+    qprev_load(clamp_t(T0 + wave), qp);
   }
   double ai[2][8];
 #pragma unroll
@@ -183,7 +200,7 @@ void k_spmm_bt(BtArgs a) {
     d2v st[4];
     const int64_t rn = R + kRingSpan + 16 * wave;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) st[i] = *qsrc(rn + 4 * i + q, i16);
+    for (int i = 0; i < 4; ++i) st[i] = qload(rn + 4 * i + q, i16);
 
     if (tw < T1) {  // wave-uniform
       const int64_t tn = clamp_t(tw + 4 * DEPTH);
@@ -257,8 +274,7 @@ void k_spmm_bt(BtArgs a) {
             acc[p][1] = mfma44(qv, bv.y, acc[p][1]);
           }
         }
-#pragma unroll
-        for (int m = 0; m < 4; ++m) qp[m] = qprev_row(clamp_t(tw + 4))[4 * m];
+        qprev_load(clamp_t(tw + 4), qp);
       }
       const int64_t ru = 16 * tw + 4 * G + q;  // this lane's U row
       d2v* urow = reinterpret_cast<d2v*>(a.U + ru * B + 2 * j);
@@ -347,35 +363,25 @@ static void launch_bt_v(const BtArgs& a, int grid, hipStream_t s) {
   hipLaunchKernelGGL((k_spmm_bt<NG, EPI, AIG, VAR>), dim3(grid), dim3(bt::kThreads), bt::kLds, s, a);
 }
 template <int NG, bool EPI, bool AIG>
-static void launch_bt_t(const BtArgs& a, int grid, hipStream_t s) {
+static void launch_bt_t(const BtArgs& a, int grid, hipStream_t s, bool f32) {
+  // default: non-temporal A loads and U stores (VAR 3): the format is read once per launch
+  // and U only by the next kernel — measured 7 % faster at C4a than the default policy;
+  // RBL_BT_VAR = 0 / 35 (diagnostics): default policy / loads-only ablation
   static const int var = [] {
     const char* e = getenv("RBL_BT_VAR");
-    return e ? atoi(e) : -1;
+    return e ? atoi(e) : 3;
   }();
-  // default: non-temporal A loads and U stores (VAR 3): the format is read once per launch
-  // and U only by the next kernel — measured 7 % faster at C4a than the default policy
-  if constexpr (NG == 9 && EPI && AIG) {  // tuning variants (diagnostics)
-    switch (var) {
-      case 0: return launch_bt_v<NG, EPI, AIG, 0>(a, grid, s);
-      case 1: return launch_bt_v<NG, EPI, AIG, 1>(a, grid, s);
-      case 2: return launch_bt_v<NG, EPI, AIG, 2>(a, grid, s);
-      case 3: return launch_bt_v<NG, EPI, AIG, 3>(a, grid, s);
-      case 4: return launch_bt_v<NG, EPI, AIG, 4>(a, grid, s);
-      case 7: return launch_bt_v<NG, EPI, AIG, 7>(a, grid, s);
-      case 8: return launch_bt_v<NG, EPI, AIG, 8>(a, grid, s);
-      case 11: return launch_bt_v<NG, EPI, AIG, 11>(a, grid, s);
-      case 16: return launch_bt_v<NG, EPI, AIG, 16>(a, grid, s);
-      case 19: return launch_bt_v<NG, EPI, AIG, 19>(a, grid, s);
-      case 32: return launch_bt_v<NG, EPI, AIG, 32>(a, grid, s);
-      case 35: return launch_bt_v<NG, EPI, AIG, 35>(a, grid, s);
-      default: break;
-    }
+  if (f32) return launch_bt_v<NG, EPI, AIG, 3 | 64>(a, grid, s);
+  if constexpr (NG == 9 && EPI && AIG) {
+    if (var == 0) return launch_bt_v<NG, EPI, AIG, 0>(a, grid, s);
+    if (var == 35) return launch_bt_v<NG, EPI, AIG, 35>(a, grid, s);
   }
   launch_bt_v<NG, EPI, AIG, 3>(a, grid, s);
 }
 
 bool spmm_bt(const CsrDev& A, const double* Qin, int64_t col_off, int b, double* U,
-             const double* Qprev, const double* Bi, hipStream_t s, double* ai_slab, int* ai_parts) {
+             const double* Qprev, const double* Bi, hipStream_t s, double* ai_slab, int* ai_parts,
+             const float* Q32, const float* Qprev32) {
   if (b != 32 || !A.bt || A.ntiles <= 0 || !(A.bt_ng == 5 || A.bt_ng == 9)) return false;
   BtArgs a;
   a.nrows = A.nrows;
@@ -390,16 +396,19 @@ bool spmm_bt(const CsrDev& A, const double* Qin, int64_t col_off, int b, double*
   a.row0 = A.row0;
   a.U = U;
   a.Qprev = Qprev;
+  a.Q32 = Q32;
+  a.Qprev32 = Qprev32;
   a.Bi = Bi;
   const int grid = (int)((A.ntiles + A.bt_tiles_per_wg - 1) / A.bt_tiles_per_wg);
-  const bool epi = Qprev != nullptr;
+  const bool f32 = Q32 != nullptr;
+  const bool epi = Qprev != nullptr || Qprev32 != nullptr;
   const bool aig = ai_slab != nullptr;
   a.ai_slab = ai_slab;
   if (ai_parts) *ai_parts = aig ? grid : 0;
   const int key = (A.bt_ng == 9 ? 4 : 0) | (epi ? 2 : 0) | (aig ? 1 : 0);
   switch (key) {
 #define RBL_BT_CASE(K, NG, E, G) \
-    case K: launch_bt_t<NG, E, G>(a, grid, s); break;
+    case K: launch_bt_t<NG, E, G>(a, grid, s, f32); break;
     RBL_BT_CASE(0, 5, false, false) RBL_BT_CASE(1, 5, false, true)
     RBL_BT_CASE(2, 5, true, false)  RBL_BT_CASE(3, 5, true, true)
     RBL_BT_CASE(4, 9, false, false) RBL_BT_CASE(5, 9, false, true)

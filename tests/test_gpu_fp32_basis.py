@@ -36,9 +36,12 @@ def c1_matrix(n, k, W=64, seed=20261015):
     return matgen.hashwindow_csr(n, W, p, seed, matgen.planted_spectrum(k))
 
 
-@pytest.mark.parametrize("b", [16, 32])
-def test_first_steps_trace_fp32(rbl, b):
-    A = c1_matrix(4000, 10)
+@pytest.mark.parametrize("b,dense", [(16, False), (32, False), (32, True)])
+def test_first_steps_trace_fp32(rbl, b, dense):
+    """dense: a 77 %-filled band, so b = 32 takes the band-tile SpMM reading the fp32 blocks
+    directly (no widening passes; rbl_step direct32)."""
+    A = (matgen.hashwindow_csr(6000, 64, 0.7734, 5, matgen.planted_spectrum(10)) if dense
+         else c1_matrix(4000, 10))
     n = A.shape[0]
     omega = np.random.default_rng(b).standard_normal((n, b))
     steps = 6
@@ -46,6 +49,7 @@ def test_first_steps_trace_fp32(rbl, b):
                           max_steps=steps, trace=True)
     with rbl.Context(0) as ctx:
         ctx.set_matrix(A)
+        assert (ctx.spmm_kernel_for(b) == 5) == dense
         _, _, info = rbl.lanczos(ctx, 10, b, omega=omega, check=False, max_steps=steps,
                                  trace=True, ritz=False, basis_bits=32)
         blocks = [ctx.get_block(j) for j in range(1, steps + 1)]
