@@ -744,6 +744,39 @@ int halo_exchange(rbl_ctx* ctx, const double* Q, const double** Qin, int64_t* of
   return RBL_OK;
 }
 
+// fp32 halo exchange (the fp32 basis read directly by the band-tile SpMM): the same row
+// ranges as halo_exchange, fp32 rows moved as byte-identical pairs (b is even)
+int halo_exchange32(rbl_ctx* ctx, const float* Q, const float** Qin, int64_t* off) {
+  if (ctx->nranks == 1) {
+    *Qin = Q;
+    *off = 0;
+    return RBL_OK;
+  }
+  StageScope t(ctx, RBL_STAGE_COMM);
+  const int b = ctx->b;
+  float* ext = reinterpret_cast<float*>(ctx->d_qext);
+  HIPC(hipMemcpyAsync(ext + (ctx->r0 - ctx->ext_lo) * b, Q, ctx->nloc * b * sizeof(float),
+                      hipMemcpyDeviceToDevice, ctx->stream));
+  std::vector<Comm::Xfer> x(ctx->nranks);
+  for (int q = 0; q < ctx->nranks; ++q) {
+    if (q == ctx->rank) continue;
+    const int64_t gl = ctx->give_lo[q], gh = ctx->give_hi[q];
+    if (gh > gl) {
+      x[q].send = reinterpret_cast<const double*>(Q + (gl - ctx->r0) * b);
+      x[q].nsend = (size_t)(gh - gl) * b / 2;
+    }
+    const int64_t nl = ctx->need_lo[q], nh = ctx->need_hi[q];
+    if (nh > nl) {
+      x[q].recv = reinterpret_cast<double*>(ext + (nl - ctx->ext_lo) * b);
+      x[q].nrecv = (size_t)(nh - nl) * b / 2;
+    }
+  }
+  COMMC(ctx->comm->exchange(x, ctx->stream, &ctx->err));
+  *Qin = ext;
+  *off = ctx->ext_lo;
+  return RBL_OK;
+}
+
 void free_run(rbl_ctx* ctx) {
   if (ctx->cstream) hipStreamSynchronize(ctx->cstream);
   hipFree(ctx->d_basis); ctx->d_basis = nullptr;
@@ -1454,10 +1487,11 @@ int rbl_step(rbl_ctx* ctx, int i, int part_reorth, double* A_out, double* B_out)
   HIPC(hipMemsetAsync(ctx->d_flags, 0, 4 * sizeof(int), ctx->stream));
   if (f32 && (part_reorth & 2))
     return fail(ctx, RBL_ERR_INVALID, "rbl_step: locked-vector reorth needs the fp64 basis");
-  // fp32 basis, single rank, band-tile SpMM: A Q_i and the 3-term update read the fp32 blocks
-  // and widen them on load — bit for bit the widened copies (RBL_gpu.jl:173-174), without the
-  // two conversion passes.  Step 1 multiplies the unrounded fp64 Q_1 of rbl_start.
-  const bool direct32 = f32 && i >= 2 && ctx->nranks == 1 && !ctx->dense &&
+  // fp32 basis with the band-tile SpMM: A Q_i (after an fp32 halo exchange) and the 3-term
+  // update read the fp32 blocks and widen them on load — bit for bit the widened copies
+  // (RBL_gpu.jl:173-174), without the two conversion passes.  Step 1 multiplies the unrounded
+  // fp64 Q_1 of rbl_start.
+  const bool direct32 = f32 && i >= 2 && !ctx->dense &&
                         (ctx->spmm_variant == 0 || ctx->spmm_variant == 4) && b == 32 &&
                         (ctx->bt_ng == 5 || ctx->bt_ng == 9);
   float* Qi32 = f32 ? slotp32(ctx, i - 1) : nullptr;
@@ -1518,13 +1552,15 @@ int rbl_step(rbl_ctx* ctx, int i, int part_reorth, double* A_out, double* B_out)
   int ai_parts = 0;
   {
     const double* Qin = nullptr;
+    const float* Qin32 = nullptr;
     int64_t off = 0;
-    CHK(halo_exchange(ctx, Qi, &Qin, &off));
+    if (direct32) CHK(halo_exchange32(ctx, Qi32, &Qin32, &off));
+    else CHK(halo_exchange(ctx, Qi, &Qin, &off));
     StageScope t(ctx, RBL_STAGE_AQ);
     // the band kernel can also form the partials of A_i = Q_i^T U while U is in registers
     if (direct32) {
-      if (!spmm_bt(csr(ctx), nullptr, 0, b, ctx->d_U, nullptr, smallp(ctx, S_BPREV), ctx->stream,
-                   ctx->d_slab, &ai_parts, Qi32, Qm32))
+      if (!spmm_bt(csr(ctx), nullptr, off, b, ctx->d_U, nullptr, smallp(ctx, S_BPREV), ctx->stream,
+                   ctx->d_slab, &ai_parts, Qin32, Qm32))
         return fail(ctx, RBL_ERR_INVALID, "internal: fp32 band-tile SpMM not applicable");
     } else {
       ai_parts = apply_A(ctx, Qin, off, b, ctx->d_U, Qm, i >= 2 ? smallp(ctx, S_BPREV) : nullptr,
