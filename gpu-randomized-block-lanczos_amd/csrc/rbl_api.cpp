@@ -1410,7 +1410,11 @@ int rbl_start(rbl_ctx* ctx, int b, int max_blocks, int basis_bits, const double*
       }
     }
   } else {
-    HIPC(hipMalloc(&ctx->d_basis32, (size_t)(max_blocks + 1) * nl * b * sizeof(float)));
+    // + 16 zeroed pad rows, and every slot zeroed once: the fp32 Gram kernel's shifted chunks
+    // may read rows past a tiny slice (reorth32.hip), which must be finite
+    const size_t bytes32 = ((size_t)(max_blocks + 1) * nl + 16) * b * sizeof(float);
+    HIPC(hipMalloc(&ctx->d_basis32, bytes32));
+    HIPC(hipMemsetAsync(ctx->d_basis32, 0, bytes32, ctx->stream));
     HIPC(hipMalloc(&ctx->d_Qi64, (nl + kRowPad) * b * sizeof(double)));
     HIPC(hipMalloc(&ctx->d_Qm64, (nl + kRowPad) * b * sizeof(double)));
   }

@@ -45,7 +45,6 @@ __global__ __launch_bounds__(256) void k_gram32(int64_t nrows, const float* __re
   const int j = pg * kG32Waves + wave;
   const bool active = j < nW;
   const float* wp = Wb + (int64_t)(active ? j : 0) * wstride + c16;
-  const int64_t rlast = r_end > 0 ? r_end - 1 : 0;
 
   f4v acc[AT][CT];
 #pragma unroll
@@ -53,32 +52,41 @@ __global__ __launch_bounds__(256) void k_gram32(int64_t nrows, const float* __re
 #pragma unroll
     for (int c = 0; c < CT; ++c) acc[a][c] = f4v{0.f, 0.f, 0.f, 0.f};
 
-  // X staging: thread (row = tid / 16, cc = tid % 16) moves X[row][cc + 16 ct] (ct < CT)
+  // X staging: thread (row = tid / 16, cc = tid % 16) moves X[row][cc + 16 ct] (ct < CT).
+  // A partial last chunk is shifted back to end at r_end (wave-uniform row base, no per-lane
+  // clamps) and its rows below rc0 — already counted — zeroed on the X side, as in
+  // reorth.hip's k_gram44.  With nrows < 16 the chunk starts at row 0 and over-reads into the
+  // next basis slot or the zeroed allocation pad (rbl_start): finite rows met by zero X.
   const int xrow = tid >> 4, xcc = tid & 15;
-  auto load_x = [&](int64_t rc0, float (&xr)[CT]) {
-    const int64_t r = rc0 + xrow;
-    const int64_t rc = r < rlast ? r : rlast;
+  const float* xsl[CT];
 #pragma unroll
-    for (int ct = 0; ct < CT; ++ct) {
-      const int c = xcc + 16 * ct;
-      const float* src = (NX == 2 && c >= W) ? X1 + rc * W + (c - W) : X0 + rc * W + c;
-      xr[ct] = *src;
-    }
+  for (int ct = 0; ct < CT; ++ct) {
+    const int c = xcc + 16 * ct;
+    xsl[ct] = ((NX == 2 && c >= W) ? X1 + (c - W) : X0 + c) + (int64_t)xrow * W;
+  }
+  const float* wl = wp + q * W;
+  auto shift = [&](int64_t rc0) -> int64_t {
+    const int64_t r = rc0 < r_end - kG32Rows ? rc0 : r_end - kG32Rows;
+    return r > 0 ? r : 0;
+  };
+  auto load_x = [&](int64_t rc0, float (&xr)[CT]) {
+    const int64_t o = shift(rc0) * W;
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) xr[ct] = xsl[ct][o];
   };
   auto store_x = [&](int buf, int64_t rc0, const float (&xr)[CT]) {
-    const bool ok = rc0 + xrow < r_end;  // rows past the split meet zero X (clamped W rows)
+    const int64_t row = shift(rc0) + xrow;
+    const bool ok = row >= rc0 && row < r_end;
     float* d = &xs[buf][xrow * 64 + 4 * xcc];
 #pragma unroll
     for (int ct = 0; ct < CT; ++ct) d[ct] = ok ? xr[ct] : 0.f;
   };
   auto load_a = [&](int64_t rc0, float (&ar)[4][AT]) {
+    const float* p = wl + shift(rc0) * W;
 #pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      const int64_t r = rc0 + 4 * ks + q;
-      const int64_t rc = r < rlast ? r : rlast;
+    for (int ks = 0; ks < 4; ++ks)
 #pragma unroll
-      for (int a = 0; a < AT; ++a) ar[ks][a] = wp[rc * W + 16 * a];
-    }
+      for (int a = 0; a < AT; ++a) ar[ks][a] = p[4 * ks * W + 16 * a];
   };
 
   const int64_t nchunks = r_end > r_begin ? (r_end - r_begin + kG32Rows - 1) / kG32Rows : 0;
@@ -256,6 +264,115 @@ __global__ __launch_bounds__(256) void k_tsmm32(int64_t nrows, const float* __re
     }
 }
 
+// Fast path of k_tsmm32 for the partial-reorth update (W = 32, 64 output columns, K a
+// multiple of 32, nrows >= 32): 32 k per chunk (half the barriers), wave-uniform bases plus
+// lane constants (no per-load clamps), a wave past nrows computes the last 32 rows and stores
+// only its own, 16-B Y stores through the wave's LDS tile.
+constexpr int kT32KF = 32;
+__global__ __launch_bounds__(256) void k_tsmm32f(int64_t nrows, const float* __restrict__ Xb,
+                                                 int64_t xstride, int nX, const double* __restrict__ C,
+                                                 int ldc, float* Y0, float* Y1, float alpha,
+                                                 float beta) {
+  constexpr int W = 32, KYP = 64, CT = 4, CLD = 64;
+  // two C buffers; after the k-loop the same LDS holds the 4 waves' 16 x (64 + 4) Y tiles
+  __shared__ __attribute__((aligned(16))) float cs[2][kT32KF * CLD + 128];
+  static_assert(2 * (kT32KF * CLD + 128) >= 4 * 16 * (KYP + 4), "epilogue tiles fit");
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int q = lane >> 4, c16 = lane & 15;
+  const int64_t r0 = ((int64_t)blockIdx.x * 4 + wave) * kT32Rows;
+  const int64_t rw = r0 + kT32Rows <= nrows ? r0 : nrows - kT32Rows;  // wave-uniform
+  const int nch = nX * W / kT32KF;
+
+  f4v acc[2][CT];
+#pragma unroll
+  for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+    for (int c = 0; c < CT; ++c) acc[rt][c] = f4v{0.f, 0.f, 0.f, 0.f};
+
+  // A: rows rw + 16 rt + c16; k = 32 ch + 16 hh + 4 q + s (one float4 per (rt, hh))
+  const int aoff = c16 * W + 4 * q;
+  auto load_a = [&](int ch, f4v (&ar)[2][2]) {
+    const int chc = ch < nch ? ch : nch - 1;
+    const float* xb = Xb + (int64_t)chc * xstride + rw * W;  // W = 32 = k per chunk: panel chc
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh)
+        ar[rt][hh] = *reinterpret_cast<const f4v*>(xb + aoff + 16 * rt * W + 16 * hh);
+  };
+  // C chunk: 32 x 64; thread (k = tid / 16 + 16 hh, cc = tid % 16) moves C[k][cc + 16 ct]
+  const int ck = tid >> 4, ccc = tid & 15;
+  auto load_c = [&](int ch, float (&cr)[2][CT]) {
+    const int chc = ch < nch ? ch : nch - 1;
+    const double* cb = C + (int64_t)(kT32KF * chc + ck) * ldc + ccc;
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct) cr[hh][ct] = alpha * (float)cb[(int64_t)(16 * hh) * ldc + 16 * ct];
+  };
+  auto store_c = [&](int buf, const float (&cr)[2][CT]) {
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh)
+      *reinterpret_cast<f4v*>(&cs[buf][(ck + 16 * hh) * CLD + 4 * ccc]) =
+          f4v{cr[hh][0], cr[hh][1], cr[hh][2], cr[hh][3]};
+  };
+
+  f4v acur[2][2], anext[2][2];
+  float cr[2][CT];
+  load_c(0, cr);
+  store_c(0, cr);
+  load_a(0, acur);
+  __syncthreads();
+  for (int ch = 0; ch < nch; ++ch) {
+    load_c(ch + 1, cr);
+    load_a(ch + 1, anext);
+    const float* cb = cs[ch & 1] + 4 * c16;
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const f4v bv = *reinterpret_cast<const f4v*>(cb + (16 * hh + 4 * q + s) * CLD);
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+          for (int c = 0; c < CT; ++c) acc[rt][c] = mfma16(acur[rt][hh][s], bv[c], acc[rt][c]);
+      }
+    store_c((ch + 1) & 1, cr);
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt) {
+      acur[rt][0] = anext[rt][0];
+      acur[rt][1] = anext[rt][1];
+    }
+    __syncthreads();
+  }
+  // epilogue: D tile (lane: rows 4q + v, column c16 of tile c) -> LDS (free after the last
+  // barrier) -> row-major float4 stores of Y0 | Y1 (rows below r0: the previous wave's)
+  float* ot = &cs[0][0] + wave * 16 * (KYP + 4);
+#pragma unroll
+  for (int rt = 0; rt < 2; ++rt) {
+#pragma unroll
+    for (int c = 0; c < CT; ++c)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) ot[(4 * q + v) * (KYP + 4) + 16 * c + c16] = acc[rt][c][v];
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const int e = 4 * lane + 256 * m, row = e / KYP, col = e % KYP;
+      const int64_t r = rw + 16 * rt + row;
+      f4v y = *reinterpret_cast<const f4v*>(ot + row * (KYP + 4) + col);
+      if (r >= r0 && r < nrows) {
+        float* yp = (col < W ? Y0 + col : Y1 + (col - W)) + r * W;
+        if (beta != 0.f) y += beta * *reinterpret_cast<const f4v*>(yp);
+        *reinterpret_cast<f4v*>(yp) = y;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
 template <int W, int KYP>
 static void launch_tsmm32(int64_t nrows, const float* Xb, int64_t xstride, int nX, const double* C,
                           int ldc, int KY, float* Y0, float* Y1, float alpha, float beta,
@@ -269,6 +386,12 @@ void tsmm32(int64_t nrows, const float* Xb, int64_t xstride, int nX, int w, cons
             float* Y0, float* Y1, int ycount, float alpha, float beta, hipStream_t st) {
   if (nrows <= 0) return;
   const int KY = ycount * w;
+  if (w == 32 && KY == 64 && nrows >= kT32Rows) {
+    const int64_t wgs = (nrows + 4 * kT32Rows - 1) / (4 * kT32Rows);
+    hipLaunchKernelGGL(k_tsmm32f, dim3((unsigned)wgs), dim3(256), 0, st, nrows, Xb, xstride, nX, C,
+                       ldc, Y0, Y1, alpha, beta);
+    return;
+  }
   if (w == 32) {
     if (KY <= 32) return launch_tsmm32<32, 32>(nrows, Xb, xstride, nX, C, ldc, KY, Y0, Y1, alpha, beta, st);
     return launch_tsmm32<32, 64>(nrows, Xb, xstride, nX, C, ldc, KY, Y0, Y1, alpha, beta, st);

@@ -114,3 +114,31 @@ def test_fp32_basis_rejects_other_b(rbl):
         ctx.set_matrix(A)
         with pytest.raises(rbl.RBLError):
             ctx.start(8, 4, seed=1, basis_bits=32)
+
+
+def test_fp32_basis_tiny_slices(rbl):
+    """Slices under 16 rows (3 ranks on n = 40, b = 16): the fp32 Gram kernel's shifted chunk
+    reads past the slice into zeroed rows; the trace must equal the single-rank run's."""
+    from test_gpu_multirank import run_ranks
+    import scipy.sparse as sp
+    rng = np.random.default_rng(11)
+    M = rng.standard_normal((40, 40))
+    A = sp.csr_matrix(M + M.T)
+    omega = rng.standard_normal((40, 16))
+    with rbl.Context(0) as ctx:
+        ctx.set_matrix(A)
+        _, _, info1 = rbl.lanczos(ctx, 2, 16, omega=omega, check=False, max_steps=2, trace=True,
+                                  ritz=False, basis_bits=32)
+
+    def fn(ctx, r):
+        ctx.set_matrix(A)
+        _, r0, r1, _ = ctx.matrix_info()
+        assert r1 - r0 < 16
+        _, _, info = rbl.lanczos(ctx, 2, 16, omega=omega[r0:r1], check=False, max_steps=2,
+                                 trace=True, ritz=False, basis_bits=32)
+        return info
+
+    for info in run_ranks(rbl, 3, fn):
+        for a, a1 in zip(info.trace_A, info1.trace_A):
+            assert np.all(np.isfinite(a))
+            assert np.abs(a - a1).max() <= 1e-5 * np.abs(a1).max()
