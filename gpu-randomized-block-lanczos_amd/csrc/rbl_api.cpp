@@ -1296,7 +1296,7 @@ int rbl_spmm_kernel_for(rbl_ctx* ctx, int b) {
   const int v = ctx->spmm_variant;
   const bool band = ctx->ntiles > 0 && ((b == 16 && ctx->band_ok16) || (b == 32 && ctx->band_ok32));
   const bool win = ctx->ntiles > 0 && ((b == 16 && ctx->window_ok16) || (b == 32 && ctx->window_ok32));
-  if ((v == 0 || v == 4) && b == 32 && (ctx->bt_ng == 5 || ctx->bt_ng == 9)) return 5;
+  if ((v == 0 || v == 4) && (b == 32 || b == 16) && (ctx->bt_ng == 5 || ctx->bt_ng == 9)) return 5;
   if ((v == 0 || v == 3 || v == 4) && band) return 3;
   if ((v == 0 || v == 2 || v == 3) && win) return 2;
   if ((v == 0 || v == 5) && ctx->seg_ntasks > 0 && (b == 16 || b == 32)) return 6;
@@ -1496,7 +1496,7 @@ int rbl_step(rbl_ctx* ctx, int i, int part_reorth, double* A_out, double* B_out)
   // (RBL_gpu.jl:173-174), without the two conversion passes.  Step 1 multiplies the unrounded
   // fp64 Q_1 of rbl_start.
   const bool direct32 = f32 && i >= 2 && !ctx->dense &&
-                        (ctx->spmm_variant == 0 || ctx->spmm_variant == 4) && b == 32 &&
+                        (ctx->spmm_variant == 0 || ctx->spmm_variant == 4) && (b == 32 || b == 16) &&
                         (ctx->bt_ng == 5 || ctx->bt_ng == 9);
   float* Qi32 = f32 ? slotp32(ctx, i - 1) : nullptr;
   float* Qm32 = f32 && i >= 2 ? slotp32(ctx, i - 2) : nullptr;

@@ -42,21 +42,26 @@ namespace rbl {
 
 namespace bt {
 constexpr int kThreads = 256;
-constexpr int kRing = 256;                       // ring rows (power of two)
-// ring row = 16 data slots of 16 B + 4 pad slots: row rho starts at bank slot 4*rho mod 16,
-// so the lanes of one ds_read_b128 lane group (rows rho, rho+1 or rho+2, rho+3 at the same
-// logical slots) land on disjoint banks
-constexpr int kRowBytes = 320;
-constexpr int kRingBytes = kRing * kRowBytes;   // 80 KiB
-constexpr int kBtOff = kRingBytes;              // epilogue B operand table: 8 x 4 x 16 d2v
-constexpr int kBtBytes = 1024 * 8;
-constexpr int kUStride = 336;                   // U stage row: 21 slots (bank shift 5 per row)
-constexpr int kUWave = 16 * kUStride;
-constexpr int kUOff = kBtOff + kBtBytes;
-constexpr int kLds = kUOff + 4 * kUWave;        // 111,104 B: one workgroup per CU
-static_assert(kLds <= 160 * 1024, "LDS budget");
-// A_i operand: lane reads ring slot pi(l & 15); pi maps the lanes {0-3, 12-15} of each
-// ds_read_b128 lane group to slot classes {0,1} mod 4 and {4-11} to {2,3} mod 4, so rows
+constexpr int kRing = 256;  // ring rows (power of two)
+// Geometry per block width B (32 or 16).  Ring row: at B = 32, 16 data slots of 16 B + 4 pad
+// slots, so row rho starts at bank slot 4 rho mod 16 and the rows rho, rho+1 (rho+2, rho+3)
+// that one ds_read_b128 lane group reads at the same logical slots land on disjoint banks;
+// at B = 16 a row is 128 B = 32 banks, so consecutive rows are disjoint already.  U stage row
+// (A_i operand): 21 slots at B = 32 (bank shift 5 per row), 128 B at B = 16.
+template <int B>
+struct Geo {
+  static constexpr int kRowBytes = B == 32 ? 320 : 128;
+  static constexpr int kRingBytes = kRing * kRowBytes;
+  static constexpr int kBtOff = kRingBytes;                  // epilogue B operand table
+  static constexpr int kBtBytes = B * B * 8;
+  static constexpr int kUStride = B == 32 ? 336 : 128;
+  static constexpr int kUWave = 16 * kUStride;
+  static constexpr int kUOff = kBtOff + kBtBytes;
+  static constexpr int kLds = kUOff + 4 * kUWave;           // B = 32: 111,104 B; B = 16: 43,008 B
+  static_assert(kLds <= 160 * 1024, "LDS budget");
+};
+// A_i operand at B = 32: lane reads ring slot pi(l & 15); pi maps the lanes {0-3, 12-15} of
+// each ds_read_b128 lane group to slot classes {0,1} mod 4 and {4-11} to {2,3} mod 4, so rows
 // rho (shift 0) and rho+1 (shift 4) never share a bank
 __device__ __forceinline__ int pi_slot(int i) {
   const int c = (i >> 2) == 0 ? 0 : (i >> 2) == 1 ? 2 : (i >> 2) == 2 ? 3 : 1;
@@ -73,7 +78,7 @@ struct BtArgs {
   int64_t ntiles;
   int64_t tiles_per_wg;
   const double* A;       // band tiles (bt_fill)
-  const double* Q;       // row c at Q + (c - col_off) * 32
+  const double* Q;       // row c at Q + (c - col_off) * b
   int64_t col_off;
   int64_t q_lo, q_hi;    // global rows present in Q; others read the zero row
   const double* zrow;    // 32 zeros
@@ -83,20 +88,21 @@ struct BtArgs {
   const float* Q32;      // VAR bit 6: Q and Q_{i-1} are fp32 blocks (the fp32 basis), widened
   const float* Qprev32;  //   exactly on load (RBL_gpu.jl:173-174 copyto!(Qg_d, Qg))
   const double* Bi;
-  double* ai_slab;       // AIG: per-workgroup partials of A_i (32 x 32 row-major)
+  double* ai_slab;       // AIG: per-workgroup partials of A_i (b x b row-major)
 };
 
-// VAR (tuning variants, RBL_BT_VAR): bit 0 non-temporal A loads, bit 1 non-temporal U
-// stores, bit 2 ring reads software-pipelined one k-step ahead (bit 3: two k-steps ahead),
-// bit 4 A prefetched two tiles ahead, bit 5 ablation: main-loop MFMAs off (loads only),
-// bit 6 fp32 Q / Q_{i-1} inputs
-template <int NG, bool EPI, bool AIG, int VAR = 0>
+// VAR: bit 0 non-temporal A loads, bit 1 non-temporal U stores, bit 5 ablation (main-loop
+// MFMAs off: loads only), bit 6 fp32 Q / Q_{i-1} inputs
+template <int B, int NG, bool EPI, bool AIG, int VAR = 0>
 __global__ __launch_bounds__(bt::kThreads) __attribute__((amdgpu_waves_per_eu(1, 1)))
 void k_spmm_bt(BtArgs a) {
-  constexpr int B = 32;
+  using L = bt::Geo<B>;
+  constexpr int NP = B / 8;     // U column pairs per lane: acc[p][s] is column 8p + 2j + s
+  constexpr int NS = B / 2;     // 16-B slots of a ring row holding data
+  constexpr int NE = B / 4;     // epilogue k-steps (Q_{i-1} columns / 4)
   constexpr int H = 8 * (NG - 1);
   constexpr int kRoundRows = 64;                          // 4 tiles
-  constexpr int kRingSpan = kRoundRows + 16 + 2 * H - 16;  // rows one round reads (64 + 2H)
+  constexpr int kRingSpan = kRoundRows + 2 * H;           // rows one round reads
   static_assert(kRingSpan + kRoundRows <= bt::kRing, "ring holds a round and the next one's rows");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
 
@@ -108,7 +114,7 @@ void k_spmm_bt(BtArgs a) {
   const int q = lane >> 4, j = lane & 3, G = (lane >> 2) & 3, i16 = lane & 15;
   const int64_t gq = a.row0 - H;  // global row of ring coordinate 0
 
-  // 16-B chunk (slot s) of the Q row at ring coordinate rho; absent rows read zeros
+  // 16-B chunk (slot s < NS) of the Q row at ring coordinate rho; absent rows read zeros
   auto qload = [&](int64_t rho, int s) -> d2v {
     const int64_t c = rho + gq;
     const bool in = c >= a.q_lo && c < a.q_hi;
@@ -122,29 +128,27 @@ void k_spmm_bt(BtArgs a) {
     }
   };
   auto ring_ptr = [&](int64_t rho, int s) -> d2v* {
-    return reinterpret_cast<d2v*>(smem + (unsigned)(rho & (bt::kRing - 1)) * bt::kRowBytes + 16u * s);
+    return reinterpret_cast<d2v*>(smem + (unsigned)(rho & (bt::kRing - 1)) * L::kRowBytes + 16u * s);
   };
 
   // ---- prologue: epilogue table, ring rows of round 0 ----
   if constexpr (EPI) {
-    // entry ((e*4 + p)*16 + q*4 + j) holds {-B_i[y][x] : s' = 0, 1} with x = 8(e>>1) + 2q +
+    // entry ((e*NP + p)*16 + q*4 + j) holds {-B_i[y][x] : s' = 0, 1} with x = 8(e>>1) + 2q +
     // (e&1) (the Q_{i-1} column k-step e feeds), y = 8p + 2j + s'
-    double* bt = reinterpret_cast<double*>(smem + bt::kBtOff);
-    for (int idx = tid; idx < 1024; idx += bt::kThreads) {
-      const int sp = idx & 1, jj = (idx >> 1) & 3, qq = (idx >> 3) & 3, p = (idx >> 5) & 3, e = idx >> 7;
+    double* btab = reinterpret_cast<double*>(smem + L::kBtOff);
+    for (int idx = tid; idx < B * B; idx += bt::kThreads) {
+      const int sp = idx & 1, jj = (idx >> 1) & 3, qq = (idx >> 3) & 3, p = (idx >> 5) % NP,
+                e = (idx >> 5) / NP;
       const int x = 8 * (e >> 1) + 2 * qq + (e & 1), y = 8 * p + 2 * jj + sp;
-      bt[idx] = -a.Bi[y * B + x];
+      btab[idx] = -a.Bi[y * B + x];
     }
   }
-  for (int idx = tid; idx < kRingSpan * 16; idx += bt::kThreads) {
-    const int64_t rho = 16 * T0 + idx / 16;
-    *ring_ptr(rho, idx & 15) = qload(rho, idx & 15);
+  for (int idx = tid; idx < kRingSpan * NS; idx += bt::kThreads) {
+    const int64_t rho = 16 * T0 + idx / NS;
+    *ring_ptr(rho, idx % NS) = qload(rho, idx % NS);
   }
 
   // ---- per-wave state ----
-  // DEPTH register sets of A: set d holds tile tw + 4d; the tile a set finishes is replaced
-  // group by group with the tile 4*DEPTH further on (VAR bit 4: DEPTH 2)
-  constexpr int DEPTH = (VAR & 16) ? 2 : 1;
   // tiles are stored in consumption order: slot ((round * grid + workgroup) * 4 + wave), so
   // at any moment the whole chip sweeps one contiguous stretch of the format
   const int64_t tslot0 = 4 * (int64_t)blockIdx.x;
@@ -157,19 +161,18 @@ void k_spmm_bt(BtArgs a) {
     return *p;
   };
   auto clamp_t = [&](int64_t t) -> int64_t { return t < T1 ? t : T1 - 1; };
-  d2v av[DEPTH][NG][2];
+  d2v av[NG][2];
 #pragma unroll
-  for (int d = 0; d < DEPTH; ++d)
-#pragma unroll
-    for (int g = 0; g < NG; ++g) {
-      av[d][g][0] = tile_a(clamp_t(T0 + wave + 4 * d), g, 0);
-      av[d][g][1] = tile_a(clamp_t(T0 + wave + 4 * d), g, 1);
-    }
-  auto qprev_load = [&](int64_t t, d2v (&qv)[4]) {
+  for (int g = 0; g < NG; ++g) {
+    av[g][0] = tile_a(clamp_t(T0 + wave), g, 0);
+    av[g][1] = tile_a(clamp_t(T0 + wave), g, 1);
+  }
+  // Q_{i-1} tile rows: lane row i16, columns 8m + 2q + {0,1}
+  auto qprev_load = [&](int64_t t, d2v (&qv)[NE / 2]) {
     int64_t r = 16 * t + i16;
     r = r < a.nrows ? r : a.nrows - 1;
 #pragma unroll
-    for (int m = 0; m < 4; ++m) {
+    for (int m = 0; m < NE / 2; ++m) {
       if constexpr (VAR & 64) {
         const float2 f = *reinterpret_cast<const float2*>(a.Qprev32 + r * B + 2 * q + 8 * m);
         qv[m] = d2v{(double)f.x, (double)f.y};
@@ -178,108 +181,83 @@ void k_spmm_bt(BtArgs a) {
       }
     }
   };
-  d2v qp[4];
-  if constexpr (EPI) {
-    qprev_load(clamp_t(T0 + wave), qp);
-  }
-  double ai[2][8];
+  d2v qp[NE / 2];
+  if constexpr (EPI) qprev_load(clamp_t(T0 + wave), qp);
+  // A_i accumulators: blocks = 4 x-quads; B = 32: x = 2 pi(4G + q) + xg (xg < 2), B = 16:
+  // x = 4G + q; y = 8(yq >> 1) + 2j + (yq & 1)
+  constexpr int NXG = B / 16, NYQ = B / 4;
+  double ai[NXG][NYQ];
 #pragma unroll
-  for (int x = 0; x < 2; ++x)
+  for (int x = 0; x < NXG; ++x)
 #pragma unroll
-    for (int y = 0; y < 8; ++y) ai[x][y] = 0.0;
+    for (int y = 0; y < NYQ; ++y) ai[x][y] = 0.0;
 
-  const unsigned lb = (unsigned)(q * bt::kRowBytes + 16 * j);                 // main-loop B
-  const unsigned lbt = (unsigned)(bt::kBtOff + 16 * (4 * q + j));             // epilogue B
-  const unsigned lus = (unsigned)(bt::kUOff + wave * bt::kUWave);             // U stage
-  const unsigned lai = (unsigned)(16 * bt::pi_slot(i16));                      // A_i A operand
+  const unsigned lb = (unsigned)(q * L::kRowBytes + 16 * j);                // main-loop B
+  const unsigned lbt = (unsigned)(L::kBtOff + 16 * (4 * q + j));            // epilogue B
+  const unsigned lus = (unsigned)(L::kUOff + wave * L::kUWave);             // U stage
+  const unsigned lai = B == 32 ? (unsigned)(16 * bt::pi_slot(i16)) : (unsigned)(8 * i16);
   __syncthreads();
 
-  // one round: this wave's tile tw (A in `avc`), then the ring rows of the next round
-  auto round = [&](int64_t R, int64_t tw, d2v (&avc)[NG][2]) {
-    // ring rows of the next round: 16 per wave, row 4i + q, slot i16
+  for (int64_t R = 16 * T0; R < 16 * T1; R += kRoundRows) {
+    const int64_t tw = R / 16 + wave;  // this wave's tile
+    // ring rows of the next round: 16 per wave (row 4i + q at B = 32, 8i + 2q + (i16 >> 3) at
+    // B = 16), slot i16 % NS
     d2v st[4];
     const int64_t rn = R + kRingSpan + 16 * wave;
+    auto st_row = [&](int i) -> int64_t {
+      return B == 32 ? rn + 4 * i + q : rn + 8 * (i >> 1) + 2 * q + 4 * (i & 1) + (i16 >> 3);
+    };
+    constexpr int NST = B == 32 ? 4 : 2;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) st[i] = qload(rn + 4 * i + q, i16);
+    for (int i = 0; i < NST; ++i) st[i] = qload(st_row(B == 32 ? i : 2 * i), i16 % NS);
 
     if (tw < T1) {  // wave-uniform
-      const int64_t tn = clamp_t(tw + 4 * DEPTH);
-      double acc[4][2];
+      const int64_t tn = clamp_t(tw + 4);
+      double acc[NP][2];
 #pragma unroll
-      for (int p = 0; p < 4; ++p) acc[p][0] = acc[p][1] = 0.0;
-      if constexpr ((VAR & 12) == 0) {
+      for (int p = 0; p < NP; ++p) acc[p][0] = acc[p][1] = 0.0;
 #pragma unroll
-        for (int g = 0; g < NG; ++g) {
-          const unsigned gb = (unsigned)((16 * (tw + g)) & (bt::kRing - 1)) * bt::kRowBytes + lb;
-          d2v bp[4][4];
+      for (int g = 0; g < NG; ++g) {
+        const unsigned gb = (unsigned)((16 * (tw + g)) & (bt::kRing - 1)) * L::kRowBytes + lb;
+        d2v bp[4][NP];
 #pragma unroll
-          for (int u = 0; u < 4; ++u)
+        for (int u = 0; u < 4; ++u)
 #pragma unroll
-            for (int p = 0; p < 4; ++p)
-              bp[u][p] = *reinterpret_cast<const d2v*>(smem + gb + u * 4 * bt::kRowBytes + 64 * p);
+          for (int p = 0; p < NP; ++p)
+            bp[u][p] = *reinterpret_cast<const d2v*>(smem + gb + u * 4 * L::kRowBytes + 64 * p);
 #pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            const double av_u = (u & 1) ? avc[g][u >> 1].y : avc[g][u >> 1].x;
+        for (int u = 0; u < 4; ++u) {
+          const double av_u = (u & 1) ? av[g][u >> 1].y : av[g][u >> 1].x;
 #pragma unroll
-            for (int p = 0; p < 4; ++p) {
-              if constexpr (VAR & 32) {  // ablation: loads only
-                if (p == 0) acc[0][0] += av_u + bp[u][0].x;
-              } else {
-                acc[p][0] = mfma44(av_u, bp[u][p].x, acc[p][0]);
-                acc[p][1] = mfma44(av_u, bp[u][p].y, acc[p][1]);
-              }
+          for (int p = 0; p < NP; ++p) {
+            if constexpr (VAR & 32) {  // ablation: loads only
+              if (p == 0) acc[0][0] += av_u + bp[u][0].x;
+            } else {
+              acc[p][0] = mfma44(av_u, bp[u][p].x, acc[p][0]);
+              acc[p][1] = mfma44(av_u, bp[u][p].y, acc[p][1]);
             }
           }
-          avc[g][0] = tile_a(tn, g, 0);  // a later tile's group g into the freed registers
-          avc[g][1] = tile_a(tn, g, 1);
         }
-      } else {
-        // k-steps flattened; the ring reads of k-step ks + D issue before the MFMAs of ks
-        constexpr int D = (VAR & 8) ? 2 : 1;
-        constexpr int KS = 4 * NG;
-        auto ldb = [&](int ks, d2v* bb) {
-          const unsigned gb = (unsigned)((16 * (tw + (ks >> 2))) & (bt::kRing - 1)) * bt::kRowBytes + lb;
-#pragma unroll
-          for (int p = 0; p < 4; ++p)
-            bb[p] = *reinterpret_cast<const d2v*>(smem + gb + (ks & 3) * 4 * bt::kRowBytes + 64 * p);
-        };
-        d2v bq[D + 1][4];
-#pragma unroll
-        for (int d = 0; d < D; ++d) ldb(d, bq[d]);
-#pragma unroll
-        for (int ks = 0; ks < KS; ++ks) {
-          if (ks + D < KS) ldb(ks + D, bq[(ks + D) % (D + 1)]);
-          const d2v* bb = bq[ks % (D + 1)];
-          const int g = ks >> 2, u = ks & 3;
-          const double av_u = (u & 1) ? avc[g][u >> 1].y : avc[g][u >> 1].x;
-#pragma unroll
-          for (int p = 0; p < 4; ++p) {
-            acc[p][0] = mfma44(av_u, bb[p].x, acc[p][0]);
-            acc[p][1] = mfma44(av_u, bb[p].y, acc[p][1]);
-          }
-          if (u == 3) {
-            avc[g][0] = tile_a(tn, g, 0);
-            avc[g][1] = tile_a(tn, g, 1);
-          }
-        }
+        av[g][0] = tile_a(tn, g, 0);  // the next tile's group g into the freed registers
+        av[g][1] = tile_a(tn, g, 1);
       }
       if constexpr (EPI) {
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
+        for (int e = 0; e < NE; ++e) {
           const double qv = (e & 1) ? qp[e >> 1].y : qp[e >> 1].x;
 #pragma unroll
-          for (int p = 0; p < 4; ++p) {
-            const d2v bv = *reinterpret_cast<const d2v*>(smem + lbt + 256 * (4 * e + p));
+          for (int p = 0; p < NP; ++p) {
+            const d2v bv = *reinterpret_cast<const d2v*>(smem + lbt + 256 * (NP * e + p));
             acc[p][0] = mfma44(qv, bv.x, acc[p][0]);
             acc[p][1] = mfma44(qv, bv.y, acc[p][1]);
           }
         }
-        qprev_load(clamp_t(tw + 4), qp);
+        qprev_load(tn, qp);
       }
       const int64_t ru = 16 * tw + 4 * G + q;  // this lane's U row
       d2v* urow = reinterpret_cast<d2v*>(a.U + ru * B + 2 * j);
 #pragma unroll
-      for (int p = 0; p < 4; ++p) {
+      for (int p = 0; p < NP; ++p) {
         const d2v uv = d2v{acc[p][0], acc[p][1]};
         if constexpr (VAR & 2) __builtin_nontemporal_store(uv, urow + 4 * p);
         else urow[4 * p] = uv;
@@ -289,23 +267,31 @@ void k_spmm_bt(BtArgs a) {
         // B operand U[4ks + q][y] shared by the blocks — staged through LDS (D layout in)
         const bool live = ru < a.nrows;
 #pragma unroll
-        for (int p = 0; p < 4; ++p)
-          *reinterpret_cast<d2v*>(smem + lus + (4 * G + q) * bt::kUStride + 16 * (4 * p + j)) =
+        for (int p = 0; p < NP; ++p)
+          *reinterpret_cast<d2v*>(smem + lus + (4 * G + q) * L::kUStride + 16 * (4 * p + j)) =
               live ? d2v{acc[p][0], acc[p][1]} : d2v{0.0, 0.0};
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks) {
-          const int64_t rho = 16 * tw + H + 4 * ks + q;  // own rows, lane parity of q
-          const d2v aq = *reinterpret_cast<const d2v*>(
-              smem + (unsigned)(rho & (bt::kRing - 1)) * bt::kRowBytes + lai);
+          const int64_t rho = 16 * tw + H + 4 * ks + q;  // own rows
+          const unsigned rb = (unsigned)(rho & (bt::kRing - 1)) * L::kRowBytes + lai;
+          double aq[NXG];
+          if constexpr (B == 32) {
+            const d2v v = *reinterpret_cast<const d2v*>(smem + rb);
+            aq[0] = v.x;
+            aq[NXG - 1] = v.y;
+          } else {
+            aq[0] = *reinterpret_cast<const double*>(smem + rb);
+          }
 #pragma unroll
-          for (int m = 0; m < 4; ++m) {
-            const d2v bu = *reinterpret_cast<const d2v*>(smem + lus + (4 * ks + q) * bt::kUStride + 16 * (4 * m + j));
-            ai[0][2 * m] = mfma44(aq.x, bu.x, ai[0][2 * m]);
-            ai[0][2 * m + 1] = mfma44(aq.x, bu.y, ai[0][2 * m + 1]);
-            ai[1][2 * m] = mfma44(aq.y, bu.x, ai[1][2 * m]);
-            ai[1][2 * m + 1] = mfma44(aq.y, bu.y, ai[1][2 * m + 1]);
+          for (int m = 0; m < NYQ / 2; ++m) {
+            const d2v bu = *reinterpret_cast<const d2v*>(smem + lus + (4 * ks + q) * L::kUStride + 16 * (4 * m + j));
+#pragma unroll
+            for (int x = 0; x < NXG; ++x) {
+              ai[x][2 * m] = mfma44(aq[x], bu.x, ai[x][2 * m]);
+              ai[x][2 * m + 1] = mfma44(aq[x], bu.y, ai[x][2 * m + 1]);
+            }
           }
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -313,56 +299,49 @@ void k_spmm_bt(BtArgs a) {
       }
     }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) *ring_ptr(rn + 4 * i + q, i16) = st[i];
+    for (int i = 0; i < NST; ++i) *ring_ptr(st_row(B == 32 ? i : 2 * i), i16 % NS) = st[i];
     __syncthreads();
-  };
-
-  for (int64_t R = 16 * T0; R < 16 * T1; R += DEPTH * kRoundRows) {
-    const int64_t tw = R / 16 + wave;
-    round(R, tw, av[0]);
-    if constexpr (DEPTH == 2) {
-      if (R + kRoundRows < 16 * T1) round(R + kRoundRows, tw + 4, av[1]);
-    }
   }
 
   if constexpr (AIG) {
-    // sum the 4 waves' partials (ring area, free after the last barrier), wave 0 stores:
-    // lane holds A_i[x = 2 pi(4G + q) + xg][y = 8(yq >> 1) + 2j + (yq & 1)] in ai[xg][yq]
+    // sum the 4 waves' partials (ring area, free after the last barrier), wave 0 stores
     double* red = reinterpret_cast<double*>(smem);
+    constexpr int NA = NXG * NYQ;
     if (wave > 0) {
 #pragma unroll
-      for (int x = 0; x < 2; ++x)
+      for (int x = 0; x < NXG; ++x)
 #pragma unroll
-        for (int y = 0; y < 8; ++y) red[((wave - 1) * 16 + x * 8 + y) * 64 + lane] = ai[x][y];
+        for (int y = 0; y < NYQ; ++y) red[((wave - 1) * NA + x * NYQ + y) * 64 + lane] = ai[x][y];
     }
     __syncthreads();
     if (wave == 0) {
       double* out = a.ai_slab + (int64_t)blockIdx.x * B * B;
-      const int xb = 2 * bt::pi_slot(4 * G + q);
+      const int xb = B == 32 ? 2 * bt::pi_slot(4 * G + q) : 4 * G + q;
 #pragma unroll
-      for (int x = 0; x < 2; ++x)
+      for (int x = 0; x < NXG; ++x)
 #pragma unroll
-        for (int y = 0; y < 8; ++y) {
+        for (int y = 0; y < NYQ; ++y) {
           double v = ai[x][y];
 #pragma unroll
-          for (int w = 0; w < 3; ++w) v += red[(w * 16 + x * 8 + y) * 64 + lane];
+          for (int w = 0; w < 3; ++w) v += red[(w * NA + x * NYQ + y) * 64 + lane];
           out[(xb + x) * B + 8 * (y >> 1) + 2 * j + (y & 1)] = v;
         }
     }
   }
 }
 
-template <int NG, bool EPI, bool AIG, int VAR>
+template <int B, int NG, bool EPI, bool AIG, int VAR>
 static void launch_bt_v(const BtArgs& a, int grid, hipStream_t s) {
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_spmm_bt<NG, EPI, AIG, VAR>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, bt::kLds);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_spmm_bt<B, NG, EPI, AIG, VAR>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, bt::Geo<B>::kLds);
     attr = true;
   }
-  hipLaunchKernelGGL((k_spmm_bt<NG, EPI, AIG, VAR>), dim3(grid), dim3(bt::kThreads), bt::kLds, s, a);
+  hipLaunchKernelGGL((k_spmm_bt<B, NG, EPI, AIG, VAR>), dim3(grid), dim3(bt::kThreads),
+                     bt::Geo<B>::kLds, s, a);
 }
-template <int NG, bool EPI, bool AIG>
+template <int B, int NG, bool EPI, bool AIG>
 static void launch_bt_t(const BtArgs& a, int grid, hipStream_t s, bool f32) {
   // default: non-temporal A loads and U stores (VAR 3): the format is read once per launch
   // and U only by the next kernel — measured 7 % faster at C4a than the default policy;
@@ -371,18 +350,18 @@ static void launch_bt_t(const BtArgs& a, int grid, hipStream_t s, bool f32) {
     const char* e = getenv("RBL_BT_VAR");
     return e ? atoi(e) : 3;
   }();
-  if (f32) return launch_bt_v<NG, EPI, AIG, 3 | 64>(a, grid, s);
-  if constexpr (NG == 9 && EPI && AIG) {
-    if (var == 0) return launch_bt_v<NG, EPI, AIG, 0>(a, grid, s);
-    if (var == 35) return launch_bt_v<NG, EPI, AIG, 35>(a, grid, s);
+  if (f32) return launch_bt_v<B, NG, EPI, AIG, 3 | 64>(a, grid, s);
+  if constexpr (B == 32 && NG == 9 && EPI && AIG) {
+    if (var == 0) return launch_bt_v<B, NG, EPI, AIG, 0>(a, grid, s);
+    if (var == 35) return launch_bt_v<B, NG, EPI, AIG, 35>(a, grid, s);
   }
-  launch_bt_v<NG, EPI, AIG, 3>(a, grid, s);
+  launch_bt_v<B, NG, EPI, AIG, 3>(a, grid, s);
 }
 
 bool spmm_bt(const CsrDev& A, const double* Qin, int64_t col_off, int b, double* U,
              const double* Qprev, const double* Bi, hipStream_t s, double* ai_slab, int* ai_parts,
              const float* Q32, const float* Qprev32) {
-  if (b != 32 || !A.bt || A.ntiles <= 0 || !(A.bt_ng == 5 || A.bt_ng == 9)) return false;
+  if ((b != 32 && b != 16) || !A.bt || A.ntiles <= 0 || !(A.bt_ng == 5 || A.bt_ng == 9)) return false;
   BtArgs a;
   a.nrows = A.nrows;
   a.ntiles = A.ntiles;
@@ -405,14 +384,18 @@ bool spmm_bt(const CsrDev& A, const double* Qin, int64_t col_off, int b, double*
   const bool aig = ai_slab != nullptr;
   a.ai_slab = ai_slab;
   if (ai_parts) *ai_parts = aig ? grid : 0;
-  const int key = (A.bt_ng == 9 ? 4 : 0) | (epi ? 2 : 0) | (aig ? 1 : 0);
+  const int key = (b == 32 ? 8 : 0) | (A.bt_ng == 9 ? 4 : 0) | (epi ? 2 : 0) | (aig ? 1 : 0);
   switch (key) {
-#define RBL_BT_CASE(K, NG, E, G) \
-    case K: launch_bt_t<NG, E, G>(a, grid, s, f32); break;
-    RBL_BT_CASE(0, 5, false, false) RBL_BT_CASE(1, 5, false, true)
-    RBL_BT_CASE(2, 5, true, false)  RBL_BT_CASE(3, 5, true, true)
-    RBL_BT_CASE(4, 9, false, false) RBL_BT_CASE(5, 9, false, true)
-    RBL_BT_CASE(6, 9, true, false)  RBL_BT_CASE(7, 9, true, true)
+#define RBL_BT_CASE(K, BB, NG, E, G) \
+    case K: launch_bt_t<BB, NG, E, G>(a, grid, s, f32); break;
+    RBL_BT_CASE(0, 16, 5, false, false) RBL_BT_CASE(1, 16, 5, false, true)
+    RBL_BT_CASE(2, 16, 5, true, false)  RBL_BT_CASE(3, 16, 5, true, true)
+    RBL_BT_CASE(4, 16, 9, false, false) RBL_BT_CASE(5, 16, 9, false, true)
+    RBL_BT_CASE(6, 16, 9, true, false)  RBL_BT_CASE(7, 16, 9, true, true)
+    RBL_BT_CASE(8, 32, 5, false, false) RBL_BT_CASE(9, 32, 5, false, true)
+    RBL_BT_CASE(10, 32, 5, true, false) RBL_BT_CASE(11, 32, 5, true, true)
+    RBL_BT_CASE(12, 32, 9, false, false) RBL_BT_CASE(13, 32, 9, false, true)
+    RBL_BT_CASE(14, 32, 9, true, false) RBL_BT_CASE(15, 32, 9, true, true)
 #undef RBL_BT_CASE
   }
   return true;

@@ -85,7 +85,7 @@ def test_eigenpairs_fp32_basis(rbl, order, b):
 @pytest.mark.parametrize("b", [16, 32])
 def test_fp32_basis_multirank_matches_single(rbl, b):
     """Three in-process ranks (row-partitioned, halo + all-reduce) give the single-rank fp32 run;
-    at b = 32 the band-tile SpMM reads the fp32 blocks through the fp32 halo exchange."""
+    the band-tile SpMM reads the fp32 blocks through the fp32 halo exchange."""
     from test_gpu_multirank import run_ranks
     k = 10
     A = c1_matrix(8000, k)
@@ -96,7 +96,7 @@ def test_fp32_basis_multirank_matches_single(rbl, b):
     def fn(ctx, r):
         ctx.set_matrix(A)
         _, r0, r1, _ = ctx.matrix_info()
-        assert (ctx.spmm_kernel_for(b) == 5) == (b == 32)
+        assert ctx.spmm_kernel_for(b) == 5   # band tiles at b = 16 and 32
         D, V, info = rbl.lanczos(ctx, k, b, omega=omega[r0:r1], basis_bits=32)
         return D, V, info
 
