@@ -43,7 +43,13 @@ __device__ __forceinline__ T ldw(const T* p) {
 // idle waves cost ~25% at 18 panels with 8-wave groups).
 // ----------------------------------------------------------------------------------------
 constexpr int kG44Waves = 4;
-constexpr int kG44Rows = 16;
+#ifndef RBL_G44_ROWS
+#define RBL_G44_ROWS 16
+#endif
+#ifndef RBL_G44_WPE
+#define RBL_G44_WPE 3
+#endif
+constexpr int kG44Rows = RBL_G44_ROWS;
 
 template <int B, int NX, int NPH>
 __device__ __forceinline__ void gram44_body(int64_t r_begin, int64_t r_end, int64_t s, int pg,
@@ -156,7 +162,7 @@ __device__ __forceinline__ void gram44_body(int64_t r_begin, int64_t r_end, int6
 }
 
 template <int B, int NX>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k_gram44(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RBL_G44_WPE))) void k_gram44(
     int64_t nrows, PanelRun W, Panels X, double* slab, int npg, int64_t rows_per, const int* skip) {
   if (skip && *skip) return;
   constexpr int KC = NX * B;
@@ -188,7 +194,7 @@ int gram44_splits(int64_t nrows, int nW) {
   (void)nW;
   // three 4-wave workgroups per CU: 3 x CUs splits, a multiple of 8 (XCD mapping), each
   // split >= 128 rows
-  int64_t s8 = 3 * window_grid() / 8;
+  int64_t s8 = RBL_G44_WPE * window_grid() / 8;
   const int64_t max_s8 = (nrows + 8 * 128 - 1) / (8 * 128);
   if (s8 > max_s8) s8 = max_s8;
   if (s8 < 1) s8 = 1;
