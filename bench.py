@@ -196,6 +196,11 @@ def main():
                  "traffic": None if traffic is None else int(traffic),
                  "algorithmic_bytes_per_launch": int(spmm_bytes),
                  "streamed_bytes_per_launch": int(streamed_bytes(spmm_kid, nloc, nnz_loc, b, args.halfwidth, m_max)),
+                 # gather kernels (unbanded patterns) also read one Q row (b * 8 B) per nonzero,
+                 # served by L2 / Infinity Cache / HBM: the traffic that bounds them
+                 **({"q_row_gather_bytes_per_launch": int(nnz_loc * b * 8),
+                     "gbs_incl_q_row_gathers": round((spmm_bytes + nnz_loc * b * 8) / (spmm_ms * 1e-3) / 1e9, 1)}
+                    if spmm_kid in (1, 6) else {}),
                  "ms_per_launch": round(spmm_ms, 4)}
     mfma_peak = FP64_MFMA_PEAK_TF if args.basis_bits == 64 else FP32_MFMA_PEAK_TF
     # the clock the chip holds under these kernels (profiles/pmc_clock.json: GRBM_GUI_ACTIVE
