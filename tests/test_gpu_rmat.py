@@ -90,3 +90,24 @@ def test_rmat_lanczos_matches_oracle(rbl):
     assert np.max(np.abs(D - ref.D) / np.abs(ref.D)) < 1e-10
     res = np.linalg.norm(A @ V - V * D, axis=0) / np.abs(D)
     assert res.max() < 1e-7
+
+
+def test_rmat_multirank_lanczos(rbl):
+    """C4b's multi-GPU form (BASELINE config 4): each rank generates its nnz-balanced rows, the
+    halo exchange brings in every Q row its columns touch (for R-MAT nearly all of them), the
+    segmented gather multiplies; the fixed-step trace equals the single-rank run's."""
+    plant = matgen.planted_spectrum(5)
+
+    def run(ctx):
+        ctx.gen_rmat(CASE["n"], CASE["scale"], CASE["edges"], CASE["seed"], plant)
+        _, _, info = rbl.lanczos(ctx, 5, 32, seed=9, check=False, max_steps=8, trace=True,
+                                 ritz=False)
+        return info
+
+    with rbl.Context(0) as ctx:
+        info1 = run(ctx)
+    for info in run_ranks(rbl, 3, lambda ctx, r: run(ctx)):
+        for a, a1 in zip(info.trace_A, info1.trace_A):
+            assert np.abs(a - a1).max() <= 1e-9 * np.abs(a1).max()
+        for bb, bb1 in zip(info.trace_B, info1.trace_B):
+            assert np.abs(bb - bb1).max() <= 1e-9 * np.abs(bb1).max()
