@@ -12,6 +12,7 @@
 #   include("common.jl"); include("RBL_hip.jl")
 #   D, V = RBL_hip(A, k, b)              # A::SparseMatrixCSC{Float64,Int64} or Matrix{Float64}
 #   D, V = RBL_hip(A, k, b; basis_bits = 32)   # FLOAT = Float32 mode (common.jl:5)
+#   D, V = RBL_hip(A, k, b; device_blocks = -1)  # hybrid buffer: what fits in HBM, rest on host
 #   D, V = RBL_hip_restarted(A, k)       # restarted.jl:106 (RBL_gpu_restarted)
 
 const librbl_hip = get(ENV, "RBL_HIP_LIB", "librbl_hip.so")
@@ -49,11 +50,14 @@ end
 
 function RBL_hip(A::Union{SparseMatrixCSC{Float64,Int64},Matrix{Float64}}, k::Int64, b::Int64;
                  device::Int = 0, seed::UInt64 = rand(UInt64), kryl_sz::Int64 = 1200,
-                 basis_bits::Int = 64)
+                 basis_bits::Int = 64, device_blocks::Int = 0)
     n = size(A, 2)
     ctx = rbl_context(device)
     try
         set_matrix!(ctx, A)
+        # RBL_OPT_DEVICE_BLOCKS = 3: the hybrid GPU/host Krylov buffer (RBL_gpu.jl:24-27, 59-81)
+        rbl_check(ctx, ccall((:rbl_set_option, librbl_hip), Cint, (Ptr{Cvoid}, Cint, Int64),
+                             ctx, 3, device_blocks), "rbl_set_option")
         # Qg_d = qr(Ag * randn(n, b)).Q (RBL_gpu.jl:213-214); the basis lives in HBM
         m_max = cld(kryl_sz, b)
         rbl_check(ctx, ccall((:rbl_start, librbl_hip), Cint,
