@@ -70,11 +70,16 @@ def streamed_bytes(kid, nloc, nnz_loc, b, halfwidth, m_max):
     """Bytes the chosen SpMM kernel itself reads and writes per launch (step launches carry the
     Q_{i-1} epilogue), beside SURVEY's CSR-based algorithmic bytes: the band-tile kernel (5)
     streams 16 x (16 + 2H) dense doubles per 16-row tile instead of 12 B per nonzero; the
-    LDS-band kernel (3) 8 B value + 2 B position per nonzero plus the row pointers."""
+    LDS-band kernel (3) 8 B value + 2 B position per nonzero plus the row pointers.  Packed
+    band tiles (RBL_BT_PACK=1; dense by default) stream the nonzeros and a header of 24
+    (H = 32) or 42 (H = 64) 8-B words per tile."""
     vec = (m_max * 3 + 2) / (m_max + 1) * nloc * b * 8
     if kid == 5:
         H = 32 if halfwidth <= 32 else 64
-        return -(-nloc // 16) * 16 * (16 + 2 * H) * 8 + vec
+        tiles = -(-nloc // 16)
+        if os.environ.get("RBL_BT_PACK", "0") == "1":
+            return nnz_loc * 8 + tiles * 8 * (24 if H == 32 else 42) + vec
+        return tiles * 16 * (16 + 2 * H) * 8 + vec
     if kid == 3:
         return nnz_loc * 10 + (nloc + 1) * 8 + vec
     return nnz_loc * 12 + (nloc + 1) * 8 + vec

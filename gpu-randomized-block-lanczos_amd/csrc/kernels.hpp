@@ -59,6 +59,12 @@ struct CsrDev {
   int64_t bt_tiles_per_wg = 0;
   int64_t q_lo = 0, q_hi = 0;
   const double* zrow = nullptr;
+  // packed band tiles (bt_pack): per tile slot a header of bt_pack_words(NG) 8-B words (per
+  // 1-KiB operand block the nonzero masks of element 0 / 1 of every lane, then the blocks'
+  // uint16 start offsets + the tile's count, then the tile's first value index) and the
+  // nonzeros per block: element 0 of the lanes, then element 1; null: the dense tiles `bt`
+  const uint64_t* btp_hdr = nullptr;
+  const double* btp_val = nullptr;
   // segmented gather (spmm.hip variant 5): wave tasks (first row, info: > 0 rows of a packed
   // short-row task, < 0 -(slot+1) of a long-row segment), segment slots' first nonzero
   // (slot_k0, nslots + 1 entries), long rows with their first slot (lslot, nlong + 1), and a
@@ -117,6 +123,11 @@ bool spmm_bt(const CsrDev& A, const double* Qin, int64_t col_off, int b, double*
 // + wave), zero-filled `out` of bt_tile_slots(ntiles, tiles_per_wg) * NG * 256 doubles
 int64_t bt_tile_slots(int64_t ntiles, int64_t tiles_per_wg);
 void bt_fill(const CsrDev& A, int H, int NG, double* out, hipStream_t s);
+// packed band tiles from the dense ones (NG in {5, 9}): header words per tile slot, and the
+// packed values (allocated here, *val_out; *nval_out values); returns 0 or a hipError_t
+constexpr int bt_pack_words(int NG) { return (4 * NG + (2 * NG + 4) / 4 + 2) & ~1; }
+int bt_pack(const double* dense, int64_t nslots, int NG, uint64_t* hdr, double** val_out,
+            int64_t* nval_out, hipStream_t s);
 constexpr int kWindowTileRows = 16;
 // Band kernel geometry (host checks in rbl_api.cpp): a tile's band [c16, cmax] with
 // c16 = cmin & ~15 spans <= kBandMaxK columns; the Q ring holds kBandRing rows; per tile a

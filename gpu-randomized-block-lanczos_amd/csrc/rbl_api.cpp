@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -39,6 +40,8 @@ struct rbl_ctx {
   uint16_t* d_bpos = nullptr;  // band kernel: per-nonzero dense-tile positions
   double* d_bt = nullptr;      // band-tile kernel: the CSR in MFMA-ordered 16-row band tiles
   int bt_ng = 0;               // its band groups (0: not applicable)
+  uint64_t* d_btp_hdr = nullptr;  // the band tiles packed (zeros dropped; replaces d_bt)
+  double* d_btp_val = nullptr;
   double* d_zrow = nullptr;    // 32 zeros: band rows the halo does not hold
   // segmented-gather task table (spmm.hip variant 5; CsrDev::seg_*)
   int64_t seg_ntasks = 0, seg_nlong = 0;
@@ -182,6 +185,8 @@ CsrDev csr(rbl_ctx* ctx) {
   A.band_pos = ctx->d_bpos;
   A.bt = ctx->d_bt;
   A.bt_ng = ctx->bt_ng;
+  A.btp_hdr = ctx->d_btp_hdr;
+  A.btp_val = ctx->d_btp_val;
   A.bt_tiles_per_wg = ctx->tiles_per_wg;
   A.q_lo = ctx->nranks > 1 ? ctx->ext_lo : ctx->r0;
   A.q_hi = ctx->nranks > 1 ? ctx->ext_hi : ctx->r0 + ctx->nloc;
@@ -392,6 +397,21 @@ int prepare_window(rbl_ctx* ctx, const std::vector<int64_t>& rp) {
       HIPC(hipGetLastError());
       HIPC(hipStreamSynchronize(ctx->stream));
       ctx->bt_ng = NG;
+      // RBL_BT_PACK = 1: pack the tiles (zeros dropped; C4a: 13.1 KB per tile instead of
+      // 18.4 KB, 3 GB less HBM at n = 1e7).  Off by default: the kernel is not bound by its
+      // A bytes (one wave per SIMD, 60 % MFMA busy, fp64 MFMA and VALU do not co-issue) and
+      // the index arithmetic of the packed loads costs more than the bytes save (3.56 vs
+      // 3.40 ms per launch at C4a)
+      const char* pk = getenv("RBL_BT_PACK");
+      if (pk && atoi(pk) == 1) {
+        const int64_t nslots = bt_tile_slots(nt, ctx->tiles_per_wg);
+        HIPC(hipMalloc(&ctx->d_btp_hdr, (size_t)nslots * bt_pack_words(NG) * sizeof(uint64_t)));
+        int64_t nval = 0;
+        const int prc = bt_pack(ctx->d_bt, nslots, NG, ctx->d_btp_hdr, &ctx->d_btp_val, &nval, ctx->stream);
+        if (prc != 0) return prc == (int)hipErrorOutOfMemory ? RBL_ERR_OOM : RBL_ERR_HIP;
+        hipFree(ctx->d_bt);
+        ctx->d_bt = nullptr;
+      }
     }
   }
   return RBL_OK;
@@ -813,6 +833,8 @@ void free_matrix(rbl_ctx* ctx) {
   hipFree(ctx->d_tinfo); ctx->d_tinfo = nullptr;
   hipFree(ctx->d_bpos); ctx->d_bpos = nullptr;
   hipFree(ctx->d_bt); ctx->d_bt = nullptr;
+  hipFree(ctx->d_btp_hdr); ctx->d_btp_hdr = nullptr;
+  hipFree(ctx->d_btp_val); ctx->d_btp_val = nullptr;
   hipFree(ctx->d_zrow); ctx->d_zrow = nullptr;
   ctx->bt_ng = 0;
   hipFree(ctx->d_seg_trow); ctx->d_seg_trow = nullptr;

@@ -36,6 +36,8 @@
 // ring row rho at 16-B slot 4p + j feeds acc[p][0] and acc[p][1].
 #include <cstdlib>
 
+#include <hipcub/hipcub.hpp>
+
 #include "kernels.hpp"
 
 namespace rbl {
@@ -89,10 +91,21 @@ struct BtArgs {
   const float* Qprev32;  //   exactly on load (RBL_gpu.jl:173-174 copyto!(Qg_d, Qg))
   const double* Bi;
   double* ai_slab;       // AIG: per-workgroup partials of A_i (b x b row-major)
+  const uint64_t* hdr;   // VAR bit 7: packed tiles (bt_pack) instead of A
+  const double* pv;
 };
 
 // VAR: bit 0 non-temporal A loads, bit 1 non-temporal U stores, bit 5 ablation (main-loop
-// MFMAs off: loads only), bit 6 fp32 Q / Q_{i-1} inputs
+// MFMAs off: loads only), bit 6 fp32 Q / Q_{i-1} inputs, bit 7 packed tiles.
+//
+// Packed tiles: the zeros of the band (31 % at C4a) are not stored.  Per operand block k =
+// 2g + h the header holds m0 / m1, bit l = element 0 / 1 of lane l is nonzero, and the block's
+// start offset off_k in the tile's value run; lane l's element 0 sits at off_k + mbcnt(m0),
+// its element 1 at off_k + popc(m0) + mbcnt(m1), and an absent element is read through a
+// buffer load past the run's end, which returns 0.0 — so the MFMA operands, and U, are
+// bit-identical to the dense format's.  The masks act directly as lane masks (inverse
+// ballot); the tile's header (<= 42 words, one per lane) is loaded one tile ahead of its
+// values.
 template <int B, int NG, bool EPI, bool AIG, int VAR = 0>
 __global__ __launch_bounds__(bt::kThreads) __attribute__((amdgpu_waves_per_eu(1, 1)))
 void k_spmm_bt(BtArgs a) {
@@ -161,11 +174,60 @@ void k_spmm_bt(BtArgs a) {
     return *p;
   };
   auto clamp_t = [&](int64_t t) -> int64_t { return t < T1 ? t : T1 - 1; };
+  // packed tiles: header words of tile t (lane w holds word w)
+  constexpr int PW = bt_pack_words(NG), POFF = 4 * NG, PVB = 4 * NG + (2 * NG + 4) / 4;
+  auto hdr_load = [&](int64_t t) -> uint64_t {
+    const int64_t lt = t - T0;
+    const int64_t ts = (lt >> 2) * tslot_r + tslot0 + (lt & 3);
+    return lane < PW ? __builtin_nontemporal_load(a.hdr + ts * PW + lane) : 0ull;
+  };
+  auto rl32 = [&](uint64_t v, int w, int half) -> unsigned {
+    return __builtin_amdgcn_readlane(half ? (unsigned)(v >> 32) : (unsigned)v, w);
+  };
+  auto rl64 = [&](uint64_t v, int w) -> uint64_t {
+    return ((uint64_t)rl32(v, w, 1) << 32) | rl32(v, w, 0);
+  };
+  auto hoff = [&](uint64_t hd, int k) -> unsigned {  // uint16 k of the offset words
+    return (rl32(hd, POFF + (k >> 2), (k >> 1) & 1) >> (16 * (k & 1))) & 0xffffu;
+  };
+  // lane's two elements of block k = 2g + h of the tile whose run is `rs`: element 0 of
+  // lane l at off_k + mbcnt(m0), element 1 at off_k + popc(m0) + mbcnt(m1) (each
+  // instruction reads one contiguous stretch); an absent element reads past the run's end,
+  // which a buffer load returns as 0.0
+  auto tile_ap = [&](uint64_t hd, __amdgpu_buffer_rsrc_t rs, int k) -> d2v {
+    const uint64_t m0 = rl64(hd, 2 * k), m1 = rl64(hd, 2 * k + 1);
+    const unsigned o = hoff(hd, k);
+    unsigned i0 = __builtin_amdgcn_mbcnt_lo((unsigned)m0, o);
+    i0 = __builtin_amdgcn_mbcnt_hi((unsigned)(m0 >> 32), i0);
+    unsigned i1 = __builtin_amdgcn_mbcnt_lo((unsigned)m1, o + (unsigned)__popcll(m0));
+    i1 = __builtin_amdgcn_mbcnt_hi((unsigned)(m1 >> 32), i1);
+    const unsigned b0 = __builtin_amdgcn_inverse_ballot_w64(m0) ? 8u * i0 : 0x80000000u;
+    const unsigned b1 = __builtin_amdgcn_inverse_ballot_w64(m1) ? 8u * i1 : 0x80000000u;
+    return d2v{__builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, b0, 0, 2)),
+               __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rs, b1, 0, 2))};
+  };
+  auto tile_run = [&](uint64_t hd) -> __amdgpu_buffer_rsrc_t {
+    const double* run = a.pv + rl64(hd, PVB);
+    return __builtin_amdgcn_make_buffer_rsrc((void*)run, (short)0, (int)(8 * hoff(hd, 2 * NG)),
+                                             0x00020000);
+  };
+  uint64_t hN = 0;  // packed: header of the tile whose values are being loaded
   d2v av[NG][2];
+  if constexpr (VAR & 128) {
+    const uint64_t h0 = hdr_load(clamp_t(T0 + wave));
+    const __amdgpu_buffer_rsrc_t rs = tile_run(h0);
 #pragma unroll
-  for (int g = 0; g < NG; ++g) {
-    av[g][0] = tile_a(clamp_t(T0 + wave), g, 0);
-    av[g][1] = tile_a(clamp_t(T0 + wave), g, 1);
+    for (int g = 0; g < NG; ++g) {
+      av[g][0] = tile_ap(h0, rs, 2 * g);
+      av[g][1] = tile_ap(h0, rs, 2 * g + 1);
+    }
+    hN = hdr_load(clamp_t(T0 + wave + 4));
+  } else {
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      av[g][0] = tile_a(clamp_t(T0 + wave), g, 0);
+      av[g][1] = tile_a(clamp_t(T0 + wave), g, 1);
+    }
   }
   // Q_{i-1} tile rows: lane row i16, columns 8m + 2q + {0,1}
   auto qprev_load = [&](int64_t t, d2v (&qv)[NE / 2]) {
@@ -213,43 +275,65 @@ void k_spmm_bt(BtArgs a) {
 
     if (tw < T1) {  // wave-uniform
       const int64_t tn = clamp_t(tw + 4);
+      uint64_t hNN = 0;
+      if constexpr (VAR & 128) hNN = hdr_load(clamp_t(tw + 8));
+      const auto rsN = [&] {
+        if constexpr (VAR & 128) return tile_run(hN);
+        else return 0;
+      }();
       double acc[NP][2];
 #pragma unroll
       for (int p = 0; p < NP; ++p) acc[p][0] = acc[p][1] = 0.0;
-#pragma unroll
-      for (int g = 0; g < NG; ++g) {
+      // B operands (ring rows) of group g: double-buffered one group ahead, so the ds_reads
+      // of group g+1 are in flight while group g's MFMAs issue (one wave per SIMD: nothing
+      // else would hide the LDS latency)
+      d2v bp[2][4][NP];
+      auto ld_bp = [&](int g, d2v (&b)[4][NP]) {
         const unsigned gb = (unsigned)((16 * (tw + g)) & (bt::kRing - 1)) * L::kRowBytes + lb;
-        d2v bp[4][NP];
 #pragma unroll
         for (int u = 0; u < 4; ++u)
 #pragma unroll
           for (int p = 0; p < NP; ++p)
-            bp[u][p] = *reinterpret_cast<const d2v*>(smem + gb + u * 4 * L::kRowBytes + 64 * p);
+            b[u][p] = *reinterpret_cast<const d2v*>(smem + gb + u * 4 * L::kRowBytes + 64 * p);
+      };
+      if constexpr (!(VAR & 256)) ld_bp(0, bp[0]);
+#pragma unroll
+      for (int g = 0; g < NG; ++g) {
+        if constexpr (VAR & 256) ld_bp(g, bp[g & 1]);  // diagnostics: no read-ahead
+        else if (g + 1 < NG) ld_bp(g + 1, bp[(g + 1) & 1]);
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           const double av_u = (u & 1) ? av[g][u >> 1].y : av[g][u >> 1].x;
 #pragma unroll
           for (int p = 0; p < NP; ++p) {
             if constexpr (VAR & 32) {  // ablation: loads only
-              if (p == 0) acc[0][0] += av_u + bp[u][0].x;
+              if (p == 0) acc[0][0] += av_u + bp[g & 1][u][0].x;
             } else {
-              acc[p][0] = mfma44(av_u, bp[u][p].x, acc[p][0]);
-              acc[p][1] = mfma44(av_u, bp[u][p].y, acc[p][1]);
+              acc[p][0] = mfma44(av_u, bp[g & 1][u][p].x, acc[p][0]);
+              acc[p][1] = mfma44(av_u, bp[g & 1][u][p].y, acc[p][1]);
             }
           }
         }
-        av[g][0] = tile_a(tn, g, 0);  // the next tile's group g into the freed registers
-        av[g][1] = tile_a(tn, g, 1);
+        if constexpr (VAR & 128) {  // the next tile's group g into the freed registers
+          av[g][0] = tile_ap(hN, rsN, 2 * g);
+          av[g][1] = tile_ap(hN, rsN, 2 * g + 1);
+        } else {
+          av[g][0] = tile_a(tn, g, 0);
+          av[g][1] = tile_a(tn, g, 1);
+        }
       }
+      if constexpr (VAR & 128) hN = hNN;
       if constexpr (EPI) {
 #pragma unroll
         for (int e = 0; e < NE; ++e) {
           const double qv = (e & 1) ? qp[e >> 1].y : qp[e >> 1].x;
+          d2v bv[NP];
+#pragma unroll
+          for (int p = 0; p < NP; ++p) bv[p] = *reinterpret_cast<const d2v*>(smem + lbt + 256 * (NP * e + p));
 #pragma unroll
           for (int p = 0; p < NP; ++p) {
-            const d2v bv = *reinterpret_cast<const d2v*>(smem + lbt + 256 * (NP * e + p));
-            acc[p][0] = mfma44(qv, bv.x, acc[p][0]);
-            acc[p][1] = mfma44(qv, bv.y, acc[p][1]);
+            acc[p][0] = mfma44(qv, bv[p].x, acc[p][0]);
+            acc[p][1] = mfma44(qv, bv[p].y, acc[p][1]);
           }
         }
         qprev_load(tn, qp);
@@ -345,15 +429,24 @@ template <int B, int NG, bool EPI, bool AIG>
 static void launch_bt_t(const BtArgs& a, int grid, hipStream_t s, bool f32) {
   // default: non-temporal A loads and U stores (VAR 3): the format is read once per launch
   // and U only by the next kernel — measured 7 % faster at C4a than the default policy;
-  // RBL_BT_VAR = 0 / 35 (diagnostics): default policy / loads-only ablation
+  // RBL_BT_VAR = 0 / 35 / 259 (diagnostics): default policy / loads-only ablation / no LDS
+  // read-ahead of the next group's B operands
   static const int var = [] {
     const char* e = getenv("RBL_BT_VAR");
     return e ? atoi(e) : 3;
   }();
+  if (a.hdr) {
+    if (f32) return launch_bt_v<B, NG, EPI, AIG, 3 | 64 | 128>(a, grid, s);
+    if constexpr (B == 32 && NG == 9 && EPI && AIG) {
+      if (var == 35) return launch_bt_v<B, NG, EPI, AIG, 35 | 128>(a, grid, s);
+    }
+    return launch_bt_v<B, NG, EPI, AIG, 3 | 128>(a, grid, s);
+  }
   if (f32) return launch_bt_v<B, NG, EPI, AIG, 3 | 64>(a, grid, s);
   if constexpr (B == 32 && NG == 9 && EPI && AIG) {
     if (var == 0) return launch_bt_v<B, NG, EPI, AIG, 0>(a, grid, s);
     if (var == 35) return launch_bt_v<B, NG, EPI, AIG, 35>(a, grid, s);
+    if (var == 259) return launch_bt_v<B, NG, EPI, AIG, 259>(a, grid, s);
   }
   launch_bt_v<B, NG, EPI, AIG, 3>(a, grid, s);
 }
@@ -361,7 +454,7 @@ static void launch_bt_t(const BtArgs& a, int grid, hipStream_t s, bool f32) {
 bool spmm_bt(const CsrDev& A, const double* Qin, int64_t col_off, int b, double* U,
              const double* Qprev, const double* Bi, hipStream_t s, double* ai_slab, int* ai_parts,
              const float* Q32, const float* Qprev32) {
-  if ((b != 32 && b != 16) || !A.bt || A.ntiles <= 0 || !(A.bt_ng == 5 || A.bt_ng == 9)) return false;
+  if ((b != 32 && b != 16) || !(A.bt || A.btp_hdr) || A.ntiles <= 0 || !(A.bt_ng == 5 || A.bt_ng == 9)) return false;
   BtArgs a;
   a.nrows = A.nrows;
   a.ntiles = A.ntiles;
@@ -378,6 +471,8 @@ bool spmm_bt(const CsrDev& A, const double* Qin, int64_t col_off, int b, double*
   a.Q32 = Q32;
   a.Qprev32 = Qprev32;
   a.Bi = Bi;
+  a.hdr = A.btp_hdr;
+  a.pv = A.btp_val;
   const int grid = (int)((A.ntiles + A.bt_tiles_per_wg - 1) / A.bt_tiles_per_wg);
   const bool f32 = Q32 != nullptr;
   const bool epi = Qprev != nullptr || Qprev32 != nullptr;
@@ -434,6 +529,94 @@ void bt_fill(const CsrDev& A, int H, int NG, double* out, hipStream_t s) {
   const int64_t tpw = A.bt_tiles_per_wg, grid = (A.ntiles + tpw - 1) / tpw;
   hipLaunchKernelGGL(k_bt_fill, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, A.nrows,
                      A.rowptr, A.col, A.val, A.row0, H, NG, tpw, grid, out);
+}
+
+// Packed tiles (see k_spmm_bt, VAR bit 7): one wave per tile slot.  Pass 1 counts the
+// nonzero operand elements, an exclusive scan gives every run's first value, pass 2 writes
+// header and run (per block: element 0 of the lanes in lane order, then element 1).
+__global__ void k_btp_count(const double* __restrict__ dense, int64_t nslots, int NG,
+                            int64_t* __restrict__ cnt) {
+  const int64_t ts = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (ts >= nslots) return;
+  int64_t c = 0;
+  for (int k = 0; k < 2 * NG; ++k) {
+    const d2v v = reinterpret_cast<const d2v*>(dense + (ts * 2 * NG + k) * 128)[lane];
+    c += __popcll(__ballot(v.x != 0.0)) + __popcll(__ballot(v.y != 0.0));
+  }
+  if (lane == 0) cnt[ts] = c;
+}
+
+__global__ void k_btp_write(const double* __restrict__ dense, int64_t nslots, int NG,
+                            const int64_t* __restrict__ vbase, uint64_t* __restrict__ hdr,
+                            double* __restrict__ val) {
+  const int64_t ts = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (ts >= nslots) return;
+  const int PW = bt_pack_words(NG), POFF = 4 * NG, PVB = 4 * NG + (2 * NG + 4) / 4;
+  uint64_t* h = hdr + ts * PW;
+  uint16_t* offs = reinterpret_cast<uint16_t*>(h + POFF);
+  double* run = val + vbase[ts];
+  unsigned off = 0;
+  for (int k = 0; k < 2 * NG; ++k) {
+    const d2v v = reinterpret_cast<const d2v*>(dense + (ts * 2 * NG + k) * 128)[lane];
+    const uint64_t m0 = __ballot(v.x != 0.0), m1 = __ballot(v.y != 0.0);
+    const unsigned i0 = __builtin_amdgcn_mbcnt_hi((unsigned)(m0 >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m0, off));
+    const unsigned i1 = __builtin_amdgcn_mbcnt_hi(
+        (unsigned)(m1 >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m1, off + (unsigned)__popcll(m0)));
+    if (v.x != 0.0) run[i0] = v.x;
+    if (v.y != 0.0) run[i1] = v.y;
+    if (lane == 0) {
+      h[2 * k] = m0;
+      h[2 * k + 1] = m1;
+      offs[k] = (uint16_t)off;
+    }
+    off += (unsigned)(__popcll(m0) + __popcll(m1));
+  }
+  if (lane == 0) {
+    offs[2 * NG] = (uint16_t)off;
+    h[PVB] = (uint64_t)vbase[ts];
+  }
+}
+
+int bt_pack(const double* dense, int64_t nslots, int NG, uint64_t* hdr, double** val_out,
+            int64_t* nval_out, hipStream_t s) {
+  *val_out = nullptr;
+  *nval_out = 0;
+  if (nslots <= 0) return 0;
+  int64_t *cnt = nullptr, *vb = nullptr;
+  void* tmp = nullptr;
+  size_t tb = 0;
+  hipError_t e = hipMalloc(&cnt, (nslots + 1) * sizeof(int64_t));
+  if (e == hipSuccess) e = hipMalloc(&vb, (nslots + 1) * sizeof(int64_t));
+  const unsigned blocks = (unsigned)((nslots * 64 + 255) / 256);
+  if (e == hipSuccess) e = hipMemsetAsync(cnt, 0, (nslots + 1) * sizeof(int64_t), s);
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(k_btp_count, dim3(blocks), dim3(256), 0, s, dense, nslots, NG, cnt);
+    e = hipcub::DeviceScan::ExclusiveSum(nullptr, tb, cnt, vb, (int)(nslots + 1), s);
+  }
+  if (e == hipSuccess) e = hipMalloc(&tmp, tb);
+  if (e == hipSuccess) e = hipcub::DeviceScan::ExclusiveSum(tmp, tb, cnt, vb, (int)(nslots + 1), s);
+  int64_t total = 0;
+  if (e == hipSuccess) e = hipMemcpyAsync(&total, vb + nslots, sizeof(int64_t), hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e == hipSuccess) e = hipMalloc(val_out, total * sizeof(double));
+  if (e == hipSuccess) e = hipMemsetAsync(hdr, 0, nslots * bt_pack_words(NG) * sizeof(uint64_t), s);
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(k_btp_write, dim3(blocks), dim3(256), 0, s, dense, nslots, NG, vb, hdr, *val_out);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  (void)hipFree(tmp);
+  (void)hipFree(cnt);
+  (void)hipFree(vb);
+  if (e != hipSuccess) {
+    (void)hipFree(*val_out);
+    *val_out = nullptr;
+    return (int)e;
+  }
+  *nval_out = total;
+  return 0;
 }
 
 }  // namespace rbl

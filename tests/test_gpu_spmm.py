@@ -130,6 +130,30 @@ def test_spmm_band_tiles(rbl, n, W, p, ng, b):
 
 
 @pytest.mark.parametrize("b", [16, 32])
+@pytest.mark.parametrize("n,W,p", [(7000, 64, 0.7734), (5003, 30, 0.9), (300, 60, 1.0), (100, 30, 0.95)])
+def test_spmm_band_tiles_packed_bit_identical(rbl, monkeypatch, n, W, p, b):
+    """Packed band tiles (zeros dropped, RBL_BT_PACK=1) against the dense tiles (the
+    default): the MFMA operands are the same values, so U and every Lanczos block A_i
+    (fused epilogue + A_i partials) must agree bit for bit."""
+    A = matgen.hashwindow_csr(n, W, p, n + 11)
+    X = np.random.default_rng(n + 1).standard_normal((n, b))
+    out = []
+    for pack in ("0", "1"):
+        monkeypatch.setenv("RBL_BT_PACK", pack)
+        with rbl.Context(0) as ctx:
+            ctx.set_matrix(A)
+            assert ctx.spmm_kernel_for(b) == 5
+            Y = ctx.apply(X)
+            _, _, info = rbl.lanczos(ctx, 4, b, seed=2, check=False, max_steps=4, trace=True,
+                                     ritz=False)
+        out.append((Y, info.trace_A))
+    _check(A, out[1][0], X)
+    assert np.array_equal(out[0][0], out[1][0])
+    for a0, a1 in zip(out[0][1], out[1][1]):
+        assert np.array_equal(a0, a1)
+
+
+@pytest.mark.parametrize("b", [16, 32])
 @pytest.mark.parametrize("variant", [0, 5])
 def test_spmm_segmented_long_rows(rbl, b, variant):
     """Segmented gather (variant 5, kernel id 6): an arrow matrix whose 3 hub rows/columns
