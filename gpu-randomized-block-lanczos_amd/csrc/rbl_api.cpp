@@ -8,6 +8,7 @@
 // (max_blocks+1 slots of n_local x b, row-major), U, one scratch block, the Gram slab and
 // b x b scalars.  Nothing but b x b blocks crosses PCIe per step.
 #include <hip/hip_runtime.h>
+#include <rocprofiler-sdk-roctx/roctx.h>
 
 #include <algorithm>
 #include <cstdlib>
@@ -430,7 +431,10 @@ struct StageScope {
   rbl_ctx* ctx;
   int stage;
   hipEvent_t a = nullptr;
+  // every stage is also a roctx range named like the reference's TimerOutputs labels
+  // (RBL_gpu.jl:152-187: "AQ", "3-term", ...): `rocprofv3 --marker-trace` shows them
   StageScope(rbl_ctx* c, int s) : ctx(c), stage(s) {
+    roctxRangePushA(kStageNames[s]);
     if (ctx->timers) {
       a = next_event(ctx);
       if (a) hipEventRecord(a, ctx->stream);
@@ -444,6 +448,7 @@ struct StageScope {
         ctx->marks.push_back({stage, a, b});
       }
     }
+    roctxRangePop();
   }
 };
 void harvest_timers(rbl_ctx* ctx) {  // after a stream sync
