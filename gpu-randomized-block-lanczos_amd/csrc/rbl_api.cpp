@@ -100,6 +100,9 @@ struct rbl_ctx {
   double* d_small = nullptr;  // R, Rinv, Rtot, Bprev, Ai, G (b x b each)
   int* d_flags = nullptr;     // [need3, skip3, status0, status1]
   double* h_pin = nullptr;    // pinned staging: Ai, Rtot (2 b x b)
+  double* h_hist = nullptr;   // rbl_step_async stash: per step i, Ai and Rtot (2 b x b)
+  int* h_hflags = nullptr;    //   and the step's 4 flags
+  int fetched = 1;            // steps < fetched have been returned by rbl_fetch
   bool have_bprev = false;
   // locked Ritz vectors of the restarted variants (restarted.jl: Qlock / Qlock_gpu), fp64,
   // vector j at d_lock + j * nloc (a width-1 panel)
@@ -824,6 +827,10 @@ void free_run(rbl_ctx* ctx) {
   ctx->nlock = ctx->lock_cap = 0;
   if (ctx->h_pin) hipHostFree(ctx->h_pin);
   ctx->h_pin = nullptr;
+  if (ctx->h_hist) hipHostFree(ctx->h_hist);
+  ctx->h_hist = nullptr;
+  if (ctx->h_hflags) hipHostFree(ctx->h_hflags);
+  ctx->h_hflags = nullptr;
   ctx->nblocks = 0;
   ctx->b = 0;
   ctx->have_bprev = false;
@@ -1470,6 +1477,8 @@ int rbl_start(rbl_ctx* ctx, int b, int max_blocks, int basis_bits, const double*
   HIPC(hipMalloc(&ctx->d_flags, 4 * sizeof(int)));
   HIPC(hipMemset(ctx->d_flags, 0, 4 * sizeof(int)));
   HIPC(hipHostMalloc(&ctx->h_pin, 2 * b * b * sizeof(double), hipHostMallocDefault));
+  HIPC(hipHostMalloc(&ctx->h_hist, (size_t)(max_blocks + 2) * 2 * b * b * sizeof(double), hipHostMallocDefault));
+  HIPC(hipHostMalloc(&ctx->h_hflags, (size_t)(max_blocks + 2) * 4 * sizeof(int), hipHostMallocDefault));
   }
 
   // Omega (row-major) in d_T
@@ -1502,10 +1511,51 @@ int rbl_start(rbl_ctx* ctx, int b, int max_blocks, int basis_bits, const double*
   HIPC(hipMemcpy(flags, ctx->d_flags, sizeof(flags), hipMemcpyDeviceToHost));
   if (flags[2]) return fail(ctx, RBL_ERR_NUMERIC, "QR breakdown in rbl_start");
   ctx->nblocks = 1;
+  ctx->fetched = 1;
   return RBL_OK;
 }
 
+namespace {
+int step_impl(rbl_ctx* ctx, int i, int part_reorth, double* A_out, double* B_out, bool async);
+}
 int rbl_step(rbl_ctx* ctx, int i, int part_reorth, double* A_out, double* B_out) {
+  if (ctx && ctx->fetched < ctx->nblocks)
+    return fail(ctx, RBL_ERR_STATE, "rbl_step: rbl_fetch the asynchronous steps first");
+  const int rc = step_impl(ctx, i, part_reorth, A_out, B_out, false);
+  if (ctx && rc >= 0) ctx->fetched = ctx->nblocks;
+  return rc;
+}
+int rbl_step_async(rbl_ctx* ctx, int i, int part_reorth) {
+  return step_impl(ctx, i, part_reorth, nullptr, nullptr, true);
+}
+int rbl_fetch(rbl_ctx* ctx, int i0, int i1, double* A_out, double* B_out, int* status_out) {
+  if (!ctx) return RBL_ERR_INVALID;
+  if (i0 != ctx->fetched || i1 < i0 || i1 > ctx->nblocks)
+    return fail(ctx, RBL_ERR_INVALID, "rbl_fetch: [i0, i1) must start at the first unfetched step");
+  HIPC(hipSetDevice(ctx->device));
+  HIPC(hipStreamSynchronize(ctx->stream));
+  harvest_timers(ctx);
+  const int b = ctx->b;
+  int rc = RBL_OK;
+  for (int j = i0; j < i1; ++j) {
+    const double* h = ctx->h_hist + (size_t)j * 2 * b * b;
+    const int* fl = ctx->h_hflags + 4 * j;
+    double* A = A_out ? A_out + (size_t)(j - i0) * b * b : nullptr;
+    double* B = B_out ? B_out + (size_t)(j - i0) * b * b : nullptr;
+    for (int r = 0; r < b; ++r)
+      for (int c = 0; c < b; ++c) {
+        if (A) A[c * b + r] = h[r * b + c];
+        if (B) B[c * b + r] = h[b * b + r * b + c];
+      }
+    const int st = fl[2] ? RBL_ERR_NUMERIC : fl[3] ? RBL_WARN_QR_SHIFTED : RBL_OK;
+    if (status_out) status_out[j - i0] = st;
+    if (st == RBL_ERR_NUMERIC && rc >= 0) rc = fail(ctx, RBL_ERR_NUMERIC, "QR breakdown (shifted CholQR failed)");
+  }
+  ctx->fetched = i1;
+  return rc;
+}
+namespace {
+int step_impl(rbl_ctx* ctx, int i, int part_reorth, double* A_out, double* B_out, bool async) {
   if (!ctx) return RBL_ERR_INVALID;
   if ((!ctx->d_basis && !ctx->d_basis32) || ctx->nblocks < 1) return fail(ctx, RBL_ERR_STATE, "rbl_step before rbl_start");
   if (i != ctx->nblocks) return fail(ctx, RBL_ERR_STATE, "rbl_step: i must equal the current block count");
@@ -1628,6 +1678,16 @@ int rbl_step(rbl_ctx* ctx, int i, int part_reorth, double* A_out, double* B_out)
     CHK(tsqr(ctx, ctx->d_U, ctx->d_Qi64, fused, slotp32(ctx, i)));
   }
   copy_small(smallp(ctx, S_RTOT), smallp(ctx, S_BPREV), (int64_t)b * b, ctx->stream);
+  if (async) {  // stash A_i, R_tot and the flags for rbl_fetch; no host round trip
+    double* h = ctx->h_hist + (size_t)i * 2 * b * b;
+    HIPC(hipMemcpyAsync(h, smallp(ctx, S_AI), (size_t)b * b * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+    HIPC(hipMemcpyAsync(h + b * b, smallp(ctx, S_RTOT), (size_t)b * b * sizeof(double),
+                        hipMemcpyDeviceToHost, ctx->stream));
+    HIPC(hipMemcpyAsync(ctx->h_hflags + 4 * i, ctx->d_flags, 4 * sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+    HIPC(hipGetLastError());
+    ctx->nblocks = i + 1;
+    return RBL_OK;
+  }
   HIPC(hipMemcpyAsync(ctx->h_pin, smallp(ctx, S_AI), (size_t)b * b * sizeof(double),
                       hipMemcpyDeviceToHost, ctx->stream));
   HIPC(hipMemcpyAsync(ctx->h_pin + b * b, smallp(ctx, S_RTOT), (size_t)b * b * sizeof(double),
@@ -1646,6 +1706,7 @@ int rbl_step(rbl_ctx* ctx, int i, int part_reorth, double* A_out, double* B_out)
   if (flags[2]) return fail(ctx, RBL_ERR_NUMERIC, "QR breakdown (shifted CholQR failed)");
   return flags[3] ? RBL_WARN_QR_SHIFTED : RBL_OK;
 }
+}  // namespace
 
 int rbl_ritz(rbl_ctx* ctx, int nblocks, int k, const double* S, double* V_out) {
   if (!ctx || nblocks < 1 || k < 1 || !S) return fail(ctx, RBL_ERR_INVALID, "rbl_ritz: bad arguments");
@@ -1721,6 +1782,7 @@ int rbl_restart(rbl_ctx* ctx, int nblocks, const double* S) {
   HIPC(hipMemsetAsync(ctx->d_flags, 0, 4 * sizeof(int), ctx->stream));
   HIPC(hipStreamSynchronize(ctx->stream));
   ctx->nblocks = 1;
+  ctx->fetched = 1;
   return RBL_OK;
 }
 

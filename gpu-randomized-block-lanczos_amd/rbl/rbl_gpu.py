@@ -204,6 +204,20 @@ class Context:
         st = self._check(lib.rbl_step(self._h, i, int(part_reorth), dptr(A), dptr(B)), "rbl_step")
         return A, B, st
 
+    def step_async(self, i: int, part_reorth) -> None:
+        """rbl_step_async: enqueue step i; A_i, B_{i+1} and its status come from fetch()."""
+        self._check(lib.rbl_step_async(self._h, i, int(part_reorth)), "rbl_step_async")
+
+    def fetch(self, i0: int, i1: int):
+        """rbl_fetch: wait, then [(A_j, B_j, status_j) for j in i0..i1-1]."""
+        b, m = self.b, i1 - i0
+        A = np.zeros((m, b, b))
+        B = np.zeros((m, b, b))
+        st = np.zeros(m, np.int32)
+        self._check(lib.rbl_fetch(self._h, i0, i1, dptr(A), dptr(B), i32ptr(st)), "rbl_fetch")
+        # each b x b block arrives column-major
+        return [(A[j].T.copy(order="F"), B[j].T.copy(order="F"), int(st[j])) for j in range(m)]
+
     # ---- restarted variants (restarted.jl) ----
     def restart(self, nblocks: int, S: np.ndarray) -> None:
         S = np.asfortranarray(S, dtype=np.float64)
@@ -283,32 +297,41 @@ def lanczos(ctx: Context, k: int, b: int, *, kryl_sz: int = KRYL_SZ_GPU, omega=N
     D = np.zeros(0)
     S = np.zeros((0, 0))
 
-    def _step(i, part):
-        A, B, st = ctx.step(i, part)
+    def _record(A, B, st):
         if st == _lib.RBL_WARN_QR_SHIFTED:
             info.qr_shifted_steps += 1
         if trace:
             info.trace_A.append(A.copy())
             info.trace_B.append(B.copy())
-        return A, B
 
-    Ai, Bi = _step(1, False)                       # first loop, RBL_gpu.jl:149-161
-    T.insert_A(Ai)
-    T.insert_B(Bi, 1)
-    i = 1
-    while i * b < kryl_sz and i < steps_cap:       # :162
-        i += 1
-        Ai, Bi = _step(i, i % 2 == 0)              # :164-184
-        T.insert_A(Ai)                             # :185
-        if check and i * b > k and i % 4 == 0:     # :186
-            t0 = time.perf_counter()
-            D, S = dsbev(T.view())                 # :187
-            D, S = sort_eig_abs(D, S, k)           # :188
-            info.eig_ms += (time.perf_counter() - t0) * 1e3
-            if check_convergence(Bi, S, b, k, tol):   # :189
-                info.converged = True
-                break
-        T.insert_B(Bi, i)                          # :193
+    # Steps are enqueued without a host round trip (rbl_step_async) and fetched where the host
+    # needs the T band: at a convergence check (:186) and after the last step.  T receives the
+    # same A_i / B_i in the same order as the reference's per-step pushes (:185, :193).
+    pending = []
+    i = 0
+    while True:
+        i += 1                                     # step 1: first loop, :149-161; then :162-194
+        ctx.step_async(i, i >= 2 and i % 2 == 0)   # :164-184
+        pending.append(i)
+        is_check = check and i >= 2 and i * b > k and i % 4 == 0
+        is_last = not (i * b < kryl_sz and i < steps_cap)
+        if not (is_check or is_last):
+            continue
+        for j, (Aj, Bj, st) in zip(pending, ctx.fetch(pending[0], i + 1)):
+            _record(Aj, Bj, st)
+            T.insert_A(Aj)                         # :185
+            if j == i and is_check:
+                t0 = time.perf_counter()
+                D, S = dsbev(T.view())             # :187
+                D, S = sort_eig_abs(D, S, k)       # :188
+                info.eig_ms += (time.perf_counter() - t0) * 1e3
+                if check_convergence(Bj, S, b, k, tol):   # :189
+                    info.converged = True
+                    break
+            T.insert_B(Bj, j)                      # :193
+        pending = []
+        if info.converged or is_last:
+            break
     info.iters = i
     info.nblocks = i                               # Q_1..Q_i (length(Q))
     D = D[::-1].copy()

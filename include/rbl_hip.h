@@ -154,6 +154,18 @@ int rbl_start(rbl_ctx* ctx, int b, int max_blocks, int basis_bits, const double*
  * A_i = Q_i^T U, U -= Q_i A_i, Q_{i+1} B_{i+1} = qr(U).  A_out/B_out: b x b column-major
  * host buffers receiving A_i and B_{i+1} (upper triangular) — the only per-step traffic. */
 int rbl_step(rbl_ctx* ctx, int i, int part_reorth, double* A_out, double* B_out);
+/* rbl_step without the per-step host round trip: the step is only enqueued; A_i, B_{i+1}
+ * and its status are stashed in pinned memory and handed over by rbl_fetch.  Steps may be
+ * enqueued back to back (the GPU never idles between them); the host fetches where it needs
+ * the T band (the reference pushes every step, RBL_gpu.jl:185/193, but reads it only at the
+ * convergence checks, :186-189).  A QR breakdown surfaces at the fetch. */
+int rbl_step_async(rbl_ctx* ctx, int i, int part_reorth);
+/* Wait for the enqueued steps and return those of [i0, i1) (i0 = the first unfetched step):
+ * A_out / B_out receive (i1-i0) consecutive b x b column-major blocks, status_out (may be
+ * NULL) each step's status (RBL_OK, RBL_WARN_QR_SHIFTED, RBL_ERR_NUMERIC).  Returns
+ * RBL_ERR_NUMERIC if any of them broke down, else RBL_OK.  rbl_step refuses to run while
+ * asynchronous steps are unfetched. */
+int rbl_fetch(rbl_ctx* ctx, int i0, int i1, double* A_out, double* B_out, int* status_out);
 /* Ritz vectors — RBL_gpu.jl:106-132 / RBL.jl:61-71 in fp64:  V = [Q_1..Q_nblocks] S.
  * S: (nblocks*b) x k column-major (host); V_out: n_local x k column-major (host). */
 int rbl_ritz(rbl_ctx* ctx, int nblocks, int k, const double* S, double* V_out);

@@ -177,3 +177,32 @@ def test_ritz_odd_k(rbl, b, k):
     assert np.all(1 - dots < VEC_TOL), dots
     res = np.linalg.norm(A @ V - V * D[None, :], axis=0) / np.abs(D)
     assert res.max() < RES_TOL
+
+
+@pytest.mark.parametrize("b", [8, 32])
+def test_async_steps_match_sync_steps(rbl, b):
+    from rbl import _lib
+    """rbl_step_async + rbl_fetch (the host loop's default) against one rbl_step per step: the
+    same kernels in the same order, so every A_i, B_{i+1} agrees bit for bit; the stashed
+    statuses and the rbl_step / rbl_fetch ordering rules hold."""
+    A = c1_matrix(6000, 6)
+    steps = 9
+    with rbl.Context(0) as ctx:
+        ctx.set_matrix(A)
+        ctx.start(b, steps, seed=3)
+        sync = [ctx.step(i, i >= 2 and i % 2 == 0)[:2] for i in range(1, steps + 1)]
+        ctx.start(b, steps, seed=3)
+        for i in range(1, 5):
+            ctx.step_async(i, i >= 2 and i % 2 == 0)
+        with pytest.raises(rbl.RBLError):
+            ctx.step(5, False)                    # unfetched asynchronous steps
+        with pytest.raises(rbl.RBLError):
+            ctx.fetch(2, 4)                       # must start at the first unfetched step
+        got = ctx.fetch(1, 3) + ctx.fetch(3, 5)
+        for i in range(5, steps + 1):
+            ctx.step_async(i, i >= 2 and i % 2 == 0)
+        got += ctx.fetch(5, steps + 1)
+    assert len(got) == steps
+    for (As, Bs), (Aa, Ba, st) in zip(sync, got):
+        assert st in (_lib.RBL_OK, _lib.RBL_WARN_QR_SHIFTED)
+        assert np.array_equal(As, Aa) and np.array_equal(Bs, Ba)
