@@ -96,7 +96,8 @@ struct BtArgs {
 };
 
 // VAR: bit 0 non-temporal A loads, bit 1 non-temporal U stores, bit 5 ablation (main-loop
-// MFMAs off: loads only), bit 6 fp32 Q / Q_{i-1} inputs, bit 7 packed tiles.
+// MFMAs off: loads only), bit 6 fp32 Q / Q_{i-1} inputs, bit 7 packed tiles, bit 8 no LDS
+// read-ahead, bit 9 ablation (no round barrier: wrong results, timing only).
 //
 // Packed tiles: the zeros of the band (31 % at C4a) are not stored.  Per operand block k =
 // 2g + h the header holds m0 / m1, bit l = element 0 / 1 of lane l is nonzero, and the block's
@@ -306,8 +307,8 @@ void k_spmm_bt(BtArgs a) {
           const double av_u = (u & 1) ? av[g][u >> 1].y : av[g][u >> 1].x;
 #pragma unroll
           for (int p = 0; p < NP; ++p) {
-            if constexpr (VAR & 32) {  // ablation: loads only
-              if (p == 0) acc[0][0] += av_u + bp[g & 1][u][0].x;
+            if constexpr (VAR & 32) {  // ablation: loads only (operands consumed, no math)
+              asm volatile("" ::"v"(av_u), "v"(bp[g & 1][u][p].x), "v"(bp[g & 1][u][p].y));
             } else {
               acc[p][0] = mfma44(av_u, bp[g & 1][u][p].x, acc[p][0]);
               acc[p][1] = mfma44(av_u, bp[g & 1][u][p].y, acc[p][1]);
@@ -384,7 +385,8 @@ void k_spmm_bt(BtArgs a) {
     }
 #pragma unroll
     for (int i = 0; i < NST; ++i) *ring_ptr(st_row(B == 32 ? i : 2 * i), i16 % NS) = st[i];
-    __syncthreads();
+    if constexpr (VAR & 512) __builtin_amdgcn_wave_barrier();  // ablation: no round barrier
+    else __syncthreads();
   }
 
   if constexpr (AIG) {
@@ -447,6 +449,7 @@ static void launch_bt_t(const BtArgs& a, int grid, hipStream_t s, bool f32) {
     if (var == 0) return launch_bt_v<B, NG, EPI, AIG, 0>(a, grid, s);
     if (var == 35) return launch_bt_v<B, NG, EPI, AIG, 35>(a, grid, s);
     if (var == 259) return launch_bt_v<B, NG, EPI, AIG, 259>(a, grid, s);
+    if (var == 515) return launch_bt_v<B, NG, EPI, AIG, 515>(a, grid, s);
   }
   launch_bt_v<B, NG, EPI, AIG, 3>(a, grid, s);
 }
