@@ -977,6 +977,51 @@ int rbl_get_unique_id(uint8_t unique_id[128]) {
   return rccl_unique_id(unique_id) == 0 ? RBL_OK : RBL_ERR_RCCL;
 }
 
+int rbl_comm_selftest(int device, char* msg, int msg_len) {
+  // one-rank RCCL communicator through the production transport (RcclComm): the three
+  // collective shapes on real device buffers, checked on the host
+  std::string err;
+  auto say = [&](const std::string& m) {
+    if (msg && msg_len > 0) snprintf(msg, (size_t)msg_len, "%s", m.c_str());
+  };
+  if (hipSetDevice(device) != hipSuccess) { say("hipSetDevice failed"); return RBL_ERR_HIP; }
+  uint8_t id[128];
+  if (rccl_unique_id(id) != 0) { say("ncclGetUniqueId failed"); return RBL_ERR_RCCL; }
+  Comm* c = make_rccl_comm(1, 0, id, &err);
+  if (!c) { say("ncclCommInitRank: " + err); return RBL_ERR_RCCL; }
+  hipStream_t st = nullptr;
+  double* d = nullptr;
+  int rc = RBL_OK;
+  const size_t n = 4096;
+  std::vector<double> h(n), back(n);
+  for (size_t k = 0; k < n; ++k) h[k] = 0.5 * (double)k - 7.0;
+  if (hipStreamCreate(&st) != hipSuccess || hipMalloc(&d, 2 * n * sizeof(double)) != hipSuccess ||
+      hipMemcpy(d, h.data(), n * sizeof(double), hipMemcpyHostToDevice) != hipSuccess) {
+    say("HIP setup failed");
+    rc = RBL_ERR_HIP;
+  }
+  if (rc == RBL_OK && c->allreduce_sum(d, n, st, &err) != 0) { say("allreduce: " + err); rc = RBL_ERR_RCCL; }
+  if (rc == RBL_OK) {
+    hipMemcpyAsync(back.data(), d, n * sizeof(double), hipMemcpyDeviceToHost, st);
+    hipStreamSynchronize(st);
+    if (back != h) { say("allreduce over one rank changed the data"); rc = RBL_ERR_RCCL; }
+  }
+  int64_t mine[3] = {11, -2, 1LL << 40}, all[3] = {0, 0, 0};
+  if (rc == RBL_OK && c->allgather_host(mine, all, 3, st, &err) != 0) { say("allgather: " + err); rc = RBL_ERR_RCCL; }
+  if (rc == RBL_OK && (all[0] != mine[0] || all[1] != mine[1] || all[2] != mine[2])) {
+    say("allgather returned other values");
+    rc = RBL_ERR_RCCL;
+  }
+  std::vector<Comm::Xfer> x(1);  // no peers: an empty grouped exchange
+  if (rc == RBL_OK && c->exchange(x, st, &err) != 0) { say("exchange: " + err); rc = RBL_ERR_RCCL; }
+  if (rc == RBL_OK && hipStreamSynchronize(st) != hipSuccess) { say("stream sync failed"); rc = RBL_ERR_HIP; }
+  if (rc == RBL_OK) say(std::string("ok: ") + c->name());
+  delete c;
+  if (d) (void)hipFree(d);
+  if (st) (void)hipStreamDestroy(st);
+  return rc;
+}
+
 int rbl_create_dist(rbl_ctx** out, int device, int nranks, int rank, const uint8_t unique_id[128]) {
   if (!out || nranks < 1 || rank < 0 || rank >= nranks) return RBL_ERR_INVALID;
   int s = rbl_create(out, device);

@@ -62,6 +62,7 @@ SIGNATURES = {
     "rbl_start": (C.c_int, [_p, C.c_int, C.c_int, C.c_int, _pd, _u64]),
     "rbl_step": (C.c_int, [_p, C.c_int, C.c_int, _pd, _pd]),
     "rbl_step_async": (C.c_int, [_p, C.c_int, C.c_int]),
+    "rbl_comm_selftest": (C.c_int, [C.c_int, C.c_char_p, C.c_int]),
     "rbl_fetch": (C.c_int, [_p, C.c_int, C.c_int, _pd, _pd, _pi32]),
     "rbl_ritz": (C.c_int, [_p, C.c_int, C.c_int, _pd, _pd]),
     "rbl_get_block": (C.c_int, [_p, C.c_int, _pd]),

@@ -76,6 +76,11 @@ int rbl_create(rbl_ctx** ctx, int device);
 /* One rank of a row-partitioned multi-GPU job (one process per GPU).  `unique_id` is the
  * 128-byte RCCL id produced by rbl_get_unique_id() on rank 0 and broadcast by the host. */
 int rbl_get_unique_id(uint8_t unique_id[128]);
+/* Self-test of the RCCL transport on one device: a one-rank communicator (ncclCommInitRank)
+ * runs the three collective shapes of a row-partitioned step — in-place all-reduce, host
+ * all-gather, grouped send/recv — on device buffers and checks them.  msg (optional) gets a
+ * one-line verdict.  RCCL refuses two ranks on one device, so a 1-GPU box can test no more. */
+int rbl_comm_selftest(int device, char* msg, int msg_len);
 int rbl_create_dist(rbl_ctx** ctx, int device, int nranks, int rank, const uint8_t unique_id[128]);
 /* In-process rank group: `nranks` contexts in ONE process, each driven by its own host thread
  * (several may share a GPU).  Same multi-rank code path as rbl_create_dist with the RCCL

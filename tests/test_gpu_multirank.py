@@ -3,8 +3,8 @@
 Ranks are contexts of one in-process LocalGroup, each driven by its own thread; the library
 code they run (nnz-balanced partition, halo tables, halo exchange before every SpMM,
 distributed Grams + sums, distributed CholQR, Ritz rows) is the code the RCCL transport runs,
-only the transport differs (comm.hpp).  RCCL itself cannot be exercised here: it rejects two
-ranks on one device.
+only the transport differs (comm.hpp).  RCCL rejects two ranks on one device, so the RCCL
+transport is exercised here at one rank only (test_rccl_transport_selftest).
 
 Tolerances: eigenvalues |dλ|/|λ| < 1e-10 against the single-rank run and the oracle (the
 partitioned sums only reorder fp64 additions); per-step A_i within 1e-9 relative; Ritz
@@ -149,3 +149,15 @@ def test_multirank_tiny_slices(rbl):
     for info in run_ranks(rbl, 4, fn):
         for a, a1 in zip(info.trace_A, info1.trace_A):
             assert np.abs(a - a1).max() <= 1e-10 * np.abs(a1).max()
+
+
+def test_rccl_transport_selftest(rbl):
+    """The production transport (RcclComm over RCCL): ncclCommInitRank at one rank, then the
+    three collective shapes of a row-partitioned step — in-place all-reduce of fp64 device
+    data, host all-gather of int64, an (empty) grouped send/recv — checked on the host."""
+    import ctypes
+    from rbl import _lib
+    msg = ctypes.create_string_buffer(256)
+    st = _lib.lib.rbl_comm_selftest(0, msg, 256)
+    assert st == _lib.RBL_OK, msg.value.decode()
+    assert msg.value.decode() == "ok: rccl"
