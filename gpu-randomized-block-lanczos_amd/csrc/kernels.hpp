@@ -59,6 +59,12 @@ struct CsrDev {
   int64_t bt_tiles_per_wg = 0;
   int64_t q_lo = 0, q_hi = 0;
   const double* zrow = nullptr;
+  // several ranks: the own rows [loc_lo, loc_hi) read straight from the block (fp64, or fp32
+  // on the fp32-basis path) instead of from Qin, whose halo buffer then holds only the
+  // neighbours' rows — no per-step copy of the local block.  Band-tile kernel only: spmm()
+  // fails if another kernel would run with qloc set.
+  const void* qloc = nullptr;
+  int64_t loc_lo = 0, loc_hi = 0;
   // packed band tiles (bt_pack): per tile slot a header of bt_pack_words(NG) 8-B words (per
   // 1-KiB operand block the nonzero masks of element 0 / 1 of every lane, then the blocks'
   // uint16 start offsets + the tile's count, then the tile's first value index) and the

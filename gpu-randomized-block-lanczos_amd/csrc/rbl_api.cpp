@@ -68,6 +68,7 @@ struct rbl_ctx {
   std::vector<int64_t> need_lo, need_hi;  // rows I need from rank q
   std::vector<int64_t> give_lo, give_hi;  // rows rank q needs from me
   int64_t ext_lo = 0, ext_hi = 0;         // global rows held in d_qext
+  bool split_halo = true;                 // RBL_OPT_SPLIT_HALO
 
   // Krylov run
   int b = 0, max_blocks = 0, nblocks = 0;
@@ -549,10 +550,19 @@ bool has_matrix(const rbl_ctx* ctx) { return ctx->d_rowptr || ctx->dense; }
 // the local rows, Q gathered to all n rows by the halo exchange).  Returns the number of
 // A_i partials the band kernel formed in `slab` (0: none), or a negative status.
 int apply_A(rbl_ctx* ctx, const double* Qin, int64_t off, int b, double* U, const double* Qprev,
-            const double* Bi, double* slab) {
+            const double* Bi, double* slab, const double* qloc = nullptr) {
   if (ctx->nloc <= 0) return 0;
-  if (!ctx->dense)
-    return spmm(csr(ctx), Qin, off, b, U, Qprev, Bi, ctx->spmm_variant, ctx->stream, slab);
+  if (!ctx->dense) {
+    CsrDev A = csr(ctx);
+    if (qloc) {  // own rows from the block itself (halo_exchange without the local copy)
+      A.qloc = qloc;
+      A.loc_lo = ctx->r0;
+      A.loc_hi = ctx->r0 + ctx->nloc;
+    }
+    const int parts = spmm(A, Qin, off, b, U, Qprev, Bi, ctx->spmm_variant, ctx->stream, slab);
+    if (parts < 0) return fail(ctx, RBL_ERR_INVALID, "internal: split-source SpMM needs the band-tile kernel");
+    return parts;
+  }
   HIPC(hipMemcpyAsync(ctx->d_qfull, Qin + (0 - off) * b, ctx->n * b * sizeof(double),
                       hipMemcpyDeviceToDevice, ctx->stream));
   PanelRun X;
@@ -740,8 +750,11 @@ int tsqr(rbl_ctx* ctx, const double* U, double* Qout, bool g1_ready = false, flo
   return RBL_OK;
 }
 
-// Bring Q (n_local x b, local rows) into the halo-extended buffer for SpMM.
-int halo_exchange(rbl_ctx* ctx, const double* Q, const double** Qin, int64_t* off) {
+// Bring Q (n_local x b, local rows) into the halo-extended buffer for SpMM.  copy_local
+// false: only the neighbours' rows land there (the band-tile SpMM reads the own rows from Q
+// itself, CsrDev::qloc), saving a read + write of the whole local block per step.
+int halo_exchange(rbl_ctx* ctx, const double* Q, const double** Qin, int64_t* off,
+                  bool copy_local = true) {
   if (ctx->nranks == 1) {
     *Qin = Q;
     *off = 0;
@@ -750,8 +763,9 @@ int halo_exchange(rbl_ctx* ctx, const double* Q, const double** Qin, int64_t* of
   StageScope t(ctx, RBL_STAGE_COMM);
   const int b = ctx->b;
   double* ext = ctx->d_qext;
-  HIPC(hipMemcpyAsync(ext + (ctx->r0 - ctx->ext_lo) * b, Q, ctx->nloc * b * sizeof(double),
-                      hipMemcpyDeviceToDevice, ctx->stream));
+  if (copy_local)
+    HIPC(hipMemcpyAsync(ext + (ctx->r0 - ctx->ext_lo) * b, Q, ctx->nloc * b * sizeof(double),
+                        hipMemcpyDeviceToDevice, ctx->stream));
   std::vector<Comm::Xfer> x(ctx->nranks);
   for (int q = 0; q < ctx->nranks; ++q) {
     if (q == ctx->rank) continue;
@@ -774,7 +788,8 @@ int halo_exchange(rbl_ctx* ctx, const double* Q, const double** Qin, int64_t* of
 
 // fp32 halo exchange (the fp32 basis read directly by the band-tile SpMM): the same row
 // ranges as halo_exchange, fp32 rows moved as byte-identical pairs (b is even)
-int halo_exchange32(rbl_ctx* ctx, const float* Q, const float** Qin, int64_t* off) {
+int halo_exchange32(rbl_ctx* ctx, const float* Q, const float** Qin, int64_t* off,
+                    bool copy_local = true) {
   if (ctx->nranks == 1) {
     *Qin = Q;
     *off = 0;
@@ -783,8 +798,9 @@ int halo_exchange32(rbl_ctx* ctx, const float* Q, const float** Qin, int64_t* of
   StageScope t(ctx, RBL_STAGE_COMM);
   const int b = ctx->b;
   float* ext = reinterpret_cast<float*>(ctx->d_qext);
-  HIPC(hipMemcpyAsync(ext + (ctx->r0 - ctx->ext_lo) * b, Q, ctx->nloc * b * sizeof(float),
-                      hipMemcpyDeviceToDevice, ctx->stream));
+  if (copy_local)
+    HIPC(hipMemcpyAsync(ext + (ctx->r0 - ctx->ext_lo) * b, Q, ctx->nloc * b * sizeof(float),
+                        hipMemcpyDeviceToDevice, ctx->stream));
   std::vector<Comm::Xfer> x(ctx->nranks);
   for (int q = 0; q < ctx->nranks; ++q) {
     if (q == ctx->rank) continue;
@@ -1095,6 +1111,7 @@ int rbl_set_option(rbl_ctx* ctx, int option, int64_t value) {
       if (value < 0 || value > 5) return fail(ctx, RBL_ERR_INVALID, "spmm kernel must be 0..5");
       ctx->spmm_variant = (int)value;
       return RBL_OK;
+    case RBL_OPT_SPLIT_HALO: ctx->split_halo = value != 0; return RBL_OK;
     default: return fail(ctx, RBL_ERR_INVALID, "unknown option");
   }
 }
@@ -1680,17 +1697,27 @@ int step_impl(rbl_ctx* ctx, int i, int part_reorth, double* A_out, double* B_out
     const double* Qin = nullptr;
     const float* Qin32 = nullptr;
     int64_t off = 0;
-    if (direct32) CHK(halo_exchange32(ctx, Qi32, &Qin32, &off));
-    else CHK(halo_exchange(ctx, Qi, &Qin, &off));
+    // several ranks with the band-tile kernel: the halo buffer takes only the neighbours'
+    // rows; the kernel reads the own rows from the block (no per-step local copy)
+    const bool split = ctx->nranks > 1 && !ctx->dense &&
+                       (direct32 || rbl_spmm_kernel_for(ctx, b) == 5) && ctx->split_halo;
+    if (direct32) CHK(halo_exchange32(ctx, Qi32, &Qin32, &off, !split));
+    else CHK(halo_exchange(ctx, Qi, &Qin, &off, !split));
     StageScope t(ctx, RBL_STAGE_AQ);
     // the band kernel can also form the partials of A_i = Q_i^T U while U is in registers
     if (direct32) {
-      if (!spmm_bt(csr(ctx), nullptr, off, b, ctx->d_U, nullptr, smallp(ctx, S_BPREV), ctx->stream,
+      CsrDev A = csr(ctx);
+      if (split) {
+        A.qloc = Qi32;
+        A.loc_lo = ctx->r0;
+        A.loc_hi = ctx->r0 + ctx->nloc;
+      }
+      if (!spmm_bt(A, nullptr, off, b, ctx->d_U, nullptr, smallp(ctx, S_BPREV), ctx->stream,
                    ctx->d_slab, &ai_parts, Qin32, Qm32))
         return fail(ctx, RBL_ERR_INVALID, "internal: fp32 band-tile SpMM not applicable");
     } else {
       ai_parts = apply_A(ctx, Qin, off, b, ctx->d_U, Qm, i >= 2 ? smallp(ctx, S_BPREV) : nullptr,
-                         ctx->d_slab);
+                         ctx->d_slab, split ? Qi : nullptr);
     }
     if (ai_parts < 0) return ai_parts;
     HIPC(hipGetLastError());

@@ -84,7 +84,9 @@ struct BtArgs {
   int64_t col_off;
   int64_t q_lo, q_hi;    // global rows present in Q; others read the zero row
   const double* zrow;    // 32 zeros
-  int64_t row0;          // global index of local row 0
+  const void* Qloc;      // non-null: rows [loc_lo, loc_hi) at Qloc + (c - loc_lo) * b (fp64,
+  int64_t loc_lo, loc_hi;  //   or fp32 with VAR bit 6), the rest of [q_lo, q_hi) from Q
+  int64_t row0;         // global index of local row 0
   double* U;             // padded to a multiple of 16 rows
   const double* Qprev;
   const float* Q32;      // VAR bit 6: Q and Q_{i-1} are fp32 blocks (the fp32 basis), widened
@@ -132,12 +134,15 @@ void k_spmm_bt(BtArgs a) {
   auto qload = [&](int64_t rho, int s) -> d2v {
     const int64_t c = rho + gq;
     const bool in = c >= a.q_lo && c < a.q_hi;
+    const bool own = c >= a.loc_lo && c < a.loc_hi;  // never when Qloc is null (empty range)
     if constexpr (VAR & 64) {
-      const float* p = in ? a.Q32 + (c - a.col_off) * B : reinterpret_cast<const float*>(a.zrow);
+      const float* p = own ? static_cast<const float*>(a.Qloc) + (c - a.loc_lo) * B
+                           : in ? a.Q32 + (c - a.col_off) * B : reinterpret_cast<const float*>(a.zrow);
       const float2 f = reinterpret_cast<const float2*>(p)[s];
       return d2v{(double)f.x, (double)f.y};
     } else {
-      const double* p = in ? a.Q + (c - a.col_off) * B : a.zrow;
+      const double* p = own ? static_cast<const double*>(a.Qloc) + (c - a.loc_lo) * B
+                            : in ? a.Q + (c - a.col_off) * B : a.zrow;
       return reinterpret_cast<const d2v*>(p)[s];
     }
   };
@@ -468,6 +473,9 @@ bool spmm_bt(const CsrDev& A, const double* Qin, int64_t col_off, int b, double*
   a.q_lo = A.q_lo;
   a.q_hi = A.q_hi;
   a.zrow = A.zrow;
+  a.Qloc = A.qloc;
+  a.loc_lo = A.qloc ? A.loc_lo : 0;
+  a.loc_hi = A.qloc ? A.loc_hi : 0;
   a.row0 = A.row0;
   a.U = U;
   a.Qprev = Qprev;

@@ -28,6 +28,7 @@ RBL_OPT_TIMERS = 0
 RBL_OPT_REORTH_ORDER = 1
 RBL_OPT_SPMM_KERNEL = 2
 RBL_OPT_DEVICE_BLOCKS = 3
+RBL_OPT_SPLIT_HALO = 4
 
 _p = C.c_void_p
 _i64 = C.c_int64

@@ -65,6 +65,10 @@ extern "C" {
                                    * |c - r| <= 64); each falls back 4 -> 3 -> 2 -> 1 when
                                    * the matrix does not fit the kernel's limits; 5: segmented
                                    * gather (power-law rows split / packed, b in {16, 32})     */
+#define RBL_OPT_SPLIT_HALO    4   /* several ranks, band-tile SpMM: 1 (default) the kernel reads
+                                   * the own rows from the block and the halo buffer holds only
+                                   * the neighbours' rows; 0 the own block is copied into the
+                                   * halo buffer every step (same results, bit for bit)         */
 
 typedef struct rbl_ctx rbl_ctx;
 

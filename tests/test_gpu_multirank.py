@@ -130,6 +130,31 @@ def test_multirank_device_generator_and_fixed_steps(rbl, P):
             assert np.abs(bb - bb1).max() <= 1e-9 * np.abs(bb1).max()
 
 
+@pytest.mark.parametrize("bits,b", [(64, 32), (64, 16), (32, 32)])
+def test_multirank_split_halo_bit_identical(rbl, bits, b):
+    """RBL_OPT_SPLIT_HALO: the band-tile SpMM reading the own rows straight from the block (the
+    halo buffer holds only the neighbours' rows) gives bit for bit the run that copies the own
+    block into the halo buffer every step — fp64 basis and the fp32-basis direct path."""
+    n, W, p, seed, k = 9000, 64, 0.7734, 41, 10
+    plant = matgen.planted_spectrum(k)
+
+    def run(split):
+        def fn(ctx, r):
+            ctx.set_option(rbl._lib.RBL_OPT_SPLIT_HALO, split)
+            ctx.gen_hashwindow(n, W, p, seed, plant)
+            assert ctx.spmm_kernel_for(b) == 5
+            _, _, info = rbl.lanczos(ctx, k, b, seed=3, check=False, max_steps=10, trace=True,
+                                     ritz=False, basis_bits=bits)
+            return info
+        return run_ranks(rbl, 3, fn)
+
+    on, off = run(1), run(0)
+    for i_on, i_off in zip(on, off):
+        assert len(i_on.trace_A) == 10
+        for a, a1 in zip(i_on.trace_A + i_on.trace_B, i_off.trace_A + i_off.trace_B):
+            assert np.array_equal(a, a1)
+
+
 def test_multirank_tiny_slices(rbl):
     """More ranks than comfortable: 4 ranks on n = 12 (3 rows each), b = 4."""
     import scipy.sparse as sp
