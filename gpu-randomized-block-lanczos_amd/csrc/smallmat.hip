@@ -20,11 +20,14 @@ __global__ __launch_bounds__(256) void k_chol(const double* __restrict__ G, int 
   __shared__ int fail;
   __shared__ double shift;
   __shared__ int zero;
+  __shared__ double Gd[kMaxB];  // diag(G): the serial pivot / trace reads hit LDS, not L2
   const int tid = threadIdx.x, nt = blockDim.x;
 
+  for (int j = tid; j < b; j += nt) Gd[j] = G[j * b + j];
+  __syncthreads();
   if (tid == 0) {
     double tr = 0.0;
-    for (int j = 0; j < b; ++j) tr += G[j * b + j];
+    for (int j = 0; j < b; ++j) tr += Gd[j];
     zero = !(tr > 0.0);
     shift = 0.0;
     // Fukaya shift, u = 2^-53; trace(G) >= ||U||_2^2
@@ -45,7 +48,7 @@ __global__ __launch_bounds__(256) void k_chol(const double* __restrict__ G, int 
       for (int j = 0; j < b; ++j) {
         if (tid == 0) {
           const double d = M[j][j];
-          const double gjj = G[j * b + j] + sh;
+          const double gjj = Gd[j] + sh;
           if (!(d > 0.0) || !isfinite(d)) {
             fail = 1;
           } else {

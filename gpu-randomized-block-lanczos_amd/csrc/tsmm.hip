@@ -170,6 +170,8 @@ __global__ __launch_bounds__(256) void k_reduce(const double* __restrict__ slab,
   double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
   if (e < len) {
     int s = j;
+    // unrolled: up to 16 loads in flight per lane (the sums keep their order: same bits)
+#pragma unroll 4
     for (; s + 48 < splits; s += 64) {
       a0 += slab[(int64_t)s * len + e];
       a1 += slab[(int64_t)(s + 16) * len + e];
