@@ -30,6 +30,8 @@ for _p in (ROOT, PKG):
 
 import numpy as np  # noqa: E402
 
+BASELINE_METRIC = ("RBL iters/sec + time-to-k=20 eigenpairs, n=1e7 nnz/row=100 b=32; "
+                   "1/2/4/8 GPU")   # BASELINE.json "metric", quoted on C4a at N GPUs
 HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FP64_MFMA_PEAK_TF = 78.6     # MI355X dense fp64 matrix spec
 FP32_MFMA_PEAK_TF = 157.3    # MI355X dense fp32 matrix spec (v_mfma_f32_16x16x4_f32)
@@ -37,7 +39,10 @@ FP32_MFMA_PEAK_TF = 157.3    # MI355X dense fp32 matrix spec (v_mfma_f32_16x16x4
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (one process each).  Under torch.distributed.run it must equal "
+                         "WORLD_SIZE; without it, N > 1 re-launches this script under "
+                         "torch.distributed.run with N processes (before any GPU call)")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--n", type=int, default=10_000_000)
@@ -47,7 +52,10 @@ def parse():
     ap.add_argument("--density", type=float, default=0.7734)
     ap.add_argument("--seed", type=int, default=20261015)
     ap.add_argument("--kryl", type=int, default=1200)
-    ap.add_argument("--cpu-sample-n", type=int, default=100_000)
+    ap.add_argument("--cpu-sample-n", type=int, default=100_000,
+                    help="rows of the CPU baseline's sample (same generator, same block steps)")
+    ap.add_argument("--cpu-one-thread", action="store_true",
+                    help="also time the CPU baseline with 1 BLAS thread (benchmark.jl:49)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-ttk", action="store_true")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
@@ -60,6 +68,9 @@ def parse():
     ap.add_argument("--device-blocks", type=int, default=0,
                     help="Krylov blocks kept in HBM (RBL_OPT_DEVICE_BLOCKS; older blocks spill to "
                          "pinned host memory, the reference's hybrid buffer); 0 = all")
+    ap.add_argument("--keep-csr", type=int, default=1, choices=(0, 1),
+                    help="0: release the device CSR once the band tiles are built "
+                         "(RBL_OPT_KEEP_CSR; frees 12 B per nonzero for the basis at n = 5e7)")
     ap.add_argument("--basis-bits", type=int, default=64, choices=(64, 32),
                     help="32: the mixed mode (fp32 Krylov basis + reorth on fp32 MFMA, fp64 A*Q / "
                          "3-term / QR) of BASELINE config 5, on this workload")
@@ -85,8 +96,58 @@ def streamed_bytes(kid, nloc, nnz_loc, b, halfwidth, m_max):
     return nnz_loc * 12 + (nloc + 1) * 8 + vec
 
 
+def launch_ranks(args) -> None:
+    """`--gpus N` outside torch.distributed.run: check the GPUs exist, then run this script
+    under torch.distributed.run with N processes (this process never touches the GPU;
+    torch.cuda.device_count() does not initialise it) and exit with its status."""
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is not None:
+        if args.gpus is not None and args.gpus != int(env_world):
+            sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={env_world}")
+        return
+    if args.gpus is None or args.gpus <= 1:
+        return
+    import subprocess
+    import socket
+    import torch
+    have = torch.cuda.device_count()
+    if have < args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} needs {args.gpus} GPUs, this node has {have}")
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr=127.0.0.1", f"--master-port={port}",
+           os.path.abspath(__file__)] + sys.argv[1:]
+    sys.exit(subprocess.run(cmd).returncode)
+
+
+def workload_name(args) -> str:
+    """BASELINE.json config this run measures, by its shape."""
+    if args.matrix == "rmat":
+        return "C4b R-MAT SpMM-Lanczos" if args.n == 10_000_000 and args.b == 32 else "R-MAT SpMM-Lanczos"
+    if args.basis_bits == 32 and args.n == 50_000_000 and args.b == 32:
+        return "C5 hash-window SpMM-Lanczos, mixed precision (fp32 basis)"
+    tag = {(10_000_000, 32): "C4a", (1_000_000, 16): "C2"}.get((args.n, args.b))
+    name = f"{tag} hash-window SpMM-Lanczos" if tag else "hash-window SpMM-Lanczos"
+    if args.basis_bits == 32:
+        name += ", mixed precision (fp32 basis, config 5 mode)"
+    return name
+
+
+def metric_name(args, nnz: int) -> str:
+    """BASELINE.json's metric string for its own config; the same form for any other shape."""
+    if (args.matrix == "hashwindow" and args.n == 10_000_000 and args.b == 32 and args.k == 20
+            and args.basis_bits == 64):
+        return BASELINE_METRIC
+    return (f"RBL iters/sec + time-to-k={args.k} eigenpairs, n={args.n:.0e} "
+            f"nnz/row={nnz / args.n:.0f} b={args.b}" + (" fp32 basis" if args.basis_bits == 32 else "")
+            + f" ({args.matrix})")
+
+
 def main():
     args = parse()
+    launch_ranks(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -115,6 +176,14 @@ def main():
         dist.all_reduce(t)
         return int(t.item())
 
+    def allgather_i64(x: int) -> list:
+        if dist is None:
+            return [int(x)]
+        import torch
+        out = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
+        dist.all_gather(out, torch.tensor([int(x)], dtype=torch.int64))
+        return [int(t.item()) for t in out]
+
     import rbl
     from rbl import _lib
     uid = None
@@ -129,6 +198,7 @@ def main():
     ctx = rbl.Context(local_rank, nranks=world, rank=rank, unique_id=uid)
 
     n, b, k = args.n, args.b, args.k
+    ctx.set_option(_lib.RBL_OPT_KEEP_CSR, args.keep_csr)
     plant = np.array([100.0 * (2 * k + 1 - l) for l in range(1, 2 * k + 1)])
     t0 = time.perf_counter()
     if args.matrix == "rmat":
@@ -214,7 +284,7 @@ def main():
     try:
         with open(os.path.join(ROOT, "profiles", "pmc_clock.json")) as f:
             kc = json.load(f)["kernels"]
-        ks = [kc[k] for k in ("k_gram44<32, 2>", "k_tsmm44<32, 64>") if k in kc]
+        ks = [kc[k] for k in ("k_gram44<32, 2>", "k_tsmm44f<32>") if k in kc]
         if ks and args.basis_bits == 64 and b == 32:
             held = sum(k["clock_ghz"] * k["avg_us"] for k in ks) / sum(k["avg_us"] for k in ks)
     except (OSError, ValueError, KeyError):
@@ -224,7 +294,7 @@ def main():
                    "achieved": round(reorth_tf, 2), "peak": mfma_peak, "unit": "TFLOP/s",
                    "frac": round(reorth_tf / mfma_peak, 4),
                    "traffic": None if traffic_reorth is None else int(traffic_reorth),
-                   "traffic_unit": "HBM bytes per run (gram + update, 18 launches each)",
+                   "traffic_unit": f"HBM bytes per run (gram + update, {len(range(4, m_max + 1, 2))} launches each)",
                    "algorithmic_flops_per_run": reorth_flops, "ms_per_run": round(reorth_ms, 3),
                    **({"held_clock_ghz": round(held, 3),
                        "frac_of_peak_at_held_clock": round(reorth_tf / (mfma_peak * held / 2.4), 4)}
@@ -239,23 +309,29 @@ def main():
     if not args.no_ttk:
         barrier()
         ctx.synchronize()
+        ctx.reset_timers()
         t0 = time.perf_counter()
         D, V, info = rbl.lanczos(ctx, k, b, kryl_sz=args.kryl, seed=args.seed + 2, check=True,
                                  ritz=True, basis_bits=args.basis_bits)
         ctx.synchronize()
         barrier()
         ttk_s = allmax(time.perf_counter() - t0)
+        ttk_stage = ctx.timers()
         ttk = {"seconds": round(ttk_s, 4), "iters": info.iters, "converged": info.converged,
-               "k": k, "top_eigenvalues": [round(float(x), 6) for x in D[:3]]}
+               "k": k, "top_eigenvalues": [round(float(x), 6) for x in D[:3]],
+               "ritz_ms": round(allmax(ttk_stage["Ritz vectors"]), 3),
+               "stage_ms": {s_: round(v, 3) for s_, v in ttk_stage.items()}}
 
     # ---- CPU baseline: the oracle (port of RBL.jl) on a bounded sample, rank 0, N = 1 ----
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args, m_max, plant)
 
+    comm = ctx.comm_info()
+    nnz_ranks = allgather_i64(nnz_loc)
     if rank == 0:
         line = {
-            "metric": "RBL iters/sec (n=1e7, nnz/row~100, b=32, 38 fixed block steps)",
+            "metric": metric_name(args, nnz),
             "value": round(value, 3),
             "unit": "block iterations/s",
             "n_gpus": world,
@@ -267,16 +343,17 @@ def main():
             "vs_baseline": None,
             "dtype": "f64" if args.basis_bits == 64 else "f64 (A*Q, 3-term, QR) + f32 (basis, reorth)",
             "data": f"synthetic (seeded {args.matrix} symmetric matrix generated on device)",
-            "config": {"workload": ("C4a hash-window SpMM-Lanczos" if args.matrix == "hashwindow"
-                                    else "C4b R-MAT SpMM-Lanczos") +
-                       ("" if args.basis_bits == 64 else ", mixed precision (fp32 basis, config 5 mode)"),
+            "config": {"workload": workload_name(args),
                        "n": n, "nnz": nnz, "b": b, "k": k, "matrix": args.matrix,
                        **({"halfwidth": args.halfwidth, "density": args.density}
                           if args.matrix == "hashwindow" else
                           {"rmat_scale": args.rmat_scale, "rmat_edges": args.rmat_edges,
                            "rmat_abcd": [0.57, 0.19, 0.19, 0.05]}),
                        "block_steps_per_run": m_max, "parallelism": f"rows{world}",
-                       **({"device_blocks": args.device_blocks} if args.device_blocks else {})},
+                       "transport": comm["transport"], "transport_ranks": comm["nranks"],
+                       "nnz_per_rank": nnz_ranks,
+                       **({"device_blocks": args.device_blocks} if args.device_blocks else {}),
+                       **({"keep_csr": 0} if not args.keep_csr else {})},
             "roofline": roofline,
             "roofline_secondary": roofline2,
             "stage_ms_per_run": {s: round(v, 3) for s, v in stage_per_run.items()},
@@ -290,34 +367,65 @@ def main():
         dist.destroy_process_group()
 
 
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(args, m_max, plant):
-    """Time the oracle (NumPy/SciPy port of RBL.jl) on n_s rows of the same generator for the
-    same 38 fixed block steps, and scale per-iteration time linearly to n (every stage of a
-    block step is O(n) at fixed b and m)."""
+    """Time the oracle (NumPy/SciPy restatement of RBL.jl) on n_s rows of the same generator
+    for the same m_max fixed block steps (measured end to end, matrix generation excluded), and
+    scale its per-iteration time linearly to n (every stage of a block step is O(n) at fixed b
+    and m).  With --cpu-one-thread the same sample runs again at 1 BLAS thread, as the
+    reference's benchmark does (benchmark.jl:49)."""
     from oracle import matgen
     from oracle import rbl_oracle as o
     try:
-        from threadpoolctl import threadpool_info
+        from threadpoolctl import threadpool_info, threadpool_limits
         threads = max([d.get("num_threads", 1) for d in threadpool_info()] or [1])
     except Exception:
+        threadpool_limits = None
         threads = 1
-    ns = args.cpu_sample_n
+    ns = min(args.cpu_sample_n, args.n)
     if args.matrix == "rmat":  # same draw density per row, ids scaled down with n
         sc = max(1, int(math.ceil(math.log2(ns))))
         A = matgen.rmat_csr(ns, sc, int(args.rmat_edges * ns / args.n), args.seed, plant)
     else:
         A = matgen.hashwindow_csr(ns, args.halfwidth, args.density, args.seed, plant)
     omega = np.random.default_rng(0).standard_normal((ns, args.b))
-    t0 = time.perf_counter()
-    o.RBL_gpu_semantics(A, args.k, args.b, omega=omega, kryl_sz=args.kryl, check=False)
-    t = time.perf_counter() - t0
+
+    def timed():
+        t0 = time.perf_counter()
+        if args.basis_bits == 32:  # RBL_gpu.jl with FLOAT = Float32
+            o.RBL_gpu_mixed(A, args.k, args.b, omega=omega, kryl_sz=args.kryl, check=False)
+        else:
+            o.RBL_gpu_semantics(A, args.k, args.b, omega=omega, kryl_sz=args.kryl, check=False)
+        return time.perf_counter() - t0
+
+    t = timed()
     scale = args.n / ns
-    return {"value": round(m_max / (t * scale), 5), "unit": "block iterations/s",
-            "cores": threads, "kind": "port",
-            "sample": f"oracle RBL (RBL.jl restated, NumPy/SciPy; SpMM single-threaded) on the "
-                      f"same generator at n={ns} for the same {m_max} block steps in {t:.2f} s, "
-                      f"scaled x{scale:.0f} to n={args.n}",
-            "sample_seconds": round(t, 3)}
+    out = {"value": round(m_max / (t * scale), 5), "unit": "block iterations/s",
+           "cores": threads, "kind": "port",
+           "sample": f"oracle RBL (RBL.jl restated, NumPy/SciPy OpenBLAS on {threads} threads; SpMM "
+                     f"single-threaded as SparseArrays) on the same generator at n={ns} "
+                     f"(nnz={A.nnz}) for the same {m_max} block steps: {t:.2f} s measured, i.e. "
+                     f"{m_max / t:.4f} iters/s at n={ns}; value = that per-iteration time scaled "
+                     f"x{scale:.0f} to n={args.n}",
+           "sample_n": ns, "sample_seconds": round(t, 3),
+           "sample_iters_per_s": round(m_max / t, 5),
+           "host_cpus": os.cpu_count(), "cpu_model": cpu_model()}
+    if args.cpu_one_thread and threadpool_limits is not None:
+        with threadpool_limits(limits=1):
+            t1 = timed()
+        out.update({"value_1thread": round(m_max / (t1 * scale), 5),
+                    "sample_seconds_1thread": round(t1, 3)})
+    return out
 
 
 if __name__ == "__main__":

@@ -40,6 +40,10 @@ struct RcclComm final : Comm {
     if (comm) ncclCommDestroy(comm);
   }
   const char* name() const override { return "rccl"; }
+  int count(int* n, std::string* err) override {
+    NCCLX(ncclCommCount(comm, n));
+    return 0;
+  }
   int allreduce_sum(double* dbuf, size_t count, hipStream_t st, std::string* err) override {
     NCCLX(ncclAllReduce(dbuf, dbuf, count, ncclDouble, ncclSum, comm, st));
     return 0;

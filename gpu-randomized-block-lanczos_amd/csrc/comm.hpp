@@ -24,6 +24,12 @@ struct Comm {
   int nranks = 1, rank = 0;
   virtual ~Comm() {}
   virtual const char* name() const = 0;
+  // ranks the transport itself reports (RCCL: ncclCommCount), a cross-check of nranks
+  virtual int count(int* n, std::string* err) {
+    (void)err;
+    *n = nranks;
+    return 0;
+  }
   // in-place sum over ranks of `count` doubles (device memory) ordered on `st`
   virtual int allreduce_sum(double* dbuf, size_t count, hipStream_t st, std::string* err) = 0;
   // blocking all-gather of `n` int64 per rank (host memory): all[p*n + i] = rank p's mine[i]

@@ -15,6 +15,7 @@ struct Panels {
 // Contiguous run of `count` panels of width w, panel j at base + j*stride (Krylov basis).
 struct PanelRun {
   const double* base = nullptr;
+  const float* base32 = nullptr;  // fp32 panels instead (tsmm44_f32x only)
   int64_t stride = 0;
   int count = 0;
   int w = 0;
@@ -114,6 +115,9 @@ bool spmm_seg_ok(const CsrDev& A, int b);
 bool spmm_window(const CsrDev& A, const double* Qin, int64_t col_off, int b, double* U,
                  const double* Qprev, const double* Bi, hipStream_t s);
 int window_grid();              // workgroups for the window kernel (= CUs)
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per (device, kernel): thread-safe
+// (in-process ranks launch from several threads) and per device (a process may drive several)
+void ensure_lds_attr(const void* kernel, int bytes);
 // spmm_band.hip: LDS-densified band tiles on fp64 MFMA (b in {16,32}); false if not applicable.
 // ai_slab / ai_parts: see spmm().
 bool spmm_band(const CsrDev& A, const double* Qin, int64_t col_off, int b, double* U,
@@ -166,6 +170,10 @@ int gram44_splits(int64_t nrows, int nW);
 void gram44_partial(int64_t nrows, const PanelRun& W, const Panels& X, double* slab, int splits,
                     const int* skip, hipStream_t s);
 bool tsmm44_ok(int xw, int ky, int yw);
+// Y = beta Y + alpha X C with X fp32 panels (X.base32), widened to fp64 as loaded: the Ritz
+// projection over the fp32 basis in one pass (fp64 S and V).  Same shape limits as tsmm44.
+void tsmm44_f32x(int64_t nrows, const PanelRun& X, const double* C, int ldc, const Panels& Y,
+                 double alpha, double beta, hipStream_t s);
 void tsmm44(int64_t nrows, const PanelRun& X, const double* C, int ldc, const Panels& Y,
             double alpha, double beta, const int* skip, hipStream_t s);
 

@@ -69,6 +69,8 @@ struct rbl_ctx {
   std::vector<int64_t> give_lo, give_hi;  // rows rank q needs from me
   int64_t ext_lo = 0, ext_hi = 0;         // global rows held in d_qext
   bool split_halo = true;                 // RBL_OPT_SPLIT_HALO
+  bool keep_csr = true;                   // RBL_OPT_KEEP_CSR
+  bool csr_dropped = false;               // values / column ids released (band tiles only)
 
   // Krylov run
   int b = 0, max_blocks = 0, nblocks = 0;
@@ -82,12 +84,15 @@ struct rbl_ctx {
   // pinned host slot j - resident once final (copied during step j + 2)
   int dev_blocks_opt = 0;
   int resident = INT32_MAX;
-  double* h_spill = nullptr;
+  // pinned host slots of the spilled blocks (block j at h_spill[j - resident]), pinned when
+  // the block is first written out: host memory grows with the blocks a run really spills
+  std::vector<void*> h_spill;
   double* d_stage = nullptr;          // one n_local x b staging block for spilled blocks
   hipStream_t cstream = nullptr;      // D2H copies of finished spilled blocks
   hipEvent_t ev_fin = nullptr, ev_d2h[2] = {nullptr, nullptr};
   bool d2h_pending[2] = {false, false};
   float* d_basis32 = nullptr;
+  float* d_stage32 = nullptr;
   double* d_Qi64 = nullptr;
   double* d_Qm64 = nullptr;
   double* d_U = nullptr;
@@ -131,6 +136,18 @@ int fail(rbl_ctx* c, int code, const std::string& msg) {
   return code;
 }
 
+// device allocation released on every return path
+struct DevBuf {
+  void* p = nullptr;
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  ~DevBuf() {
+    if (p) (void)hipFree(p);
+  }
+  double* d() const { return static_cast<double*>(p); }
+};
+
 #define HIPC(expr)                                                                    \
   do {                                                                                \
     hipError_t _e = (expr);                                                           \
@@ -161,12 +178,38 @@ bool spilled(const rbl_ctx* ctx) { return ctx->resident != INT32_MAX; }
 const double* block_dev(rbl_ctx* ctx, int j, int nblocks, int* st) {
   *st = 0;
   if (j < ctx->resident || j >= nblocks - 2) return slotp(ctx, j);
-  const hipError_t e = hipMemcpyAsync(ctx->d_stage, ctx->h_spill + (int64_t)(j - ctx->resident) * ctx->slot,
+  const hipError_t e = hipMemcpyAsync(ctx->d_stage, ctx->h_spill[j - ctx->resident],
                                       ctx->slot * sizeof(double), hipMemcpyHostToDevice, ctx->stream);
   if (e != hipSuccess) *st = RBL_ERR_HIP;
   return ctx->d_stage;
 }
-float* slotp32(rbl_ctx* ctx, int j) { return ctx->d_basis32 + (int64_t)j * ctx->slot; }
+// fp32 basis: the same slot plan as slotp / block_dev
+// pin the host slot of spilled block j on first use (non-coherent pages: the DMA engines
+// stream them at PCIe rate both ways)
+int spill_slot(rbl_ctx* ctx, int j, size_t elem) {
+  void*& h = ctx->h_spill[j - ctx->resident];
+  if (!h) {
+    const hipError_t e = hipHostMalloc(&h, (size_t)ctx->slot * elem, hipHostMallocNonCoherent);
+    if (e != hipSuccess) {
+      h = nullptr;
+      return fail(ctx, e == hipErrorOutOfMemory ? RBL_ERR_OOM : RBL_ERR_HIP,
+                  std::string("host spill: hipHostMalloc: ") + hipGetErrorString(e));
+    }
+  }
+  return RBL_OK;
+}
+float* slotp32(rbl_ctx* ctx, int j) {
+  const int s = j < ctx->resident ? j : ctx->resident + (j & 1);
+  return ctx->d_basis32 + (int64_t)s * ctx->slot;
+}
+const float* block_dev32(rbl_ctx* ctx, int j, int nblocks, int* st) {
+  *st = 0;
+  if (j < ctx->resident || j >= nblocks - 2) return slotp32(ctx, j);
+  const hipError_t e = hipMemcpyAsync(ctx->d_stage32, ctx->h_spill[j - ctx->resident],
+                                      ctx->slot * sizeof(float), hipMemcpyHostToDevice, ctx->stream);
+  if (e != hipSuccess) *st = RBL_ERR_HIP;
+  return ctx->d_stage32;
+}
 
 CsrDev csr(rbl_ctx* ctx) {
   CsrDev A;
@@ -375,14 +418,6 @@ int prepare_window(rbl_ctx* ctx, const std::vector<int64_t>& rp) {
   }
   HIPC(hipMalloc(&ctx->d_tinfo, 8 * nt * sizeof(int64_t)));
   HIPC(hipMemcpy(ctx->d_tinfo, info.data(), 8 * nt * sizeof(int64_t), hipMemcpyHostToDevice));
-  if (ctx->band_ok16 || ctx->band_ok32) {  // dense-tile positions for the band kernel
-    HIPC(hipMalloc(&ctx->d_bpos, (ctx->nnz + kCsrPad) * sizeof(uint16_t)));
-    HIPC(hipMemsetAsync(ctx->d_bpos + ctx->nnz, 0, kCsrPad * sizeof(uint16_t), ctx->stream));
-    CsrDev A2 = csr(ctx);
-    band_positions(A2, ctx->d_bpos, ctx->stream);
-    HIPC(hipGetLastError());
-    HIPC(hipStreamSynchronize(ctx->stream));
-  }
   const int64_t grid = window_grid();
   ctx->tiles_per_wg = std::max<int64_t>(1, (nt + grid - 1) / grid);
   {
@@ -418,6 +453,31 @@ int prepare_window(rbl_ctx* ctx, const std::vector<int64_t>& rp) {
         ctx->d_bt = nullptr;
       }
     }
+  }
+  if (!ctx->keep_csr && ctx->bt_ng) {
+    // RBL_OPT_KEEP_CSR = 0: the band tiles are the matrix from here on
+    hipFree(ctx->d_col); ctx->d_col = nullptr;
+    hipFree(ctx->d_val); ctx->d_val = nullptr;
+    hipFree(ctx->d_seg_trow); ctx->d_seg_trow = nullptr;
+    hipFree(ctx->d_seg_tinfo); ctx->d_seg_tinfo = nullptr;
+    hipFree(ctx->d_seg_slot_k0); ctx->d_seg_slot_k0 = nullptr;
+    hipFree(ctx->d_seg_lrow); ctx->d_seg_lrow = nullptr;
+    hipFree(ctx->d_seg_lslot); ctx->d_seg_lslot = nullptr;
+    hipFree(ctx->d_seg_scratch); ctx->d_seg_scratch = nullptr;
+    ctx->seg_ntasks = ctx->seg_nlong = 0;
+    ctx->window_ok16 = ctx->window_ok32 = false;
+    ctx->band_ok16 = ctx->band_ok32 = false;
+    ctx->band_gram = ctx->band_pair = false;
+    ctx->csr_dropped = true;
+    return RBL_OK;
+  }
+  if (ctx->band_ok16 || ctx->band_ok32) {  // dense-tile positions for the band kernel
+    HIPC(hipMalloc(&ctx->d_bpos, (ctx->nnz + kCsrPad) * sizeof(uint16_t)));
+    HIPC(hipMemsetAsync(ctx->d_bpos + ctx->nnz, 0, kCsrPad * sizeof(uint16_t), ctx->stream));
+    CsrDev A2 = csr(ctx);
+    band_positions(A2, ctx->d_bpos, ctx->stream);
+    HIPC(hipGetLastError());
+    HIPC(hipStreamSynchronize(ctx->stream));
   }
   return RBL_OK;
 }
@@ -545,6 +605,19 @@ int rowop(rbl_ctx* ctx, const double* X, const double* C, double* Y, double alph
 
 bool has_matrix(const rbl_ctx* ctx) { return ctx->d_rowptr || ctx->dense; }
 
+// fp32 basis: the band-tile SpMM and the 3-term update read the fp32 blocks directly
+bool direct32_ok(const rbl_ctx* ctx, int b) {
+  return !ctx->dense && (ctx->spmm_variant == 0 || ctx->spmm_variant == 4) && (b == 32 || b == 16) &&
+         (ctx->bt_ng == 5 || ctx->bt_ng == 9);
+}
+// the fp64 scratch block of the fp32 path (widened Q_{i-1}, Ritz / get_block widening),
+// allocated on first use when the direct path made it unnecessary at rbl_start
+int ensure_qm64(rbl_ctx* ctx) {
+  if (ctx->d_Qm64) return RBL_OK;
+  HIPC(hipMalloc(&ctx->d_Qm64, (std::max<int64_t>(ctx->nloc, 1) + kRowPad) * ctx->b * sizeof(double)));
+  return RBL_OK;
+}
+
 // U = A Qin (+ U -= Qprev Bi^T when Qprev): the SpMM of RBL_gpu.jl:176-177, or for a dense
 // A (RBL_gpu.jl:205 with A::Matrix) the panel GEMM on fp64 MFMA (tsmm44 over the panels of
 // the local rows, Q gathered to all n rows by the halo exchange).  Returns the number of
@@ -552,6 +625,9 @@ bool has_matrix(const rbl_ctx* ctx) { return ctx->d_rowptr || ctx->dense; }
 int apply_A(rbl_ctx* ctx, const double* Qin, int64_t off, int b, double* U, const double* Qprev,
             const double* Bi, double* slab, const double* qloc = nullptr) {
   if (ctx->nloc <= 0) return 0;
+  if (ctx->csr_dropped && rbl_spmm_kernel_for(ctx, b) != 5)
+    return fail(ctx, RBL_ERR_STATE, "the CSR was released (RBL_OPT_KEEP_CSR = 0): only the band-tile "
+                                    "SpMM (b in {16, 32}) can run");
   if (!ctx->dense) {
     CsrDev A = csr(ctx);
     if (qloc) {  // own rows from the block itself (halo_exchange without the local copy)
@@ -673,6 +749,36 @@ int basis_combine(rbl_ctx* ctx, int nblocks, int kcols, const double* S, double*
   hipFree(d_S);
   hipFree(d_Scm);
   return st;
+}
+
+// Y = [Q_1 .. Q_nblocks] S_dev over the fp32 basis, widened on load, V and S fp64 (P3: fp64
+// Ritz): one launch over the resident blocks when the fp32-input tsmm44 applies, else each
+// block widened into a scratch block and accumulated; spilled blocks stream from the host
+int combine_blocks32(rbl_ctx* ctx, int nblocks, int kcols, const double* d_S, double* Y) {
+  const int b = ctx->b;
+  if (ctx->nloc <= 0) return RBL_OK;
+  const int nres = std::min(nblocks, ctx->resident);
+  int j0 = 0;
+  if (tsmm44_ok(b, kcols, kcols) && nres > 0) {
+    PanelRun X;
+    X.base32 = slotp32(ctx, 0);
+    X.stride = ctx->slot;
+    X.count = nres;
+    X.w = b;
+    tsmm44_f32x(ctx->nloc, X, d_S, kcols, pan1(Y, kcols), 1.0, 0.0, ctx->stream);
+    HIPC(hipGetLastError());
+    j0 = nres;
+  }
+  if (j0 < nblocks) CHK(ensure_qm64(ctx));
+  for (int j = j0; j < nblocks; ++j) {
+    int st = 0;
+    const float* Qj = block_dev32(ctx, j, ctx->nblocks, &st);
+    if (st) return fail(ctx, st, "Ritz: H2D of a spilled block failed");
+    cvt_f32_to_f64(Qj, ctx->d_Qm64, ctx->nloc * b, ctx->stream);
+    CHK(tsmm_checked(ctx, run1(ctx->d_Qm64, b), d_S + (int64_t)j * b * kcols, kcols, pan1(Y, kcols),
+                     1.0, j == 0 ? 0.0 : 1.0, nullptr));
+  }
+  return RBL_OK;
 }
 
 // fp32 basis: Gram C = W^T [X0, X1] over all ranks (fp32 MFMA per split, fp64 sum), C fp64
@@ -824,11 +930,14 @@ int halo_exchange32(rbl_ctx* ctx, const float* Q, const float** Qin, int64_t* of
 void free_run(rbl_ctx* ctx) {
   if (ctx->cstream) hipStreamSynchronize(ctx->cstream);
   hipFree(ctx->d_basis); ctx->d_basis = nullptr;
-  hipHostFree(ctx->h_spill); ctx->h_spill = nullptr;
+  for (void* h : ctx->h_spill)
+    if (h) hipHostFree(h);
+  ctx->h_spill.clear();
   hipFree(ctx->d_stage); ctx->d_stage = nullptr;
   ctx->resident = INT32_MAX;
   ctx->d2h_pending[0] = ctx->d2h_pending[1] = false;
   hipFree(ctx->d_basis32); ctx->d_basis32 = nullptr;
+  hipFree(ctx->d_stage32); ctx->d_stage32 = nullptr;
   hipFree(ctx->d_Qi64); ctx->d_Qi64 = nullptr;
   hipFree(ctx->d_Qm64); ctx->d_Qm64 = nullptr;
   ctx->basis_bits = 64;
@@ -880,6 +989,7 @@ void free_matrix(rbl_ctx* ctx) {
   ctx->ntiles = ctx->tiles_per_wg = 0;
   ctx->window_ok16 = ctx->window_ok32 = false;
   ctx->band_ok16 = ctx->band_ok32 = false;
+  ctx->csr_dropped = false;
 }
 
 // Exchange halo needs among ranks and size the extended buffer.
@@ -1094,6 +1204,22 @@ int rbl_free(rbl_ctx* ctx) {
 
 const char* rbl_last_error(const rbl_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
 
+int rbl_comm_info(rbl_ctx* ctx, int* nranks, int* rank, char* transport, int transport_len) {
+  if (!ctx || !nranks || !rank) return RBL_ERR_INVALID;
+  int cnt = 1;
+  const char* name = "none";
+  if (ctx->comm) {
+    hipSetDevice(ctx->device);
+    const int s = ctx->comm->count(&cnt, &ctx->err);
+    if (s < 0) return s;
+    name = ctx->comm->name();
+  }
+  *nranks = cnt;
+  *rank = ctx->rank;
+  if (transport && transport_len > 0) snprintf(transport, (size_t)transport_len, "%s", name);
+  return RBL_OK;
+}
+
 int rbl_set_option(rbl_ctx* ctx, int option, int64_t value) {
   if (!ctx) return RBL_ERR_INVALID;
   switch (option) {
@@ -1112,6 +1238,7 @@ int rbl_set_option(rbl_ctx* ctx, int option, int64_t value) {
       ctx->spmm_variant = (int)value;
       return RBL_OK;
     case RBL_OPT_SPLIT_HALO: ctx->split_halo = value != 0; return RBL_OK;
+    case RBL_OPT_KEEP_CSR: ctx->keep_csr = value != 0; return RBL_OK;
     default: return fail(ctx, RBL_ERR_INVALID, "unknown option");
   }
 }
@@ -1373,6 +1500,8 @@ int rbl_matrix_info(rbl_ctx* ctx, int64_t* n, int64_t* row_begin, int64_t* row_e
 }
 
 int rbl_get_matrix_csr(rbl_ctx* ctx, int64_t* rowptr, int32_t* colind, double* val) {
+  if (ctx && ctx->csr_dropped)
+    return fail(ctx, RBL_ERR_STATE, "rbl_get_matrix_csr: the CSR was released (RBL_OPT_KEEP_CSR = 0)");
   if (!ctx || !ctx->d_rowptr)
     return fail(ctx, RBL_ERR_STATE, ctx && ctx->dense ? "dense matrix: no CSR" : "no matrix");
   HIPC(hipSetDevice(ctx->device));
@@ -1406,39 +1535,36 @@ int rbl_apply(rbl_ctx* ctx, int b, const double* X, double* Y) {
     return fail(ctx, RBL_ERR_STATE, "rbl_apply: b differs from the running Krylov block size");
   HIPC(hipSetDevice(ctx->device));
   const int64_t nl = std::max<int64_t>(ctx->nloc, 1);
-  double *d_x = nullptr, *d_xr = nullptr, *d_y = nullptr, *d_ext = nullptr;
-  HIPC(hipMalloc(&d_x, nl * b * sizeof(double)));
-  HIPC(hipMalloc(&d_xr, nl * b * sizeof(double)));
-  HIPC(hipMalloc(&d_y, (nl + kRowPad) * b * sizeof(double)));
-  HIPC(hipMemcpyAsync(d_x, X, ctx->nloc * b * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
-  colmajor_to_rowmajor(d_x, ctx->nloc, b, d_xr, ctx->stream);
-  const double* Qin = d_xr;
+  DevBuf x, xr, y, ext;
+  HIPC(hipMalloc(&x.p, nl * b * sizeof(double)));
+  HIPC(hipMalloc(&xr.p, nl * b * sizeof(double)));
+  HIPC(hipMalloc(&y.p, (nl + kRowPad) * b * sizeof(double)));
+  HIPC(hipMemcpyAsync(x.p, X, ctx->nloc * b * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+  colmajor_to_rowmajor(x.d(), ctx->nloc, b, xr.d(), ctx->stream);
+  const double* Qin = xr.d();
   int64_t off = 0;
   if (ctx->nranks > 1) {  // halo exchange through a private extended buffer
-    HIPC(hipMalloc(&d_ext, std::max<int64_t>(ctx->ext_hi - ctx->ext_lo, 1) * b * sizeof(double)));
+    const int64_t ext_rows = std::max<int64_t>(ctx->ext_hi - ctx->ext_lo, 1);
+    HIPC(hipMalloc(&ext.p, ext_rows * b * sizeof(double)));
     // rows between the received ranges stay finite (band-tile kernel multiplies them by 0)
-    HIPC(hipMemsetAsync(d_ext, 0, std::max<int64_t>(ctx->ext_hi - ctx->ext_lo, 1) * b * sizeof(double), ctx->stream));
+    HIPC(hipMemsetAsync(ext.p, 0, ext_rows * b * sizeof(double), ctx->stream));
     double* keep_ext = ctx->d_qext;
     const int keep_b = ctx->b;
-    ctx->d_qext = d_ext;
+    ctx->d_qext = ext.d();
     ctx->b = b;
-    const int st = halo_exchange(ctx, d_xr, &Qin, &off);
+    const int st = halo_exchange(ctx, xr.d(), &Qin, &off);
     ctx->d_qext = keep_ext;
     ctx->b = keep_b;
     if (st < 0) return st;
   }
   {
-    const int st = apply_A(ctx, Qin, off, b, d_y, nullptr, nullptr, nullptr);
+    const int st = apply_A(ctx, Qin, off, b, y.d(), nullptr, nullptr, nullptr);
     if (st < 0) return st;
   }
   HIPC(hipGetLastError());
-  rowmajor_to_colmajor(d_y, ctx->nloc, b, d_x, ctx->stream);
-  HIPC(hipMemcpyAsync(Y, d_x, ctx->nloc * b * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+  rowmajor_to_colmajor(y.d(), ctx->nloc, b, x.d(), ctx->stream);
+  HIPC(hipMemcpyAsync(Y, x.p, ctx->nloc * b * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
   HIPC(hipStreamSynchronize(ctx->stream));
-  hipFree(d_x);
-  hipFree(d_xr);
-  hipFree(d_y);
-  hipFree(d_ext);
   return RBL_OK;
 }
 
@@ -1451,27 +1577,33 @@ int rbl_start(rbl_ctx* ctx, int b, int max_blocks, int basis_bits, const double*
   if (max_blocks < 1) return fail(ctx, RBL_ERR_INVALID, "max_blocks must be >= 1");
   if (basis_bits != 64 && basis_bits != 32)
     return fail(ctx, RBL_ERR_INVALID, "basis_bits must be 64 or 32");
-  if (basis_bits == 32 && b != 16 && b != 32)
-    return fail(ctx, RBL_ERR_INVALID, "the fp32 basis needs b in {16, 32}");
   HIPC(hipSetDevice(ctx->device));
   HIPC(hipStreamSynchronize(ctx->stream));
   // a repeated run with the same shape reuses the HBM plan (allocating ~100 GB of basis
   // per run costs more than the run itself at n = 1e7)
   // device slots of the basis (RBL_OPT_DEVICE_BLOCKS; RBL_gpu.jl:95-104 gpu_buffer_size)
   int dev_slots = max_blocks + 1;
-  if (ctx->dev_blocks_opt != 0 && basis_bits == 64) {
+  if (ctx->dev_blocks_opt != 0) {
     int g = ctx->dev_blocks_opt;
     if (g < 0) {
       size_t fr = 0, tot = 0;
       HIPC(hipMemGetInfo(&fr, &tot));
-      const double blk = (double)std::max<int64_t>(ctx->nloc, 1) * b * 8.0;
-      // what the run needs beside the basis: U, T, the halo copy, staging, ~slab
-      const double other = 6.0 * blk + (double)(max_blocks + 1) * b * 2 * b * 8.0 * 64;
-      g = (int)std::max(3.0, std::floor((0.8 * (double)fr - other) / blk));
+      // the basis is typed FLOAT (RBL_gpu.jl:59-81, 95-104): slots of n_local x b x s bytes
+      const double blk64 = (double)std::max<int64_t>(ctx->nloc, 1) * b * 8.0;
+      const double blk = blk64 * (basis_bits == 64 ? 1.0 : 0.5);
+      // what the run needs beside the basis: U, T, the halo copy, staging, the fp64 working
+      // block of the fp32 path, ~slab; a run already planned frees its buffers first
+      const double mine = ctx->d_basis ? (double)(ctx->resident == INT32_MAX ? ctx->max_blocks + 1 : ctx->resident + 2) * blk64
+                        : ctx->d_basis32 ? (double)(ctx->resident == INT32_MAX ? ctx->max_blocks + 1 : ctx->resident + 2) * blk64 * 0.5
+                        : 0.0;
+      // U, T (+ the halo buffer on several ranks; + the fp32 path's fp64 Q_i, and Q_{i-1}
+      // when the SpMM cannot read fp32), one staging block, the Gram slab
+      const double work = 2.0 + (ctx->nranks > 1 ? 1.0 : 0.0) +
+                          (basis_bits == 32 ? 1.0 + (direct32_ok(ctx, b) ? 0.0 : 1.0) : 0.0);
+      const double other = work * blk64 + blk + (double)(max_blocks + 1) * b * 2 * b * 8.0 * 64;
+      g = (int)std::max(3.0, std::floor((0.8 * ((double)fr + mine) - other) / blk));
     }
     dev_slots = std::min(dev_slots, std::max(3, g));
-  } else if (ctx->dev_blocks_opt != 0) {
-    return fail(ctx, RBL_ERR_INVALID, "RBL_OPT_DEVICE_BLOCKS: fp64 basis only");
   }
   const bool reuse = (ctx->d_basis || ctx->d_basis32) && ctx->b == b &&
                      ctx->max_blocks == max_blocks && ctx->slot == ctx->nloc * b &&
@@ -1495,8 +1627,7 @@ int rbl_start(rbl_ctx* ctx, int b, int max_blocks, int basis_bits, const double*
     if (dev_slots < max_blocks + 1) {  // host spill: pinned slots for blocks resident..max_blocks
       ctx->resident = dev_slots - 2;
       // non-coherent pinned pages: the DMA engines stream them at PCIe rate both ways
-      HIPC(hipHostMalloc(&ctx->h_spill, (size_t)(max_blocks + 1 - ctx->resident) * nl * b * sizeof(double),
-                         hipHostMallocNonCoherent));
+      ctx->h_spill.assign(max_blocks + 1 - ctx->resident, nullptr);
       HIPC(hipMalloc(&ctx->d_stage, (size_t)nl * b * sizeof(double)));
       if (!ctx->cstream) {
         HIPC(hipStreamCreateWithFlags(&ctx->cstream, hipStreamNonBlocking));
@@ -1508,11 +1639,25 @@ int rbl_start(rbl_ctx* ctx, int b, int max_blocks, int basis_bits, const double*
   } else {
     // + 16 zeroed pad rows, and every slot zeroed once: the fp32 Gram kernel's shifted chunks
     // may read rows past a tiny slice (reorth32.hip), which must be finite
-    const size_t bytes32 = ((size_t)(max_blocks + 1) * nl + 16) * b * sizeof(float);
+    const size_t bytes32 = ((size_t)dev_slots * nl + 16) * b * sizeof(float);
     HIPC(hipMalloc(&ctx->d_basis32, bytes32));
     HIPC(hipMemsetAsync(ctx->d_basis32, 0, bytes32, ctx->stream));
+    if (dev_slots < max_blocks + 1) {  // host spill of the FLOAT basis (RBL_gpu.jl:59-81)
+      ctx->resident = dev_slots - 2;
+      ctx->h_spill.assign(max_blocks + 1 - ctx->resident, nullptr);
+      // + 16 zero rows like the slots (the Gram's shifted chunks)
+      HIPC(hipMalloc(&ctx->d_stage32, ((size_t)nl + 16) * b * sizeof(float)));
+      HIPC(hipMemsetAsync(ctx->d_stage32, 0, ((size_t)nl + 16) * b * sizeof(float), ctx->stream));
+      if (!ctx->cstream) {
+        HIPC(hipStreamCreateWithFlags(&ctx->cstream, hipStreamNonBlocking));
+        HIPC(hipEventCreateWithFlags(&ctx->ev_fin, hipEventDisableTiming));
+        HIPC(hipEventCreateWithFlags(&ctx->ev_d2h[0], hipEventDisableTiming));
+        HIPC(hipEventCreateWithFlags(&ctx->ev_d2h[1], hipEventDisableTiming));
+      }
+    }
     HIPC(hipMalloc(&ctx->d_Qi64, (nl + kRowPad) * b * sizeof(double)));
-    HIPC(hipMalloc(&ctx->d_Qm64, (nl + kRowPad) * b * sizeof(double)));
+    // the widened Q_{i-1}: only when the SpMM cannot read the fp32 blocks directly
+    if (!direct32_ok(ctx, b)) HIPC(hipMalloc(&ctx->d_Qm64, (nl + kRowPad) * b * sizeof(double)));
   }
   HIPC(hipMalloc(&ctx->d_U, (nl + kRowPad) * b * sizeof(double)));
   ctx->T_cols = b;
@@ -1545,7 +1690,7 @@ int rbl_start(rbl_ctx* ctx, int b, int max_blocks, int basis_bits, const double*
 
   // Omega (row-major) in d_T
   if (omega) {
-    double* d_tmp = basis_bits == 64 ? slotp(ctx, 1 <= max_blocks ? 1 : 0) : ctx->d_Qm64;
+    double* d_tmp = ctx->d_U;  // free until A * Omega
     HIPC(hipMemcpyAsync(d_tmp, omega, ctx->nloc * b * sizeof(double), hipMemcpyHostToDevice,
                         ctx->stream));
     colmajor_to_rowmajor(d_tmp, ctx->nloc, b, ctx->d_T, ctx->stream);
@@ -1625,8 +1770,6 @@ int step_impl(rbl_ctx* ctx, int i, int part_reorth, double* A_out, double* B_out
   HIPC(hipSetDevice(ctx->device));
   const int b = ctx->b;
   const bool f32 = ctx->basis_bits == 32;
-  double* Qi = f32 ? ctx->d_Qi64 : slotp(ctx, i - 1);
-  double* Qm = i >= 2 ? (f32 ? ctx->d_Qm64 : slotp(ctx, i - 2)) : nullptr;
   HIPC(hipMemsetAsync(ctx->d_flags, 0, 4 * sizeof(int), ctx->stream));
   if (f32 && (part_reorth & 2))
     return fail(ctx, RBL_ERR_INVALID, "rbl_step: locked-vector reorth needs the fp64 basis");
@@ -1634,9 +1777,10 @@ int step_impl(rbl_ctx* ctx, int i, int part_reorth, double* A_out, double* B_out
   // update read the fp32 blocks and widen them on load — bit for bit the widened copies
   // (RBL_gpu.jl:173-174), without the two conversion passes.  Step 1 multiplies the unrounded
   // fp64 Q_1 of rbl_start.
-  const bool direct32 = f32 && i >= 2 && !ctx->dense &&
-                        (ctx->spmm_variant == 0 || ctx->spmm_variant == 4) && (b == 32 || b == 16) &&
-                        (ctx->bt_ng == 5 || ctx->bt_ng == 9);
+  const bool direct32 = f32 && i >= 2 && direct32_ok(ctx, b);
+  if (f32 && !direct32) CHK(ensure_qm64(ctx));
+  double* Qi = f32 ? ctx->d_Qi64 : slotp(ctx, i - 1);
+  double* Qm = i >= 2 ? (f32 ? ctx->d_Qm64 : slotp(ctx, i - 2)) : nullptr;
   float* Qi32 = f32 ? slotp32(ctx, i - 1) : nullptr;
   float* Qm32 = f32 && i >= 2 ? slotp32(ctx, i - 2) : nullptr;
   if (f32) {
@@ -1645,15 +1789,35 @@ int step_impl(rbl_ctx* ctx, int i, int part_reorth, double* A_out, double* B_out
     if ((part_reorth & 1) && i >= 3) {
       StageScope t(ctx, RBL_STAGE_PART_REORTH);
       const int nW = i - 2;
+      const int nres = std::min(nW, ctx->resident);  // HBM-resident part of W
       if (ctx->reorth_order == 0) {
-        CHK(gram32(ctx, slotp32(ctx, 0), nW, Qi32, Qm32, 2, ctx->d_C));
-        CHK(upd32(ctx, slotp32(ctx, 0), nW, ctx->d_C, 2 * b, Qi32, Qm32, 2));
+        CHK(gram32(ctx, slotp32(ctx, 0), nres, Qi32, Qm32, 2, ctx->d_C));
+        CHK(upd32(ctx, slotp32(ctx, 0), nres, ctx->d_C, 2 * b, Qi32, Qm32, 2));
       } else {
-        for (int j = 0; j < nW; ++j) {
+        for (int j = 0; j < nres; ++j) {
           CHK(gram32(ctx, slotp32(ctx, j), 1, Qi32, Qm32, 2, ctx->d_C));
           CHK(upd32(ctx, slotp32(ctx, j), 1, ctx->d_C, 2 * b, Qi32, Qm32, 2));
         }
       }
+      // spilled fp32 blocks streamed back in ascending j (RBL_gpu.jl:65-68 with FLOAT)
+      for (int j = nres; j < nW; ++j) {
+        int st = 0;
+        const float* Wj = block_dev32(ctx, j, i, &st);
+        if (st) return fail(ctx, st, "partial reorth: H2D of a spilled block failed");
+        CHK(gram32(ctx, Wj, 1, Qi32, Qm32, 2, ctx->d_C));
+        CHK(upd32(ctx, Wj, 1, ctx->d_C, 2 * b, Qi32, Qm32, 2));
+      }
+    }
+    // host spill: block i-2 is final (RBL_gpu.jl:76) — copied out on the side stream; the
+    // QR of this step, which rewrites its working slot, waits for the copy
+    if (spilled(ctx) && i >= 2 && i - 2 >= ctx->resident) {
+      HIPC(hipEventRecord(ctx->ev_fin, ctx->stream));
+      HIPC(hipStreamWaitEvent(ctx->cstream, ctx->ev_fin, 0));
+      CHK(spill_slot(ctx, i - 2, sizeof(float)));
+      HIPC(hipMemcpyAsync(ctx->h_spill[i - 2 - ctx->resident], Qm32,
+                          ctx->slot * sizeof(float), hipMemcpyDeviceToHost, ctx->cstream));
+      HIPC(hipEventRecord(ctx->ev_d2h[i & 1], ctx->cstream));
+      ctx->d2h_pending[i & 1] = true;
     }
     if (i >= 2) {
       StageScope t(ctx, RBL_STAGE_LOC_REORTH);
@@ -1676,7 +1840,8 @@ int step_impl(rbl_ctx* ctx, int i, int part_reorth, double* A_out, double* B_out
   if (!f32 && spilled(ctx) && i >= 2 && i - 2 >= ctx->resident) {
     HIPC(hipEventRecord(ctx->ev_fin, ctx->stream));
     HIPC(hipStreamWaitEvent(ctx->cstream, ctx->ev_fin, 0));
-    HIPC(hipMemcpyAsync(ctx->h_spill + (int64_t)(i - 2 - ctx->resident) * ctx->slot, slotp(ctx, i - 2),
+    CHK(spill_slot(ctx, i - 2, sizeof(double)));
+    HIPC(hipMemcpyAsync(ctx->h_spill[i - 2 - ctx->resident], slotp(ctx, i - 2),
                         ctx->slot * sizeof(double), hipMemcpyDeviceToHost, ctx->cstream));
     HIPC(hipEventRecord(ctx->ev_d2h[i & 1], ctx->cstream));
     ctx->d2h_pending[i & 1] = true;
@@ -1740,7 +1905,7 @@ int step_impl(rbl_ctx* ctx, int i, int part_reorth, double* A_out, double* B_out
       CHK(tsmm_checked(ctx, run1(Qi, b), smallp(ctx, S_AI), b, pan1(ctx->d_U, b), -1.0, 1.0, nullptr));
   }
   // Q_{i+1} B_{i+1} = qr(U)   (RBL_gpu.jl:180-184)
-  if (!f32 && ctx->d2h_pending[i & 1]) {  // the working slot's previous block is on the host
+  if (ctx->d2h_pending[i & 1]) {  // the working slot's previous block is on the host
     HIPC(hipStreamWaitEvent(ctx->stream, ctx->ev_d2h[i & 1], 0));
     ctx->d2h_pending[i & 1] = false;
   }
@@ -1788,35 +1953,42 @@ int rbl_ritz(rbl_ctx* ctx, int nblocks, int k, const double* S, double* V_out) {
   const int b = ctx->b;
   const int64_t rows = (int64_t)nblocks * b;
   const int64_t nl = std::max<int64_t>(ctx->nloc, 1);
-  double *d_S = nullptr, *d_Scm = nullptr, *d_V = nullptr, *d_Vcm = nullptr;
-  HIPC(hipMalloc(&d_Scm, rows * k * sizeof(double)));
-  HIPC(hipMalloc(&d_S, rows * k * sizeof(double)));
-  HIPC(hipMalloc(&d_V, nl * k * sizeof(double)));
-  HIPC(hipMalloc(&d_Vcm, nl * k * sizeof(double)));
-  HIPC(hipMemcpyAsync(d_Scm, S, rows * k * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
-  colmajor_to_rowmajor(d_Scm, rows, k, d_S, ctx->stream);
-  {
-    StageScope t(ctx, RBL_STAGE_RITZ);
-    if (ctx->basis_bits == 64) {
-      CHK(combine_blocks(ctx, nblocks, k, d_S, d_V));
-    } else {  // fp32 basis: each block widened to fp64, V accumulated in fp64 (P3: fp64 Ritz)
-      for (int j = 0; j < nblocks; ++j) {
-        cvt_f32_to_f64(slotp32(ctx, j), ctx->d_Qm64, ctx->nloc * b, ctx->stream);
-        CHK(tsmm_checked(ctx, run1(ctx->d_Qm64, b), d_S + (int64_t)j * b * k, k, pan1(d_V, k), 1.0,
-                         j == 0 ? 0.0 : 1.0, nullptr));
-      }
+  // Ritz columns in chunks of <= 64 (one tsmm44 launch each), halved while a chunk's buffers
+  // (S rows, V and its column-major copy) exceed 0.7 of free HBM — RBL_gpu.jl:24-27, 110-125
+  // (`blocksize`).  Each chunk reads the basis once.
+  size_t free_b = 0, total_b = 0;
+  HIPC(hipMemGetInfo(&free_b, &total_b));
+  int kc = std::min(k, 64);
+  auto chunk_bytes = [&](int w) { return (double)((w + 1) & ~1) * (double)(rows + 2 * nl) * 8.0; };
+  while (kc > 1 && chunk_bytes(kc) > 0.7 * (double)free_b) kc = (kc + 1) / 2;
+  const int kcp = (kc + 1) & ~1;  // even panel width (16-B row stores), zero-padded column
+  if (chunk_bytes(kc) > 0.7 * (double)free_b)
+    return fail(ctx, RBL_ERR_OOM, "rbl_ritz: no room for one Ritz column");
+  DevBuf d_S, d_V, d_Vcm;
+  HIPC(hipMalloc(&d_S.p, rows * kcp * sizeof(double)));
+  HIPC(hipMalloc(&d_V.p, nl * kcp * sizeof(double)));
+  HIPC(hipMalloc(&d_Vcm.p, nl * kcp * sizeof(double)));
+  std::vector<double> srm((size_t)rows * kcp);
+  for (int c0 = 0; c0 < k; c0 += kc) {
+    const int w = std::min(kc, k - c0);
+    // S columns [c0, c0 + w) (column-major, ld = rows) -> row-major rows x kcp, zero-padded
+    for (int64_t r = 0; r < rows; ++r)
+      for (int c = 0; c < kcp; ++c) srm[(size_t)r * kcp + c] = c < w ? S[(size_t)(c0 + c) * rows + r] : 0.0;
+    HIPC(hipStreamSynchronize(ctx->stream));  // srm is reused by the next chunk
+    HIPC(hipMemcpyAsync(d_S.p, srm.data(), rows * kcp * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+    {
+      StageScope t(ctx, RBL_STAGE_RITZ);
+      if (ctx->basis_bits == 64) CHK(combine_blocks(ctx, nblocks, kcp, d_S.d(), d_V.d()));
+      else CHK(combine_blocks32(ctx, nblocks, kcp, d_S.d(), d_V.d()));
     }
+    if (ctx->nloc > 0) rowmajor_to_colmajor(d_V.d(), ctx->nloc, kcp, d_Vcm.d(), ctx->stream);
+    HIPC(hipGetLastError());
+    if (V_out && ctx->nloc > 0)
+      HIPC(hipMemcpyAsync(V_out + (size_t)c0 * ctx->nloc, d_Vcm.p, ctx->nloc * w * sizeof(double),
+                          hipMemcpyDeviceToHost, ctx->stream));
   }
-  rowmajor_to_colmajor(d_V, ctx->nloc, k, d_Vcm, ctx->stream);
-  if (V_out)
-    HIPC(hipMemcpyAsync(V_out, d_Vcm, ctx->nloc * k * sizeof(double), hipMemcpyDeviceToHost,
-                        ctx->stream));
   HIPC(hipStreamSynchronize(ctx->stream));
   harvest_timers(ctx);
-  hipFree(d_S);
-  hipFree(d_Scm);
-  hipFree(d_V);
-  hipFree(d_Vcm);
   return RBL_OK;
 }
 
@@ -1828,7 +2000,10 @@ int rbl_get_block(rbl_ctx* ctx, int j, double* Q_out) {
   const double* src = ctx->basis_bits == 64 ? block_dev(ctx, j - 1, ctx->nblocks, &st) : nullptr;
   if (st) return fail(ctx, st, "rbl_get_block: H2D of a spilled block failed");
   if (ctx->basis_bits == 32) {  // fp32 slot, returned widened
-    cvt_f32_to_f64(slotp32(ctx, j - 1), ctx->d_Qm64, ctx->nloc * b, ctx->stream);
+    CHK(ensure_qm64(ctx));
+    const float* s32 = block_dev32(ctx, j - 1, ctx->nblocks, &st);
+    if (st) return fail(ctx, st, "rbl_get_block: H2D of a spilled block failed");
+    cvt_f32_to_f64(s32, ctx->d_Qm64, ctx->nloc * b, ctx->stream);
     src = ctx->d_Qm64;
   }
   rowmajor_to_colmajor(src, ctx->nloc, b, ctx->d_T, ctx->stream);

@@ -229,7 +229,7 @@ void gram44_partial(int64_t nrows, const PanelRun& W, const Panels& X, double* s
 constexpr int kT44Rows = 32;   // rows per wave
 constexpr int kT44K = 32;      // k per chunk
 
-template <int B, int KYP>
+template <int B, int KYP, bool F32X = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k_tsmm44(int64_t nrows, PanelRun X, const double* __restrict__ C,
                                                 int ldc, int KY, Panels Y, double alpha, double beta,
                                                 const int* skip) {
@@ -287,9 +287,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
       const int k = k0 < K ? k0 : K - 2;
       const int pan = k / B;
       const int col = k - pan * B;
-      const double* xp = X.base + (int64_t)pan * X.stride + col;
+      if constexpr (F32X) {  // fp32 basis: two floats widened exactly
+        const float* xp = X.base32 + (int64_t)pan * X.stride + col;
 #pragma unroll
-      for (int rt = 0; rt < 2; ++rt) ar[rt][h] = ldw(reinterpret_cast<const d2v*>(xp + arow[rt] * B));
+        for (int rt = 0; rt < 2; ++rt) {
+          const float2 f = *reinterpret_cast<const float2*>(xp + arow[rt] * B);
+          ar[rt][h].x = (double)f.x;
+          ar[rt][h].y = (double)f.y;
+        }
+      } else {
+        const double* xp = X.base + (int64_t)pan * X.stride + col;
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt) ar[rt][h] = ldw(reinterpret_cast<const d2v*>(xp + arow[rt] * B));
+      }
     }
   };
   // C chunk: 32 x KYP, 256 threads; element e -> (k = e / KYP, c = e % KYP)
@@ -481,13 +491,26 @@ bool tsmm44_ok(int xw, int ky, int yw) {
   return (xw == 16 || xw == 32) && ky >= 1 && ky <= 64 && yw % 2 == 0;
 }
 
-template <int B, int KYP>
+template <int B, int KYP, bool F32X = false>
 static void launch_tsmm44(int64_t nrows, const PanelRun& X, const double* C, int ldc, int KY,
                           const Panels& Y, double alpha, double beta, const int* skip,
                           hipStream_t st) {
   const int64_t wgs = (nrows + 4 * kT44Rows - 1) / (4 * kT44Rows);
-  hipLaunchKernelGGL((k_tsmm44<B, KYP>), dim3((unsigned)wgs), dim3(256), 0, st, nrows, X, C, ldc,
-                     KY, Y, alpha, beta, skip);
+  hipLaunchKernelGGL((k_tsmm44<B, KYP, F32X>), dim3((unsigned)wgs), dim3(256), 0, st, nrows, X, C,
+                     ldc, KY, Y, alpha, beta, skip);
+}
+
+void tsmm44_f32x(int64_t nrows, const PanelRun& X, const double* C, int ldc, const Panels& Y,
+                 double alpha, double beta, hipStream_t st) {
+  const int KY = Y.count * Y.w;
+  if (X.w == 32) {
+    if (KY <= 16) return launch_tsmm44<32, 16, true>(nrows, X, C, ldc, KY, Y, alpha, beta, nullptr, st);
+    if (KY <= 32) return launch_tsmm44<32, 32, true>(nrows, X, C, ldc, KY, Y, alpha, beta, nullptr, st);
+    return launch_tsmm44<32, 64, true>(nrows, X, C, ldc, KY, Y, alpha, beta, nullptr, st);
+  }
+  if (KY <= 16) return launch_tsmm44<16, 16, true>(nrows, X, C, ldc, KY, Y, alpha, beta, nullptr, st);
+  if (KY <= 32) return launch_tsmm44<16, 32, true>(nrows, X, C, ldc, KY, Y, alpha, beta, nullptr, st);
+  return launch_tsmm44<16, 64, true>(nrows, X, C, ldc, KY, Y, alpha, beta, nullptr, st);
 }
 
 void tsmm44(int64_t nrows, const PanelRun& X, const double* C, int ldc, const Panels& Y,

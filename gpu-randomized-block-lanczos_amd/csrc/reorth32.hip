@@ -150,8 +150,56 @@ static void launch_gram32(int64_t nrows, const float* Wb, int64_t wstride, int n
                      nW, X0, X1, slab, npg, rows_per);
 }
 
+// ----------------------------------------------------------------------------------------
+// Any panel width (mixed precision at b not in {16, 32}: C1's b = 8, the reference tests'
+// b = 5): one thread per Gram entry and split, fp32 products accumulated in fp32 over the
+// split's rows (sgemm's arithmetic), splits summed in fp64 by reduce_slab.
+// ----------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_gram32_any(int64_t nrows, const float* __restrict__ Wb,
+                                                    int64_t wstride, int nW, int w,
+                                                    const float* __restrict__ X0,
+                                                    const float* __restrict__ X1, int xcount,
+                                                    double* __restrict__ slab, int64_t rows_per) {
+  const int KW = nW * w, KC = xcount * w;
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t s = blockIdx.y;
+  if (e >= (int64_t)KW * KC) return;
+  const int a = (int)(e / KC), c = (int)(e % KC);
+  const float* wp = Wb + (int64_t)(a / w) * wstride + (a % w);
+  const float* xp = (c < w ? X0 : X1) + (c % w);
+  const int64_t r0 = s * rows_per, r1 = r0 + rows_per < nrows ? r0 + rows_per : nrows;
+  float acc = 0.f;
+  for (int64_t r = r0; r < r1; ++r) acc = fmaf(wp[r * w], xp[r * w], acc);
+  slab[s * KW * KC + e] = (double)acc;
+}
+
+// Y = beta Y + alpha X C at any width: one thread per element of Y (Y must not alias X)
+__global__ __launch_bounds__(256) void k_tsmm32_any(int64_t nrows, const float* __restrict__ Xb,
+                                                    int64_t xstride, int nX, int w,
+                                                    const double* __restrict__ C, int ldc,
+                                                    float* Y0, float* Y1, int ycount, float alpha,
+                                                    float beta) {
+  const int KY = ycount * w, K = nX * w;
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= nrows * KY) return;
+  const int64_t r = e / KY;
+  const int c = (int)(e % KY);
+  float acc = 0.f;
+  for (int k = 0; k < K; ++k)
+    acc = fmaf(Xb[(int64_t)(k / w) * xstride + r * w + (k % w)], (float)C[(int64_t)k * ldc + c], acc);
+  float* y = (c < w ? Y0 : Y1) + r * w + (c % w);
+  *y = beta != 0.f ? beta * *y + alpha * acc : alpha * acc;
+}
+
 void gram32_partial(int64_t nrows, const float* Wb, int64_t wstride, int nW, int w, const float* X0,
                     const float* X1, int xcount, double* slab, int splits, hipStream_t st) {
+  if (w != 16 && w != 32) {
+    const int64_t len = (int64_t)nW * w * xcount * w;
+    const int64_t rows_per = (nrows + splits - 1) / splits;
+    hipLaunchKernelGGL(k_gram32_any, dim3((unsigned)((len + 255) / 256), (unsigned)splits), dim3(256), 0,
+                       st, nrows, Wb, wstride, nW, w, X0, X1, xcount, slab, rows_per);
+    return;
+  }
   if (w == 32) {
     if (xcount == 2) return launch_gram32<32, 2>(nrows, Wb, wstride, nW, X0, X1, slab, splits, st);
     return launch_gram32<32, 1>(nrows, Wb, wstride, nW, X0, X1, slab, splits, st);
@@ -386,6 +434,12 @@ void tsmm32(int64_t nrows, const float* Xb, int64_t xstride, int nX, int w, cons
             float* Y0, float* Y1, int ycount, float alpha, float beta, hipStream_t st) {
   if (nrows <= 0) return;
   const int KY = ycount * w;
+  if (w != 16 && w != 32) {
+    const int64_t thr = nrows * KY;
+    hipLaunchKernelGGL(k_tsmm32_any, dim3((unsigned)((thr + 255) / 256)), dim3(256), 0, st, nrows, Xb,
+                       xstride, nX, w, C, ldc, Y0, Y1, ycount, alpha, beta);
+    return;
+  }
   if (w == 32 && KY == 64 && nrows >= kT32Rows) {
     const int64_t wgs = (nrows + 4 * kT32Rows - 1) / (4 * kT32Rows);
     hipLaunchKernelGGL(k_tsmm32f, dim3((unsigned)wgs), dim3(256), 0, st, nrows, Xb, xstride, nX, C,
@@ -401,6 +455,18 @@ void tsmm32(int64_t nrows, const float* Xb, int64_t xstride, int nX, int w, cons
 }
 
 // ---- conversions -------------------------------------------------------------------------
+// element-wise conversions for blocks whose slot offset is not 16-B aligned (b odd)
+__global__ void k_f32_to_f64_s(const float* __restrict__ src, double* __restrict__ dst, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) dst[i] = src[i];
+}
+__global__ void k_f64_to_f32_s(const double* __restrict__ src, float* __restrict__ dst, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) dst[i] = (float)src[i];
+}
+static bool aligned16(const void* a, const void* b) {
+  return (((uintptr_t)a | (uintptr_t)b) & 15) == 0;
+}
 __global__ void k_f32_to_f64(const float* __restrict__ src, double* __restrict__ dst, int64_t n) {
   const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
   if (i + 3 < n) {
@@ -422,11 +488,19 @@ __global__ void k_f64_to_f32(const double* __restrict__ src, float* __restrict__
 }
 void cvt_f32_to_f64(const float* src, double* dst, int64_t n, hipStream_t s) {
   if (n <= 0) return;
+  if (!aligned16(src, dst)) {
+    hipLaunchKernelGGL(k_f32_to_f64_s, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, src, dst, n);
+    return;
+  }
   const int64_t thr = (n + 3) / 4;
   hipLaunchKernelGGL(k_f32_to_f64, dim3((unsigned)((thr + 255) / 256)), dim3(256), 0, s, src, dst, n);
 }
 void cvt_f64_to_f32(const double* src, float* dst, int64_t n, hipStream_t s) {
   if (n <= 0) return;
+  if (!aligned16(src, dst)) {
+    hipLaunchKernelGGL(k_f64_to_f32_s, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, src, dst, n);
+    return;
+  }
   const int64_t thr = (n + 3) / 4;
   hipLaunchKernelGGL(k_f64_to_f32, dim3((unsigned)((thr + 255) / 256)), dim3(256), 0, s, src, dst, n);
 }

@@ -504,18 +504,12 @@ __global__ __launch_bounds__(band::kThreads) void k_spmm_band(BandArgs a) {
 
 template <int B, bool EPI, bool AIG, bool PAIR>
 static void launch_band_t(const BandArgs& a0, int grid, hipStream_t s) {
-  static bool attr = false;
   static const bool prof = [] {
     const char* e = getenv("RBL_SPMM_PROF");
     return e && atoi(e) != 0;
   }();
-  if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_spmm_band<B, EPI, false, AIG, PAIR>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, BandLayout<B>::kLds);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_spmm_band<B, EPI, true, AIG, PAIR>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, BandLayout<B>::kLds);
-    attr = true;
-  }
+  ensure_lds_attr(reinterpret_cast<const void*>(&k_spmm_band<B, EPI, false, AIG, PAIR>), BandLayout<B>::kLds);
+  ensure_lds_attr(reinterpret_cast<const void*>(&k_spmm_band<B, EPI, true, AIG, PAIR>), BandLayout<B>::kLds);
   if (!prof) {
     hipLaunchKernelGGL((k_spmm_band<B, EPI, false, AIG, PAIR>), dim3(grid), dim3(band::kThreads),
                        BandLayout<B>::kLds, s, a0);

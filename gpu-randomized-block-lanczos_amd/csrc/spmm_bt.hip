@@ -423,12 +423,7 @@ void k_spmm_bt(BtArgs a) {
 
 template <int B, int NG, bool EPI, bool AIG, int VAR>
 static void launch_bt_v(const BtArgs& a, int grid, hipStream_t s) {
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_spmm_bt<B, NG, EPI, AIG, VAR>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, bt::Geo<B>::kLds);
-    attr = true;
-  }
+  ensure_lds_attr(reinterpret_cast<const void*>(&k_spmm_bt<B, NG, EPI, AIG, VAR>), bt::Geo<B>::kLds);
   hipLaunchKernelGGL((k_spmm_bt<B, NG, EPI, AIG, VAR>), dim3(grid), dim3(bt::kThreads),
                      bt::Geo<B>::kLds, s, a);
 }

@@ -26,6 +26,11 @@
 #include <type_traits>
 #include <utility>
 
+#include <atomic>
+#include <mutex>
+#include <set>
+#include <utility>
+
 #include "kernels.hpp"
 
 namespace rbl {
@@ -350,27 +355,34 @@ __global__ __launch_bounds__(win::kThreads) void k_spmm_window(WinArgs a) {
   }
 }
 
-static int g_num_cus = 0;
-
 int window_grid() {
-  if (g_num_cus == 0) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
+  static std::atomic<int> num_cus[64];  // per device; zero-initialised (static storage)
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (dev < 0 || dev >= 64) dev = 0;
+  int n = num_cus[dev].load(std::memory_order_relaxed);
+  if (n == 0) {
     hipDeviceProp_t p;
-    if (hipGetDeviceProperties(&p, dev) == hipSuccess) g_num_cus = p.multiProcessorCount;
-    if (g_num_cus <= 0) g_num_cus = 256;
+    if (hipGetDeviceProperties(&p, dev) == hipSuccess) n = p.multiProcessorCount;
+    if (n <= 0) n = 256;
+    num_cus[dev].store(n, std::memory_order_relaxed);
   }
-  return g_num_cus;
+  return n;
+}
+
+void ensure_lds_attr(const void* kernel, int bytes) {
+  static std::mutex mu;
+  static std::set<std::pair<int, const void*>> done;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  std::lock_guard<std::mutex> lk(mu);
+  if (done.insert({dev, kernel}).second)
+    (void)hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
 }
 
 template <int VEC, bool EPI>
 static void launch_window_t(const WinArgs& a, int grid, hipStream_t s) {
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&k_spmm_window<VEC, EPI>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)win::kLds);
-    attr = true;
-  }
+  ensure_lds_attr(reinterpret_cast<const void*>(&k_spmm_window<VEC, EPI>), (int)win::kLds);
   hipLaunchKernelGGL((k_spmm_window<VEC, EPI>), dim3(grid), dim3(win::kThreads), win::kLds, s, a);
 }
 

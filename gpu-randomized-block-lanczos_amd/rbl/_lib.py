@@ -29,6 +29,7 @@ RBL_OPT_REORTH_ORDER = 1
 RBL_OPT_SPMM_KERNEL = 2
 RBL_OPT_DEVICE_BLOCKS = 3
 RBL_OPT_SPLIT_HALO = 4
+RBL_OPT_KEEP_CSR = 5
 
 _p = C.c_void_p
 _i64 = C.c_int64
@@ -49,6 +50,7 @@ SIGNATURES = {
     "rbl_create_local": (C.c_int, [C.POINTER(_p), C.c_int, _p, C.c_int]),
     "rbl_free": (C.c_int, [_p]),
     "rbl_last_error": (C.c_char_p, [_p]),
+    "rbl_comm_info": (C.c_int, [_p, C.POINTER(C.c_int), C.POINTER(C.c_int), C.c_char_p, C.c_int]),
     "rbl_set_option": (C.c_int, [_p, C.c_int, _i64]),
     "rbl_set_matrix_csc": (C.c_int, [_p, _i64, _i64, _pi64, _pi64, _pd, C.c_int]),
     "rbl_set_matrix_csr_rows": (C.c_int, [_p, _i64, _i64, _i64, _pi64, _pi64, _pd, C.c_int]),

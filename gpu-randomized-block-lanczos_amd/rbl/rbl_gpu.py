@@ -263,6 +263,14 @@ class Context:
     def reset_timers(self) -> None:
         self._check(lib.rbl_reset_timers(self._h), "rbl_reset_timers")
 
+    def comm_info(self) -> dict:
+        """Ranks as the transport counts them (RCCL: ncclCommCount), this rank, transport name."""
+        import ctypes as C
+        n, r = C.c_int(0), C.c_int(0)
+        buf = C.create_string_buffer(32)
+        self._check(lib.rbl_comm_info(self._h, C.byref(n), C.byref(r), buf, 32), "rbl_comm_info")
+        return {"nranks": n.value, "rank": r.value, "transport": buf.value.decode()}
+
     def synchronize(self) -> None:
         self._check(lib.rbl_synchronize(self._h), "rbl_synchronize")
 

@@ -58,7 +58,8 @@ extern "C" {
                                    * G >= 3 = G slots: blocks 0..G-3 resident, the two newest
                                    * in two working slots, every older block in pinned host
                                    * memory, streamed back over PCIe for partial reorth and
-                                   * Ritz.  fp64 basis only; set before rbl_start.              */
+                                   * Ritz.  fp64 or fp32 basis (the reference's buffer is typed
+                                   * FLOAT, RBL_gpu.jl:59-81); set before rbl_start.            */
 #define RBL_OPT_SPMM_KERNEL   2   /* 0: auto; 1: global-gather CSR; 2: LDS-window CSR (DPP);
                                    * 3: LDS-densified band on fp64 MFMA; 4: band-tile format
                                    * (CSR densified once into MFMA operand order, b = 32,
@@ -69,6 +70,12 @@ extern "C" {
                                    * the own rows from the block and the halo buffer holds only
                                    * the neighbours' rows; 0 the own block is copied into the
                                    * halo buffer every step (same results, bit for bit)         */
+#define RBL_OPT_KEEP_CSR      5   /* 1 (default): the device CSR stays beside any SpMM format
+                                   * built from it; 0: once the band tiles are built the CSR
+                                   * (values, column ids, band positions, gather tables) is
+                                   * released — 12 B per nonzero of HBM for the Krylov basis
+                                   * (n = 5e7: 60 GB).  Then only b in {16, 32} can run and
+                                   * rbl_get_matrix_csr fails.  Set before the matrix.          */
 
 typedef struct rbl_ctx rbl_ctx;
 
@@ -97,6 +104,9 @@ int rbl_local_group_free(rbl_group* group);
 int rbl_create_local(rbl_ctx** ctx, int device, rbl_group* group, int rank);
 int rbl_free(rbl_ctx* ctx);
 const char* rbl_last_error(const rbl_ctx* ctx);
+/* Ranks as the transport itself counts them (RCCL: ncclCommCount; in-process group: its size;
+ * one rank: 1, transport "none"), this context's rank, and the transport's name. */
+int rbl_comm_info(rbl_ctx* ctx, int* nranks, int* rank, char* transport, int transport_len);
 int rbl_set_option(rbl_ctx* ctx, int option, int64_t value);
 
 /* ---- matrix --------------------------------------------------------------------------

@@ -117,3 +117,45 @@ def rmat_csr(n: int, scale: int, edges: int, seed: int, plant=None, row_begin=0,
 def planted_spectrum(k: int, scale: float = 100.0):
     """Planted diagonal of SURVEY §8(d) C1: 2k entries at scale*(2k+1-l), l = 1..2k."""
     return np.array([scale * (2 * k + 1 - l) for l in range(1, 2 * k + 1)], dtype=np.float64)
+
+
+_CIRC_K = np.uint64(0x9FB21C651E98DF25)
+G3_CIRCUIT_N = 1_585_478          # SuiteSparse G3_circuit (BASELINE config 3): n
+G3_CIRCUIT_NNZ = 7_660_826        #   and stored nonzeros, both triangles (4.83 per row)
+
+
+def circuit_like_csr(n: int = G3_CIRCUIT_N, seed: int = 20261015, plant=None, width: int = 1259,
+                     p_edge: float = 0.95873):
+    """A circuit-like SPD matrix of G3_circuit's shape (BASELINE config 3; the real .mtx is not
+    in this image and is not fetched): a weighted graph Laplacian on a 5-point stencil over
+    rows of `width` nodes (nodes i, i+1 in one row; i, i+width), each edge kept iff
+    u53(h(seed, lo, hi)) < p_edge (so ~4.83 nonzeros per row at the defaults, like
+    G3_circuit's 7.66 M over 1.59 M rows), weight 0.5 + u53(mix64(h ^ K)); diagonal = the row's
+    weight sum + 0.01 (+ plant[l] at node l * floor(n / len(plant))).  Then a seeded symmetric
+    permutation scatters the pattern over the whole index range, as circuit matrices are: no
+    band, so the gather SpMM runs, not the band tiles.  Returns SciPy CSR (n x n)."""
+    i = np.arange(n, dtype=np.int64)
+    lo_h = i[(i % width) != width - 1]
+    lo_h = lo_h[lo_h + 1 < n]
+    lo_v = i[i + width < n]
+    lo = np.concatenate([lo_h, lo_v])
+    hi = np.concatenate([lo_h + 1, lo_v + width])
+    h = pair_hash(seed, lo, hi)
+    keep = u53(h) < p_edge
+    lo, hi, h = lo[keep], hi[keep], h[keep]
+    w = 0.5 + u53(mix64(h ^ _CIRC_K))
+    diag = np.full(n, 0.01)
+    np.add.at(diag, lo, w)
+    np.add.at(diag, hi, w)
+    if plant is not None and len(plant):
+        plant = np.asarray(plant, dtype=np.float64)
+        stride = n // len(plant)
+        diag[np.arange(len(plant)) * stride] += plant
+    # seeded symmetric permutation (node i -> perm[i])
+    perm = np.random.default_rng(seed).permutation(n).astype(np.int64)
+    R = np.concatenate([perm[lo], perm[hi], perm])
+    C = np.concatenate([perm[hi], perm[lo], perm])
+    V = np.concatenate([-w, -w, diag])
+    A = sp.csr_matrix((V, (R, C)), shape=(n, n))
+    A.sort_indices()
+    return A

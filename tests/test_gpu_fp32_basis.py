@@ -108,12 +108,42 @@ def test_fp32_basis_multirank_matches_single(rbl, b):
     assert np.all(1 - np.abs(np.sum(V * V1, axis=0)) < 1e-6)
 
 
-def test_fp32_basis_rejects_other_b(rbl):
-    A = c1_matrix(2000, 4)
+@pytest.mark.parametrize("b", [5, 8])
+def test_fp32_basis_any_b(rbl, b):
+    """FLOAT = Float32 at any block size (RBL_gpu.jl:205 takes any b): widths other than 16 / 32
+    run the generic fp32 Gram / update kernels (fp32 products, fp32 accumulation per split) and
+    the fp64 SpMM / QR on widened blocks."""
+    k = 6
+    A = c1_matrix(4000, k)
+    n = A.shape[0]
+    omega = np.random.default_rng(b).standard_normal((n, b))
+    ref = o.RBL_gpu_mixed(A, k, b, omega=omega, reorth_mode="cgs")
+    ref64 = o.RBL_gpu_semantics(A, k, b, omega=omega, qr_mode="posdiag", reorth_mode="cgs")
+    D, V, info = rbl.RBL_gpu(A, k, b, omega=omega, return_info=True, basis_bits=32)
+    assert ref.converged and info.converged
+    assert np.all(np.abs(D - ref.D) <= EIG_TOL_MIXED * np.abs(ref.D)), np.abs(D - ref.D) / np.abs(ref.D)
+    assert np.all(np.abs(D - ref64.D) <= EIG_TOL_F64 * np.abs(ref64.D))
+    res = np.linalg.norm(A @ V - V * D[None, :], axis=0) / np.abs(D)
+    assert res.max() < RES_TOL, res
+
+
+@pytest.mark.parametrize("b,k", [(32, 20), (16, 7), (8, 5)])
+def test_fp32_basis_ritz_one_pass(rbl, b, k):
+    """rbl_ritz over the fp32 basis (one fp32-input tsmm44 launch at b in {16, 32}, widened
+    per block otherwise) equals [Q_1..Q_m] S formed on the host from the widened blocks."""
+    A = c1_matrix(3000, 10)
+    n = A.shape[0]
+    omega = np.random.default_rng(2).standard_normal((n, b))
+    steps = 6
     with rbl.Context(0) as ctx:
         ctx.set_matrix(A)
-        with pytest.raises(rbl.RBLError):
-            ctx.start(8, 4, seed=1, basis_bits=32)
+        rbl.lanczos(ctx, k, b, omega=omega, check=False, max_steps=steps, ritz=False,
+                    basis_bits=32)
+        Q = np.hstack([ctx.get_block(j) for j in range(1, steps + 1)])
+        S = np.asfortranarray(np.random.default_rng(9).standard_normal((steps * b, k)))
+        V = ctx.ritz(steps, k, S)
+    ref = Q @ S
+    assert np.abs(V - ref).max() <= 1e-13 * np.abs(Q).max() * np.abs(S).sum(axis=0).max()
 
 
 def test_fp32_basis_tiny_slices(rbl):

@@ -79,10 +79,53 @@ def test_spill_auto_and_guards(rbl, problem):
         with pytest.raises(rbl.RBLError):
             ctx.set_option(rbl._lib.RBL_OPT_DEVICE_BLOCKS, 2)
         ctx.set_option(rbl._lib.RBL_OPT_DEVICE_BLOCKS, 3)
-        with pytest.raises(rbl.RBLError):
-            ctx.start(B, 10, omega=omega, basis_bits=32)   # fp64 basis only
         ctx.start(B, 10, omega=omega)
         for i in range(1, 6):
             ctx.step(i, i % 2 == 0)
         with pytest.raises(rbl.RBLError):
             ctx.restart(5, np.eye(5 * B)[:, :B].copy(order="F"))
+
+
+# ---- the fp32 basis spilled (the reference's hybrid buffer is typed FLOAT: RBL_gpu.jl:59-81,
+# 95-104 with FLOAT = Float32) ----------------------------------------------------------------
+def _run32(rbl, A, omega, device_blocks, order=0, steps=None, check=True, k=K):
+    b = omega.shape[1]
+    with rbl.Context(0) as ctx:
+        ctx.set_matrix(A)
+        ctx.set_option(rbl._lib.RBL_OPT_REORTH_ORDER, order)
+        ctx.set_option(rbl._lib.RBL_OPT_DEVICE_BLOCKS, device_blocks)
+        D, V, info = rbl.lanczos(ctx, k, b, omega=omega, check=check, max_steps=steps,
+                                 trace=True, basis_bits=32)
+        blocks = [ctx.get_block(j) for j in range(1, ctx.num_blocks() + 1)]
+    return D, V, info, blocks
+
+
+@pytest.mark.parametrize("G,b", [(3, 16), (6, 32)])
+def test_spill_fp32_mgs_order_bit_identical(rbl, G, b):
+    """Block-MGS order: the resident run applies each block's Gram + update one at a time, the
+    spilled run the same kernels on the block staged back from pinned memory: same bits."""
+    A = matgen.hashwindow_csr(6000, 64, 0.7734, 21, matgen.planted_spectrum(K))
+    omega = np.random.default_rng(5).standard_normal((A.shape[0], b))
+    _, _, i1, b1 = _run32(rbl, A, omega, 0, order=1, steps=14, check=False)
+    _, _, i2, b2 = _run32(rbl, A, omega, G, order=1, steps=14, check=False)
+    for a1, a2 in zip(i1.trace_A + i1.trace_B, i2.trace_A + i2.trace_B):
+        assert np.array_equal(a1, a2)
+    for q1, q2 in zip(b1, b2):          # spilled blocks read back from the host
+        assert np.array_equal(q1, q2)
+        assert np.array_equal(q2, q2.astype(np.float32).astype(np.float64))
+
+
+@pytest.mark.parametrize("G", [3, 5])
+def test_spill_fp32_cgs_full_run(rbl, problem, G):
+    """Default block CGS: resident part batched, spilled part block by block; eigenvalues vs
+    the resident fp32 run and the mixed-mode oracle within the fp32-basis tolerance (1e-7)."""
+    A, omega = problem
+    D1, V1, i1, _ = _run32(rbl, A, omega, 0)
+    D2, V2, i2, _ = _run32(rbl, A, omega, G)
+    assert i1.converged and i2.converged and i2.iters == i1.iters
+    assert np.max(np.abs(D2 - D1) / np.abs(D1)) < 1e-7
+    ref = o.RBL_gpu_mixed(A, K, B, omega=omega, reorth_mode="cgs")
+    assert np.max(np.abs(D2 - ref.D) / np.abs(ref.D)) < 1e-7
+    res = np.linalg.norm(A @ V2 - V2 * D2, axis=0) / np.abs(D2)
+    assert res.max() < 1e-5
+    assert np.all(1 - np.abs(np.sum(V1 * V2, axis=0)) < 1e-6)
