@@ -1,0 +1,78 @@
+#!/usr/bin/env python3
+"""Full-size eigenvalue fixtures for BASELINE configs 2 and 3 (committed; regenerate from the
+repo root with ``python tests/golden/make_fullsize.py [c2|c3]``; ~2-10 min each on 8 cores).
+
+The expected outputs come from the oracle (oracle/rbl_oracle.py: the CPU restatement of
+RBL.jl:74-142 with the GPU driver's bounds, RBL_gpu.jl:134-219, and the HIP path's choices —
+positive-diagonal QR, block-CGS partial reorth), run here on the configs' own sizes.
+Fixtures are data only: the generator parameters, Omega's seed, and the outputs.
+
+  golden_c2.npz  C2: n = 1e6 hash-window (half-width 32, density 0.7734: ~50 nnz/row),
+                 planted top spectrum, b = 16, k = 20.
+  golden_c3.npz  C3-shaped: matgen.circuit_like_csr — n = 1,585,478 and 7.66 M nonzeros like
+                 SuiteSparse G3_circuit (BASELINE config 3; the real file is not in this image
+                 and is not fetched), SPD weighted Laplacian, scattered by a symmetric
+                 permutation (no band), planted top spectrum; b = 16, k = 20.
+
+Each holds D (k, descending |lambda|), the iteration count, and per Ritz vector its 16
+largest-magnitude entries (row ids + values) — enough to compare vectors up to sign without
+storing n x k numbers — and the residual norms ||A v - lambda v|| / |lambda|.
+"""
+import os
+import sys
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+
+from oracle import matgen  # noqa: E402
+from oracle import rbl_oracle as o  # noqa: E402
+
+C2 = dict(n=1_000_000, halfwidth=32, density=0.7734, seed=20261015, b=16, k=20, omega_seed=2)
+C3 = dict(n=matgen.G3_CIRCUIT_N, seed=20261015, b=16, k=20, omega_seed=3)
+TOP = 16
+
+
+def c2_matrix():
+    return matgen.hashwindow_csr(C2["n"], C2["halfwidth"], C2["density"], C2["seed"],
+                                 matgen.planted_spectrum(C2["k"]))
+
+
+def c3_matrix():
+    return matgen.circuit_like_csr(C3["n"], C3["seed"], matgen.planted_spectrum(C3["k"]))
+
+
+def omega_for(cfg):
+    return np.random.default_rng(cfg["omega_seed"]).standard_normal((cfg["n"], cfg["b"]))
+
+
+def run(name, cfg, A):
+    t0 = time.perf_counter()
+    res = o.RBL_gpu_semantics(A, cfg["k"], cfg["b"], omega=omega_for(cfg), qr_mode="posdiag",
+                              reorth_mode="cgs")
+    dt = time.perf_counter() - t0
+    assert res.converged, name
+    V = res.V
+    idx = np.argsort(-np.abs(V), axis=0)[:TOP]            # TOP x k row ids
+    vals = np.take_along_axis(V, idx, axis=0)
+    r = np.linalg.norm(A @ V - V * res.D, axis=0) / np.abs(res.D)
+    out = os.path.join(HERE, f"golden_{name}.npz")
+    np.savez_compressed(out, D=res.D, iters=res.iters, top_idx=idx.astype(np.int64), top_val=vals,
+                        residual=r, nnz=A.nnz, oracle_seconds=dt,
+                        **{f"cfg_{key}": v for key, v in cfg.items()})
+    print(f"{name}: n={A.shape[0]} nnz={A.nnz} iters={res.iters} D[:3]={res.D[:3]} "
+          f"max residual={r.max():.2e} ({dt:.1f} s) -> {out}", flush=True)
+
+
+def main(which):
+    if "c2" in which:
+        run("c2", C2, c2_matrix())
+    if "c3" in which:
+        run("c3", C3, c3_matrix())
+
+
+if __name__ == "__main__":
+    main(sys.argv[1:] or ["c2", "c3"])

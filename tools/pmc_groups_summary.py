@@ -16,8 +16,12 @@ for f in glob.glob(os.path.join(d, "g*", "p_counter_collection.csv")):
             agg[k][r["Counter_Name"]] += float(r["Counter_Value"])
 for k, a in agg.items():
     wc = a["SQ_WAVE_CYCLES"] or 1
-    gui = a["GRBM_GUI_ACTIVE"] or 1
+    # GRBM_GUI_ACTIVE is summed over the 8 XCDs (MI355X_MICROARCH.md 'DVFS give-back'):
+    # per-XCD active cycles = sum / 8; 256 CUs / 1024 SIMDs on the chip
+    gui = (a["GRBM_GUI_ACTIVE"] or 8) / 8.0
     print(f"== {k}")
+    nonmfma = a["SQ_INSTS_VALU"] - a["SQ_INSTS_MFMA"]
+    print("  non-MFMA VALU instructions per MFMA %.3f" % (nonmfma / (a["SQ_INSTS_MFMA"] or 1)))
     print("  per-CU-cycle: LDS busy %.3f  bank-conflict %.3f  MFMA busy/SIMD %.3f  CU busy %.3f" % (
         a["SQ_LDS_IDX_ACTIVE"] / (gui * 256), a["SQ_LDS_BANK_CONFLICT"] / (gui * 256),
         a["SQ_VALU_MFMA_BUSY_CYCLES"] / (gui * 1024), a["SQ_BUSY_CU_CYCLES"] / (gui * 256)))
