@@ -110,22 +110,19 @@ __device__ __forceinline__ void gram44_body(int64_t r_begin, int64_t r_end, int6
 
   const int64_t nchunks = r_end > r_begin ? (r_end - r_begin + kG44Rows - 1) / kG44Rows : 0;
   double xr[EPT];
-  double a0[KS][AG], a1[KS][AG];
+  double acur[KS][AG], anext[KS][AG];
   if (nchunks > 0) {
     load_x(r_begin, xr);
     store_x(0, r_begin, xr);
-    load_a(r_begin, a0);
+    load_a(r_begin, acur);
   }
   __syncthreads();
-  // one chunk: prefetch chunk c + 1 into `nxt` while `cur` (chunk c) feeds the MFMAs; the
-  // loop body runs two chunks with the operand sets swapped (ping-pong), so no register copies
-  // (v_mov) sit between the MFMAs — fp64 MFMA and VALU do not co-issue on gfx950
-  auto chunk = [&](int64_t c, double (&cur)[KS][AG], double (&nxt)[KS][AG]) {
+  for (int64_t c = 0; c < nchunks; ++c) {
     const int64_t rc0 = r_begin + c * kG44Rows;
     // unconditional (clamped on the last chunk): a uniform branch here would make the
     // waitcnt pass merge a no-load path and drain the prefetch before the MFMAs
     load_x(rc0 + kG44Rows, xr);
-    load_a(rc0 + kG44Rows, nxt);
+    load_a(rc0 + kG44Rows, anext);
     const double* xb = xs[c & 1] + 8 * cp0;
     if (active) {  // idle waves (a 3-panel group) only help stage X
 #pragma unroll
@@ -135,8 +132,8 @@ __device__ __forceinline__ void gram44_body(int64_t r_begin, int64_t r_end, int6
           const d2v bf = *reinterpret_cast<const d2v*>(xb + (4 * ks + q) * LD + 8 * cp + 2 * (lane & 3));
 #pragma unroll
           for (int ag = 0; ag < AG; ++ag) {
-            acc[ag][2 * cp] = mfma4(cur[ks][ag], bf.x, acc[ag][2 * cp]);
-            acc[ag][2 * cp + 1] = mfma4(cur[ks][ag], bf.y, acc[ag][2 * cp + 1]);
+            acc[ag][2 * cp] = mfma4(acur[ks][ag], bf.x, acc[ag][2 * cp]);
+            acc[ag][2 * cp + 1] = mfma4(acur[ks][ag], bf.y, acc[ag][2 * cp + 1]);
           }
         }
       }
@@ -144,14 +141,12 @@ __device__ __forceinline__ void gram44_body(int64_t r_begin, int64_t r_end, int6
     // unconditional as well: a consumer under `if (more)` lets LLVM sink the loads into it
     // (after the MFMAs); on the last chunk this writes the dead spare buffer
     store_x((int)((c + 1) & 1), rc0 + kG44Rows, xr);
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int ag = 0; ag < AG; ++ag) acur[ks][ag] = anext[ks][ag];
     __syncthreads();
-  };
-  int64_t c = 0;
-  for (; c + 1 < nchunks; c += 2) {
-    chunk(c, a0, a1);
-    chunk(c + 1, a1, a0);
   }
-  if (c < nchunks) chunk(c, a0, a1);
   if (!active) return;
   const int KW = W.count * B;
   double* out = slab + (s * KW + (int64_t)j * B) * KC + 4 * (2 * cp0);
@@ -435,16 +430,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
     for (int v = 0; v < CEPT; ++v) cs[buf][cso + 4 * v * LDC] = cr[v];
   };
 
-  d2v a0[2][4], a1[2][4];
+  d2v acur[2][4], anext[2][4];
   double cr[CEPT];
   load_c(0, cr);
   store_c(0, cr);
-  load_a(0, a0);
+  load_a(0, acur);
   __syncthreads();
-  // ping-pong over chunk pairs (no operand copies between the MFMAs, see k_gram44)
-  auto chunk = [&](int ch, d2v (&cur)[2][4], d2v (&nxt)[2][4]) {
+  for (int ch = 0; ch < nch; ++ch) {
     load_c(ch + 1, cr);
-    load_a(ch + 1, nxt);
+    load_a(ch + 1, anext);
     const double* cb = cs[ch & 1] + 2 * q * LDC + 2 * (lane & 3);
 #pragma unroll
     for (int hv = 0; hv < 8; ++hv) {
@@ -455,20 +449,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
         const d2v bf = *reinterpret_cast<const d2v*>(cr0 + 8 * cp);
 #pragma unroll
         for (int rt = 0; rt < 2; ++rt) {
-          acc[rt][2 * cp] = mfma4(cur[rt][h][v], bf.x, acc[rt][2 * cp]);
-          acc[rt][2 * cp + 1] = mfma4(cur[rt][h][v], bf.y, acc[rt][2 * cp + 1]);
+          acc[rt][2 * cp] = mfma4(acur[rt][h][v], bf.x, acc[rt][2 * cp]);
+          acc[rt][2 * cp + 1] = mfma4(acur[rt][h][v], bf.y, acc[rt][2 * cp + 1]);
         }
       }
     }
     store_c((ch + 1) & 1, cr);
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+      for (int h = 0; h < 4; ++h) acur[rt][h] = anext[rt][h];
     __syncthreads();
-  };
-  int ch = 0;
-  for (; ch + 1 < nch; ch += 2) {
-    chunk(ch, a0, a1);
-    chunk(ch + 1, a1, a0);
   }
-  if (ch < nch) chunk(ch, a0, a1);
   // epilogue as k_tsmm44 (D layout -> LDS -> row-major 16-B stores); rows below r0 belong
   // to the previous wave (shifted last tile)
   double* ot = &cs[0][0] + wave * 16 * KYP;

@@ -1,9 +1,22 @@
-# Diagnostics: build a copy of librbl_hip.so with extra defines into tools/variants/<name>.so
-# usage: bash tools/build_variant.sh <name> "-DRBL_BAND_RD_ABLATE=4"   (run with RBL_LIB=...)
+# Diagnostics: build a copy of librbl_hip.so with extra defines into
+# tools/variants/<name>/librbl_hip.so (run against it with LD_LIBRARY_PATH=tools/variants/<name>,
+# or RBL_LIB=tools/variants/<name>/librbl_hip.so for the Python package).
+# usage: bash tools/build_variant.sh <name> "-DRBL_G44_ROWS=32"
 set -eu
 name=$1; defs=$2
 cd "$(dirname "$0")/../gpu-randomized-block-lanczos_amd/csrc"
-mkdir -p ../../tools/variants
-/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wno-unused-result $defs \
-  rbl_api.cpp comm.cpp plan.cpp rowop.hip spmm.hip spmm_window.hip spmm_band.hip tsmm.hip reorth.hip reorth32.hip smallmat.hip gen.hip \
-  -x none -shared -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib -o ../../tools/variants/$name.so
+out=../../tools/variants/$name
+mkdir -p $out/obj
+srcs=$(sed -n 's/^SRCS := //p' Makefile)
+pids=""
+for s in $srcs; do
+  o=$out/obj/${s%.*}.o
+  if [ "${s##*.}" = "cpp" ]; then x="-x hip"; else x=""; fi
+  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wno-unused-result $defs $x -c $s -o $o &
+  pids="$pids $!"
+done
+for p in $pids; do wait $p; done
+/opt/rocm/bin/hipcc -fPIC --offload-arch=gfx950 $out/obj/*.o -shared -L/opt/rocm/lib -lrccl \
+  -lrocprofiler-sdk-roctx -Wl,-rpath,/opt/rocm/lib -o $out/librbl_hip.so
+rm -rf $out/obj
+echo "built $out/librbl_hip.so"
