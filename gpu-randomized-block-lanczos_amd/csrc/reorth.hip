@@ -25,6 +25,12 @@ __device__ __forceinline__ double mfma4(double a, double b, double c) {
 }
 // The Krylov basis W is read once per launch (up to 92 GB at C4a: no L2 / Infinity Cache
 // reuse); non-temporal loads measured no faster here (596 vs 600 ms per run), so off
+// RBL_REORTH_ABL (diagnostics only, wrong results): bit 0 drops the next chunk's basis loads
+// (the MFMAs reuse the current operands), bit 1 the per-chunk barrier, bit 2 the LDS staging
+// store of the next chunk — in k_gram44 and k_tsmm44f
+#ifndef RBL_REORTH_ABL
+#define RBL_REORTH_ABL 0
+#endif
 #ifndef RBL_REORTH_NT
 #define RBL_REORTH_NT 0
 #endif
@@ -122,7 +128,7 @@ __device__ __forceinline__ void gram44_body(int64_t r_begin, int64_t r_end, int6
     // unconditional (clamped on the last chunk): a uniform branch here would make the
     // waitcnt pass merge a no-load path and drain the prefetch before the MFMAs
     load_x(rc0 + kG44Rows, xr);
-    load_a(rc0 + kG44Rows, anext);
+    if (!(RBL_REORTH_ABL & 1)) load_a(rc0 + kG44Rows, anext);
     const double* xb = xs[c & 1] + 8 * cp0;
     if (active) {  // idle waves (a 3-panel group) only help stage X
 #pragma unroll
@@ -140,12 +146,12 @@ __device__ __forceinline__ void gram44_body(int64_t r_begin, int64_t r_end, int6
     }
     // unconditional as well: a consumer under `if (more)` lets LLVM sink the loads into it
     // (after the MFMAs); on the last chunk this writes the dead spare buffer
-    store_x((int)((c + 1) & 1), rc0 + kG44Rows, xr);
+    if (!(RBL_REORTH_ABL & 4)) store_x((int)((c + 1) & 1), rc0 + kG44Rows, xr);
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
       for (int ag = 0; ag < AG; ++ag) acur[ks][ag] = anext[ks][ag];
-    __syncthreads();
+    if (!(RBL_REORTH_ABL & 2)) __syncthreads();
   }
   if (!active) return;
   const int KW = W.count * B;
@@ -438,7 +444,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
   __syncthreads();
   for (int ch = 0; ch < nch; ++ch) {
     load_c(ch + 1, cr);
-    load_a(ch + 1, anext);
+    if (!(RBL_REORTH_ABL & 1)) load_a(ch + 1, anext);
     const double* cb = cs[ch & 1] + 2 * q * LDC + 2 * (lane & 3);
 #pragma unroll
     for (int hv = 0; hv < 8; ++hv) {
@@ -454,12 +460,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
         }
       }
     }
-    store_c((ch + 1) & 1, cr);
+    if (!(RBL_REORTH_ABL & 4)) store_c((ch + 1) & 1, cr);
 #pragma unroll
     for (int rt = 0; rt < 2; ++rt)
 #pragma unroll
       for (int h = 0; h < 4; ++h) acur[rt][h] = anext[rt][h];
-    __syncthreads();
+    if (!(RBL_REORTH_ABL & 2)) __syncthreads();
   }
   // epilogue as k_tsmm44 (D layout -> LDS -> row-major 16-B stores); rows below r0 belong
   // to the previous wave (shifted last tile)
