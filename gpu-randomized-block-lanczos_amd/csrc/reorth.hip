@@ -55,6 +55,9 @@ constexpr int kG44Waves = 4;
 #ifndef RBL_G44_WPE
 #define RBL_G44_WPE 3
 #endif
+#ifndef RBL_G44_PF
+#define RBL_G44_PF 2
+#endif
 constexpr int kG44Rows = RBL_G44_ROWS;
 
 template <int B, int NX, int NPH>
@@ -116,6 +119,45 @@ __device__ __forceinline__ void gram44_body(int64_t r_begin, int64_t r_end, int6
 
   const int64_t nchunks = r_end > r_begin ? (r_end - r_begin + kG44Rows - 1) / kG44Rows : 0;
   double xr[EPT];
+#if RBL_G44_PF >= 2
+  // basis operands two chunks ahead in three rotating register sets (no copies: a copy of a
+  // landing prefetch would make the wave wait for it one chunk early)
+  double a0[KS][AG], a1[KS][AG], a2[KS][AG];
+  if (nchunks > 0) {
+    load_x(r_begin, xr);
+    store_x(0, r_begin, xr);
+    load_a(r_begin, a0);
+    load_a(r_begin + kG44Rows, a1);
+  }
+  __syncthreads();
+  auto step = [&](int64_t c, const double (&acur)[KS][AG], double (&afut)[KS][AG]) {
+    const int64_t rc0 = r_begin + c * kG44Rows;
+    load_x(rc0 + kG44Rows, xr);
+    load_a(rc0 + 2 * kG44Rows, afut);
+    const double* xb = xs[c & 1] + 8 * cp0;
+    if (active && c < nchunks) {  // no loads inside: the vmcnt bookkeeping is unaffected
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+#pragma unroll
+        for (int cp = 0; cp < CGP / 2; ++cp) {
+          const d2v bf = *reinterpret_cast<const d2v*>(xb + (4 * ks + q) * LD + 8 * cp + 2 * (lane & 3));
+#pragma unroll
+          for (int ag = 0; ag < AG; ++ag) {
+            acc[ag][2 * cp] = mfma4(acur[ks][ag], bf.x, acc[ag][2 * cp]);
+            acc[ag][2 * cp + 1] = mfma4(acur[ks][ag], bf.y, acc[ag][2 * cp + 1]);
+          }
+        }
+      }
+    }
+    store_x((int)((c + 1) & 1), rc0 + kG44Rows, xr);
+    __syncthreads();
+  };
+  for (int64_t c = 0; c < nchunks; c += 3) {
+    step(c, a0, a2);
+    step(c + 1, a1, a0);
+    step(c + 2, a2, a1);
+  }
+#else
   double acur[KS][AG], anext[KS][AG];
   if (nchunks > 0) {
     load_x(r_begin, xr);
@@ -153,6 +195,7 @@ __device__ __forceinline__ void gram44_body(int64_t r_begin, int64_t r_end, int6
       for (int ag = 0; ag < AG; ++ag) acur[ks][ag] = anext[ks][ag];
     if (!(RBL_REORTH_ABL & 2)) __syncthreads();
   }
+#endif
   if (!active) return;
   const int KW = W.count * B;
   double* out = slab + (s * KW + (int64_t)j * B) * KC + 4 * (2 * cp0);
@@ -390,20 +433,31 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
 // no per-load VALU (k_tsmm44 spent ~0.6 VALU per MFMA on clamps and 64-bit address math, and
 // on gfx950 fp64 MFMA does not co-execute with VALU).  A wave whose 32 rows pass nrows computes
 // the last 32 rows instead and stores only its own.
-template <int B>
+// KC: k per chunk (C chunk staged in LDS per chunk); PF: chunks of basis operands in flight
+// ahead of the MFMAs (PF = 2: three rotating register sets, the loop unrolled by 3).
+#ifndef RBL_T44_KC
+#define RBL_T44_KC 32
+#endif
+#ifndef RBL_T44_PF
+#define RBL_T44_PF 1
+#endif
+template <int B, int KC = RBL_T44_KC, int PF = RBL_T44_PF>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k_tsmm44f(
     int64_t nrows, PanelRun X, const double* __restrict__ C, int ldc, Panels Y, double alpha,
     double beta, const int* skip) {
   if (skip && *skip) return;
   constexpr int KYP = 64, CG = KYP / 4, LDC = KYP + 8;
-  constexpr int CEPT = kT44K * KYP / 256;
-  __shared__ __attribute__((aligned(16))) double cs[2][kT44K * LDC];
+  constexpr int NH = KC / 8;  // 16-B A loads per row tile per chunk
+  constexpr int CEPT = KC * KYP / 256;
+  constexpr int CS = 2 * KC * LDC > 4 * 16 * KYP ? 2 * KC * LDC : 4 * 16 * KYP;  // + epilogue stage
+  __shared__ __attribute__((aligned(16))) double cs_raw[CS];
+  double(*cs)[KC * LDC] = reinterpret_cast<double(*)[KC * LDC]>(cs_raw);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int q = lane >> 4;
   const int64_t r0 = ((int64_t)blockIdx.x * 4 + wave) * kT44Rows;
   const int64_t rw = r0 + kT44Rows <= nrows ? r0 : nrows - kT44Rows;  // wave-uniform
-  const int nch = X.count * B / kT44K;
+  const int nch = X.count * B / KC;
 
   double acc[2][CG];
 #pragma unroll
@@ -411,22 +465,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
 #pragma unroll
     for (int cg = 0; cg < CG; ++cg) acc[rt][cg] = 0.0;
 
-  // A: rows rw + 16 rt + (lane&15), k = 32 ch + 8 h + 2 q + v
+  // A: rows rw + 16 rt + (lane&15), k = KC ch + 8 h + 2 q + v
   const int aoff0 = (lane & 15) * B + 2 * q, aoff1 = aoff0 + 16 * B;
-  auto load_a = [&](int ch, d2v (&ar)[2][4]) {
+  auto load_a = [&](int ch, d2v (&ar)[2][NH]) {
     const int chc = ch < nch ? ch : nch - 1;
 #pragma unroll
-    for (int h = 0; h < 4; ++h) {
-      const int kk = kT44K * chc + 8 * h;
+    for (int h = 0; h < NH; ++h) {
+      const int kk = KC * chc + 8 * h;
       const double* xb = X.base + (int64_t)(kk / B) * X.stride + rw * B + (kk % B);
       ar[0][h] = *reinterpret_cast<const d2v*>(xb + aoff0);
       ar[1][h] = *reinterpret_cast<const d2v*>(xb + aoff1);
     }
   };
-  // C chunk rows 32 chc + wave + 4 v, column lane
+  // C chunk rows KC chc + wave + 4 v, column lane
   auto load_c = [&](int ch, double (&cr)[CEPT]) {
     const int chc = ch < nch ? ch : nch - 1;
-    const double* cb = C + (int64_t)(kT44K * chc + wave) * ldc;
+    const double* cb = C + (int64_t)(KC * chc + wave) * ldc;
 #pragma unroll
     for (int v = 0; v < CEPT; ++v) cr[v] = cb[(int64_t)(4 * v) * ldc + lane];
   };
@@ -435,19 +489,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
 #pragma unroll
     for (int v = 0; v < CEPT; ++v) cs[buf][cso + 4 * v * LDC] = cr[v];
   };
-
-  d2v acur[2][4], anext[2][4];
-  double cr[CEPT];
-  load_c(0, cr);
-  store_c(0, cr);
-  load_a(0, acur);
-  __syncthreads();
-  for (int ch = 0; ch < nch; ++ch) {
-    load_c(ch + 1, cr);
-    if (!(RBL_REORTH_ABL & 1)) load_a(ch + 1, anext);
+  auto mfmas = [&](int ch, const d2v (&acur)[2][NH]) {
     const double* cb = cs[ch & 1] + 2 * q * LDC + 2 * (lane & 3);
 #pragma unroll
-    for (int hv = 0; hv < 8; ++hv) {
+    for (int hv = 0; hv < 2 * NH; ++hv) {
       const int h = hv >> 1, v = hv & 1;
       const double* cr0 = cb + (8 * h + v) * LDC;
 #pragma unroll
@@ -460,16 +505,47 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
         }
       }
     }
-    if (!(RBL_REORTH_ABL & 4)) store_c((ch + 1) & 1, cr);
+  };
+
+  double cr[CEPT];
+  load_c(0, cr);
+  store_c(0, cr);
+  if constexpr (PF >= 2) {
+    d2v a0[2][NH], a1[2][NH], a2[2][NH];
+    load_a(0, a0);
+    load_a(1, a1);
+    __syncthreads();
+    auto step = [&](int ch, const d2v (&acur)[2][NH], d2v (&afut)[2][NH]) {
+      load_c(ch + 1, cr);
+      load_a(ch + 2, afut);
+      if (ch < nch) mfmas(ch, acur);  // no loads inside: the vmcnt bookkeeping is unaffected
+      store_c((ch + 1) & 1, cr);
+      __syncthreads();
+    };
+    for (int ch = 0; ch < nch; ch += 3) {
+      step(ch, a0, a2);
+      step(ch + 1, a1, a0);
+      step(ch + 2, a2, a1);
+    }
+  } else {
+    d2v acur[2][NH], anext[2][NH];
+    load_a(0, acur);
+    __syncthreads();
+    for (int ch = 0; ch < nch; ++ch) {
+      load_c(ch + 1, cr);
+      if (!(RBL_REORTH_ABL & 1)) load_a(ch + 1, anext);
+      mfmas(ch, acur);
+      if (!(RBL_REORTH_ABL & 4)) store_c((ch + 1) & 1, cr);
 #pragma unroll
-    for (int rt = 0; rt < 2; ++rt)
+      for (int rt = 0; rt < 2; ++rt)
 #pragma unroll
-      for (int h = 0; h < 4; ++h) acur[rt][h] = anext[rt][h];
-    if (!(RBL_REORTH_ABL & 2)) __syncthreads();
+        for (int h = 0; h < NH; ++h) acur[rt][h] = anext[rt][h];
+      if (!(RBL_REORTH_ABL & 2)) __syncthreads();
+    }
   }
   // epilogue as k_tsmm44 (D layout -> LDS -> row-major 16-B stores); rows below r0 belong
   // to the previous wave (shifted last tile)
-  double* ot = &cs[0][0] + wave * 16 * KYP;
+  double* ot = cs_raw + wave * 16 * KYP;
   const int g = (lane >> 2) & 3;
   constexpr int kYPer = 16 * KYP / 128;
 #pragma unroll

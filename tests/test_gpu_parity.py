@@ -66,6 +66,33 @@ def test_first_steps_trace(rbl, b):
         assert np.abs(Bg - Br).max() <= 1e-9 * sb, (i, np.abs(Bg - Br).max(), sb)
 
 
+@pytest.mark.parametrize("b", [16, 32])
+def test_long_trace_every_panel_remainder(rbl, b):
+    """16 block steps (partial reorth over nW = 2 .. 14 basis panels: every remainder of the
+    4-panel groups of k_gram44, including the tail groups that cover 2 or 4 splits' rows)
+    against the oracle's per-step A_i, B_{i+1}; a slowly decaying spectrum keeps the blocks
+    away from rounding-dominated directions.  Relative 1e-8 of the block's max entry."""
+    n = 3000
+    rng = np.random.default_rng(11)
+    import scipy.sparse as sp
+    R = sp.random(n, n, density=0.004, random_state=5, format="csr")
+    A = (R + R.T + sp.diags(np.linspace(1.0, 3.0, n))).tocsr()
+    omega = rng.standard_normal((n, b))
+    steps = 16
+    ref = o.RBL_gpu_semantics(A, 10, b, omega=omega, qr_mode="posdiag", reorth_mode="cgs",
+                              check=False, max_steps=steps, trace=True)
+    with rbl.Context(0) as ctx:
+        ctx.set_matrix(A)
+        _, _, info = rbl.lanczos(ctx, 10, b, omega=omega, check=False, max_steps=steps,
+                                 trace=True, ritz=False)
+    assert len(info.trace_A) == steps
+    for i in range(steps):
+        Ar, Br = ref.trace["A"][i], ref.trace["B"][i]
+        da = np.abs(info.trace_A[i] - Ar).max() / np.abs(Ar).max()
+        db = np.abs(info.trace_B[i] - Br).max() / np.abs(Br).max()
+        assert da < 1e-8 and db < 1e-8, (i, da, db)
+
+
 @pytest.mark.parametrize("order,b", [(0, 8), (1, 8), (0, 16), (1, 16), (0, 32)])
 def test_eigenpairs_c1(rbl, order, b):
     """C1 (n = 10,000, k = 10; b = 8 as configured, plus the 16/32 fast paths): eigenvalues

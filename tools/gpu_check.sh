@@ -2,7 +2,7 @@
 set -u
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 900 python -m pytest tests -m gpu -q --timeout 300 -x > gpurun_out/t1.log 2>&1; rc=$?
+timeout -k 10 900 python -u -m pytest tests -m gpu -q -x --timeout 300 --timeout-method thread > gpurun_out/t1.log 2>&1; rc=$?
 echo "pytest rc=$rc"; tail -3 gpurun_out/t1.log
 if [ $rc -ne 0 ]; then exit $rc; fi
 timeout -k 10 900 python bench.py --steps 2 > gpurun_out/b2.log 2>&1; rc=$?

@@ -7,8 +7,8 @@ for rep in ${REPS:-1 2}; do
   for v in "$@"; do
     echo "== $v (rep $rep)"
     test -f tools/variants/$v/librbl_hip.so || { echo "missing variant $v"; exit 3; }
-    LD_LIBRARY_PATH=tools/variants/$v timeout -k 10 120 ./tools/reorth_probe | tail -1 || exit $?
+    LD_LIBRARY_PATH=tools/variants/$v timeout -k 10 120 ./tools/reorth_probe | tail -2 || exit $?
   done
   echo "== tree (rep $rep)"
-  timeout -k 10 120 ./tools/reorth_probe | tail -1 || exit $?
+  timeout -k 10 120 ./tools/reorth_probe | tail -2 || exit $?
 done
