@@ -198,10 +198,13 @@ void cvt_f64_to_f32(const double* src, float* dst, int64_t n, hipStream_t s);
 //   mode 1: later pass — unshifted (falls back to shift if it still breaks).
 // Writes R (upper), Rinv, and Rtot = R * Rtot_prev (first pass: Rtot = R).
 // If *skip != 0 the kernel does nothing (used for the conditional third pass).
+// scratch: 2 b^2 doubles (used only for b > 64: the factor and R^-1 do not fit in LDS there)
 void chol_step(const double* G, int b, int64_t nglobal, int mode, double* R, double* Rinv,
-               double* Rtot, int* need3, int* status, const int* skip, hipStream_t s);
-// dst = src (b x b), used to stash B_i for the next step's epilogue.
-void copy_small(const double* src, double* dst, int64_t len, hipStream_t s);
+               double* Rtot, int* need3, int* status, const int* skip, hipStream_t s,
+               double* scratch);
+// dst = src (len doubles): B_i stashed for the next step's epilogue, and the out-of-place
+// CholQR applies at b > 64; nothing when *skip != 0.
+void copy_small(const double* src, double* dst, int64_t len, hipStream_t s, const int* skip = nullptr);
 // dst = src^T (b x b row-major).
 void transpose_small(const double* src, double* dst, int b, hipStream_t s);
 

@@ -59,6 +59,7 @@ struct rbl_ctx {
   double* d_dense = nullptr;
   int64_t dense_panels = 0;
   double* d_qfull = nullptr;
+  int qfull_cols = 0;         // columns d_qfull was sized for
   int64_t ntiles = 0, tiles_per_wg = 0;
   bool window_ok16 = false, window_ok32 = false;
   bool band_ok16 = false, band_ok32 = false;
@@ -574,7 +575,7 @@ Panels pan2(const double* p0, const double* p1, int w) {
 }
 
 // small-buffer carve (b x b each)
-enum { S_R = 0, S_RINV, S_RTOT, S_BPREV, S_AI, S_G, S_BT, S_NSMALL };
+enum { S_R = 0, S_RINV, S_RTOT, S_BPREV, S_AI, S_G, S_BT, S_CHS0, S_CHS1, S_NSMALL };  // S_CHS*: chol scratch (b > 64)
 double* smallp(rbl_ctx* ctx, int which) { return ctx->d_small + (int64_t)which * ctx->b * ctx->b; }
 
 int tsmm_checked(rbl_ctx* ctx, const PanelRun& X, const double* C, int ldc, const Panels& Y,
@@ -638,6 +639,14 @@ int apply_A(rbl_ctx* ctx, const double* Qin, int64_t off, int b, double* U, cons
     const int parts = spmm(A, Qin, off, b, U, Qprev, Bi, ctx->spmm_variant, ctx->stream, slab);
     if (parts < 0) return fail(ctx, RBL_ERR_INVALID, "internal: split-source SpMM needs the band-tile kernel");
     return parts;
+  }
+  if (b > ctx->qfull_cols) {  // Q gathered to all n rows, zero-padded to 32 * dense_panels
+    hipFree(ctx->d_qfull);
+    ctx->d_qfull = nullptr;
+    ctx->qfull_cols = 0;
+    HIPC(hipMalloc(&ctx->d_qfull, (size_t)ctx->dense_panels * 32 * b * sizeof(double)));
+    HIPC(hipMemsetAsync(ctx->d_qfull, 0, (size_t)ctx->dense_panels * 32 * b * sizeof(double), ctx->stream));
+    ctx->qfull_cols = b;
   }
   HIPC(hipMemcpyAsync(ctx->d_qfull, Qin + (0 - off) * b, ctx->n * b * sizeof(double),
                       hipMemcpyDeviceToDevice, ctx->stream));
@@ -822,10 +831,19 @@ int tsqr(rbl_ctx* ctx, const double* U, double* Qout, bool g1_ready = false, flo
   double* G = smallp(ctx, S_G);
   const int* skip3 = need3 + 1;
   const bool fused = rowgram_ok(b);
+  // Qout = Qout R^-1: in place while one wave owns whole rows (tsmm: b <= 64), else through
+  // the scratch block T
+  auto apply_inplace = [&](const int* skip) -> int {
+    if (b <= 64)
+      return tsmm_checked(ctx, run1(Qout, b), smallp(ctx, S_RINV), b, pan1(Qout, b), 1.0, 0.0, skip);
+    CHK(tsmm_checked(ctx, run1(Qout, b), smallp(ctx, S_RINV), b, pan1(ctx->d_T, b), 1.0, 0.0, skip));
+    copy_small(ctx->d_T, Qout, ctx->nloc * b, ctx->stream, skip);
+    return RBL_OK;
+  };
   // pass 1 (shift decided on device)
   if (!g1_ready) CHK(gram(ctx, run1(U, b), pan1(U, b), G, nullptr));
   chol_step(G, b, ctx->n, 0, smallp(ctx, S_R), smallp(ctx, S_RINV), smallp(ctx, S_RTOT), need3,
-            status, nullptr, ctx->stream);
+            status, nullptr, ctx->stream, smallp(ctx, S_CHS0));
   if (fused) {
     CHK(rowop(ctx, U, smallp(ctx, S_RINV), Qout, 1.0, 0.0, G, nullptr));
   } else {
@@ -834,22 +852,22 @@ int tsqr(rbl_ctx* ctx, const double* U, double* Qout, bool g1_ready = false, flo
   }
   // pass 2
   chol_step(G, b, ctx->n, 1, smallp(ctx, S_R), smallp(ctx, S_RINV), smallp(ctx, S_RTOT), need3,
-            status, nullptr, ctx->stream);
+            status, nullptr, ctx->stream, smallp(ctx, S_CHS0));
   if (fused) {  // in place; the Gram feeds pass 3 when a shifted first pass asked for it
     // (fp32 basis: the result goes straight to Qout32 unless pass 3 follows)
     CHK(rowop(ctx, Qout, smallp(ctx, S_RINV), Qout, 1.0, 0.0, G, nullptr, nullptr, Qout32,
               Qout32 ? need3 : nullptr));
   } else {
-    CHK(tsmm_checked(ctx, run1(Qout, b), smallp(ctx, S_RINV), b, pan1(Qout, b), 1.0, 0.0, nullptr));
+    CHK(apply_inplace(nullptr));
     CHK(gram(ctx, run1(Qout, b), pan1(Qout, b), G, skip3));
   }
   // pass 3 only after a shifted first pass (device flag; kernels early-exit otherwise)
   chol_step(G, b, ctx->n, 1, smallp(ctx, S_R), smallp(ctx, S_RINV), smallp(ctx, S_RTOT), need3,
-            status, skip3, ctx->stream);
+            status, skip3, ctx->stream, smallp(ctx, S_CHS0));
   if (fused) {
     CHK(rowop(ctx, Qout, smallp(ctx, S_RINV), Qout, 1.0, 0.0, nullptr, skip3, nullptr, Qout32));
   } else {
-    CHK(tsmm_checked(ctx, run1(Qout, b), smallp(ctx, S_RINV), b, pan1(Qout, b), 1.0, 0.0, skip3));
+    CHK(apply_inplace(skip3));
     if (Qout32) cvt_f64_to_f32(Qout, Qout32, ctx->nloc * b, ctx->stream);
   }
   HIPC(hipGetLastError());
@@ -982,7 +1000,7 @@ void free_matrix(rbl_ctx* ctx) {
   hipFree(ctx->d_seg_scratch); ctx->d_seg_scratch = nullptr;
   ctx->seg_ntasks = ctx->seg_nlong = 0;
   hipFree(ctx->d_dense); ctx->d_dense = nullptr;
-  hipFree(ctx->d_qfull); ctx->d_qfull = nullptr;
+  hipFree(ctx->d_qfull); ctx->d_qfull = nullptr; ctx->qfull_cols = 0;
   ctx->dense = false;
   ctx->dense_panels = 0;
   ctx->n = ctx->nloc = ctx->nnz = 0;
@@ -1322,6 +1340,7 @@ int rbl_set_matrix_dense(rbl_ctx* ctx, int64_t n, int64_t row_begin, int64_t row
   HIPC(hipMalloc(&ctx->d_dense, (size_t)P * ml * 32 * sizeof(double)));
   HIPC(hipMalloc(&ctx->d_qfull, (size_t)P * 32 * 64 * sizeof(double)));
   HIPC(hipMemsetAsync(ctx->d_qfull, 0, (size_t)P * 32 * 64 * sizeof(double), ctx->stream));
+  ctx->qfull_cols = 64;
   // column-major slice -> row-major 32-column panels, one panel at a time through a scratch
   double* d_tmp = nullptr;
   HIPC(hipMalloc(&d_tmp, (size_t)ml * 32 * sizeof(double)));
@@ -1529,7 +1548,7 @@ int rbl_spmm_kernel_for(rbl_ctx* ctx, int b) {
 }
 
 int rbl_apply(rbl_ctx* ctx, int b, const double* X, double* Y) {
-  if (!ctx || b < 1 || b > 64 || !X || !Y) return fail(ctx, RBL_ERR_INVALID, "rbl_apply: bad arguments");
+  if (!ctx || b < 1 || b > RBL_MAX_BLOCK || !X || !Y) return fail(ctx, RBL_ERR_INVALID, "rbl_apply: bad arguments");
   if (!has_matrix(ctx)) return fail(ctx, RBL_ERR_STATE, "rbl_apply: no matrix");
   if (ctx->b != 0 && ctx->b != b && ctx->nranks > 1)
     return fail(ctx, RBL_ERR_STATE, "rbl_apply: b differs from the running Krylov block size");
@@ -1572,8 +1591,8 @@ int rbl_start(rbl_ctx* ctx, int b, int max_blocks, int basis_bits, const double*
               uint64_t seed) {
   if (!ctx) return RBL_ERR_INVALID;
   if (!has_matrix(ctx)) return fail(ctx, RBL_ERR_STATE, "rbl_start: no matrix");
-  if (ctx->dense && b > 64) return fail(ctx, RBL_ERR_INVALID, "dense A: b <= 64");
-  if (b < 1 || b > 64) return fail(ctx, RBL_ERR_INVALID, "block size must be in [1,64]");
+  if (b < 1 || b > RBL_MAX_BLOCK)
+    return fail(ctx, RBL_ERR_INVALID, "block size must be in [1," + std::to_string(RBL_MAX_BLOCK) + "]");
   if (max_blocks < 1) return fail(ctx, RBL_ERR_INVALID, "max_blocks must be >= 1");
   if (basis_bits != 64 && basis_bits != 32)
     return fail(ctx, RBL_ERR_INVALID, "basis_bits must be 64 or 32");

@@ -79,7 +79,6 @@ __device__ __forceinline__ void gram44_body(int64_t r_begin, int64_t r_end, int6
   const int ph = wave / r;                  // column phase
   const bool active = ph < NPH;
   const int cp0 = ph < NPH ? ph * (CGP / 2) : 0;
-  const double* wp = W.base + (int64_t)j * W.stride + (lane & 15);
 
   double acc[AG][CGP];
 #pragma unroll

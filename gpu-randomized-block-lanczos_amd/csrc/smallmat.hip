@@ -9,25 +9,40 @@
 
 namespace rbl {
 
-constexpr int kMaxB = 64;
+constexpr int kMaxB = 64;  // b x b work in LDS up to here; larger b: global scratch (L2)
 
+// M (the factor) and X (R^-1, then the Rtot product's scratch) live in LDS for b <= kMaxB and
+// in a caller scratch of 2 b^2 doubles (L2-resident) above that: the block sizes past 64 that
+// RBL_gpu(A, k, b) accepts (RBL_gpu.jl:205) take one more L2 trip per element, no LDS limit.
+template <bool LDS>
+struct SmallMat {
+  double* p;
+  int ld;
+  __device__ double& operator()(int r, int c) const { return p[r * ld + c]; }
+};
+
+template <bool LDS>
 __global__ __launch_bounds__(256) void k_chol(const double* __restrict__ G, int b, int64_t nglob,
                                               int mode, double* R, double* Rinv, double* Rtot,
-                                              int* need3, int* status, const int* skip) {
+                                              int* need3, int* status, const int* skip,
+                                              double* scratch) {
   if (skip && *skip) return;
-  __shared__ double M[kMaxB][kMaxB + 1];
-  __shared__ double X[kMaxB][kMaxB + 1];
+  __shared__ double Ml[LDS ? kMaxB * (kMaxB + 1) : 1];
+  __shared__ double Xl[LDS ? kMaxB * (kMaxB + 1) : 1];
   __shared__ int fail;
   __shared__ double shift;
   __shared__ int zero;
-  __shared__ double Gd[kMaxB];  // diag(G): the serial pivot / trace reads hit LDS, not L2
+  __shared__ double Gd[LDS ? kMaxB : 1];  // diag(G): the serial pivot / trace reads hit LDS, not L2
+  const SmallMat<LDS> M{LDS ? Ml : scratch, LDS ? kMaxB + 1 : b};
+  const SmallMat<LDS> X{LDS ? Xl : scratch + (int64_t)b * b, LDS ? kMaxB + 1 : b};
+  double* gd = LDS ? Gd : Rinv;  // Rinv is written only after the factorisation
   const int tid = threadIdx.x, nt = blockDim.x;
 
-  for (int j = tid; j < b; j += nt) Gd[j] = G[j * b + j];
+  for (int j = tid; j < b; j += nt) gd[j] = G[j * b + j];
   __syncthreads();
   if (tid == 0) {
     double tr = 0.0;
-    for (int j = 0; j < b; ++j) tr += Gd[j];
+    for (int j = 0; j < b; ++j) tr += gd[j];
     zero = !(tr > 0.0);
     shift = 0.0;
     // Fukaya shift, u = 2^-53; trace(G) >= ||U||_2^2
@@ -41,32 +56,32 @@ __global__ __launch_bounds__(256) void k_chol(const double* __restrict__ G, int 
       const double sh = attempt ? shift : 0.0;
       for (int e = tid; e < b * b; e += nt) {
         const int r = e / b, c = e % b;
-        M[r][c] = (r <= c) ? G[r * b + c] + (r == c ? sh : 0.0) : 0.0;
+        M(r, c) = (r <= c) ? G[r * b + c] + (r == c ? sh : 0.0) : 0.0;
       }
       if (tid == 0) fail = 0;
       __syncthreads();
       for (int j = 0; j < b; ++j) {
         if (tid == 0) {
-          const double d = M[j][j];
-          const double gjj = Gd[j] + sh;
+          const double d = M(j, j);
+          const double gjj = gd[j] + sh;
           if (!(d > 0.0) || !isfinite(d)) {
             fail = 1;
           } else {
             // relative pivot: sin^2 of the angle between u_j and span(u_<j); below 1e-15 the
             // block's condition number exceeds ~3e7 and plain CholQR2 loses orthogonality
             if (attempt == 0 && mode == 0 && d < 1e-15 * gjj) fail = 2;
-            M[j][j] = sqrt(d);
+            M(j, j) = sqrt(d);
           }
         }
         __syncthreads();
         if (fail) break;
-        const double rjj = M[j][j];
-        for (int c = j + 1 + tid; c < b; c += nt) M[j][c] /= rjj;
+        const double rjj = M(j, j);
+        for (int c = j + 1 + tid; c < b; c += nt) M(j, c) /= rjj;
         __syncthreads();
         const int m = b - j - 1;
         for (int e = tid; e < m * m; e += nt) {
           const int r = j + 1 + e / m, c = j + 1 + e % m;
-          if (r <= c) M[r][c] -= M[j][r] * M[j][c];
+          if (r <= c) M(r, c) -= M(j, r) * M(j, c);
         }
         __syncthreads();
       }
@@ -82,12 +97,12 @@ __global__ __launch_bounds__(256) void k_chol(const double* __restrict__ G, int 
   // Rinv: column c by thread c (back substitution on the upper triangle)
   if (!zero && !bad) {
     for (int c = tid; c < b; c += nt) {
-      for (int i = 0; i < b; ++i) X[i][c] = 0.0;
-      X[c][c] = 1.0 / M[c][c];
+      for (int i = 0; i < b; ++i) X(i, c) = 0.0;
+      X(c, c) = 1.0 / M(c, c);
       for (int i = c - 1; i >= 0; --i) {
         double acc = 0.0;
-        for (int k = i + 1; k <= c; ++k) acc += M[i][k] * X[k][c];
-        X[i][c] = -acc / M[i][i];
+        for (int k = i + 1; k <= c; ++k) acc += M(i, k) * X(k, c);
+        X(i, c) = -acc / M(i, i);
       }
     }
   }
@@ -95,8 +110,8 @@ __global__ __launch_bounds__(256) void k_chol(const double* __restrict__ G, int 
   for (int e = tid; e < b * b; e += nt) {
     const int r = e / b, c = e % b;
     const bool up = r <= c;
-    const double rv = (zero || bad || !up) ? 0.0 : M[r][c];
-    const double xv = (zero || bad || !up) ? 0.0 : X[r][c];
+    const double rv = (zero || bad || !up) ? 0.0 : M(r, c);
+    const double xv = (zero || bad || !up) ? 0.0 : X(r, c);
     R[e] = rv;
     Rinv[e] = xv;
   }
@@ -105,13 +120,13 @@ __global__ __launch_bounds__(256) void k_chol(const double* __restrict__ G, int 
   if (mode == 0) {
     for (int e = tid; e < b * b; e += nt) Rtot[e] = R[e];
   } else {
-    for (int e = tid; e < b * b; e += nt) X[e / b][e % b] = Rtot[e];
+    for (int e = tid; e < b * b; e += nt) X(e / b, e % b) = Rtot[e];
     __syncthreads();
     for (int e = tid; e < b * b; e += nt) {
       const int r = e / b, c = e % b;
       double acc = 0.0;
       if (r <= c && !zero && !bad)
-        for (int k = r; k <= c; ++k) acc += M[r][k] * X[k][c];
+        for (int k = r; k <= c; ++k) acc += M(r, k) * X(k, c);
       Rtot[e] = acc;
     }
   }
@@ -123,17 +138,28 @@ __global__ __launch_bounds__(256) void k_chol(const double* __restrict__ G, int 
 }
 
 void chol_step(const double* G, int b, int64_t nglobal, int mode, double* R, double* Rinv,
-               double* Rtot, int* need3, int* status, const int* skip, hipStream_t s) {
-  hipLaunchKernelGGL(k_chol, dim3(1), dim3(256), 0, s, G, b, nglobal, mode, R, Rinv, Rtot, need3,
-                     status, skip);
+               double* Rtot, int* need3, int* status, const int* skip, hipStream_t s,
+               double* scratch) {
+  if (b <= kMaxB)
+    hipLaunchKernelGGL(k_chol<true>, dim3(1), dim3(256), 0, s, G, b, nglobal, mode, R, Rinv, Rtot,
+                       need3, status, skip, scratch);
+  else
+    hipLaunchKernelGGL(k_chol<false>, dim3(1), dim3(256), 0, s, G, b, nglobal, mode, R, Rinv, Rtot,
+                       need3, status, skip, scratch);
 }
 
-__global__ void k_copy(const double* __restrict__ src, double* __restrict__ dst, int64_t len) {
-  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e < len) dst[e] = src[e];
+__global__ void k_copy(const double* __restrict__ src, double* __restrict__ dst, int64_t len,
+                       const int* skip) {
+  if (skip && *skip) return;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < len;
+       e += (int64_t)gridDim.x * blockDim.x)
+    dst[e] = src[e];
 }
-void copy_small(const double* src, double* dst, int64_t len, hipStream_t s) {
-  hipLaunchKernelGGL(k_copy, dim3((unsigned)((len + 255) / 256)), dim3(256), 0, s, src, dst, len);
+void copy_small(const double* src, double* dst, int64_t len, hipStream_t s, const int* skip) {
+  int64_t blocks = (len + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(k_copy, dim3((unsigned)blocks), dim3(256), 0, s, src, dst, len, skip);
 }
 
 // dst = src^T (b x b row-major): B_i^T for the dense path's 3-term epilogue

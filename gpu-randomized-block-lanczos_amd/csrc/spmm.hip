@@ -22,12 +22,14 @@ __global__ __launch_bounds__(256) void k_spmm_gather(int64_t nrows, const int64_
                                                      const double* __restrict__ Q, int64_t col_off,
                                                      int b, double* __restrict__ U,
                                                      const double* __restrict__ Qprev,
-                                                     const double* __restrict__ Bi) {
+                                                     const double* __restrict__ Bi, int ncb) {
   constexpr int G = kWave / BP;
   const int lane = threadIdx.x & 63;
-  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  // b > 64: ncb waves per row, wave cb owning columns [64 cb, 64 cb + 64)
+  const int64_t wid = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t row = wid / ncb;
   if (row >= nrows) return;
-  const int g = lane / BP, c = lane % BP;
+  const int g = lane / BP, c = (int)(wid % ncb) * BP + lane % BP;
   const bool cv = c < b;
   const int cs = cv ? c : 0;
   const int64_t s = rowptr[row], e = rowptr[row + 1];
@@ -178,9 +180,10 @@ bool spmm_seg_ok(const CsrDev& A, int b) { return A.seg_ntasks > 0 && (b == 16 |
 template <int BP>
 static void launch_gather(const CsrDev& A, const double* Q, int64_t off, int b, double* U,
                           const double* Qprev, const double* Bi, hipStream_t s) {
-  const int64_t blocks = (A.nrows + 3) / 4;
+  const int ncb = (b + BP - 1) / BP;
+  const int64_t blocks = (A.nrows * ncb + 3) / 4;
   hipLaunchKernelGGL((k_spmm_gather<BP>), dim3((unsigned)blocks), dim3(256), 0, s, A.nrows,
-                     A.rowptr, A.col, A.val, Q, off, b, U, Qprev, Bi);
+                     A.rowptr, A.col, A.val, Q, off, b, U, Qprev, Bi, ncb);
 }
 
 int spmm(const CsrDev& A, const double* Qin, int64_t col_off, int b, double* U,

@@ -26,17 +26,19 @@ __device__ inline d4 mfma16(double a, double b, d4 c) {
 // ----------------------------------------------------------------------------------------
 template <int AT, int CT>
 __global__ __launch_bounds__(256) void k_gram(int64_t nrows, PanelRun W, Panels X, double* slab,
-                                              int splits, int ncg, int64_t rows_per,
+                                              int splits, int ncg, int nag, int64_t rows_per,
                                               const int* skip) {
   if (skip && *skip) return;
   const int lane = threadIdx.x & 63;
   const int wid = blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int njobs = W.count * ncg;
+  // job = (panel j, W column group ag of 16 AT columns, X column group cg of 16 CT columns)
+  const int njobs = W.count * nag * ncg;
   const int job = wid % njobs;
   const int s = wid / njobs;
   if (s >= splits) return;
   const int j = job % W.count;
-  const int cg = job / W.count;
+  const int ag = (job / W.count) % nag;
+  const int cg = job / (W.count * nag);
   const int w = W.w, xw = X.w;
   const int KC = X.count * xw;
   const int KW = W.count * w;
@@ -49,7 +51,7 @@ __global__ __launch_bounds__(256) void k_gram(int64_t nrows, PanelRun W, Panels 
   bool wv[AT];
 #pragma unroll
   for (int at = 0; at < AT; ++at) {
-    const int a = at * 16 + li;
+    const int a = (ag * AT + at) * 16 + li;
     wv[at] = a < w;
     wp[at] = W.base + (int64_t)j * W.stride + (wv[at] ? a : 0);
   }
@@ -103,7 +105,7 @@ __global__ __launch_bounds__(256) void k_gram(int64_t nrows, PanelRun W, Panels 
     for (int ct = 0; ct < CT; ++ct)
 #pragma unroll
       for (int reg = 0; reg < 4; ++reg) {
-        const int a = at * 16 + q + 4 * reg;
+        const int a = (ag * AT + at) * 16 + q + 4 * reg;
         const int c = (cg * CT + ct) * 16 + li;
         if (a < w && c < KC) out[(int64_t)(j * w + a) * KC + c] = acc[at][ct][reg];
       }
@@ -117,7 +119,7 @@ int gram_splits(int64_t nrows, int nW, int w, int xcols) {
   const int ctt = tiles16(xcols);
   const int ct = ctt <= 1 ? 1 : (ctt <= 2 ? 2 : 4);
   const int ncg = (ctt + ct - 1) / ct;
-  const int64_t njobs = (int64_t)nW * ncg;
+  const int64_t njobs = (int64_t)nW * ((tiles16(w) + pick_at(w) - 1) / pick_at(w)) * ncg;
   int64_t splits = (4096 + njobs - 1) / njobs;
   const int64_t max_by_rows = (nrows + 63) / 64;
   if (splits > max_by_rows) splits = max_by_rows;
@@ -134,10 +136,11 @@ static void launch_gram_t(int64_t nrows, const PanelRun& W, const Panels& X, dou
                           int splits, int ncg, const int* skip, hipStream_t s) {
   int64_t rows_per = (nrows + splits - 1) / splits;
   rows_per = (rows_per + 3) / 4 * 4;
-  const int64_t waves = (int64_t)W.count * ncg * splits;
+  const int nag = (tiles16(W.w) + AT - 1) / AT;  // W wider than 16 AT columns (b > 64)
+  const int64_t waves = (int64_t)W.count * nag * ncg * splits;
   const int blocks = (int)((waves + 3) / 4);
   hipLaunchKernelGGL((k_gram<AT, CT>), dim3(blocks), dim3(256), 0, s, nrows, W, X, slab, splits,
-                     ncg, rows_per, skip);
+                     ncg, nag, rows_per, skip);
 }
 
 void gram_partial(int64_t nrows, const PanelRun& W, const Panels& X, double* slab, int splits,

@@ -27,6 +27,9 @@ extern "C" {
 #endif
 
 #define RBL_ABI_VERSION 1
+/* Largest Krylov block size b (RBL_gpu(A, k, b) takes any b, RBL_gpu.jl:205; the reference's
+ * scripts use b <= 8, the north star b = 32).  The MFMA fast paths cover b in {16, 32}. */
+#define RBL_MAX_BLOCK 512
 
 #define RBL_OK                  0
 #define RBL_WARN_NOT_CONVERGED  1   /* host-side status for the P6 case */
@@ -123,7 +126,7 @@ int rbl_set_matrix_csr_rows(rbl_ctx* ctx, int64_t n, int64_t row_begin, int64_t 
 /* Dense symmetric A (RBL_gpu(A::Matrix{Float64}, k, b), RBL_gpu.jl:205; images.jl's B^T B):
  * the local rows [row_begin,row_end) as a column-major slice with leading dimension lda
  * (one rank: the whole n x n matrix, lda >= n — Julia's Matrix pointer as-is).  A * Q then
- * runs as a panel GEMM on fp64 MFMA with Q gathered to all n rows on every rank; b <= 64.
+ * runs as a panel GEMM on fp64 MFMA with Q gathered to all n rows on every rank.
  * rbl_spmm_kernel_for reports 4; rbl_get_matrix_csr fails (RBL_ERR_STATE). */
 int rbl_set_matrix_dense(rbl_ctx* ctx, int64_t n, int64_t row_begin, int64_t row_end,
                          const double* A, int64_t lda);

@@ -173,7 +173,7 @@ def test_invalid_arguments_fail_loudly(rbl):
             ctx.start(8, 10)                      # no matrix
         ctx.set_matrix(c1_matrix(1000, 2))
         with pytest.raises(rbl.RBLError):
-            ctx.start(65, 10)                     # b > 64
+            ctx.start(513, 10)                    # b > RBL_MAX_BLOCK
         ctx.start(8, 4, seed=1)
         with pytest.raises(rbl.RBLError):
             ctx.step(3, False)                    # out of order
@@ -233,3 +233,43 @@ def test_async_steps_match_sync_steps(rbl, b):
     for (As, Bs), (Aa, Ba, st) in zip(sync, got):
         assert st in (_lib.RBL_OK, _lib.RBL_WARN_QR_SHIFTED)
         assert np.array_equal(As, Aa) and np.array_equal(Bs, Ba)
+
+
+@pytest.mark.parametrize("b", [80, 128])
+def test_block_sizes_past_64(rbl, b):
+    """RBL_gpu(A, k, b) takes any b (RBL_gpu.jl:205): b > 64 runs the generic MFMA Gram /
+    update kernels with wide panels, the column-blocked gather SpMM and the b x b Cholesky in
+    an L2 scratch.  Eigenvalues vs the oracle < 1e-10, residuals < 1e-7."""
+    k = 20
+    A = c1_matrix(4000, k)
+    n = A.shape[0]
+    omega = np.random.default_rng(b).standard_normal((n, b))
+    ref = o.RBL_gpu_semantics(A, k, b, omega=omega, qr_mode="posdiag", reorth_mode="cgs")
+    D, V, info = rbl.RBL_gpu(A, k, b, omega=omega, return_info=True)
+    assert ref.converged and info.converged and info.iters == ref.iters
+    rel = np.abs(D - ref.D) / np.abs(ref.D)
+    assert rel.max() < EIG_TOL, rel
+    res = np.linalg.norm(A @ V - V * D, axis=0) / np.abs(D)
+    assert res.max() < RES_TOL, res
+    with rbl.Context(0) as ctx:
+        ctx.set_matrix(A)
+        X = np.random.default_rng(3).standard_normal((n, b))
+        Y = ctx.apply(X)
+    ref_y = A @ X
+    assert np.abs(Y - ref_y).max() <= 1e-12 * np.abs(ref_y).max()
+
+
+def test_dense_block_size_past_64(rbl):
+    """Dense A with b = 96: the gathered-Q buffer is re-sized past its 64-column default.
+    (n stays above the Krylov dimension at the first convergence check: once a block only
+    partly fits in R^n, the reference's own answer carries spurious Ritz values that depend
+    on its QR's junk columns — DESIGN §4, not a parity case.)"""
+    n, k, b = 2000, 6, 96
+    rng = np.random.default_rng(2)
+    B = rng.standard_normal((n, n)) / np.sqrt(n)
+    A = B + B.T + np.diag(np.r_[np.linspace(40, 30, 2 * k), np.zeros(n - 2 * k)])
+    omega = rng.standard_normal((n, b))
+    ref = o.RBL_gpu_semantics(A, k, b, omega=omega, qr_mode="posdiag", reorth_mode="cgs")
+    D, V, info = rbl.RBL_gpu(A, k, b, omega=omega, return_info=True)
+    assert ref.converged and info.converged
+    assert (np.abs(D - ref.D) / np.abs(ref.D)).max() < EIG_TOL
