@@ -93,12 +93,36 @@ constexpr int64_t kSegPack = 512;   // nonzeros per packed short-row task (<= 64
 // slab != null the Gram Y'^T Y' as grid partials slab[grid][b][b] (reduce with reduce_slab).
 // X may equal Y (in place).  b in {16, 32}.
 bool rowgram_ok(int b);
-int rowgram_grid(int64_t nrows);
+int rowgram_grid(int64_t nrows, int per_cu = 2);
+constexpr int kRowgramMaxPerCu = 4;  // rowgram_ex's grids stay <= rowgram_grid(nrows, this)
 // X32 (optional): X read from fp32 instead (widened exactly).  Y32 (optional): Y' written to
 // Y32 rounded to fp32 instead of Y — unless f64flag is non-null and *f64flag != 0 (device).
 void rowgram(int64_t nrows, int b, const double* X, const double* C, int ldc, double* Y,
              double alpha, double beta, double* slab, int grid, const int* skip, hipStream_t s,
              const float* X32 = nullptr, float* Y32 = nullptr, const int* f64flag = nullptr);
+// The CholQR forms of the fused row op (b in {16, 32}, X fp64):
+//   mode 1: slab <- Gram of X C (no store);  mode 2: Y = (X C) C2 (slab must be null);
+//   Z != null (modes 0 and 2): slab2 <- per-workgroup partials of Z^T Y (grid x b x b).
+// grid <= 0: as many persistent workgroups as the instantiation keeps resident (its register
+// budget), reported in *grid_out.  Returns false for an unsupported combination.
+struct RowOpArgs {
+  const double* X = nullptr;
+  const double* C = nullptr;
+  int ldc = 0;
+  double* Y = nullptr;
+  double alpha = 1.0, beta = 0.0;
+  double* slab = nullptr;
+  const int* skip = nullptr;
+  const float* X32 = nullptr;
+  float* Y32 = nullptr;
+  const int* f64flag = nullptr;
+  const double* C2 = nullptr;
+  const double* Z = nullptr;
+  double* slab2 = nullptr;
+  int mode = 0;
+  int* grid_out = nullptr;  // rowgram_ex with grid <= 0: the grid it chose (per-CU occupancy)
+};
+bool rowgram_ex(int64_t nrows, int b, const RowOpArgs& a, int grid, hipStream_t s);
 
 // --- spmm.hip ----------------------------------------------------------------------------
 // U = A * Qin  (+ epilogue U -= Qprev * Bt^T with Bt = B_i row-major b x b, if Qprev).

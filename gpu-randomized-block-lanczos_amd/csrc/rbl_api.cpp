@@ -120,6 +120,11 @@ struct rbl_ctx {
   bool timers = false;
   int reorth_order = 0;
   int spmm_variant = 0;
+  int fuse = 3;               // RBL_OPT_FUSE
+  // the local-reorth coefficient Q_{i-1}^T Q_i of step cloc_step, formed by the QR of step
+  // cloc_step - 1 (S_CLOC); 0: none
+  int cloc_step = 0;
+  std::vector<int> step_flags;  // part_reorth flags per step (the fusion's schedule guess)
   double stage_ms[RBL_NUM_STAGES] = {0};
   struct Mark { int stage; hipEvent_t a, b; };
   std::vector<Mark> marks;
@@ -575,7 +580,9 @@ Panels pan2(const double* p0, const double* p1, int w) {
 }
 
 // small-buffer carve (b x b each)
-enum { S_R = 0, S_RINV, S_RTOT, S_BPREV, S_AI, S_G, S_BT, S_CHS0, S_CHS1, S_NSMALL };  // S_CHS*: chol scratch (b > 64)
+// S_CHS*: chol scratch (b > 64); S_RINV1: R1^-1 kept for the 3-pass CholQR; S_CLOC: the next
+// step's local-reorth Gram
+enum { S_R = 0, S_RINV, S_RTOT, S_BPREV, S_AI, S_G, S_BT, S_CHS0, S_CHS1, S_RINV1, S_CLOC, S_NSMALL };
 double* smallp(rbl_ctx* ctx, int which) { return ctx->d_small + (int64_t)which * ctx->b * ctx->b; }
 
 int tsmm_checked(rbl_ctx* ctx, const PanelRun& X, const double* C, int ldc, const Panels& Y,
@@ -595,8 +602,9 @@ int rowop(rbl_ctx* ctx, const double* X, const double* C, double* Y, double alph
   const int grid = rowgram_grid(ctx->nloc);
   if (G && (size_t)grid * b * b > ctx->slab_elems)
     return fail(ctx, RBL_ERR_INVALID, "internal: row-op slab too small");
-  rowgram(ctx->nloc, b, X, C, b, Y, alpha, beta, G ? ctx->d_slab : nullptr, grid, skip, ctx->stream,
-          X32, Y32, f64flag);
+  // without a Gram the grid follows the kernel's occupancy (no partials to count)
+  rowgram(ctx->nloc, b, X, C, b, Y, alpha, beta, G ? ctx->d_slab : nullptr, G ? grid : 0, skip,
+          ctx->stream, X32, Y32, f64flag);
   HIPC(hipGetLastError());
   if (!G) return RBL_OK;
   reduce_slab(ctx->d_slab, grid, (int64_t)b * b, G, skip, ctx->stream);
@@ -817,13 +825,46 @@ int upd32(rbl_ctx* ctx, const float* Xb, int nX, const double* C, int ldc, float
   return RBL_OK;
 }
 
+// Fused row op in one of the CholQR forms (RowOpArgs: mode 1 Gram only, mode 2 two-stage
+// apply, Z for a cross Gram).  G: the Gram (mode 1) over all ranks; Gx: Z^T Y over all ranks
+// (reduced only when reduce_x).
+int rowop_ex(rbl_ctx* ctx, RowOpArgs a, double* G, double* Gx, bool reduce_x) {
+  const int b = ctx->b;
+  const int gmax = rowgram_grid(ctx->nloc, kRowgramMaxPerCu);
+  if ((size_t)2 * gmax * b * b > ctx->slab_elems)
+    return fail(ctx, RBL_ERR_INVALID, "internal: row-op slab too small");
+  if (G) a.slab = ctx->d_slab;
+  if (a.Z) a.slab2 = ctx->d_slab + (size_t)gmax * b * b;
+  // the cross-Gram launches (pass 2, and pass 3 when it runs) share one grid: the reduce
+  // after pass 3 does not know which of them wrote the partials last
+  const int xgrid = rowgram_grid(ctx->nloc, 2);
+  int grid = a.Z ? xgrid : 0;
+  a.grid_out = &grid;
+  if (ctx->nloc > 0 && !rowgram_ex(ctx->nloc, b, a, grid, ctx->stream))
+    return fail(ctx, RBL_ERR_INVALID, "internal: unsupported fused row-op form");
+  if (ctx->nloc <= 0) grid = 1;
+  HIPC(hipGetLastError());
+  if (G) {
+    reduce_slab(ctx->d_slab, grid, (int64_t)b * b, G, a.skip, ctx->stream);
+    CHK(allreduce(ctx, G, (size_t)b * b));
+  }
+  if (Gx && reduce_x) {
+    reduce_slab(ctx->d_slab + (size_t)gmax * b * b, xgrid, (int64_t)b * b, Gx, nullptr, ctx->stream);
+    CHK(allreduce(ctx, Gx, (size_t)b * b));
+  }
+  return RBL_OK;
+}
+
 // Tall-skinny QR of U (n_local x b) into Qout; B = R (b x b, upper, row-major) in S_RTOT.
 // Shifted CholQR2 (+ a third pass after a shifted first pass).  `g1_ready`: S_G already holds
 // U^T U (the fused 3-term update computed it); each apply computes the next pass's Gram in the
 // same pass over the rows when b allows (rowop).
 // Qout32 (fp32 basis): the final Q goes to Qout32 rounded to fp32 (Qout then holds only a
 // pass-2 intermediate when the shifted pass 3 runs).
-int tsqr(rbl_ctx* ctx, const double* U, double* Qout, bool g1_ready = false, float* Qout32 = nullptr) {
+// Zloc (fp64 basis, RBL_OPT_FUSE bit 1): also form Zloc^T Q into S_CLOC — the next step's
+// local-reorth coefficient (Zloc = Q_i, Q = Q_{i+1}).
+int tsqr(rbl_ctx* ctx, const double* U, double* Qout, bool g1_ready = false, float* Qout32 = nullptr,
+         const double* Zloc = nullptr) {
   StageScope t(ctx, RBL_STAGE_QR);
   const int b = ctx->b;
   int* need3 = ctx->d_flags;      // [need3, skip3]
@@ -844,6 +885,47 @@ int tsqr(rbl_ctx* ctx, const double* U, double* Qout, bool g1_ready = false, flo
   if (!g1_ready) CHK(gram(ctx, run1(U, b), pan1(U, b), G, nullptr));
   chol_step(G, b, ctx->n, 0, smallp(ctx, S_R), smallp(ctx, S_RINV), smallp(ctx, S_RTOT), need3,
             status, nullptr, ctx->stream, smallp(ctx, S_CHS0));
+  if (fused && (ctx->fuse & 1)) {
+    // 3 passes: G2 = Gram of Q1 = U R1^-1 without storing Q1; then Q = (U R1^-1) R2^-1 in
+    // one pass (Q1 recomputed bit for bit) — the same bits as the 4-pass form below
+    RowOpArgs a1;
+    a1.X = U;
+    a1.C = smallp(ctx, S_RINV);
+    a1.ldc = b;
+    a1.mode = 1;
+    CHK(rowop_ex(ctx, a1, G, nullptr, false));
+    copy_small(smallp(ctx, S_RINV), smallp(ctx, S_RINV1), (int64_t)b * b, ctx->stream);
+    chol_step(G, b, ctx->n, 1, smallp(ctx, S_R), smallp(ctx, S_RINV), smallp(ctx, S_RTOT), need3,
+              status, nullptr, ctx->stream, smallp(ctx, S_CHS0));
+    RowOpArgs a2;
+    a2.X = U;
+    a2.C = smallp(ctx, S_RINV1);
+    a2.C2 = smallp(ctx, S_RINV);
+    a2.ldc = b;
+    a2.Y = Qout;
+    a2.Y32 = Qout32;
+    a2.f64flag = Qout32 ? need3 : nullptr;
+    a2.Z = Zloc;
+    a2.mode = 2;
+    CHK(rowop_ex(ctx, a2, nullptr, Zloc ? smallp(ctx, S_CLOC) : nullptr, false));
+    // pass 3 only after a shifted first pass (device flag; kernels early-exit otherwise)
+    CHK(gram(ctx, run1(Qout, b), pan1(Qout, b), G, skip3));
+    chol_step(G, b, ctx->n, 1, smallp(ctx, S_R), smallp(ctx, S_RINV), smallp(ctx, S_RTOT), need3,
+              status, skip3, ctx->stream, smallp(ctx, S_CHS0));
+    RowOpArgs a3;
+    a3.X = Qout;
+    a3.C = smallp(ctx, S_RINV);
+    a3.ldc = b;
+    a3.Y = Qout;
+    a3.skip = skip3;
+    a3.Y32 = Qout32;
+    a3.Z = Zloc;
+    a3.mode = 0;
+    CHK(rowop_ex(ctx, a3, nullptr, Zloc ? smallp(ctx, S_CLOC) : nullptr, Zloc != nullptr));
+    HIPC(hipGetLastError());
+    return RBL_OK;
+  }
+  if (Zloc) return fail(ctx, RBL_ERR_INVALID, "internal: local-reorth Gram fusion needs the 3-pass QR");
   if (fused) {
     CHK(rowop(ctx, U, smallp(ctx, S_RINV), Qout, 1.0, 0.0, G, nullptr));
   } else {
@@ -1257,6 +1339,10 @@ int rbl_set_option(rbl_ctx* ctx, int option, int64_t value) {
       return RBL_OK;
     case RBL_OPT_SPLIT_HALO: ctx->split_halo = value != 0; return RBL_OK;
     case RBL_OPT_KEEP_CSR: ctx->keep_csr = value != 0; return RBL_OK;
+    case RBL_OPT_FUSE:
+      if (value < 0 || value > 3) return fail(ctx, RBL_ERR_INVALID, "RBL_OPT_FUSE is a 2-bit mask");
+      ctx->fuse = (int)value;
+      return RBL_OK;
     default: return fail(ctx, RBL_ERR_INVALID, "unknown option");
   }
 }
@@ -1629,6 +1715,8 @@ int rbl_start(rbl_ctx* ctx, int b, int max_blocks, int basis_bits, const double*
                      ctx->basis_bits == basis_bits &&
                      (ctx->resident == INT32_MAX ? max_blocks + 1 : ctx->resident + 2) == dev_slots;
   ctx->nlock = 0;  // a new problem: no locked vectors
+  ctx->cloc_step = 0;
+  ctx->step_flags.clear();
   if (reuse) {
     ctx->nblocks = 0;
     if (ctx->cstream) HIPC(hipStreamSynchronize(ctx->cstream));
@@ -1692,7 +1780,7 @@ int rbl_start(rbl_ctx* ctx, int b, int max_blocks, int basis_bits, const double*
       const size_t sp = (size_t)gram_splits(ctx->nloc, nW, b, xc);
       slab = std::max(slab, sp * nW * b * xc);
     }
-  slab = std::max(slab, (size_t)rowgram_grid(ctx->nloc) * b * b);  // rowop partials
+  slab = std::max(slab, (size_t)2 * rowgram_grid(ctx->nloc, kRowgramMaxPerCu) * b * b);  // rowop partials (+ cross Gram)
   if (basis_bits == 32)  // fp32 Grams: up to (max_blocks-1) panels x 2b per split
     slab = std::max(slab, (size_t)gram32_splits(ctx->nloc) * std::max(1, max_blocks - 1) * b * 2 * b);
   ctx->slab_elems = slab;
@@ -1867,14 +1955,24 @@ int step_impl(rbl_ctx* ctx, int i, int part_reorth, double* A_out, double* B_out
   }
   // local reorth: Q_i -= Q_{i-1} (Q_{i-1}^T Q_i), one projection (RBL_gpu.jl:83-93, P1)
   const bool fused = rowgram_ok(b);
+  // Q_i / Q_{i-1} change before the local reorth of this step iff it runs a partial or
+  // locked-vector reorth; otherwise the Gram formed by the previous step's QR is current
+  auto modifies = [&](int step, int flags) {
+    return ((flags & 1) && step >= 3) || ((flags & 2) && ctx->nlock > 0);
+  };
+  if ((int)ctx->step_flags.size() <= i) ctx->step_flags.resize(i + 1, 0);
+  ctx->step_flags[i] = part_reorth;
   if (!f32 && i >= 2) {
     StageScope t(ctx, RBL_STAGE_LOC_REORTH);
-    CHK(gram(ctx, run1(Qm, b), pan1(Qi, b), ctx->d_C, nullptr));
+    const bool have = ctx->cloc_step == i && !modifies(i, part_reorth);
+    const double* C = have ? smallp(ctx, S_CLOC) : ctx->d_C;
+    if (!have) CHK(gram(ctx, run1(Qm, b), pan1(Qi, b), ctx->d_C, nullptr));
     if (fused)
-      CHK(rowop(ctx, Qm, ctx->d_C, Qi, -1.0, 1.0, nullptr, nullptr));
+      CHK(rowop(ctx, Qm, C, Qi, -1.0, 1.0, nullptr, nullptr));
     else
-      CHK(tsmm_checked(ctx, run1(Qm, b), ctx->d_C, b, pan1(Qi, b), -1.0, 1.0, nullptr));
+      CHK(tsmm_checked(ctx, run1(Qm, b), C, b, pan1(Qi, b), -1.0, 1.0, nullptr));
   }
+  ctx->cloc_step = 0;
   // U = A Q_i - Q_{i-1} B_i^T   (RBL_gpu.jl:176-177)
   int ai_parts = 0;
   {
@@ -1929,7 +2027,13 @@ int step_impl(rbl_ctx* ctx, int i, int part_reorth, double* A_out, double* B_out
     ctx->d2h_pending[i & 1] = false;
   }
   if (!f32) {
-    CHK(tsqr(ctx, ctx->d_U, slotp(ctx, i), fused));
+    // the next step's local-reorth Gram Q_i^T Q_{i+1} rides on this QR when that step is
+    // expected to run no partial reorth (the schedule repeats with period 2 in RBL_gpu.jl:164,
+    // so step i + 1 is guessed from step i - 1; a wrong guess costs one pass, never bits)
+    const int guess = i >= 2 ? ctx->step_flags[i - 1] : 0;
+    const bool zfuse = fused && (ctx->fuse & 3) == 3 && !modifies(i + 1, guess) && i + 1 <= ctx->max_blocks;
+    CHK(tsqr(ctx, ctx->d_U, slotp(ctx, i), fused, nullptr, zfuse ? Qi : nullptr));
+    if (zfuse) ctx->cloc_step = i + 1;
   } else {  // Qg = FLOAT(Qg_d) (RBL_gpu.jl:182): the new block enters the basis rounded to fp32
     CHK(tsqr(ctx, ctx->d_U, ctx->d_Qi64, fused, slotp32(ctx, i)));
   }
@@ -2036,6 +2140,7 @@ int rbl_num_blocks(rbl_ctx* ctx) { return ctx ? ctx->nblocks : 0; }
 
 // ---- restarted variants (restarted.jl) -------------------------------------------------
 int rbl_restart(rbl_ctx* ctx, int nblocks, const double* S) {
+  if (ctx) ctx->cloc_step = 0;  // the basis changes outside the step
   if (!ctx || !S || nblocks < 1 || nblocks > ctx->nblocks)
     return fail(ctx, RBL_ERR_INVALID, "rbl_restart: bad arguments");
   if (!ctx->d_basis) return fail(ctx, RBL_ERR_STATE, "rbl_restart: needs an fp64 run (rbl_start)");
@@ -2053,6 +2158,7 @@ int rbl_restart(rbl_ctx* ctx, int nblocks, const double* S) {
 }
 
 int rbl_lock(rbl_ctx* ctx, int nblocks, int nvec, const double* S) {
+  if (ctx) ctx->cloc_step = 0;  // the basis changes outside the step
   if (!ctx || !S || nblocks < 1 || nblocks > ctx->nblocks || nvec < 0)
     return fail(ctx, RBL_ERR_INVALID, "rbl_lock: bad arguments");
   if (!ctx->d_basis) return fail(ctx, RBL_ERR_STATE, "rbl_lock: needs an fp64 run (rbl_start)");
@@ -2093,6 +2199,7 @@ int rbl_get_locked(rbl_ctx* ctx, double* V_out) {
 }
 
 int rbl_reorth_last(rbl_ctx* ctx, int nblocks, int flags) {
+  if (ctx) ctx->cloc_step = 0;  // the basis changes outside the step
   if (!ctx || nblocks < 1 || nblocks > ctx->nblocks)
     return fail(ctx, RBL_ERR_INVALID, "rbl_reorth_last: bad arguments");
   if (!ctx->d_basis) return fail(ctx, RBL_ERR_STATE, "rbl_reorth_last: needs an fp64 run");

@@ -30,6 +30,7 @@ RBL_OPT_SPMM_KERNEL = 2
 RBL_OPT_DEVICE_BLOCKS = 3
 RBL_OPT_SPLIT_HALO = 4
 RBL_OPT_KEEP_CSR = 5
+RBL_OPT_FUSE = 6
 
 _p = C.c_void_p
 _i64 = C.c_int64

@@ -79,6 +79,12 @@ extern "C" {
                                    * released — 12 B per nonzero of HBM for the Krylov basis
                                    * (n = 5e7: 60 GB).  Then only b in {16, 32} can run and
                                    * rbl_get_matrix_csr fails.  Set before the matrix.          */
+#define RBL_OPT_FUSE          6   /* pass fusions of the memory-bound b x b stages (b in {16, 32},
+                                   * fp64 basis), bit for bit the same results: bit 0 (default
+                                   * on) CholQR2 in 3 passes over the block instead of 4 (Q1 is
+                                   * recomputed, never stored); bit 1 (default on) the next
+                                   * step's local-reorth Gram Q_i^T Q_{i+1} formed while the QR
+                                   * writes Q_{i+1}, used when that step runs no partial reorth */
 
 typedef struct rbl_ctx rbl_ctx;
 

@@ -273,3 +273,26 @@ def test_dense_block_size_past_64(rbl):
     D, V, info = rbl.RBL_gpu(A, k, b, omega=omega, return_info=True)
     assert ref.converged and info.converged
     assert (np.abs(D - ref.D) / np.abs(ref.D)).max() < EIG_TOL
+
+
+@pytest.mark.parametrize("b,bits", [(16, 64), (32, 64), (32, 32)])
+def test_pass_fusions(rbl, b, bits):
+    """RBL_OPT_FUSE: the 3-pass CholQR2 (bit 0) gives the same bits as the 4-pass form; the
+    local-reorth Gram formed inside the QR (bit 1) agrees to rounding (1e-12 relative) —
+    over 12 steps of the C1-like matrix, per-step A_i and B_{i+1}."""
+    from rbl import _lib
+    A = c1_matrix(4000, 10)
+    n = A.shape[0]
+    omega = np.random.default_rng(b).standard_normal((n, b))
+    out = {}
+    for fuse in (0, 1, 3):
+        with rbl.Context(0) as ctx:
+            ctx.set_option(_lib.RBL_OPT_FUSE, fuse)
+            ctx.set_matrix(A)
+            _, _, info = rbl.lanczos(ctx, 10, b, omega=omega, check=False, max_steps=12,
+                                     trace=True, ritz=False, basis_bits=bits)
+        out[fuse] = (np.array(info.trace_A), np.array(info.trace_B))
+    assert np.array_equal(out[0][0], out[1][0]) and np.array_equal(out[0][1], out[1][1])
+    for t in (0, 1):
+        d = np.abs(out[3][t] - out[1][t]).max() / np.abs(out[1][t]).max()
+        assert d < 1e-12, (t, d)
