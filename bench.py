@@ -71,6 +71,9 @@ def parse():
     ap.add_argument("--keep-csr", type=int, default=1, choices=(0, 1),
                     help="0: release the device CSR once the band tiles are built "
                          "(RBL_OPT_KEEP_CSR; frees 12 B per nonzero for the basis at n = 5e7)")
+    ap.add_argument("--fuse", type=int, default=3, choices=(0, 1, 2, 3),
+                    help="RBL_OPT_FUSE: bit 0 the 3-pass CholQR2, bit 1 the local-reorth Gram formed "
+                         "by the producing QR / partial-reorth update (same results; A/B switch)")
     ap.add_argument("--basis-bits", type=int, default=64, choices=(64, 32),
                     help="32: the mixed mode (fp32 Krylov basis + reorth on fp32 MFMA, fp64 A*Q / "
                          "3-term / QR) of BASELINE config 5, on this workload")
@@ -214,6 +217,7 @@ def main():
     ctx.set_option(_lib.RBL_OPT_TIMERS, 1)
     ctx.set_option(_lib.RBL_OPT_SPMM_KERNEL, args.spmm_kernel)
     ctx.set_option(_lib.RBL_OPT_DEVICE_BLOCKS, args.device_blocks)
+    ctx.set_option(_lib.RBL_OPT_FUSE, args.fuse)
     m_max = rbl.rbl_gpu.max_steps_for(args.kryl, b)
     spmm_kid = ctx.spmm_kernel_for(b)
     spmm_kernel = {1: "gather", 2: "lds-window", 3: "lds-band-mfma", 5: "band-tile-mfma",
@@ -353,7 +357,8 @@ def main():
                        "transport": comm["transport"], "transport_ranks": comm["nranks"],
                        "nnz_per_rank": nnz_ranks,
                        **({"device_blocks": args.device_blocks} if args.device_blocks else {}),
-                       **({"keep_csr": 0} if not args.keep_csr else {})},
+                       **({"keep_csr": 0} if not args.keep_csr else {}),
+                       **({"fuse": args.fuse} if args.fuse != 3 else {})},
             "roofline": roofline,
             "roofline_secondary": roofline2,
             "stage_ms_per_run": {s: round(v, 3) for s, v in stage_per_run.items()},

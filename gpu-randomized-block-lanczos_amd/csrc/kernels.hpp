@@ -185,7 +185,8 @@ void reduce_slab(const double* slab, int splits, int64_t len, double* out, const
 // Y = beta*Y + alpha * X * C, X a run of panels (k = nX*X.w), C row-major k x (Y.count*Y.w)
 // with leading dimension ldc.  Y may alias X's panels row-for-row (in-place apply).
 void tsmm(int64_t nrows, const PanelRun& X, const double* C, int ldc, const Panels& Y,
-          double alpha, double beta, const int* skip, hipStream_t s);
+          double alpha, double beta, const int* skip, hipStream_t s, double* xslab = nullptr,
+          int* xgrid = nullptr);
 
 // --- reorth.hip: v_mfma_f64_4x4x4f64 fast paths (panel widths 16 / 32), selected by
 // gram_splits / gram_partial / tsmm above when applicable.
@@ -198,8 +199,13 @@ bool tsmm44_ok(int xw, int ky, int yw);
 // projection over the fp32 basis in one pass (fp64 S and V).  Same shape limits as tsmm44.
 void tsmm44_f32x(int64_t nrows, const PanelRun& X, const double* C, int ldc, const Panels& Y,
                  double alpha, double beta, hipStream_t s);
+// xslab (optional, Y = [Q_i, Q_{i-1}] of width 32 on the 64-column fast path): also the
+// partials of Q_{i-1}^T Q_i, *xgrid = tsmm44_xg_grid(nrows) blocks of 32 x 32 in xslab (one per
+// 128-row tile; reduce_slab over *xgrid); *xgrid = 0 when this form does not apply.
+int tsmm44_xg_grid(int64_t nrows);
 void tsmm44(int64_t nrows, const PanelRun& X, const double* C, int ldc, const Panels& Y,
-            double alpha, double beta, const int* skip, hipStream_t s);
+            double alpha, double beta, const int* skip, hipStream_t s, double* xslab = nullptr,
+            int* xgrid = nullptr);
 
 // --- reorth32.hip: the fp32 Krylov basis (mixed precision, b in {16, 32}) ---------------
 // Gram partials slab[s][a][c] = sum over split s of W[r][a] X[r][c] (W: nW fp32 panels of

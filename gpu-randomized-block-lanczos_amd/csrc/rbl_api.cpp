@@ -121,9 +121,10 @@ struct rbl_ctx {
   int reorth_order = 0;
   int spmm_variant = 0;
   int fuse = 3;               // RBL_OPT_FUSE
-  // the local-reorth coefficient Q_{i-1}^T Q_i of step cloc_step, formed by the QR of step
-  // cloc_step - 1 (S_CLOC); 0: none
+  // the local-reorth coefficient Q_{i-1}^T Q_i of step cloc_step (S_CLOC), formed by the QR of
+  // step cloc_step - 1 or by the last partial-reorth update of step cloc_step; 0: none
   int cloc_step = 0;
+  bool cloc_final = false;    // formed after this step's reorth (valid whatever its flags)
   std::vector<int> step_flags;  // part_reorth flags per step (the fusion's schedule guess)
   double stage_ms[RBL_NUM_STAGES] = {0};
   struct Mark { int stage; hipEvent_t a, b; };
@@ -586,9 +587,11 @@ enum { S_R = 0, S_RINV, S_RTOT, S_BPREV, S_AI, S_G, S_BT, S_CHS0, S_CHS1, S_RINV
 double* smallp(rbl_ctx* ctx, int which) { return ctx->d_small + (int64_t)which * ctx->b * ctx->b; }
 
 int tsmm_checked(rbl_ctx* ctx, const PanelRun& X, const double* C, int ldc, const Panels& Y,
-                 double alpha, double beta, const int* skip) {
+                 double alpha, double beta, const int* skip, double* xslab = nullptr,
+                 int* xgrid = nullptr) {
+  if (xgrid) *xgrid = 0;
   if (ctx->nloc <= 0) return RBL_OK;
-  tsmm(ctx->nloc, X, C, ldc, Y, alpha, beta, skip, ctx->stream);
+  tsmm(ctx->nloc, X, C, ldc, Y, alpha, beta, skip, ctx->stream, xslab, xgrid);
   HIPC(hipGetLastError());
   return RBL_OK;
 }
@@ -701,6 +704,15 @@ int reorth_pair(rbl_ctx* ctx, int i, int flags) {
     StageScope t(ctx, RBL_STAGE_PART_REORTH);
     const int nW = i - 2;
     const int nres = std::min(nW, ctx->resident);  // HBM-resident part of W
+    // the last update of the pair also forms this step's local-reorth Gram Q_{i-1}^T Q_i
+    // (RBL_OPT_FUSE bit 1; the 64-column fast path at b = 32 only)
+    const bool xg = (ctx->fuse & 2) && b == 32 && ctx->nloc >= 32 &&
+                    (size_t)tsmm44_xg_grid(ctx->nloc) * b * b <= ctx->slab_elems;
+    int xgrid = 0;
+    auto update = [&](const PanelRun& W, bool last) -> int {
+      return tsmm_checked(ctx, W, ctx->d_C, 2 * b, pan2(Qi, Qm, b), -1.0, 1.0, nullptr,
+                          xg && last ? ctx->d_slab : nullptr, xg && last ? &xgrid : nullptr);
+    };
     if (ctx->reorth_order == 0) {  // block CGS: one Gram over every resident j, one update
       PanelRun W;
       W.base = slotp(ctx, 0);
@@ -708,12 +720,12 @@ int reorth_pair(rbl_ctx* ctx, int i, int flags) {
       W.count = nres;
       W.w = b;
       CHK(gram(ctx, W, pan2(Qi, Qm, b), ctx->d_C, nullptr));
-      CHK(tsmm_checked(ctx, W, ctx->d_C, 2 * b, pan2(Qi, Qm, b), -1.0, 1.0, nullptr));
+      CHK(update(W, nres == nW));
     } else {  // ascending-j block MGS, exactly the reference order
       for (int j = 0; j < nres; ++j) {
         const PanelRun W = run1(slotp(ctx, j), b);
         CHK(gram(ctx, W, pan2(Qi, Qm, b), ctx->d_C, nullptr));
-        CHK(tsmm_checked(ctx, W, ctx->d_C, 2 * b, pan2(Qi, Qm, b), -1.0, 1.0, nullptr));
+        CHK(update(W, j == nW - 1));
       }
     }
     // spilled blocks (host, final): streamed back one at a time, ascending j, each applied
@@ -724,7 +736,13 @@ int reorth_pair(rbl_ctx* ctx, int i, int flags) {
       const double* Wj = block_dev(ctx, j, i, &st);
       if (st) return fail(ctx, st, "partial reorth: H2D of a spilled block failed");
       CHK(gram(ctx, run1(Wj, b), pan2(Qi, Qm, b), ctx->d_C, nullptr));
-      CHK(tsmm_checked(ctx, run1(Wj, b), ctx->d_C, 2 * b, pan2(Qi, Qm, b), -1.0, 1.0, nullptr));
+      CHK(update(run1(Wj, b), j == nW - 1));
+    }
+    if (xgrid > 0) {  // the partials of the last update (its Gram slab was reduced before it)
+      reduce_slab(ctx->d_slab, xgrid, (int64_t)b * b, smallp(ctx, S_CLOC), nullptr, ctx->stream);
+      CHK(allreduce(ctx, smallp(ctx, S_CLOC), (size_t)b * b));
+      ctx->cloc_step = i;
+      ctx->cloc_final = true;
     }
   }
   return RBL_OK;
@@ -1781,6 +1799,10 @@ int rbl_start(rbl_ctx* ctx, int b, int max_blocks, int basis_bits, const double*
       slab = std::max(slab, sp * nW * b * xc);
     }
   slab = std::max(slab, (size_t)2 * rowgram_grid(ctx->nloc, kRowgramMaxPerCu) * b * b);  // rowop partials (+ cross Gram)
+  // the partial-reorth update's local-reorth Gram partials (b = 32: one per 128-row tile,
+  // n_local / 4 doubles, a quarter of a block)
+  if (b == 32 && basis_bits == 64 && (ctx->fuse & 2))
+    slab = std::max(slab, (size_t)tsmm44_xg_grid(ctx->nloc) * b * b);
   if (basis_bits == 32)  // fp32 Grams: up to (max_blocks-1) panels x 2b per split
     slab = std::max(slab, (size_t)gram32_splits(ctx->nloc) * std::max(1, max_blocks - 1) * b * 2 * b);
   ctx->slab_elems = slab;
@@ -1964,7 +1986,7 @@ int step_impl(rbl_ctx* ctx, int i, int part_reorth, double* A_out, double* B_out
   ctx->step_flags[i] = part_reorth;
   if (!f32 && i >= 2) {
     StageScope t(ctx, RBL_STAGE_LOC_REORTH);
-    const bool have = ctx->cloc_step == i && !modifies(i, part_reorth);
+    const bool have = ctx->cloc_step == i && (ctx->cloc_final || !modifies(i, part_reorth));
     const double* C = have ? smallp(ctx, S_CLOC) : ctx->d_C;
     if (!have) CHK(gram(ctx, run1(Qm, b), pan1(Qi, b), ctx->d_C, nullptr));
     if (fused)
@@ -1973,6 +1995,7 @@ int step_impl(rbl_ctx* ctx, int i, int part_reorth, double* A_out, double* B_out
       CHK(tsmm_checked(ctx, run1(Qm, b), C, b, pan1(Qi, b), -1.0, 1.0, nullptr));
   }
   ctx->cloc_step = 0;
+  ctx->cloc_final = false;
   // U = A Q_i - Q_{i-1} B_i^T   (RBL_gpu.jl:176-177)
   int ai_parts = 0;
   {
@@ -2033,7 +2056,10 @@ int step_impl(rbl_ctx* ctx, int i, int part_reorth, double* A_out, double* B_out
     const int guess = i >= 2 ? ctx->step_flags[i - 1] : 0;
     const bool zfuse = fused && (ctx->fuse & 3) == 3 && !modifies(i + 1, guess) && i + 1 <= ctx->max_blocks;
     CHK(tsqr(ctx, ctx->d_U, slotp(ctx, i), fused, nullptr, zfuse ? Qi : nullptr));
-    if (zfuse) ctx->cloc_step = i + 1;
+    if (zfuse) {
+      ctx->cloc_step = i + 1;
+      ctx->cloc_final = false;
+    }
   } else {  // Qg = FLOAT(Qg_d) (RBL_gpu.jl:182): the new block enters the basis rounded to fp32
     CHK(tsqr(ctx, ctx->d_U, ctx->d_Qi64, fused, slotp32(ctx, i)));
   }

@@ -440,10 +440,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
 #ifndef RBL_T44_PF
 #define RBL_T44_PF 1
 #endif
-template <int B, int KC = RBL_T44_KC, int PF = RBL_T44_PF>
+// XG (Y = [Q_i | Q_{i-1}], 32 columns each): each workgroup also forms Q_{i-1}^T Q_i over its
+// final rows (16x16x4 MFMAs from the output stage) into xslab[blockIdx] (one 32 x 32 partial
+// per 128-row tile) — the local-reorth coefficient of the same step (RBL_gpu.jl:87), formed
+// while the partial-reorth update writes the blocks instead of in another pass over both.
+template <int B, int KC = RBL_T44_KC, int PF = RBL_T44_PF, bool XG = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k_tsmm44f(
     int64_t nrows, PanelRun X, const double* __restrict__ C, int ldc, Panels Y, double alpha,
-    double beta, const int* skip) {
+    double beta, const int* skip, double* __restrict__ xslab) {
   if (skip && *skip) return;
   constexpr int KYP = 64, CG = KYP / 4, LDC = KYP + 8;
   constexpr int NH = KC / 8;  // 16-B A loads per row tile per chunk
@@ -454,9 +458,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int q = lane >> 4;
-  const int64_t r0 = ((int64_t)blockIdx.x * 4 + wave) * kT44Rows;
-  const int64_t rw = r0 + kT44Rows <= nrows ? r0 : nrows - kT44Rows;  // wave-uniform
   const int nch = X.count * B / KC;
+  const int64_t ntiles = (nrows + 4 * kT44Rows - 1) / (4 * kT44Rows);
+  // one 128-row tile per workgroup, or (XG) persistent over tiles
+  auto tile_body = [&](int64_t tile) {
+  typedef double d4x __attribute__((ext_vector_type(4)));
+  d4x gx[XG ? 2 : 1][XG ? 2 : 1];
+  if constexpr (XG) {
+#pragma unroll
+    for (int it = 0; it < 2; ++it)
+#pragma unroll
+      for (int jt = 0; jt < 2; ++jt) gx[it][jt] = d4x{0.0, 0.0, 0.0, 0.0};
+  }
+  const int64_t r0 = (tile * 4 + wave) * kT44Rows;
+  const int64_t rw = r0 + kT44Rows <= nrows ? r0 : nrows - kT44Rows;  // wave-uniform
 
   double acc[2][CG];
 #pragma unroll
@@ -557,14 +572,55 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
       const int e = 2 * lane + 128 * m, row = e / KYP, c = e % KYP;
       const int64_t r = rw + 16 * rt + row;
       d2v v = *reinterpret_cast<const d2v*>(ot + row * KYP + (c ^ (4 * ((row >> 2) & 3))));
-      if (r >= r0 && r < nrows) {
+      const bool own = r >= r0 && r < nrows;
+      if (own) {
         const int t = c / Y.w;
         d2v* yp = reinterpret_cast<d2v*>(const_cast<double*>(Y.ptr[t]) + r * Y.w + (c - t * Y.w));
         if (beta != 0.0) v += beta * *yp;
         *yp = v;
       }
+      if constexpr (XG)  // final values back into the stage (0 for rows this wave does not own)
+        *reinterpret_cast<d2v*>(ot + row * KYP + (c ^ (4 * ((row >> 2) & 3)))) = own ? v : d2v{0.0, 0.0};
+    }
+    if constexpr (XG) {
+      // (Q_{i-1}^T Q_i)[16 it + .][16 jt + .] += sum over the 16 rows; row 4 s4 + q sits at
+      // column c ^ (4 s4) of the stage
+      const int li = lane & 15;
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4) {
+        const double* orow = ot + (4 * s4 + q) * KYP;
+        double za[2], yb[2];
+#pragma unroll
+        for (int t2 = 0; t2 < 2; ++t2) {
+          za[t2] = orow[(32 + 16 * t2 + li) ^ (4 * s4)];
+          yb[t2] = orow[(16 * t2 + li) ^ (4 * s4)];
+        }
+#pragma unroll
+        for (int it = 0; it < 2; ++it)
+#pragma unroll
+          for (int jt = 0; jt < 2; ++jt)
+            gx[it][jt] = __builtin_amdgcn_mfma_f64_16x16x4f64(za[it], yb[jt], gx[it][jt], 0, 0, 0);
+      }
     }
   }
+  if constexpr (XG) {
+    // the four waves' partials summed in LDS (fixed order), one 32 x 32 partial per workgroup
+    __syncthreads();
+    const int li = lane & 15;
+    double* gw = cs_raw + wave * 1024;
+#pragma unroll
+    for (int it = 0; it < 2; ++it)
+#pragma unroll
+      for (int jt = 0; jt < 2; ++jt)
+#pragma unroll
+        for (int reg = 0; reg < 4; ++reg) gw[(16 * it + q + 4 * reg) * 32 + 16 * jt + li] = gx[it][jt][reg];
+    __syncthreads();
+    double* out = xslab + tile * 1024;
+    for (int e = tid; e < 1024; e += 256)
+      out[e] = (cs_raw[e] + cs_raw[1024 + e]) + (cs_raw[2048 + e] + cs_raw[3072 + e]);
+  }
+  };
+  tile_body(blockIdx.x);
 }
 
 // the epilogue stores Y row-major 16 B (two columns) per lane: Y panel widths must be even
@@ -594,8 +650,14 @@ void tsmm44_f32x(int64_t nrows, const PanelRun& X, const double* C, int ldc, con
   return launch_tsmm44<16, 64, true>(nrows, X, C, ldc, KY, Y, alpha, beta, nullptr, st);
 }
 
+int tsmm44_xg_grid(int64_t nrows) {
+  // one partial per 128-row tile
+  return (int)((nrows + 4 * kT44Rows - 1) / (4 * kT44Rows));
+}
+
 void tsmm44(int64_t nrows, const PanelRun& X, const double* C, int ldc, const Panels& Y,
-            double alpha, double beta, const int* skip, hipStream_t st) {
+            double alpha, double beta, const int* skip, hipStream_t st, double* xslab, int* xgrid) {
+  if (xgrid) *xgrid = 0;
   const int KY = Y.count * Y.w;
   static const bool fast_ok = [] {
     const char* e = getenv("RBL_TSMM44_FAST");
@@ -603,12 +665,23 @@ void tsmm44(int64_t nrows, const PanelRun& X, const double* C, int ldc, const Pa
   }();
   if (fast_ok && KY == 64 && (X.count * X.w) % kT44K == 0 && nrows >= kT44Rows && Y.w % 2 == 0) {
     const int64_t wgs = (nrows + 4 * kT44Rows - 1) / (4 * kT44Rows);
+    if (xslab && Y.w == 32 && Y.count == 2) {
+      const int grid = (int)wgs;
+      *xgrid = grid;
+      if (X.w == 32)
+        hipLaunchKernelGGL((k_tsmm44f<32, RBL_T44_KC, RBL_T44_PF, true>), dim3(grid), dim3(256), 0, st, nrows,
+                           X, C, ldc, Y, alpha, beta, skip, xslab);
+      else
+        hipLaunchKernelGGL((k_tsmm44f<16, RBL_T44_KC, RBL_T44_PF, true>), dim3(grid), dim3(256), 0, st, nrows,
+                           X, C, ldc, Y, alpha, beta, skip, xslab);
+      return;
+    }
     if (X.w == 32)
       hipLaunchKernelGGL((k_tsmm44f<32>), dim3((unsigned)wgs), dim3(256), 0, st, nrows, X, C, ldc, Y,
-                         alpha, beta, skip);
+                         alpha, beta, skip, nullptr);
     else
       hipLaunchKernelGGL((k_tsmm44f<16>), dim3((unsigned)wgs), dim3(256), 0, st, nrows, X, C, ldc, Y,
-                         alpha, beta, skip);
+                         alpha, beta, skip, nullptr);
     return;
   }
   if (X.w == 32) {

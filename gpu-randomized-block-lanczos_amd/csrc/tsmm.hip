@@ -287,8 +287,10 @@ static void launch_tsmm_t(int64_t nrows, const PanelRun& X, const double* C, int
 }
 
 void tsmm(int64_t nrows, const PanelRun& X, const double* C, int ldc, const Panels& Y,
-          double alpha, double beta, const int* skip, hipStream_t s) {
-  if (tsmm44_ok(X.w, Y.count * Y.w, Y.w)) return tsmm44(nrows, X, C, ldc, Y, alpha, beta, skip, s);
+          double alpha, double beta, const int* skip, hipStream_t s, double* xslab, int* xgrid) {
+  if (xgrid) *xgrid = 0;
+  if (tsmm44_ok(X.w, Y.count * Y.w, Y.w))
+    return tsmm44(nrows, X, C, ldc, Y, alpha, beta, skip, s, xslab, xgrid);
   const int ctt = tiles16(Y.count * Y.w);
   const int ct = ctt <= 1 ? 1 : (ctt <= 2 ? 2 : 4);
   const int ncg = (ctt + ct - 1) / ct;

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <vector>
 
 #include "../gpu-randomized-block-lanczos_amd/csrc/kernels.hpp"
@@ -36,6 +37,11 @@ int main(int argc, char** argv) {
   (void)hipMalloc(&C, (size_t)nWmax * b * 64 * 8);
   fill(C, nWmax * b * 64, 4);
   (void)hipMalloc(&Cg, (size_t)nWmax * b * 64 * 8);
+  // PROBE_XG=1: the update also forms Q_{i-1}^T Q_i (the fused local-reorth Gram)
+  const bool xg = getenv("PROBE_XG") && atoi(getenv("PROBE_XG"));
+  double* xslab = nullptr;
+  int xgrid = 0;
+  if (hipMalloc(&xslab, (size_t)rbl::tsmm44_xg_grid(n) * 1024 * 8) != hipSuccess) return 1;
   hipEvent_t e0, e1, e2;
   (void)hipEventCreate(&e0);
   (void)hipEventCreate(&e1);
@@ -59,7 +65,7 @@ int main(int argc, char** argv) {
       rbl::gram44_partial(n, Wr, X, slab, splits, nullptr, 0);
       rbl::reduce_slab(slab, splits, (int64_t)nW * b * 64, Cg, nullptr, 0);  // C stays fixed: X must not blow up
       (void)hipEventRecord(e1);
-      rbl::tsmm44(n, Wr, C, 64, X, -1.0, 1.0, nullptr, 0);
+      rbl::tsmm44(n, Wr, C, 64, X, -1.0, 1.0, nullptr, 0, xg ? xslab : nullptr, &xgrid);
       (void)hipEventRecord(e2);
       (void)hipEventSynchronize(e2);
       float g, t;
