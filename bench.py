@@ -58,6 +58,10 @@ def parse():
                     help="also time the CPU baseline with 1 BLAS thread (benchmark.jl:49)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-ttk", action="store_true")
+    ap.add_argument("--no-ttk-slow", action="store_true",
+                    help="skip the second time-to-k on a slowly decaying planted spectrum "
+                         "(12 + 0.25 (2k+1-l), l = 1..2k: its top eigenvalues sit just above the "
+                         "bulk, as the reference's slow_dec suite, so convergence takes ~24 steps)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     ap.add_argument("--spmm-kernel", type=int, default=0)
     ap.add_argument("--matrix", default="hashwindow", choices=("hashwindow", "rmat"),
@@ -326,6 +330,30 @@ def main():
                "ritz_ms": round(allmax(ttk_stage["Ritz vectors"]), 3),
                "stage_ms": {s_: round(v, 3) for s_, v in ttk_stage.items()}}
 
+    # ---- time-to-k on a slowly decaying spectrum (same generator and n, another plant) ----
+    ttk_slow = None
+    if not args.no_ttk and not args.no_ttk_slow and args.matrix == "hashwindow":
+        slow_plant = np.array([12.0 + 0.25 * (2 * k + 1 - l) for l in range(1, 2 * k + 1)])
+        ctx.gen_hashwindow(n, args.halfwidth, args.density, args.seed, slow_plant)
+        # one untimed start + step builds the band tiles and run buffers of the new matrix
+        rbl.lanczos(ctx, k, b, kryl_sz=args.kryl, seed=args.seed + 2, check=False, ritz=False,
+                    max_steps=2, basis_bits=args.basis_bits)
+        barrier()
+        ctx.synchronize()
+        ctx.reset_timers()
+        t0 = time.perf_counter()
+        D, V, info = rbl.lanczos(ctx, k, b, kryl_sz=args.kryl, seed=args.seed + 2, check=True,
+                                 ritz=True, basis_bits=args.basis_bits)
+        ctx.synchronize()
+        barrier()
+        ts = allmax(time.perf_counter() - t0)
+        st_ = ctx.timers()
+        ttk_slow = {"seconds": round(ts, 4), "iters": info.iters, "converged": info.converged,
+                    "k": k, "spectrum": "planted 12 + 0.25 (2k+1-l), l = 1..2k",
+                    "top_eigenvalues": [round(float(x), 6) for x in D[:3]],
+                    "kth_eigenvalue": round(float(D[k - 1]), 6),
+                    "stage_ms": {s_: round(v, 3) for s_, v in st_.items()}}
+
     # ---- CPU baseline: the oracle (port of RBL.jl) on a bounded sample, rank 0, N = 1 ----
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -363,6 +391,7 @@ def main():
             "roofline_secondary": roofline2,
             "stage_ms_per_run": {s: round(v, 3) for s, v in stage_per_run.items()},
             "time_to_k": ttk,
+            "time_to_k_slow_spectrum": ttk_slow,
             "matrix_gen_s": round(gen_s, 3),
             "cpu_baseline": cpu,
         }
