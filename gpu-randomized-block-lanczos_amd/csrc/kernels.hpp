@@ -199,8 +199,8 @@ bool tsmm44_ok(int xw, int ky, int yw);
 // projection over the fp32 basis in one pass (fp64 S and V).  Same shape limits as tsmm44.
 void tsmm44_f32x(int64_t nrows, const PanelRun& X, const double* C, int ldc, const Panels& Y,
                  double alpha, double beta, hipStream_t s);
-// xslab (optional, Y = [Q_i, Q_{i-1}] of width 32 on the 64-column fast path): also the
-// partials of Q_{i-1}^T Q_i, *xgrid = tsmm44_xg_grid(nrows) blocks of 32 x 32 in xslab (one per
+// xslab (optional, Y = [Q_i, Q_{i-1}] of width w = 16 or 32 on the fast path): also the
+// partials of Q_{i-1}^T Q_i, *xgrid = tsmm44_xg_grid(nrows) blocks of w x w in xslab (one per
 // 128-row tile; reduce_slab over *xgrid); *xgrid = 0 when this form does not apply.
 int tsmm44_xg_grid(int64_t nrows);
 void tsmm44(int64_t nrows, const PanelRun& X, const double* C, int ldc, const Panels& Y,

@@ -705,7 +705,7 @@ int reorth_pair(rbl_ctx* ctx, int i, int flags) {
     const int nW = i - 2;
     const int nres = std::min(nW, ctx->resident);  // HBM-resident part of W
     // the last update of the pair also forms this step's local-reorth Gram Q_{i-1}^T Q_i
-    // (RBL_OPT_FUSE bit 1; the 64-column fast path at b = 32 only)
+    // (RBL_OPT_FUSE bit 1; the update's 64-column fast path: b = 32)
     const bool xg = (ctx->fuse & 2) && b == 32 && ctx->nloc >= 32 &&
                     (size_t)tsmm44_xg_grid(ctx->nloc) * b * b <= ctx->slab_elems;
     int xgrid = 0;
@@ -1799,8 +1799,8 @@ int rbl_start(rbl_ctx* ctx, int b, int max_blocks, int basis_bits, const double*
       slab = std::max(slab, sp * nW * b * xc);
     }
   slab = std::max(slab, (size_t)2 * rowgram_grid(ctx->nloc, kRowgramMaxPerCu) * b * b);  // rowop partials (+ cross Gram)
-  // the partial-reorth update's local-reorth Gram partials (b = 32: one per 128-row tile,
-  // n_local / 4 doubles, a quarter of a block)
+  // the partial-reorth update's local-reorth Gram partials (one b x b per 128-row tile:
+  // n_local b^2 / 128 doubles, a quarter of a block at b = 32)
   if (b == 32 && basis_bits == 64 && (ctx->fuse & 2))
     slab = std::max(slab, (size_t)tsmm44_xg_grid(ctx->nloc) * b * b);
   if (basis_bits == 32)  // fp32 Grams: up to (max_blocks-1) panels x 2b per split

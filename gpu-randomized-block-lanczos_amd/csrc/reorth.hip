@@ -60,12 +60,15 @@ constexpr int kG44Waves = 4;
 #endif
 constexpr int kG44Rows = RBL_G44_ROWS;
 
-template <int B, int NX, int NPH>
+// PAIR (B = 16): a wave's "panel" j is the pair of basis panels 2j, 2j+1 (32 columns, as one
+// B = 32 panel: the same registers and MFMAs per chunk), so b = 16 runs the b = 32 tile shape
+template <int B, int NX, int NPH, bool PAIR = false>
 __device__ __forceinline__ void gram44_body(int64_t r_begin, int64_t r_end, int64_t s, int pg,
                                             int r, const PanelRun& W, const Panels& X,
                                             double* slab, double* xs_base) {
   constexpr int KC = NX * B;
-  constexpr int AG = B / 16;
+  constexpr int WB = PAIR ? 2 * B : B;  // basis columns per wave
+  constexpr int AG = WB / 16;
   constexpr int CG = KC / 4;
   constexpr int CGP = CG / NPH;  // column groups of this wave (even: read in pairs)
   constexpr int LD = KC + 8;     // rows of a ds_read_b128 lane group differ by one: disjoint banks
@@ -95,7 +98,9 @@ __device__ __forceinline__ void gram44_body(int64_t r_begin, int64_t r_end, int6
   const int xe0 = tid * EPT;
   const int xrow = xe0 / KC, xcol = xe0 % KC;
   const double* xsl = X.ptr[xcol / B] + (xcol % B) + (int64_t)xrow * B;
-  const double* wl = W.base + (int64_t)j * W.stride + (lane & 15) + q * B;
+  // column group ag of the wave's panel (PAIR: ag = the pair member)
+  const double* wl = W.base + (int64_t)(PAIR ? 2 * j : j) * W.stride + (lane & 15) + q * B;
+  const int64_t wag = PAIR ? W.stride : 16;
   auto shift = [&](int64_t rc0) -> int64_t { return rc0 < r_end - kG44Rows ? rc0 : r_end - kG44Rows; };
   auto load_x = [&](int64_t rc0, double (&xr)[EPT]) {
     const double* p = xsl + shift(rc0) * B;
@@ -113,7 +118,7 @@ __device__ __forceinline__ void gram44_body(int64_t r_begin, int64_t r_end, int6
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
-      for (int ag = 0; ag < AG; ++ag) ar[ks][ag] = ldw(p + 4 * ks * B + 16 * ag);
+      for (int ag = 0; ag < AG; ++ag) ar[ks][ag] = ldw(p + 4 * ks * B + wag * ag);
   };
 
   const int64_t nchunks = r_end > r_begin ? (r_end - r_begin + kG44Rows - 1) / kG44Rows : 0;
@@ -197,7 +202,7 @@ __device__ __forceinline__ void gram44_body(int64_t r_begin, int64_t r_end, int6
 #endif
   if (!active) return;
   const int KW = W.count * B;
-  double* out = slab + (s * KW + (int64_t)j * B) * KC + 4 * (2 * cp0);
+  double* out = slab + (s * KW + (int64_t)j * WB) * KC + 4 * (2 * cp0);
   const int g = (lane >> 2) & 3;
 #pragma unroll
   for (int ag = 0; ag < AG; ++ag)
@@ -209,7 +214,7 @@ __device__ __forceinline__ void gram44_body(int64_t r_begin, int64_t r_end, int6
     }
 }
 
-template <int B, int NX>
+template <int B, int NX, bool PAIR = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RBL_G44_WPE))) void k_gram44(
     int64_t nrows, PanelRun W, Panels X, double* slab, int npg, int64_t rows_per, const int* skip) {
   if (skip && *skip) return;
@@ -226,11 +231,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RBL_G44_WPE
   const int64_t s = (int64_t)(t / npg) * 8 + xcd;
   const int64_t r_begin = s * rows_per;
   const int64_t r_end = r_begin + rows_per < nrows ? r_begin + rows_per : nrows;
-  const int rem = W.count - pg * kG44Waves;
+  const int rem = (PAIR ? W.count / 2 : W.count) - pg * kG44Waves;
   const int r = rem < kG44Waves ? rem : kG44Waves;  // panels in this group (workgroup-uniform)
-  if (r >= 3) gram44_body<B, NX, 1>(r_begin, r_end, s, pg, r, W, X, slab, xs);
-  else if (r == 2) gram44_body<B, NX, NPH2>(r_begin, r_end, s, pg, r, W, X, slab, xs);
-  else gram44_body<B, NX, NPH4>(r_begin, r_end, s, pg, r, W, X, slab, xs);
+  if (r >= 3) gram44_body<B, NX, 1, PAIR>(r_begin, r_end, s, pg, r, W, X, slab, xs);
+  else if (r == 2) gram44_body<B, NX, NPH2, PAIR>(r_begin, r_end, s, pg, r, W, X, slab, xs);
+  else gram44_body<B, NX, NPH4, PAIR>(r_begin, r_end, s, pg, r, W, X, slab, xs);
 }
 
 bool gram44_ok(int64_t nrows, int nW, int w, int xcount, int xw) {
@@ -249,13 +254,14 @@ int gram44_splits(int64_t nrows, int nW) {
   return (int)(s8 * 8);
 }
 
-template <int B, int NX>
+template <int B, int NX, bool PAIR = false>
 static void launch_gram44(int64_t nrows, const PanelRun& W, const Panels& X, double* slab,
                           int splits, const int* skip, hipStream_t st) {
-  const int npg = (W.count + kG44Waves - 1) / kG44Waves;
+  const int units = PAIR ? W.count / 2 : W.count;
+  const int npg = (units + kG44Waves - 1) / kG44Waves;
   int64_t rows_per = (nrows + splits - 1) / splits;
   rows_per = (rows_per + kG44Rows - 1) / kG44Rows * kG44Rows;
-  hipLaunchKernelGGL((k_gram44<B, NX>), dim3(npg * splits), dim3(256), 0, st, nrows, W, X, slab,
+  hipLaunchKernelGGL((k_gram44<B, NX, PAIR>), dim3(npg * splits), dim3(256), 0, st, nrows, W, X, slab,
                      npg, rows_per, skip);
 }
 
@@ -264,6 +270,15 @@ void gram44_partial(int64_t nrows, const PanelRun& W, const Panels& X, double* s
   if (W.w == 32) {
     if (X.count == 2) return launch_gram44<32, 2>(nrows, W, X, slab, splits, skip, st);
     return launch_gram44<32, 1>(nrows, W, X, slab, splits, skip, st);
+  }
+  // b = 16 with an even panel count (partial reorth: i - 2 panels at even i): panel pairs
+  static const bool pair_ok = [] {
+    const char* e = getenv("RBL_G44_PAIR");
+    return !e || atoi(e) != 0;
+  }();
+  if (pair_ok && W.count % 2 == 0) {
+    if (X.count == 2) return launch_gram44<16, 2, true>(nrows, W, X, slab, splits, skip, st);
+    return launch_gram44<16, 1, true>(nrows, W, X, slab, splits, skip, st);
   }
   if (X.count == 2) return launch_gram44<16, 2>(nrows, W, X, slab, splits, skip, st);
   return launch_gram44<16, 1>(nrows, W, X, slab, splits, skip, st);
@@ -444,12 +459,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
 // final rows (16x16x4 MFMAs from the output stage) into xslab[blockIdx] (one 32 x 32 partial
 // per 128-row tile) — the local-reorth coefficient of the same step (RBL_gpu.jl:87), formed
 // while the partial-reorth update writes the blocks instead of in another pass over both.
-template <int B, int KC = RBL_T44_KC, int PF = RBL_T44_PF, bool XG = false>
+template <int B, int KC = RBL_T44_KC, int PF = RBL_T44_PF, bool XG = false, int KYP = 64>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k_tsmm44f(
     int64_t nrows, PanelRun X, const double* __restrict__ C, int ldc, Panels Y, double alpha,
     double beta, const int* skip, double* __restrict__ xslab) {
   if (skip && *skip) return;
-  constexpr int KYP = 64, CG = KYP / 4, LDC = KYP + 8;
+  constexpr int CG = KYP / 4, LDC = KYP + 8;
+  constexpr int YW = KYP / 2, NT = YW / 16;  // XG: Y = [Q_i | Q_{i-1}], YW columns each
   constexpr int NH = KC / 8;  // 16-B A loads per row tile per chunk
   constexpr int CEPT = KC * KYP / 256;
   constexpr int CS = 2 * KC * LDC > 4 * 16 * KYP ? 2 * KC * LDC : 4 * 16 * KYP;  // + epilogue stage
@@ -463,12 +479,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
   // one 128-row tile per workgroup, or (XG) persistent over tiles
   auto tile_body = [&](int64_t tile) {
   typedef double d4x __attribute__((ext_vector_type(4)));
-  d4x gx[XG ? 2 : 1][XG ? 2 : 1];
+  d4x gx[XG ? NT : 1][XG ? NT : 1];
   if constexpr (XG) {
 #pragma unroll
-    for (int it = 0; it < 2; ++it)
+    for (int it = 0; it < NT; ++it)
 #pragma unroll
-      for (int jt = 0; jt < 2; ++jt) gx[it][jt] = d4x{0.0, 0.0, 0.0, 0.0};
+      for (int jt = 0; jt < NT; ++jt) gx[it][jt] = d4x{0.0, 0.0, 0.0, 0.0};
   }
   const int64_t r0 = (tile * 4 + wave) * kT44Rows;
   const int64_t rw = r0 + kT44Rows <= nrows ? r0 : nrows - kT44Rows;  // wave-uniform
@@ -491,17 +507,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
       ar[1][h] = *reinterpret_cast<const d2v*>(xb + aoff1);
     }
   };
-  // C chunk rows KC chc + wave + 4 v, column lane
+  // C chunk element tid + 256 v: row KC chc + tid / KYP + (256 / KYP) v, column tid % KYP
+  constexpr int CRS = 256 / KYP;
   auto load_c = [&](int ch, double (&cr)[CEPT]) {
     const int chc = ch < nch ? ch : nch - 1;
-    const double* cb = C + (int64_t)(KC * chc + wave) * ldc;
+    const double* cb = C + (int64_t)(KC * chc + tid / KYP) * ldc + tid % KYP;
 #pragma unroll
-    for (int v = 0; v < CEPT; ++v) cr[v] = cb[(int64_t)(4 * v) * ldc + lane];
+    for (int v = 0; v < CEPT; ++v) cr[v] = cb[(int64_t)(CRS * v) * ldc];
   };
-  const int cso = wave * LDC + perm8(lane);
+  const int cso = (tid / KYP) * LDC + perm8(tid % KYP);
   auto store_c = [&](int buf, const double (&cr)[CEPT]) {
 #pragma unroll
-    for (int v = 0; v < CEPT; ++v) cs[buf][cso + 4 * v * LDC] = cr[v];
+    for (int v = 0; v < CEPT; ++v) cs[buf][cso + CRS * v * LDC] = cr[v];
   };
   auto mfmas = [&](int ch, const d2v (&acur)[2][NH]) {
     const double* cb = cs[ch & 1] + 2 * q * LDC + 2 * (lane & 3);
@@ -589,16 +606,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
 #pragma unroll
       for (int s4 = 0; s4 < 4; ++s4) {
         const double* orow = ot + (4 * s4 + q) * KYP;
-        double za[2], yb[2];
+        double za[NT], yb[NT];
 #pragma unroll
-        for (int t2 = 0; t2 < 2; ++t2) {
-          za[t2] = orow[(32 + 16 * t2 + li) ^ (4 * s4)];
+        for (int t2 = 0; t2 < NT; ++t2) {
+          za[t2] = orow[(YW + 16 * t2 + li) ^ (4 * s4)];
           yb[t2] = orow[(16 * t2 + li) ^ (4 * s4)];
         }
 #pragma unroll
-        for (int it = 0; it < 2; ++it)
+        for (int it = 0; it < NT; ++it)
 #pragma unroll
-          for (int jt = 0; jt < 2; ++jt)
+          for (int jt = 0; jt < NT; ++jt)
             gx[it][jt] = __builtin_amdgcn_mfma_f64_16x16x4f64(za[it], yb[jt], gx[it][jt], 0, 0, 0);
       }
     }
@@ -607,17 +624,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
     // the four waves' partials summed in LDS (fixed order), one 32 x 32 partial per workgroup
     __syncthreads();
     const int li = lane & 15;
-    double* gw = cs_raw + wave * 1024;
+    constexpr int G2 = YW * YW;
+    double* gw = cs_raw + wave * G2;
 #pragma unroll
-    for (int it = 0; it < 2; ++it)
+    for (int it = 0; it < NT; ++it)
 #pragma unroll
-      for (int jt = 0; jt < 2; ++jt)
+      for (int jt = 0; jt < NT; ++jt)
 #pragma unroll
-        for (int reg = 0; reg < 4; ++reg) gw[(16 * it + q + 4 * reg) * 32 + 16 * jt + li] = gx[it][jt][reg];
+        for (int reg = 0; reg < 4; ++reg) gw[(16 * it + q + 4 * reg) * YW + 16 * jt + li] = gx[it][jt][reg];
     __syncthreads();
-    double* out = xslab + tile * 1024;
-    for (int e = tid; e < 1024; e += 256)
-      out[e] = (cs_raw[e] + cs_raw[1024 + e]) + (cs_raw[2048 + e] + cs_raw[3072 + e]);
+    double* out = xslab + tile * G2;
+    for (int e = tid; e < G2; e += 256)
+      out[e] = (cs_raw[e] + cs_raw[G2 + e]) + (cs_raw[2 * G2 + e] + cs_raw[3 * G2 + e]);
   }
   };
   tile_body(blockIdx.x);
@@ -663,25 +681,30 @@ void tsmm44(int64_t nrows, const PanelRun& X, const double* C, int ldc, const Pa
     const char* e = getenv("RBL_TSMM44_FAST");
     return !e || atoi(e) != 0;
   }();
-  if (fast_ok && KY == 64 && (X.count * X.w) % kT44K == 0 && nrows >= kT44Rows && Y.w % 2 == 0) {
+  // fast path: 64 or 32 output columns, K a multiple of 32, Y not aliasing the X panels (a
+  // wave writes its rows after the whole k-loop; the shifted last tile re-reads rows below it)
+  bool alias = false;
+  for (int t = 0; t < Y.count; ++t)
+    alias |= Y.ptr[t] >= X.base && Y.ptr[t] < X.base + (int64_t)X.count * X.stride;
+  // (KYP = 32 builds but stays off: at b = 16 the update is HBM-bound and the generic kernel
+  // ran 4 % faster on C2, its cross-Gram form 6 % slower than the Gram pass it replaces —
+  // tools/r02_c2_ab.sh)
+  if (fast_ok && KY == 64 && (X.count * X.w) % kT44K == 0 && nrows >= kT44Rows &&
+      Y.w % 2 == 0 && !alias) {
     const int64_t wgs = (nrows + 4 * kT44Rows - 1) / (4 * kT44Rows);
-    if (xslab && Y.w == 32 && Y.count == 2) {
-      const int grid = (int)wgs;
-      *xgrid = grid;
-      if (X.w == 32)
-        hipLaunchKernelGGL((k_tsmm44f<32, RBL_T44_KC, RBL_T44_PF, true>), dim3(grid), dim3(256), 0, st, nrows,
-                           X, C, ldc, Y, alpha, beta, skip, xslab);
-      else
-        hipLaunchKernelGGL((k_tsmm44f<16, RBL_T44_KC, RBL_T44_PF, true>), dim3(grid), dim3(256), 0, st, nrows,
-                           X, C, ldc, Y, alpha, beta, skip, xslab);
-      return;
+    const bool xg = xslab && Y.count == 2 && 2 * Y.w == KY;
+    if (xg) *xgrid = (int)wgs;
+#define RBL_T44F(BB, XGG, KK)                                                                      \
+  hipLaunchKernelGGL((k_tsmm44f<BB, RBL_T44_KC, RBL_T44_PF, XGG, KK>), dim3((unsigned)wgs), dim3(256), 0, \
+                     st, nrows, X, C, ldc, Y, alpha, beta, skip, XGG ? xslab : nullptr)
+    if (KY == 64) {
+      if (X.w == 32) { if (xg) RBL_T44F(32, true, 64); else RBL_T44F(32, false, 64); }
+      else { if (xg) RBL_T44F(16, true, 64); else RBL_T44F(16, false, 64); }
+    } else {
+      if (X.w == 32) { if (xg) RBL_T44F(32, true, 32); else RBL_T44F(32, false, 32); }
+      else { if (xg) RBL_T44F(16, true, 32); else RBL_T44F(16, false, 32); }
     }
-    if (X.w == 32)
-      hipLaunchKernelGGL((k_tsmm44f<32>), dim3((unsigned)wgs), dim3(256), 0, st, nrows, X, C, ldc, Y,
-                         alpha, beta, skip, nullptr);
-    else
-      hipLaunchKernelGGL((k_tsmm44f<16>), dim3((unsigned)wgs), dim3(256), 0, st, nrows, X, C, ldc, Y,
-                         alpha, beta, skip, nullptr);
+#undef RBL_T44F
     return;
   }
   if (X.w == 32) {
