@@ -297,16 +297,30 @@ def main():
             held = sum(k["clock_ghz"] * k["avg_us"] for k in ks) / sum(k["avg_us"] for k in ks)
     except (OSError, ValueError, KeyError):
         pass
+    # bytes (2m + 6) B_blk per even step (the basis read by the Gram and by the
+    # update, plus the pair read / written); below the ridge (b = 16: AI ~ b/2) the stage is
+    # HBM-bound and priced against the HBM peak instead
+    s_basis = 8 if args.basis_bits == 64 else 4
+    reorth_bytes = sum((2 * (i - 2) + 6) * nloc * b * s_basis for i in range(4, m_max + 1, 2))
+    ai = reorth_flops / reorth_bytes if reorth_bytes else 0.0
+    ridge = mfma_peak * 1e12 / (HBM_PEAK_GBS * 1e9)
+    reorth_gbs = reorth_bytes / (reorth_ms * 1e-3) / 1e9 if reorth_ms > 0 else 0.0
+    mbound = ai >= ridge
     roof_reorth = {"kernel": "partial reorth (gram+update)" + ("" if args.basis_bits == 64 else ", fp32"),
-                   "bound": "mfma",
-                   "achieved": round(reorth_tf, 2), "peak": mfma_peak, "unit": "TFLOP/s",
-                   "frac": round(reorth_tf / mfma_peak, 4),
+                   "bound": "mfma" if mbound else "hbm",
+                   "achieved": round(reorth_tf, 2) if mbound else round(reorth_gbs, 1),
+                   "peak": mfma_peak if mbound else HBM_PEAK_GBS,
+                   "unit": "TFLOP/s" if mbound else "GB/s",
+                   "frac": round(reorth_tf / mfma_peak if mbound else reorth_gbs / HBM_PEAK_GBS, 4),
+                   "arithmetic_intensity": round(ai, 2), "ridge": round(ridge, 2),
+                   "algorithmic_bytes_per_run": int(reorth_bytes),
+                   "tflops": round(reorth_tf, 2),
                    "traffic": None if traffic_reorth is None else int(traffic_reorth),
                    "traffic_unit": f"HBM bytes per run (gram + update, {len(range(4, m_max + 1, 2))} launches each)",
                    "algorithmic_flops_per_run": reorth_flops, "ms_per_run": round(reorth_ms, 3),
                    **({"held_clock_ghz": round(held, 3),
                        "frac_of_peak_at_held_clock": round(reorth_tf / (mfma_peak * held / 2.4), 4)}
-                      if held else {})}
+                      if held and mbound else {})}
     if stage["part reorth"] > stage["AQ"]:
         roofline, roofline2 = roof_reorth, roof_spmm
     else:
