@@ -342,6 +342,7 @@ def main():
         ttk = {"seconds": round(ttk_s, 4), "iters": info.iters, "converged": info.converged,
                "k": k, "top_eigenvalues": [round(float(x), 6) for x in D[:3]],
                "ritz_ms": round(allmax(ttk_stage["Ritz vectors"]), 3),
+               "host_eig_ms": round(info.eig_ms, 3),
                "stage_ms": {s_: round(v, 3) for s_, v in ttk_stage.items()}}
 
     # ---- time-to-k on a slowly decaying spectrum (same generator and n, another plant) ----
@@ -366,6 +367,7 @@ def main():
                     "k": k, "spectrum": "planted 12 + 0.25 (2k+1-l), l = 1..2k",
                     "top_eigenvalues": [round(float(x), 6) for x in D[:3]],
                     "kth_eigenvalue": round(float(D[k - 1]), 6),
+                    "host_eig_ms": round(info.eig_ms, 3),
                     "stage_ms": {s_: round(v, 3) for s_, v in st_.items()}}
 
     # ---- CPU baseline: the oracle (port of RBL.jl) on a bounded sample, rank 0, N = 1 ----

@@ -4,10 +4,13 @@ Restates Julia/common.jl:9-65 for the product's host loop:
   * ``TBand``       — insertA!/insertB! (common.jl:9-26), kept as one preallocated lower band
                       instead of the reference's per-step ``T = [T insertA!(...)]`` reallocation
                       (RBL_gpu.jl:185);
-  * ``dsbev``       — LAPACK dsbev(jobz='V', uplo='L') (common.jl:28-48), via SciPy's LAPACK;
+  * ``dsbev``       — LAPACK dsbev(jobz='V', uplo='L') (common.jl:28-48), via SciPy's LAPACK
+                      (dsbevd, the same eigenpairs to rounding, from N = 256 on: see below);
   * ``sort_eig_abs``  (common.jl:50-54) and ``check_convergence`` (common.jl:56-65).
 """
 from __future__ import annotations
+
+import os
 
 import numpy as np
 from scipy.linalg import lapack
@@ -40,11 +43,21 @@ class TBand:
         return self.data[:, : self.nblocks * self.b]
 
 
+# The reference calls LAPACK dsbev (QR iteration, common.jl:32-33).  From N = 256 on, dsbevd
+# (divide and conquer on the same band reduction) returns the same eigenpairs to ~1e-13 and
+# runs 3-6x faster (tools/host_eig_probe.py: N = 896, kd = 32: 1.11 s -> 0.18 s) — the host
+# eigensolve is most of the time-to-k on slowly decaying spectra.  RBL_HOST_EIGEN=dsbev forces
+# the reference's routine throughout.
+_EIGEN = os.environ.get("RBL_HOST_EIGEN", "auto")
+DSBEVD_MIN_N = 256
+
+
 def dsbev(T: np.ndarray):
     """common.jl:36-48 — eigenpairs of the symmetric band matrix T (lower, kd = b)."""
-    w, z, info = lapack.dsbev(T, compute_v=1, lower=1)
+    use_d = _EIGEN == "dsbevd" or (_EIGEN == "auto" and T.shape[1] >= DSBEVD_MIN_N)
+    w, z, info = (lapack.dsbevd if use_d else lapack.dsbev)(T, compute_v=1, lower=1)
     if info != 0:
-        raise np.linalg.LinAlgError(f"dsbev info={info}")
+        raise np.linalg.LinAlgError(f"{'dsbevd' if use_d else 'dsbev'} info={info}")
     return w, z
 
 

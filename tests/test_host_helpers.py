@@ -35,3 +35,26 @@ def test_dsbev_sort_convergence_match_oracle():
     assert np.array_equal(s1[0], s2[0]) and np.array_equal(s1[1], s2[1])
     B = np.triu(rng.standard_normal((b, b))) * 1e-9
     assert host.check_convergence(B, s1[1], b, 7, 1e-7) == o.check_convergence(B, s2[1], b, 7, 1e-7)
+
+
+def test_large_band_eigensolve_matches_reference_routine():
+    """From N = 256 on the host uses dsbevd: the same eigenvalues as the reference's dsbev to
+    rounding, eigenvectors orthonormal with small residuals, and the same top-k selection."""
+    from rbl import host
+    rng = np.random.default_rng(4)
+    b, N = 32, 512
+    T = rng.standard_normal((b + 1, N))
+    d1, v1 = host.dsbev(T)
+    d2, v2 = o.dsbev(T)
+    scale = np.abs(d2).max()
+    assert np.abs(d1 - d2).max() < 1e-12 * scale
+    full = np.zeros((N, N))
+    for r in range(b + 1):  # lower band storage -> dense symmetric
+        idx = np.arange(N - r)
+        full[idx + r, idx] = T[r, : N - r]
+        full[idx, idx + r] = T[r, : N - r]
+    assert np.abs(full @ v1 - v1 * d1).max() < 1e-11 * scale
+    assert np.abs(v1.T @ v1 - np.eye(N)).max() < 1e-11
+    s1 = host.sort_eig_abs(d1, v1, 20)
+    s2 = o.sort_eig_abs(d2, v2, 20)
+    assert np.abs(s1[0] - s2[0]).max() < 1e-12 * scale
