@@ -292,7 +292,8 @@ def main():
     try:
         with open(os.path.join(ROOT, "profiles", "pmc_clock.json")) as f:
             kc = json.load(f)["kernels"]
-        ks = [kc[k] for k in ("k_gram44<32, 2>", "k_tsmm44f<32>") if k in kc]
+        # the partial-reorth kernels at b = 32 (the Gram and the 64-column update, any variant)
+        ks = [v for k_, v in kc.items() if k_.startswith(("k_gram44<32, 2", "k_tsmm44f<32"))]
         if ks and args.basis_bits == 64 and b == 32:
             held = sum(k["clock_ghz"] * k["avg_us"] for k in ks) / sum(k["avg_us"] for k in ks)
     except (OSError, ValueError, KeyError):
