@@ -91,6 +91,9 @@ struct rbl_ctx {
   double* d_stage = nullptr;          // one n_local x b staging block for spilled blocks
   hipStream_t cstream = nullptr;      // D2H copies of finished spilled blocks
   hipEvent_t ev_fin = nullptr, ev_d2h[2] = {nullptr, nullptr};
+  // rbl_step_async: step i's stash (A_i, R_tot, flags) has landed when step_ev[i] completes, so
+  // rbl_fetch waits for the steps it returns, not for steps enqueued after them
+  std::vector<hipEvent_t> step_ev;
   bool d2h_pending[2] = {false, false};
   float* d_basis32 = nullptr;
   float* d_stage32 = nullptr;
@@ -522,13 +525,20 @@ struct StageScope {
     roctxRangePop();
   }
 };
-void harvest_timers(rbl_ctx* ctx) {  // after a stream sync
+void harvest_timers(rbl_ctx* ctx) {
+  // stages whose end event has completed; the rest (steps still running after an rbl_fetch
+  // that waited only for earlier steps) stay for a later harvest, their events in use
+  std::vector<rbl_ctx::Mark> keep;
   for (auto& m : ctx->marks) {
+    if (hipEventQuery(m.b) != hipSuccess) {
+      keep.push_back(m);
+      continue;
+    }
     float ms = 0.f;
     if (hipEventElapsedTime(&ms, m.a, m.b) == hipSuccess) ctx->stage_ms[m.stage] += ms;
   }
-  ctx->marks.clear();
-  ctx->ev_used = 0;
+  ctx->marks.swap(keep);
+  if (ctx->marks.empty()) ctx->ev_used = 0;
 }
 
 // ---- collectives ---------------------------------------------------------------------
@@ -1311,6 +1321,8 @@ int rbl_free(rbl_ctx* ctx) {
   free_run(ctx);
   free_matrix(ctx);
   for (auto e : ctx->ev_pool) hipEventDestroy(e);
+  for (auto e : ctx->step_ev)
+    if (e) hipEventDestroy(e);
   delete ctx->comm;
   if (ctx->stream) hipStreamDestroy(ctx->stream);
   if (ctx->cstream) hipStreamDestroy(ctx->cstream);
@@ -1869,7 +1881,12 @@ int rbl_fetch(rbl_ctx* ctx, int i0, int i1, double* A_out, double* B_out, int* s
   if (i0 != ctx->fetched || i1 < i0 || i1 > ctx->nblocks)
     return fail(ctx, RBL_ERR_INVALID, "rbl_fetch: [i0, i1) must start at the first unfetched step");
   HIPC(hipSetDevice(ctx->device));
-  HIPC(hipStreamSynchronize(ctx->stream));
+  // steps enqueued after i1 - 1 (speculatively, while the host works on the T band) keep running
+  const int last = i1 - 1;
+  if (last >= 1 && last < (int)ctx->step_ev.size() && ctx->step_ev[last])
+    HIPC(hipEventSynchronize(ctx->step_ev[last]));
+  else
+    HIPC(hipStreamSynchronize(ctx->stream));
   harvest_timers(ctx);
   const int b = ctx->b;
   int rc = RBL_OK;
@@ -2070,6 +2087,9 @@ int step_impl(rbl_ctx* ctx, int i, int part_reorth, double* A_out, double* B_out
     HIPC(hipMemcpyAsync(h + b * b, smallp(ctx, S_RTOT), (size_t)b * b * sizeof(double),
                         hipMemcpyDeviceToHost, ctx->stream));
     HIPC(hipMemcpyAsync(ctx->h_hflags + 4 * i, ctx->d_flags, 4 * sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+    if ((int)ctx->step_ev.size() <= i) ctx->step_ev.resize(i + 1, nullptr);
+    if (!ctx->step_ev[i]) HIPC(hipEventCreateWithFlags(&ctx->step_ev[i], hipEventDisableTiming));
+    HIPC(hipEventRecord(ctx->step_ev[i], ctx->stream));
     HIPC(hipGetLastError());
     ctx->nblocks = i + 1;
     return RBL_OK;

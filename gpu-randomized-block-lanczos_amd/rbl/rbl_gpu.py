@@ -282,7 +282,10 @@ class RBLInfo:
     converged: bool = False
     status: int = 0
     qr_shifted_steps: int = 0
-    eig_ms: float = 0.0
+    eig_ms: float = 0.0          # host T-band eigensolves (dsbev / dsbevd)
+    fetch_ms: float = 0.0        # host waits in rbl_fetch (the GPU finishing enqueued steps)
+    ritz_ms: float = 0.0         # host wall time of rbl_ritz (device work + D2H of V)
+    start_ms: float = 0.0        # host wall time of rbl_start (A Omega + QR)
     trace_A: list = field(default_factory=list)
     trace_B: list = field(default_factory=list)
 
@@ -294,13 +297,16 @@ def max_steps_for(kryl_sz: int, b: int) -> int:
 
 def lanczos(ctx: Context, k: int, b: int, *, kryl_sz: int = KRYL_SZ_GPU, omega=None, seed=0,
             check: bool = True, max_steps: int | None = None, tol: float = RESIDUAL_TOL,
-            trace: bool = False, ritz: bool = True, basis_bits: int = 64):
+            trace: bool = False, ritz: bool = True, basis_bits: int = 64,
+            speculate: "bool | int" = False):
     """RBL_gpu.jl:134-203 + :219 on an already-loaded context.  Returns (D, V_local, info)."""
     steps_cap = max_steps_for(kryl_sz, b)
     if max_steps is not None:
         steps_cap = min(steps_cap, max_steps)
-    ctx.start(b, steps_cap, omega=omega, seed=seed, basis_bits=basis_bits)
     info = RBLInfo()
+    t0 = time.perf_counter()
+    ctx.start(b, steps_cap, omega=omega, seed=seed, basis_bits=basis_bits)
+    info.start_ms = (time.perf_counter() - t0) * 1e3
     T = TBand(b, steps_cap)
     D = np.zeros(0)
     S = np.zeros((0, 0))
@@ -315,29 +321,67 @@ def lanczos(ctx: Context, k: int, b: int, *, kryl_sz: int = KRYL_SZ_GPU, omega=N
     # Steps are enqueued without a host round trip (rbl_step_async) and fetched where the host
     # needs the T band: at a convergence check (:186) and after the last step.  T receives the
     # same A_i / B_i in the same order as the reference's per-step pushes (:185, :193).
-    pending = []
+    # Speculation: before blocking at a check the host enqueues as many further steps as its
+    # T-band eigensolve is expected to last (the previous one scaled by (N/N_prev)^2.7, over the
+    # measured time per step; at most up to the next check), so the GPU keeps working during
+    # dsbev.  The check reads only steps <= i, and steps after an even i touch no block <= i
+    # (partial reorth at even steps), so D, S and the Ritz vectors are unchanged; a converged
+    # run discards the extra steps.  Off by default: on the C4a slow-spectrum time-to-k (28
+    # steps, dsbevd) it hid ~60 ms of eigensolves and wasted as much on the steps after the
+    # converging check (0.91 s vs 0.87-0.89 s strict).
+    last_i = min(steps_cap, math.ceil(kryl_sz / b))
+    enq = 0
+
+    def enqueue(upto):
+        nonlocal enq
+        while enq < upto:
+            enq += 1
+            ctx.step_async(enq, enq >= 2 and enq % 2 == 0)   # :164-184
+
+    first = 1                                      # first unfetched step
     i = 0
+    last_eig = last_n = None
+    step_ms = None
+    t_prev, i_prev, eig_prev = time.perf_counter(), 0, 0.0
     while True:
         i += 1                                     # step 1: first loop, :149-161; then :162-194
-        ctx.step_async(i, i >= 2 and i % 2 == 0)   # :164-184
-        pending.append(i)
         is_check = check and i >= 2 and i * b > k and i % 4 == 0
         is_last = not (i * b < kryl_sz and i < steps_cap)
         if not (is_check or is_last):
             continue
-        for j, (Aj, Bj, st) in zip(pending, ctx.fetch(pending[0], i + 1)):
+        enqueue(i)
+        # (one rank only: the count comes from host timings, and every rank must issue the
+        # same steps — their collectives pair up)
+        # (speculate may also be a fixed count of extra steps per check: tests)
+        if speculate and ctx.nranks == 1 and is_check and not is_last and i % 2 == 0:
+            if speculate is True:
+                extra = int(last_eig * (i * b / last_n) ** 2.7 // step_ms) if last_eig and step_ms else 0
+            else:
+                extra = int(speculate)
+            enqueue(min(last_i, i + 4, i + extra))
+        t0 = time.perf_counter()
+        fetched = ctx.fetch(first, i + 1)
+        t1 = time.perf_counter()
+        info.fetch_ms += (t1 - t0) * 1e3
+        if i > i_prev and t1 - t_prev > eig_prev:  # GPU time per step since the last fetch
+            step_ms = ((t1 - t_prev) - eig_prev) * 1e3 / (i - i_prev)
+        t_prev, i_prev, eig_prev = t1, i, 0.0
+        for j, (Aj, Bj, st) in zip(range(first, i + 1), fetched):
             _record(Aj, Bj, st)
             T.insert_A(Aj)                         # :185
             if j == i and is_check:
                 t0 = time.perf_counter()
                 D, S = dsbev(T.view())             # :187
                 D, S = sort_eig_abs(D, S, k)       # :188
-                info.eig_ms += (time.perf_counter() - t0) * 1e3
+                dt = time.perf_counter() - t0
+                info.eig_ms += dt * 1e3
+                eig_prev = dt
+                last_eig, last_n = dt * 1e3, i * b
                 if check_convergence(Bj, S, b, k, tol):   # :189
                     info.converged = True
                     break
             T.insert_B(Bj, j)                      # :193
-        pending = []
+        first = i + 1
         if info.converged or is_last:
             break
     info.iters = i
@@ -347,7 +391,9 @@ def lanczos(ctx: Context, k: int, b: int, *, kryl_sz: int = KRYL_SZ_GPU, omega=N
     info.status = _lib.RBL_OK if info.converged else _lib.RBL_WARN_NOT_CONVERGED
     V = None
     if ritz and S.size:
+        t0 = time.perf_counter()
         V = ctx.ritz(S.shape[0] // b, min(k, S.shape[1]), S)   # RBL_gpu.jl:219
+        info.ritz_ms = (time.perf_counter() - t0) * 1e3
     return D, V, info
 
 

@@ -188,7 +188,10 @@ int rbl_step(rbl_ctx* ctx, int i, int part_reorth, double* A_out, double* B_out)
  * the T band (the reference pushes every step, RBL_gpu.jl:185/193, but reads it only at the
  * convergence checks, :186-189).  A QR breakdown surfaces at the fetch. */
 int rbl_step_async(rbl_ctx* ctx, int i, int part_reorth);
-/* Wait for the enqueued steps and return those of [i0, i1) (i0 = the first unfetched step):
+/* Wait for steps up to i1 - 1 and return those of [i0, i1) (i0 = the first unfetched step);
+ * steps enqueued after i1 - 1 keep running (the host may enqueue ahead of a convergence check
+ * and work on the T band meanwhile: with partial reorth at even steps, the steps after an even
+ * i1 - 1 never touch blocks 1..i1-1):
  * A_out / B_out receive (i1-i0) consecutive b x b column-major blocks, status_out (may be
  * NULL) each step's status (RBL_OK, RBL_WARN_QR_SHIFTED, RBL_ERR_NUMERIC).  Returns
  * RBL_ERR_NUMERIC if any of them broke down, else RBL_OK.  rbl_step refuses to run while

@@ -296,3 +296,28 @@ def test_pass_fusions(rbl, b, bits):
     for t in (0, 1):
         d = np.abs(out[3][t] - out[1][t]).max() / np.abs(out[1][t]).max()
         assert d < 1e-12, (t, d)
+
+
+@pytest.mark.parametrize("case", ["converges", "runs_out"])
+def test_speculative_steps_change_nothing(rbl, case):
+    """Steps enqueued ahead of a convergence check (rbl.lanczos speculate) leave D, V, the step
+    count and every A_i / B_{i+1} bit for bit as in the strict alternation (reference order):
+    a run converging at a check (the extra steps are discarded) and one using all its steps."""
+    k, b = 10, 16
+    if case == "converges":
+        A = c1_matrix(4000, k)
+    else:
+        A, _ = o.slow_decay_matrix(3000, k)
+        A = (A + matgen.hashwindow_csr(3000, 8, 0.5, 3, None) * 1e-3).tocsr()
+    omega = np.random.default_rng(5).standard_normal((A.shape[0], b))
+    out = []
+    for spec in (False, 3):
+        with rbl.Context(0) as ctx:
+            ctx.set_matrix(A)
+            D, V, info = rbl.lanczos(ctx, k, b, omega=omega, trace=True, speculate=spec)
+        out.append((D, V, info))
+    (D0, V0, i0), (D1, V1, i1) = out
+    assert i0.iters == i1.iters and i0.converged == i1.converged
+    assert np.array_equal(D0, D1) and np.array_equal(V0, V1)
+    assert all(np.array_equal(a, c) for a, c in zip(i0.trace_A, i1.trace_A))
+    assert all(np.array_equal(a, c) for a, c in zip(i0.trace_B, i1.trace_B))
