@@ -615,10 +615,14 @@ int rowop(rbl_ctx* ctx, const double* X, const double* C, double* Y, double alph
   const int grid = rowgram_grid(ctx->nloc);
   if (G && (size_t)grid * b * b > ctx->slab_elems)
     return fail(ctx, RBL_ERR_INVALID, "internal: row-op slab too small");
-  // without a Gram the grid follows the kernel's occupancy (no partials to count)
-  rowgram(ctx->nloc, b, X, C, b, Y, alpha, beta, G ? ctx->d_slab : nullptr, G ? grid : 0, skip,
-          ctx->stream, X32, Y32, f64flag);
-  HIPC(hipGetLastError());
+  if (ctx->nloc > 0) {
+    // without a Gram the grid follows the kernel's occupancy (no partials to count)
+    rowgram(ctx->nloc, b, X, C, b, Y, alpha, beta, G ? ctx->d_slab : nullptr, G ? grid : 0, skip,
+            ctx->stream, X32, Y32, f64flag);
+    HIPC(hipGetLastError());
+  } else if (G) {  // no rows on this rank: its share of the Gram is zero (the all-reduce still runs)
+    HIPC(hipMemsetAsync(ctx->d_slab, 0, (size_t)grid * b * b * sizeof(double), ctx->stream));
+  }
   if (!G) return RBL_OK;
   reduce_slab(ctx->d_slab, grid, (int64_t)b * b, G, skip, ctx->stream);
   HIPC(hipGetLastError());
@@ -716,12 +720,15 @@ int reorth_pair(rbl_ctx* ctx, int i, int flags) {
     const int nres = std::min(nW, ctx->resident);  // HBM-resident part of W
     // the last update of the pair also forms this step's local-reorth Gram Q_{i-1}^T Q_i
     // (RBL_OPT_FUSE bit 1; the update's 64-column fast path: b = 32)
-    const bool xg = (ctx->fuse & 2) && b == 32 && ctx->nloc >= 32 &&
-                    (size_t)tsmm44_xg_grid(ctx->nloc) * b * b <= ctx->slab_elems;
+    // (the same decision on every rank: the all-reduce below pairs up; a rank where the fast
+    // path does not apply — too few rows, slab too small — forms its share with the Gram kernel)
+    const bool xg = (ctx->fuse & 2) && b == 32;
+    const bool xslab_ok = (size_t)tsmm44_xg_grid(ctx->nloc) * b * b <= ctx->slab_elems;
     int xgrid = 0;
     auto update = [&](const PanelRun& W, bool last) -> int {
+      const bool here = xg && last && xslab_ok;
       return tsmm_checked(ctx, W, ctx->d_C, 2 * b, pan2(Qi, Qm, b), -1.0, 1.0, nullptr,
-                          xg && last ? ctx->d_slab : nullptr, xg && last ? &xgrid : nullptr);
+                          here ? ctx->d_slab : nullptr, here ? &xgrid : nullptr);
     };
     if (ctx->reorth_order == 0) {  // block CGS: one Gram over every resident j, one update
       PanelRun W;
@@ -748,8 +755,17 @@ int reorth_pair(rbl_ctx* ctx, int i, int flags) {
       CHK(gram(ctx, run1(Wj, b), pan2(Qi, Qm, b), ctx->d_C, nullptr));
       CHK(update(run1(Wj, b), j == nW - 1));
     }
-    if (xgrid > 0) {  // the partials of the last update (its Gram slab was reduced before it)
-      reduce_slab(ctx->d_slab, xgrid, (int64_t)b * b, smallp(ctx, S_CLOC), nullptr, ctx->stream);
+    if (xg) {  // the partials of the last update (its Gram slab was reduced before it)
+      if (xgrid > 0) {
+        reduce_slab(ctx->d_slab, xgrid, (int64_t)b * b, smallp(ctx, S_CLOC), nullptr, ctx->stream);
+      } else if (ctx->nloc > 0) {
+        const int sp = gram_splits(ctx->nloc, 1, b, b);
+        gram_partial(ctx->nloc, run1(Qm, b), pan1(Qi, b), ctx->d_slab, sp, nullptr, ctx->stream);
+        reduce_slab(ctx->d_slab, sp, (int64_t)b * b, smallp(ctx, S_CLOC), nullptr, ctx->stream);
+      } else {
+        HIPC(hipMemsetAsync(smallp(ctx, S_CLOC), 0, (size_t)b * b * sizeof(double), ctx->stream));
+      }
+      HIPC(hipGetLastError());
       CHK(allreduce(ctx, smallp(ctx, S_CLOC), (size_t)b * b));
       ctx->cloc_step = i;
       ctx->cloc_final = true;
@@ -868,9 +884,15 @@ int rowop_ex(rbl_ctx* ctx, RowOpArgs a, double* G, double* Gx, bool reduce_x) {
   const int xgrid = rowgram_grid(ctx->nloc, 2);
   int grid = a.Z ? xgrid : 0;
   a.grid_out = &grid;
-  if (ctx->nloc > 0 && !rowgram_ex(ctx->nloc, b, a, grid, ctx->stream))
-    return fail(ctx, RBL_ERR_INVALID, "internal: unsupported fused row-op form");
-  if (ctx->nloc <= 0) grid = 1;
+  if (ctx->nloc > 0) {
+    if (!rowgram_ex(ctx->nloc, b, a, grid, ctx->stream))
+      return fail(ctx, RBL_ERR_INVALID, "internal: unsupported fused row-op form");
+  } else {  // no rows on this rank: zero partials (the all-reduces still run on every rank)
+    grid = 1;
+    if (G) HIPC(hipMemsetAsync(a.slab, 0, (size_t)b * b * sizeof(double), ctx->stream));
+    if (a.Z && a.skip == nullptr)
+      HIPC(hipMemsetAsync(a.slab2, 0, (size_t)xgrid * b * b * sizeof(double), ctx->stream));
+  }
   HIPC(hipGetLastError());
   if (G) {
     reduce_slab(ctx->d_slab, grid, (int64_t)b * b, G, a.skip, ctx->stream);
