@@ -182,6 +182,10 @@ void gram_partial(int64_t nrows, const PanelRun& W, const Panels& X, double* sla
 // out[e] = sum_s slab[s][e], e < len.
 void reduce_slab(const double* slab, int splits, int64_t len, double* out, const int* skip,
                  hipStream_t s);
+// The same for tens of thousands of splits: a two-level sum whose first level writes
+// reduce_scratch_splits(splits) x len doubles right after the partials (reserve them).
+int reduce_scratch_splits(int splits);
+void reduce_slab_many(double* slab, int splits, int64_t len, double* out, hipStream_t s);
 // Y = beta*Y + alpha * X * C, X a run of panels (k = nX*X.w), C row-major k x (Y.count*Y.w)
 // with leading dimension ldc.  Y may alias X's panels row-for-row (in-place apply).
 void tsmm(int64_t nrows, const PanelRun& X, const double* C, int ldc, const Panels& Y,

@@ -723,7 +723,8 @@ int reorth_pair(rbl_ctx* ctx, int i, int flags) {
     // (the same decision on every rank: the all-reduce below pairs up; a rank where the fast
     // path does not apply — too few rows, slab too small — forms its share with the Gram kernel)
     const bool xg = (ctx->fuse & 2) && b == 32;
-    const bool xslab_ok = (size_t)tsmm44_xg_grid(ctx->nloc) * b * b <= ctx->slab_elems;
+    const int xg_parts = tsmm44_xg_grid(ctx->nloc);
+    const bool xslab_ok = (size_t)(xg_parts + reduce_scratch_splits(xg_parts)) * b * b <= ctx->slab_elems;
     int xgrid = 0;
     auto update = [&](const PanelRun& W, bool last) -> int {
       const bool here = xg && last && xslab_ok;
@@ -757,7 +758,7 @@ int reorth_pair(rbl_ctx* ctx, int i, int flags) {
     }
     if (xg) {  // the partials of the last update (its Gram slab was reduced before it)
       if (xgrid > 0) {
-        reduce_slab(ctx->d_slab, xgrid, (int64_t)b * b, smallp(ctx, S_CLOC), nullptr, ctx->stream);
+        reduce_slab_many(ctx->d_slab, xgrid, (int64_t)b * b, smallp(ctx, S_CLOC), ctx->stream);
       } else if (ctx->nloc > 0) {
         const int sp = gram_splits(ctx->nloc, 1, b, b);
         gram_partial(ctx->nloc, run1(Qm, b), pan1(Qi, b), ctx->d_slab, sp, nullptr, ctx->stream);
@@ -1835,8 +1836,10 @@ int rbl_start(rbl_ctx* ctx, int b, int max_blocks, int basis_bits, const double*
   slab = std::max(slab, (size_t)2 * rowgram_grid(ctx->nloc, kRowgramMaxPerCu) * b * b);  // rowop partials (+ cross Gram)
   // the partial-reorth update's local-reorth Gram partials (one b x b per 128-row tile:
   // n_local b^2 / 128 doubles, a quarter of a block at b = 32)
-  if (b == 32 && basis_bits == 64 && (ctx->fuse & 2))
-    slab = std::max(slab, (size_t)tsmm44_xg_grid(ctx->nloc) * b * b);
+  if (b == 32 && basis_bits == 64 && (ctx->fuse & 2)) {
+    const int xg = tsmm44_xg_grid(ctx->nloc);
+    slab = std::max(slab, (size_t)(xg + reduce_scratch_splits(xg)) * b * b);
+  }
   if (basis_bits == 32)  // fp32 Grams: up to (max_blocks-1) panels x 2b per split
     slab = std::max(slab, (size_t)gram32_splits(ctx->nloc) * std::max(1, max_blocks - 1) * b * 2 * b);
   ctx->slab_elems = slab;

@@ -193,10 +193,55 @@ __global__ __launch_bounds__(256) void k_reduce(const double* __restrict__ slab,
   }
 }
 
+// Many splits (the partial-reorth update's local-reorth Gram: one partial per 128-row tile,
+// ~78 k at C4a): sum fixed chunks of splits in parallel (256 per chunk, then 16) until at most
+// 64 remain, each level into the scratch after the previous one, then k_reduce — a fixed order
+// (bitwise reproducible); one k_reduce pass over 78 k partials is latency-bound (16 split lanes
+// per element, 64 workgroups): 310 us against ~130 us.
+static int red_chunk(int splits) { return splits > 4096 ? 256 : 16; }
+int reduce_scratch_splits(int splits) {
+  int tot = 0;
+  while (splits > 64) {
+    splits = (splits + red_chunk(splits) - 1) / red_chunk(splits);
+    tot += splits;
+  }
+  return tot;
+}
+__global__ __launch_bounds__(256) void k_reduce_chunks(const double* __restrict__ slab, int splits,
+                                                       int chunk, int64_t len,
+                                                       double* __restrict__ part) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int c = blockIdx.y;
+  if (e >= len) return;
+  const int s0 = c * chunk, s1 = s0 + chunk < splits ? s0 + chunk : splits;
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+  int sp = s0;
+  for (; sp + 3 < s1; sp += 4) {
+    a0 += slab[(int64_t)sp * len + e];
+    a1 += slab[(int64_t)(sp + 1) * len + e];
+    a2 += slab[(int64_t)(sp + 2) * len + e];
+    a3 += slab[(int64_t)(sp + 3) * len + e];
+  }
+  for (; sp < s1; ++sp) a0 += slab[(int64_t)sp * len + e];
+  part[(int64_t)c * len + e] = (a0 + a1) + (a2 + a3);
+}
+
 void reduce_slab(const double* slab, int splits, int64_t len, double* out, const int* skip,
                  hipStream_t s) {
   const int blocks = (int)((len + 15) / 16);
   hipLaunchKernelGGL(k_reduce, dim3(blocks), dim3(256), 0, s, slab, splits, len, out, skip);
+}
+
+void reduce_slab_many(double* slab, int splits, int64_t len, double* out, hipStream_t s) {
+  while (splits > 64) {  // scratch: reduce_scratch_splits(splits) x len after the partials
+    const int chunk = red_chunk(splits), nc = (splits + chunk - 1) / chunk;
+    double* part = slab + (int64_t)splits * len;
+    hipLaunchKernelGGL(k_reduce_chunks, dim3((unsigned)((len + 255) / 256), (unsigned)nc), dim3(256), 0,
+                       s, slab, splits, chunk, len, part);
+    slab = part;
+    splits = nc;
+  }
+  reduce_slab(slab, splits, len, out, nullptr, s);
 }
 
 // ----------------------------------------------------------------------------------------
