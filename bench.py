@@ -75,9 +75,10 @@ def parse():
     ap.add_argument("--keep-csr", type=int, default=1, choices=(0, 1),
                     help="0: release the device CSR once the band tiles are built "
                          "(RBL_OPT_KEEP_CSR; frees 12 B per nonzero for the basis at n = 5e7)")
-    ap.add_argument("--fuse", type=int, default=3, choices=(0, 1, 2, 3),
+    ap.add_argument("--fuse", type=int, default=7, choices=tuple(range(8)),
                     help="RBL_OPT_FUSE: bit 0 the 3-pass CholQR2, bit 1 the local-reorth Gram formed "
-                         "by the producing QR / partial-reorth update (same results; A/B switch)")
+                         "by the producing QR / partial-reorth update, bit 2 the local-reorth "
+                         "update applied by the band-tile SpMM (A/B switch)")
     ap.add_argument("--basis-bits", type=int, default=64, choices=(64, 32),
                     help="32: the mixed mode (fp32 Krylov basis + reorth on fp32 MFMA, fp64 A*Q / "
                          "3-term / QR) of BASELINE config 5, on this workload")
@@ -256,7 +257,11 @@ def main():
     # (+ read Q_{i-1} for the fused 3-term epilogue on the m_max step launches)
     bytes_step = nnz_loc * 12 + (nloc + 1) * 8 + 3 * nloc * b * 8
     bytes_start = nnz_loc * 12 + (nloc + 1) * 8 + 2 * nloc * b * 8
-    spmm_bytes = (m_max * bytes_step + bytes_start) / (m_max + 1)
+    # RBL_OPT_FUSE bit 2: the step launches from i = 2 on also apply the local reorth to the Q_i
+    # rows they stage (Q_i and Q_{i-1} are read anyway) and write Q_i back: + n b 8 each
+    lfused = bool(args.fuse & 4) and world == 1 and spmm_kid == 5 and b == 32 and args.basis_bits == 64 \
+        and os.environ.get("RBL_BT_PACK", "0") != "1"
+    spmm_bytes = (m_max * bytes_step + bytes_start + (m_max - 1) * nloc * b * 8 * lfused) / (m_max + 1)
     spmm_gbs = spmm_bytes / (spmm_ms * 1e-3) / 1e9
     reorth_flops = sum(8.0 * nloc * b * b * (i - 2) for i in range(4, m_max + 1, 2))
     reorth_ms = stage_per_run["part reorth"]
@@ -284,6 +289,7 @@ def main():
                  **({"q_row_gather_bytes_per_launch": int(nnz_loc * b * 8),
                      "gbs_incl_q_row_gathers": round((spmm_bytes + nnz_loc * b * 8) / (spmm_ms * 1e-3) / 1e9, 1)}
                     if spmm_kid in (1, 6) else {}),
+                 "fused_local_reorth": lfused,
                  "ms_per_launch": round(spmm_ms, 4)}
     mfma_peak = FP64_MFMA_PEAK_TF if args.basis_bits == 64 else FP32_MFMA_PEAK_TF
     # the clock the chip holds under these kernels (profiles/pmc_clock.json: GRBM_GUI_ACTIVE
@@ -410,7 +416,7 @@ def main():
                        "nnz_per_rank": nnz_ranks,
                        **({"device_blocks": args.device_blocks} if args.device_blocks else {}),
                        **({"keep_csr": 0} if not args.keep_csr else {}),
-                       **({"fuse": args.fuse} if args.fuse != 3 else {})},
+                       **({"fuse": args.fuse} if args.fuse != 7 else {})},
             "roofline": roofline,
             "roofline_secondary": roofline2,
             "stage_ms_per_run": {s: round(v, 3) for s, v in stage_per_run.items()},

@@ -66,6 +66,13 @@ struct CsrDev {
   // fails if another kernel would run with qloc set.
   const void* qloc = nullptr;
   int64_t loc_lo = 0, loc_hi = 0;
+  // local reorth fused into the band-tile SpMM (RBL_OPT_FUSE bit 2, one rank, b = 32, dense
+  // tiles): the kernel stages every Q ring row as Q_i - Q_{i-1} C (C = lfix_c, b x b on the
+  // device; Q_{i-1} = the SpMM's Qprev) and writes the corrected own rows back into lfix_q
+  // (= Qin) except the first and last H rows of each workgroup's range, which neighbours read
+  // raw — spmm_bt_locfix_rest corrects those after the SpMM (spmm_bt_locfix_ok: applicable)
+  const double* lfix_c = nullptr;
+  double* lfix_q = nullptr;
   // packed band tiles (bt_pack): per tile slot a header of bt_pack_words(NG) 8-B words (per
   // 1-KiB operand block the nonzero masks of element 0 / 1 of every lane, then the blocks'
   // uint16 start offsets + the tile's count, then the tile's first value index) and the
@@ -150,6 +157,9 @@ bool spmm_band(const CsrDev& A, const double* Qin, int64_t col_off, int b, doubl
 // spmm_bt.hip: band tiles in MFMA operand order streamed to VGPRs (b = 32, H in {32, 64});
 // false if not applicable.
 // Q32 / Qprev32 (optional, the fp32 basis): read fp32 blocks instead of Qin / Qprev.
+bool spmm_bt_locfix_ok(const CsrDev& A, int b);
+void spmm_bt_locfix_rest(const CsrDev& A, double* Q, const double* Qprev, const double* C,
+                         hipStream_t s);
 bool spmm_bt(const CsrDev& A, const double* Qin, int64_t col_off, int b, double* U,
              const double* Qprev, const double* Bi, hipStream_t s, double* ai_slab = nullptr,
              int* ai_parts = nullptr, const float* Q32 = nullptr, const float* Qprev32 = nullptr);

@@ -123,7 +123,7 @@ struct rbl_ctx {
   bool timers = false;
   int reorth_order = 0;
   int spmm_variant = 0;
-  int fuse = 3;               // RBL_OPT_FUSE
+  int fuse = 7;               // RBL_OPT_FUSE
   // the local-reorth coefficient Q_{i-1}^T Q_i of step cloc_step (S_CLOC), formed by the QR of
   // step cloc_step - 1 or by the last partial-reorth update of step cloc_step; 0: none
   int cloc_step = 0;
@@ -649,7 +649,8 @@ int ensure_qm64(rbl_ctx* ctx) {
 // the local rows, Q gathered to all n rows by the halo exchange).  Returns the number of
 // A_i partials the band kernel formed in `slab` (0: none), or a negative status.
 int apply_A(rbl_ctx* ctx, const double* Qin, int64_t off, int b, double* U, const double* Qprev,
-            const double* Bi, double* slab, const double* qloc = nullptr) {
+            const double* Bi, double* slab, const double* qloc = nullptr,
+            const double* lfix_c = nullptr) {
   if (ctx->nloc <= 0) return 0;
   if (ctx->csr_dropped && rbl_spmm_kernel_for(ctx, b) != 5)
     return fail(ctx, RBL_ERR_STATE, "the CSR was released (RBL_OPT_KEEP_CSR = 0): only the band-tile "
@@ -661,8 +662,16 @@ int apply_A(rbl_ctx* ctx, const double* Qin, int64_t off, int b, double* U, cons
       A.loc_lo = ctx->r0;
       A.loc_hi = ctx->r0 + ctx->nloc;
     }
+    if (lfix_c) {  // local reorth fused into the SpMM's staging (RBL_OPT_FUSE bit 2)
+      A.lfix_c = lfix_c;
+      A.lfix_q = const_cast<double*>(Qin);
+    }
     const int parts = spmm(A, Qin, off, b, U, Qprev, Bi, ctx->spmm_variant, ctx->stream, slab);
     if (parts < 0) return fail(ctx, RBL_ERR_INVALID, "internal: split-source SpMM needs the band-tile kernel");
+    if (lfix_c) {
+      StageScope t(ctx, RBL_STAGE_LOC_REORTH);
+      spmm_bt_locfix_rest(A, const_cast<double*>(Qin), Qprev, lfix_c, ctx->stream);
+    }
     return parts;
   }
   if (b > ctx->qfull_cols) {  // Q gathered to all n rows, zero-padded to 32 * dense_panels
@@ -1393,7 +1402,7 @@ int rbl_set_option(rbl_ctx* ctx, int option, int64_t value) {
     case RBL_OPT_SPLIT_HALO: ctx->split_halo = value != 0; return RBL_OK;
     case RBL_OPT_KEEP_CSR: ctx->keep_csr = value != 0; return RBL_OK;
     case RBL_OPT_FUSE:
-      if (value < 0 || value > 3) return fail(ctx, RBL_ERR_INVALID, "RBL_OPT_FUSE is a 2-bit mask");
+      if (value < 0 || value > 7) return fail(ctx, RBL_ERR_INVALID, "RBL_OPT_FUSE is a 3-bit mask");
       ctx->fuse = (int)value;
       return RBL_OK;
     default: return fail(ctx, RBL_ERR_INVALID, "unknown option");
@@ -2026,12 +2035,20 @@ int step_impl(rbl_ctx* ctx, int i, int part_reorth, double* A_out, double* B_out
   };
   if ((int)ctx->step_flags.size() <= i) ctx->step_flags.resize(i + 1, 0);
   ctx->step_flags[i] = part_reorth;
+  // fuse bit 2: the update itself rides on the SpMM below, which stages Q_i's rows corrected
+  // (one rank, fp64 basis, band tiles at b = 32; the same decision on every rank)
+  const bool lfuse = !f32 && i >= 2 && (ctx->fuse & 4) && ctx->nranks == 1 && fused && !ctx->dense &&
+                     rbl_spmm_kernel_for(ctx, b) == 5 &&
+                     spmm_bt_locfix_ok(csr(ctx), b);
+  const double* Cloc = nullptr;
   if (!f32 && i >= 2) {
     StageScope t(ctx, RBL_STAGE_LOC_REORTH);
     const bool have = ctx->cloc_step == i && (ctx->cloc_final || !modifies(i, part_reorth));
     const double* C = have ? smallp(ctx, S_CLOC) : ctx->d_C;
     if (!have) CHK(gram(ctx, run1(Qm, b), pan1(Qi, b), ctx->d_C, nullptr));
-    if (fused)
+    if (lfuse)
+      Cloc = C;
+    else if (fused)
       CHK(rowop(ctx, Qm, C, Qi, -1.0, 1.0, nullptr, nullptr));
     else
       CHK(tsmm_checked(ctx, run1(Qm, b), C, b, pan1(Qi, b), -1.0, 1.0, nullptr));
@@ -2064,7 +2081,7 @@ int step_impl(rbl_ctx* ctx, int i, int part_reorth, double* A_out, double* B_out
         return fail(ctx, RBL_ERR_INVALID, "internal: fp32 band-tile SpMM not applicable");
     } else {
       ai_parts = apply_A(ctx, Qin, off, b, ctx->d_U, Qm, i >= 2 ? smallp(ctx, S_BPREV) : nullptr,
-                         ctx->d_slab, split ? Qi : nullptr);
+                         ctx->d_slab, split ? Qi : nullptr, Cloc);
     }
     if (ai_parts < 0) return ai_parts;
     HIPC(hipGetLastError());

@@ -195,7 +195,7 @@ int spmm(const CsrDev& A, const double* Qin, int64_t col_off, int b, double* U,
   if ((variant == 0 || variant == 4) &&
       spmm_bt(A, Qin, col_off, b, U, Qprev, Bi, s, ai_slab, &parts))
     return parts;
-  if (A.qloc) return -2;  // the other kernels read the own rows from Qin: caller bug
+  if (A.qloc || A.lfix_c) return -2;  // band-tile kernel only (caller bug)
   if ((variant == 0 || variant == 3 || variant == 4) &&
       spmm_band(A, Qin, col_off, b, U, Qprev, Bi, s, ai_slab, &parts))
     return parts;

@@ -60,7 +60,8 @@ struct Geo {
   static constexpr int kUWave = 16 * kUStride;
   static constexpr int kUOff = kBtOff + kBtBytes;
   static constexpr int kLds = kUOff + 4 * kUWave;           // B = 32: 111,104 B; B = 16: 43,008 B
-  static_assert(kLds <= 160 * 1024, "LDS budget");
+  static constexpr int kCtOff = kLds;                       // VAR bit 10: the -C table
+  static_assert(kLds + 9216 <= 160 * 1024, "LDS budget");
 };
 // A_i operand at B = 32: lane reads ring slot pi(l & 15); pi maps the lanes {0-3, 12-15} of
 // each ds_read_b128 lane group to slot classes {0,1} mod 4 and {4-11} to {2,3} mod 4, so rows
@@ -95,7 +96,52 @@ struct BtArgs {
   double* ai_slab;       // AIG: per-workgroup partials of A_i (b x b row-major)
   const uint64_t* hdr;   // VAR bit 7: packed tiles (bt_pack) instead of A
   const double* pv;
+  const double* Cl;      // VAR bit 10: local reorth on staging (ring rows = Q - Qprev Cl),
+  double* Qw;            //   interior own rows written back here (CsrDev::lfix_q)
 };
+
+// ---- local reorth fused into the ring staging (VAR bit 10, B = 32) ----
+// Q_i -= Q_{i-1} (Q_{i-1}^T Q_i), one projection (RBL_gpu.jl:83-93, P1), applied to a 16-row
+// block as the SpMM stages it: D layout (lane: row 4G + q, columns 8p + 2j + {0, 1}) started
+// from the raw rows, then 8 k-steps of 4 MFMAs pairs with A = Q_{i-1} rows (lane & 15, columns
+// 8m + 2q + s: the EPI's A layout) and B = -C from an LDS table (row stride kCtLd: the four
+// lane groups q read rows 2 apart = 16 banks apart).  k_spmm_bt and k_locfix run this same
+// sequence, so a row has the same bits whichever kernel corrects it.
+constexpr int kCtLd = 36;
+constexpr int kCtBytes = 32 * kCtLd * 8;
+__device__ __forceinline__ void lf_loads(const double* rraw, const double* rprev, int lane,
+                                         d2v (&raw)[4], d2v (&qa)[4]) {
+  const int q = lane >> 4, j = lane & 3;
+#pragma unroll
+  for (int p = 0; p < 4; ++p) raw[p] = reinterpret_cast<const d2v*>(rraw + 2 * j)[4 * p];
+#pragma unroll
+  for (int m = 0; m < 4; ++m) qa[m] = reinterpret_cast<const d2v*>(rprev + 2 * q)[4 * m];
+}
+__device__ __forceinline__ void lf_table(const double* C, double* ct, int tid, int nthreads) {
+  for (int idx = tid; idx < 32 * 32; idx += nthreads) ct[(idx >> 5) * kCtLd + (idx & 31)] = -C[idx];
+}
+__device__ __forceinline__ void lf_block(const d2v (&raw)[4], const d2v (&qa)[4], const double* ct,
+                                         int lane, double (&acc)[4][2]) {
+  const int q = lane >> 4, j = lane & 3;
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    acc[p][0] = raw[p].x;
+    acc[p][1] = raw[p].y;
+  }
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const double av = s ? qa[m].y : qa[m].x;
+      const double* crow = ct + (8 * m + 2 * q + s) * kCtLd + 2 * j;
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        const d2v bv = *reinterpret_cast<const d2v*>(crow + 8 * p);
+        acc[p][0] = __builtin_amdgcn_mfma_f64_4x4x4f64(av, bv.x, acc[p][0], 0, 0, 0);
+        acc[p][1] = __builtin_amdgcn_mfma_f64_4x4x4f64(av, bv.y, acc[p][1], 0, 0, 0);
+      }
+    }
+}
 
 // VAR: bit 0 non-temporal A loads, bit 1 non-temporal U stores, bit 5 ablation (main-loop
 // MFMAs off: loads only), bit 6 fp32 Q / Q_{i-1} inputs, bit 7 packed tiles, bit 8 no LDS
@@ -162,9 +208,45 @@ void k_spmm_bt(BtArgs a) {
       btab[idx] = -a.Bi[y * B + x];
     }
   }
-  for (int idx = tid; idx < kRingSpan * NS; idx += bt::kThreads) {
-    const int64_t rho = 16 * T0 + idx / NS;
-    *ring_ptr(rho, idx % NS) = qload(rho, idx % NS);
+  // VAR bit 10: ring rows are staged corrected (local reorth), 16-row blocks per wave
+  constexpr bool LF = (VAR & 1024) != 0;
+  static_assert(!LF || (B == 32 && !(VAR & (64 | 128))), "fused local reorth: b = 32, fp64, dense tiles");
+  double* const ct = reinterpret_cast<double*>(smem + L::kCtOff);
+  const int64_t own_lo = 16 * T0 + H;                                  // written back here:
+  const int64_t own_hi = 16 * T1 - H < a.nrows ? 16 * T1 - H : a.nrows;  // the range's interior
+  // 16-row block at ring coordinate rho0: raw rows (D layout) and Q_{i-1} rows (A layout)
+  auto lf_issue = [&](int64_t rho0, d2v (&raw)[4], d2v (&qa)[4]) {
+    const int64_t cr = rho0 + gq + 4 * G + q, ca = rho0 + gq + i16;
+    const bool inr = cr >= a.q_lo && cr < a.q_hi, ina = ca >= a.q_lo && ca < a.q_hi;
+    lf_loads(inr ? a.Q + (cr - a.col_off) * B : a.zrow, ina ? a.Qprev + (ca - a.row0) * B : a.zrow,
+             lane, raw, qa);
+  };
+  auto lf_finish = [&](int64_t rho0, const d2v (&raw)[4], const d2v (&qa)[4]) {
+    double f[4][2];
+    lf_block(raw, qa, ct, lane, f);
+    const int64_t rr = rho0 + 4 * G + q;  // ring coordinate of the lane's row
+    const int64_t lr = rr + gq - a.row0;  // its local row
+    const bool wb = lr >= own_lo && lr < own_hi;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const d2v v = d2v{f[p][0], f[p][1]};
+      *ring_ptr(rr, 4 * p + j) = v;
+      if (wb) reinterpret_cast<d2v*>(a.Qw + lr * B + 2 * j)[4 * p] = v;
+    }
+  };
+  if constexpr (LF) {
+    lf_table(a.Cl, ct, tid, bt::kThreads);
+    __syncthreads();
+    for (int bb = wave; bb < kRingSpan / 16; bb += 4) {
+      d2v raw[4], qa[4];
+      lf_issue(16 * T0 + 16 * bb, raw, qa);
+      lf_finish(16 * T0 + 16 * bb, raw, qa);
+    }
+  } else {
+    for (int idx = tid; idx < kRingSpan * NS; idx += bt::kThreads) {
+      const int64_t rho = 16 * T0 + idx / NS;
+      *ring_ptr(rho, idx % NS) = qload(rho, idx % NS);
+    }
   }
 
   // ---- per-wave state ----
@@ -276,8 +358,13 @@ void k_spmm_bt(BtArgs a) {
       return B == 32 ? rn + 4 * i + q : rn + 8 * (i >> 1) + 2 * q + 4 * (i & 1) + (i16 >> 3);
     };
     constexpr int NST = B == 32 ? 4 : 2;
+    d2v lraw[4], lqa[4];
+    if constexpr (LF) {
+      lf_issue(rn, lraw, lqa);
+    } else {
 #pragma unroll
-    for (int i = 0; i < NST; ++i) st[i] = qload(st_row(B == 32 ? i : 2 * i), i16 % NS);
+      for (int i = 0; i < NST; ++i) st[i] = qload(st_row(B == 32 ? i : 2 * i), i16 % NS);
+    }
 
     if (tw < T1) {  // wave-uniform
       const int64_t tn = clamp_t(tw + 4);
@@ -388,8 +475,12 @@ void k_spmm_bt(BtArgs a) {
         __builtin_amdgcn_wave_barrier();
       }
     }
+    if constexpr (LF) {
+      lf_finish(rn, lraw, lqa);
+    } else {
 #pragma unroll
-    for (int i = 0; i < NST; ++i) *ring_ptr(st_row(B == 32 ? i : 2 * i), i16 % NS) = st[i];
+      for (int i = 0; i < NST; ++i) *ring_ptr(st_row(B == 32 ? i : 2 * i), i16 % NS) = st[i];
+    }
     if constexpr (VAR & 512) __builtin_amdgcn_wave_barrier();  // ablation: no round barrier
     else __syncthreads();
   }
@@ -423,9 +514,9 @@ void k_spmm_bt(BtArgs a) {
 
 template <int B, int NG, bool EPI, bool AIG, int VAR>
 static void launch_bt_v(const BtArgs& a, int grid, hipStream_t s) {
-  ensure_lds_attr(reinterpret_cast<const void*>(&k_spmm_bt<B, NG, EPI, AIG, VAR>), bt::Geo<B>::kLds);
-  hipLaunchKernelGGL((k_spmm_bt<B, NG, EPI, AIG, VAR>), dim3(grid), dim3(bt::kThreads),
-                     bt::Geo<B>::kLds, s, a);
+  constexpr int lds = bt::Geo<B>::kLds + ((VAR & 1024) ? kCtBytes : 0);
+  ensure_lds_attr(reinterpret_cast<const void*>(&k_spmm_bt<B, NG, EPI, AIG, VAR>), lds);
+  hipLaunchKernelGGL((k_spmm_bt<B, NG, EPI, AIG, VAR>), dim3(grid), dim3(bt::kThreads), lds, s, a);
 }
 template <int B, int NG, bool EPI, bool AIG>
 static void launch_bt_t(const BtArgs& a, int grid, hipStream_t s, bool f32) {
@@ -485,6 +576,15 @@ bool spmm_bt(const CsrDev& A, const double* Qin, int64_t col_off, int b, double*
   const bool aig = ai_slab != nullptr;
   a.ai_slab = ai_slab;
   if (ai_parts) *ai_parts = aig ? grid : 0;
+  a.Cl = A.lfix_c;
+  a.Qw = A.lfix_q;
+  if (A.lfix_c) {  // fused local reorth (spmm_bt_locfix_ok checked the format; EPI + A_i here)
+    if (b != 32 || f32 || a.hdr || !epi || !aig || A.qloc || A.lfix_q != Qin || col_off != 0)
+      return false;
+    if (A.bt_ng == 9) launch_bt_v<32, 9, true, true, 3 | 1024>(a, grid, s);
+    else launch_bt_v<32, 5, true, true, 3 | 1024>(a, grid, s);
+    return true;
+  }
   const int key = (b == 32 ? 8 : 0) | (A.bt_ng == 9 ? 4 : 0) | (epi ? 2 : 0) | (aig ? 1 : 0);
   switch (key) {
 #define RBL_BT_CASE(K, BB, NG, E, G) \
@@ -500,6 +600,54 @@ bool spmm_bt(const CsrDev& A, const double* Qin, int64_t col_off, int b, double*
 #undef RBL_BT_CASE
   }
   return true;
+}
+
+// The own rows the fused SpMM left raw (the first and last H rows of each workgroup's tile
+// range: its neighbours read them raw as halo), corrected in place after it, one wave per
+// 16-row block — the same lf_block sequence, so the same bits as the rows written in the SpMM.
+template <int H>
+__global__ __launch_bounds__(64) void k_locfix(double* Q, const double* __restrict__ Qprev,
+                                               const double* __restrict__ C, int64_t nrows,
+                                               int64_t ntiles, int64_t tpw, const double* zrow) {
+  __shared__ __attribute__((aligned(16))) double ct[32 * kCtLd];
+  const int lane = threadIdx.x;
+  lf_table(C, ct, lane, 64);
+  __syncthreads();
+  constexpr int per = H / 16;
+  const int64_t wg = blockIdx.x / (2 * per);
+  const int side = (blockIdx.x / per) & 1, kb = blockIdx.x % per;
+  const int64_t T0 = wg * tpw, T1 = T0 + tpw < ntiles ? T0 + tpw : ntiles;
+  const int64_t lo = side == 0 ? 16 * T0 : (16 * T0 + H > 16 * T1 - H ? 16 * T0 + H : 16 * T1 - H);
+  int64_t hi = side == 0 ? (16 * T1 < 16 * T0 + H ? 16 * T1 : 16 * T0 + H) : 16 * T1;
+  hi = hi < nrows ? hi : nrows;
+  const int64_t r0 = lo + 16 * kb;
+  if (r0 >= hi) return;
+  const int q = lane >> 4, j = lane & 3, G = (lane >> 2) & 3, i16 = lane & 15;
+  const int64_t rr = r0 + 4 * G + q, ra = r0 + i16;
+  d2v raw[4], qa[4];
+  lf_loads(rr < nrows ? Q + rr * 32 : zrow, ra < nrows ? Qprev + ra * 32 : zrow, lane, raw, qa);
+  double f[4][2];
+  lf_block(raw, qa, ct, lane, f);
+  if (rr < hi) {
+#pragma unroll
+    for (int p = 0; p < 4; ++p) reinterpret_cast<d2v*>(Q + rr * 32 + 2 * j)[4 * p] = d2v{f[p][0], f[p][1]};
+  }
+}
+
+bool spmm_bt_locfix_ok(const CsrDev& A, int b) {
+  return b == 32 && A.bt && !A.btp_hdr && A.ntiles > 0 && (A.bt_ng == 5 || A.bt_ng == 9) &&
+         !A.qloc && A.row0 == 0 && A.q_lo == 0 && A.q_hi == A.nrows;
+}
+
+void spmm_bt_locfix_rest(const CsrDev& A, double* Q, const double* Qprev, const double* C,
+                         hipStream_t s) {
+  const int64_t grid = (A.ntiles + A.bt_tiles_per_wg - 1) / A.bt_tiles_per_wg;
+  if (A.bt_ng == 9)
+    hipLaunchKernelGGL(k_locfix<64>, dim3((unsigned)(grid * 8)), dim3(64), 0, s, Q, Qprev, C, A.nrows,
+                       A.ntiles, A.bt_tiles_per_wg, A.zrow);
+  else
+    hipLaunchKernelGGL(k_locfix<32>, dim3((unsigned)(grid * 4)), dim3(64), 0, s, Q, Qprev, C, A.nrows,
+                       A.ntiles, A.bt_tiles_per_wg, A.zrow);
 }
 
 // ---- format (once per matrix) -----------------------------------------------------------

@@ -80,11 +80,16 @@ extern "C" {
                                    * (n = 5e7: 60 GB).  Then only b in {16, 32} can run and
                                    * rbl_get_matrix_csr fails.  Set before the matrix.          */
 #define RBL_OPT_FUSE          6   /* pass fusions of the memory-bound b x b stages (b in {16, 32},
-                                   * fp64 basis), bit for bit the same results: bit 0 (default
+                                   * fp64 basis); bits 0 and 1 give the same results bit for
+                                   * bit, bits 1 and 2 to rounding: bit 0 (default
                                    * on) CholQR2 in 3 passes over the block instead of 4 (Q1 is
                                    * recomputed, never stored); bit 1 (default on) the next
                                    * step's local-reorth Gram Q_i^T Q_{i+1} formed while the QR
-                                   * writes Q_{i+1}, used when that step runs no partial reorth */
+                                   * writes Q_{i+1}, used when that step runs no partial reorth;
+                                   * bit 2 (default on) the local-reorth update
+                                   * Q_i -= Q_{i-1} C applied by the SpMM as it stages Q_i's
+                                   * rows (one rank, band tiles, b = 32; rounding differs from
+                                   * the separate pass at the 1e-16 level, not bit for bit) */
 
 typedef struct rbl_ctx rbl_ctx;
 

@@ -298,6 +298,35 @@ def test_pass_fusions(rbl, b, bits):
         assert d < 1e-12, (t, d)
 
 
+@pytest.mark.parametrize("n,W", [(4000, 64), (40003, 64), (100003, 64), (50001, 32)])
+def test_local_reorth_fused_into_spmm(rbl, n, W):
+    """RBL_OPT_FUSE bit 2: the local reorth Q_i -= Q_{i-1} C (RBL_gpu.jl:83-93) applied by the
+    band-tile SpMM as it stages Q_i's rows — interior rows written back by the SpMM, the first
+    and last H rows of every workgroup range by k_locfix afterwards.  n covers ranges shorter
+    than 2H (all rows by k_locfix), just over it, long ones, H = 32 and a ragged last tile.
+    Per-step A_i / B_{i+1} and the Ritz pairs agree with the separate pass (fuse 3) to 1e-12."""
+    from rbl import _lib
+    k, b = 10, 32
+    plant = matgen.planted_spectrum(k)
+    omega = np.random.default_rng(n).standard_normal((n, b))
+    out = {}
+    for fuse in (3, 7):
+        with rbl.Context(0) as ctx:
+            ctx.set_option(_lib.RBL_OPT_FUSE, fuse)
+            ctx.gen_hashwindow(n, W, 0.7734, 11, plant)
+            assert ctx.spmm_kernel_for(b) == 5  # band tiles: the fused path applies
+            D, V, info = rbl.lanczos(ctx, k, b, omega=omega, trace=True)
+        assert info.converged
+        out[fuse] = (np.array(info.trace_A), np.array(info.trace_B), D, V)
+    assert out[3][0].shape == out[7][0].shape
+    for t in (0, 1):
+        d = np.abs(out[7][t] - out[3][t]).max() / np.abs(out[3][t]).max()
+        assert d < 1e-12, (t, d)
+    D3, V3, D7, V7 = out[3][2], out[3][3], out[7][2], out[7][3]
+    assert (np.abs(D7 - D3) / np.abs(D3)).max() < 1e-12
+    assert (1 - np.abs(np.sum(V7 * V3, axis=0))).max() < 1e-10
+
+
 @pytest.mark.parametrize("case", ["converges", "runs_out"])
 def test_speculative_steps_change_nothing(rbl, case):
     """Steps enqueued ahead of a convergence check (rbl.lanczos speculate) leave D, V, the step
