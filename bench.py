@@ -259,7 +259,7 @@ def main():
     bytes_start = nnz_loc * 12 + (nloc + 1) * 8 + 2 * nloc * b * 8
     # RBL_OPT_FUSE bit 2: the step launches from i = 2 on also apply the local reorth to the Q_i
     # rows they stage (Q_i and Q_{i-1} are read anyway) and write Q_i back: + n b 8 each
-    lfused = bool(args.fuse & 4) and world == 1 and spmm_kid == 5 and b == 32 and args.basis_bits == 64 \
+    lfused = bool(args.fuse & 4) and spmm_kid == 5 and b == 32 and args.basis_bits == 64 \
         and os.environ.get("RBL_BT_PACK", "0") != "1"
     spmm_bytes = (m_max * bytes_step + bytes_start + (m_max - 1) * nloc * b * 8 * lfused) / (m_max + 1)
     spmm_gbs = spmm_bytes / (spmm_ms * 1e-3) / 1e9

@@ -69,10 +69,13 @@ struct CsrDev {
   // local reorth fused into the band-tile SpMM (RBL_OPT_FUSE bit 2, one rank, b = 32, dense
   // tiles): the kernel stages every Q ring row as Q_i - Q_{i-1} C (C = lfix_c, b x b on the
   // device; Q_{i-1} = the SpMM's Qprev) and writes the corrected own rows back into lfix_q
-  // (= Qin) except the first and last H rows of each workgroup's range, which neighbours read
-  // raw — spmm_bt_locfix_rest corrects those after the SpMM (spmm_bt_locfix_ok: applicable)
+  // (the block Q_i) except the first and last H rows of each workgroup's range, which
+  // neighbours read raw — spmm_bt_locfix_rest corrects those after the SpMM
+  // (spmm_bt_locfix_ok: applicable; spmm_bt_locfix_edges: the rank-edge rows beforehand)
   const double* lfix_c = nullptr;
   double* lfix_q = nullptr;
+  int64_t lfix_lo = 0, lfix_hi = 0;  // local rows still raw (several ranks: the rank's first and
+                                     // last H rows were corrected before the halo exchange)
   // packed band tiles (bt_pack): per tile slot a header of bt_pack_words(NG) 8-B words (per
   // 1-KiB operand block the nonzero masks of element 0 / 1 of every lane, then the blocks'
   // uint16 start offsets + the tile's count, then the tile's first value index) and the
@@ -158,6 +161,9 @@ bool spmm_band(const CsrDev& A, const double* Qin, int64_t col_off, int b, doubl
 // false if not applicable.
 // Q32 / Qprev32 (optional, the fp32 basis): read fp32 blocks instead of Qin / Qprev.
 bool spmm_bt_locfix_ok(const CsrDev& A, int b);
+int spmm_bt_halfwidth(const CsrDev& A);
+void spmm_bt_locfix_edges(const CsrDev& A, double* Q, const double* Qprev, const double* C,
+                          int64_t lo0, int64_t hi0, int64_t lo1, int64_t hi1, hipStream_t s);
 void spmm_bt_locfix_rest(const CsrDev& A, double* Q, const double* Qprev, const double* C,
                          hipStream_t s);
 bool spmm_bt(const CsrDev& A, const double* Qin, int64_t col_off, int b, double* U,

@@ -650,7 +650,8 @@ int ensure_qm64(rbl_ctx* ctx) {
 // A_i partials the band kernel formed in `slab` (0: none), or a negative status.
 int apply_A(rbl_ctx* ctx, const double* Qin, int64_t off, int b, double* U, const double* Qprev,
             const double* Bi, double* slab, const double* qloc = nullptr,
-            const double* lfix_c = nullptr) {
+            const double* lfix_c = nullptr, double* lfix_q = nullptr, int64_t lf_lo = 0,
+            int64_t lf_hi = 0) {
   if (ctx->nloc <= 0) return 0;
   if (ctx->csr_dropped && rbl_spmm_kernel_for(ctx, b) != 5)
     return fail(ctx, RBL_ERR_STATE, "the CSR was released (RBL_OPT_KEEP_CSR = 0): only the band-tile "
@@ -664,13 +665,15 @@ int apply_A(rbl_ctx* ctx, const double* Qin, int64_t off, int b, double* U, cons
     }
     if (lfix_c) {  // local reorth fused into the SpMM's staging (RBL_OPT_FUSE bit 2)
       A.lfix_c = lfix_c;
-      A.lfix_q = const_cast<double*>(Qin);
+      A.lfix_q = lfix_q;
+      A.lfix_lo = lf_lo;
+      A.lfix_hi = lf_hi;
     }
     const int parts = spmm(A, Qin, off, b, U, Qprev, Bi, ctx->spmm_variant, ctx->stream, slab);
     if (parts < 0) return fail(ctx, RBL_ERR_INVALID, "internal: split-source SpMM needs the band-tile kernel");
     if (lfix_c) {
       StageScope t(ctx, RBL_STAGE_LOC_REORTH);
-      spmm_bt_locfix_rest(A, const_cast<double*>(Qin), Qprev, lfix_c, ctx->stream);
+      spmm_bt_locfix_rest(A, lfix_q, Qprev, lfix_c, ctx->stream);
     }
     return parts;
   }
@@ -2036,19 +2039,26 @@ int step_impl(rbl_ctx* ctx, int i, int part_reorth, double* A_out, double* B_out
   if ((int)ctx->step_flags.size() <= i) ctx->step_flags.resize(i + 1, 0);
   ctx->step_flags[i] = part_reorth;
   // fuse bit 2: the update itself rides on the SpMM below, which stages Q_i's rows corrected
-  // (one rank, fp64 basis, band tiles at b = 32; the same decision on every rank)
-  const bool lfuse = !f32 && i >= 2 && (ctx->fuse & 4) && ctx->nranks == 1 && fused && !ctx->dense &&
-                     rbl_spmm_kernel_for(ctx, b) == 5 &&
-                     spmm_bt_locfix_ok(csr(ctx), b);
+  // (fp64 basis, band tiles at b = 32; no collective depends on the choice)
+  const bool lfuse = !f32 && i >= 2 && (ctx->fuse & 4) && fused && !ctx->dense && ctx->nloc > 0 &&
+                     rbl_spmm_kernel_for(ctx, b) == 5 && spmm_bt_locfix_ok(csr(ctx), b);
   const double* Cloc = nullptr;
+  int64_t lf_lo = 0, lf_hi = ctx->nloc;
   if (!f32 && i >= 2) {
     StageScope t(ctx, RBL_STAGE_LOC_REORTH);
     const bool have = ctx->cloc_step == i && (ctx->cloc_final || !modifies(i, part_reorth));
     const double* C = have ? smallp(ctx, S_CLOC) : ctx->d_C;
     if (!have) CHK(gram(ctx, run1(Qm, b), pan1(Qi, b), ctx->d_C, nullptr));
-    if (lfuse)
+    if (lfuse) {
       Cloc = C;
-    else if (fused)
+      if (ctx->nranks > 1) {  // the rows the neighbours receive: corrected before the exchange
+        const int64_t H = spmm_bt_halfwidth(csr(ctx));
+        lf_lo = std::min<int64_t>(H, ctx->nloc);
+        lf_hi = std::max<int64_t>(lf_lo, ctx->nloc - H);
+        spmm_bt_locfix_edges(csr(ctx), Qi, Qm, C, 0, lf_lo, lf_hi, ctx->nloc, ctx->stream);
+        HIPC(hipGetLastError());
+      }
+    } else if (fused)
       CHK(rowop(ctx, Qm, C, Qi, -1.0, 1.0, nullptr, nullptr));
     else
       CHK(tsmm_checked(ctx, run1(Qm, b), C, b, pan1(Qi, b), -1.0, 1.0, nullptr));
@@ -2081,7 +2091,7 @@ int step_impl(rbl_ctx* ctx, int i, int part_reorth, double* A_out, double* B_out
         return fail(ctx, RBL_ERR_INVALID, "internal: fp32 band-tile SpMM not applicable");
     } else {
       ai_parts = apply_A(ctx, Qin, off, b, ctx->d_U, Qm, i >= 2 ? smallp(ctx, S_BPREV) : nullptr,
-                         ctx->d_slab, split ? Qi : nullptr, Cloc);
+                         ctx->d_slab, split ? Qi : nullptr, Cloc, Qi, lf_lo, lf_hi);
     }
     if (ai_parts < 0) return ai_parts;
     HIPC(hipGetLastError());

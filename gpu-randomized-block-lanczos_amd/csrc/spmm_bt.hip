@@ -97,7 +97,8 @@ struct BtArgs {
   const uint64_t* hdr;   // VAR bit 7: packed tiles (bt_pack) instead of A
   const double* pv;
   const double* Cl;      // VAR bit 10: local reorth on staging (ring rows = Q - Qprev Cl),
-  double* Qw;            //   interior own rows written back here (CsrDev::lfix_q)
+  double* Qw;            //   interior own rows written back here (CsrDev::lfix_q); only the
+  int64_t lf_lo, lf_hi;  //   local rows [lf_lo, lf_hi) are raw, the others already corrected
 };
 
 // ---- local reorth fused into the ring staging (VAR bit 10, B = 32) ----
@@ -212,14 +213,22 @@ void k_spmm_bt(BtArgs a) {
   constexpr bool LF = (VAR & 1024) != 0;
   static_assert(!LF || (B == 32 && !(VAR & (64 | 128))), "fused local reorth: b = 32, fp64, dense tiles");
   double* const ct = reinterpret_cast<double*>(smem + L::kCtOff);
-  const int64_t own_lo = 16 * T0 + H;                                  // written back here:
-  const int64_t own_hi = 16 * T1 - H < a.nrows ? 16 * T1 - H : a.nrows;  // the range's interior
-  // 16-row block at ring coordinate rho0: raw rows (D layout) and Q_{i-1} rows (A layout)
+  // written back here: the raw rows of the range's interior (its first and last H rows are
+  // read raw by the neighbouring workgroups: k_locfix corrects them after the SpMM)
+  const int64_t own_lo = 16 * T0 + H > a.lf_lo ? 16 * T0 + H : a.lf_lo;
+  int64_t own_hi = 16 * T1 - H < a.nrows ? 16 * T1 - H : a.nrows;
+  own_hi = own_hi < a.lf_hi ? own_hi : a.lf_hi;
+  // 16-row block at ring coordinate rho0: rows (D layout) as qload reads them, and the Q_{i-1}
+  // rows (A layout) of the raw ones — zero for the rest (rank-edge rows corrected before the
+  // halo exchange, neighbours' rows, rows past the matrix), which the MFMAs then leave as read
   auto lf_issue = [&](int64_t rho0, d2v (&raw)[4], d2v (&qa)[4]) {
     const int64_t cr = rho0 + gq + 4 * G + q, ca = rho0 + gq + i16;
-    const bool inr = cr >= a.q_lo && cr < a.q_hi, ina = ca >= a.q_lo && ca < a.q_hi;
-    lf_loads(inr ? a.Q + (cr - a.col_off) * B : a.zrow, ina ? a.Qprev + (ca - a.row0) * B : a.zrow,
-             lane, raw, qa);
+    const bool inr = cr >= a.q_lo && cr < a.q_hi;
+    const bool ownr = cr >= a.loc_lo && cr < a.loc_hi;  // split halo: own rows from the block
+    const int64_t la = ca - a.row0;
+    const double* rp = ownr ? static_cast<const double*>(a.Qloc) + (cr - a.loc_lo) * B
+                            : inr ? a.Q + (cr - a.col_off) * B : a.zrow;
+    lf_loads(rp, la >= a.lf_lo && la < a.lf_hi ? a.Qprev + la * B : a.zrow, lane, raw, qa);
   };
   auto lf_finish = [&](int64_t rho0, const d2v (&raw)[4], const d2v (&qa)[4]) {
     double f[4][2];
@@ -579,8 +588,9 @@ bool spmm_bt(const CsrDev& A, const double* Qin, int64_t col_off, int b, double*
   a.Cl = A.lfix_c;
   a.Qw = A.lfix_q;
   if (A.lfix_c) {  // fused local reorth (spmm_bt_locfix_ok checked the format; EPI + A_i here)
-    if (b != 32 || f32 || a.hdr || !epi || !aig || A.qloc || A.lfix_q != Qin || col_off != 0)
-      return false;
+    if (b != 32 || f32 || a.hdr || !epi || !aig) return false;
+    a.lf_lo = A.lfix_lo;
+    a.lf_hi = A.lfix_hi;
     if (A.bt_ng == 9) launch_bt_v<32, 9, true, true, 3 | 1024>(a, grid, s);
     else launch_bt_v<32, 5, true, true, 3 | 1024>(a, grid, s);
     return true;
@@ -608,7 +618,8 @@ bool spmm_bt(const CsrDev& A, const double* Qin, int64_t col_off, int b, double*
 template <int H>
 __global__ __launch_bounds__(64) void k_locfix(double* Q, const double* __restrict__ Qprev,
                                                const double* __restrict__ C, int64_t nrows,
-                                               int64_t ntiles, int64_t tpw, const double* zrow) {
+                                               int64_t ntiles, int64_t tpw, const double* zrow,
+                                               int64_t wlo, int64_t whi) {
   __shared__ __attribute__((aligned(16))) double ct[32 * kCtLd];
   const int lane = threadIdx.x;
   lf_table(C, ct, lane, 64);
@@ -628,6 +639,33 @@ __global__ __launch_bounds__(64) void k_locfix(double* Q, const double* __restri
   lf_loads(rr < nrows ? Q + rr * 32 : zrow, ra < nrows ? Qprev + ra * 32 : zrow, lane, raw, qa);
   double f[4][2];
   lf_block(raw, qa, ct, lane, f);
+  if (rr < hi && rr >= wlo && rr < whi) {  // the raw rows only
+#pragma unroll
+    for (int p = 0; p < 4; ++p) reinterpret_cast<d2v*>(Q + rr * 32 + 2 * j)[4 * p] = d2v{f[p][0], f[p][1]};
+  }
+}
+
+// Several ranks: the first and last H local rows — the neighbours' halo — corrected in place
+// before the halo exchange, so every rank stages them as final rows.  Rows [lo0, hi0) then
+// [lo1, hi1), one wave per 16-row block.
+__global__ __launch_bounds__(64) void k_locfix_ranges(double* Q, const double* __restrict__ Qprev,
+                                                      const double* __restrict__ C, int64_t nrows,
+                                                      const double* zrow, int64_t lo0, int64_t hi0,
+                                                      int64_t lo1, int64_t hi1) {
+  __shared__ __attribute__((aligned(16))) double ct[32 * kCtLd];
+  const int lane = threadIdx.x;
+  lf_table(C, ct, lane, 64);
+  __syncthreads();
+  const int64_t nb0 = (hi0 - lo0 + 15) / 16;
+  const int64_t r0 = blockIdx.x < nb0 ? lo0 + 16 * (int64_t)blockIdx.x : lo1 + 16 * ((int64_t)blockIdx.x - nb0);
+  const int64_t hi = blockIdx.x < nb0 ? hi0 : hi1;
+  if (r0 >= hi) return;
+  const int q = lane >> 4, j = lane & 3, G = (lane >> 2) & 3, i16 = lane & 15;
+  const int64_t rr = r0 + 4 * G + q, ra = r0 + i16;
+  d2v raw[4], qa[4];
+  lf_loads(rr < nrows ? Q + rr * 32 : zrow, ra < nrows ? Qprev + ra * 32 : zrow, lane, raw, qa);
+  double f[4][2];
+  lf_block(raw, qa, ct, lane, f);
   if (rr < hi) {
 #pragma unroll
     for (int p = 0; p < 4; ++p) reinterpret_cast<d2v*>(Q + rr * 32 + 2 * j)[4 * p] = d2v{f[p][0], f[p][1]};
@@ -635,8 +673,17 @@ __global__ __launch_bounds__(64) void k_locfix(double* Q, const double* __restri
 }
 
 bool spmm_bt_locfix_ok(const CsrDev& A, int b) {
-  return b == 32 && A.bt && !A.btp_hdr && A.ntiles > 0 && (A.bt_ng == 5 || A.bt_ng == 9) &&
-         !A.qloc && A.row0 == 0 && A.q_lo == 0 && A.q_hi == A.nrows;
+  return b == 32 && A.bt && !A.btp_hdr && A.ntiles > 0 && (A.bt_ng == 5 || A.bt_ng == 9);
+}
+
+int spmm_bt_halfwidth(const CsrDev& A) { return 8 * (A.bt_ng - 1); }
+
+void spmm_bt_locfix_edges(const CsrDev& A, double* Q, const double* Qprev, const double* C,
+                          int64_t lo0, int64_t hi0, int64_t lo1, int64_t hi1, hipStream_t s) {
+  const int64_t nb = (hi0 - lo0 + 15) / 16 + (hi1 - lo1 + 15) / 16;
+  if (nb > 0)
+    hipLaunchKernelGGL(k_locfix_ranges, dim3((unsigned)nb), dim3(64), 0, s, Q, Qprev, C, A.nrows, A.zrow,
+                       lo0, hi0, lo1, hi1);
 }
 
 void spmm_bt_locfix_rest(const CsrDev& A, double* Q, const double* Qprev, const double* C,
@@ -644,10 +691,10 @@ void spmm_bt_locfix_rest(const CsrDev& A, double* Q, const double* Qprev, const 
   const int64_t grid = (A.ntiles + A.bt_tiles_per_wg - 1) / A.bt_tiles_per_wg;
   if (A.bt_ng == 9)
     hipLaunchKernelGGL(k_locfix<64>, dim3((unsigned)(grid * 8)), dim3(64), 0, s, Q, Qprev, C, A.nrows,
-                       A.ntiles, A.bt_tiles_per_wg, A.zrow);
+                       A.ntiles, A.bt_tiles_per_wg, A.zrow, A.lfix_lo, A.lfix_hi);
   else
     hipLaunchKernelGGL(k_locfix<32>, dim3((unsigned)(grid * 4)), dim3(64), 0, s, Q, Qprev, C, A.nrows,
-                       A.ntiles, A.bt_tiles_per_wg, A.zrow);
+                       A.ntiles, A.bt_tiles_per_wg, A.zrow, A.lfix_lo, A.lfix_hi);
 }
 
 // ---- format (once per matrix) -----------------------------------------------------------
