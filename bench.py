@@ -85,19 +85,23 @@ def parse():
     return ap.parse_args()
 
 
-def streamed_bytes(kid, nloc, nnz_loc, b, halfwidth, m_max):
+def streamed_bytes(kid, nloc, nnz_loc, b, halfwidth, m_max, fmt=1):
     """Bytes the chosen SpMM kernel itself reads and writes per launch (step launches carry the
     Q_{i-1} epilogue), beside SURVEY's CSR-based algorithmic bytes: the band-tile kernel (5)
     streams 16 x (16 + 2H) dense doubles per 16-row tile instead of 12 B per nonzero; the
     LDS-band kernel (3) 8 B value + 2 B position per nonzero plus the row pointers.  Packed
     band tiles (RBL_BT_PACK=1; dense by default) stream the nonzeros and a header of 24
-    (H = 32) or 42 (H = 64) 8-B words per tile."""
+    (H = 32) or 42 (H = 64) 8-B words per tile; half band tiles (format 3, the default for a
+    symmetric A) the diagonal block and the right strip, 16 x (16 + H) doubles per tile (the
+    left part is the previous tiles' strips again, read back through L2)."""
     vec = (m_max * 3 + 2) / (m_max + 1) * nloc * b * 8
     if kid == 5:
         H = 32 if halfwidth <= 32 else 64
         tiles = -(-nloc // 16)
-        if os.environ.get("RBL_BT_PACK", "0") == "1":
+        if fmt == 2:
             return nnz_loc * 8 + tiles * 8 * (24 if H == 32 else 42) + vec
+        if fmt == 3:
+            return tiles * 16 * (16 + H) * 8 + vec
         return tiles * 16 * (16 + 2 * H) * 8 + vec
     if kid == 3:
         return nnz_loc * 10 + (nloc + 1) * 8 + vec
@@ -225,6 +229,7 @@ def main():
     ctx.set_option(_lib.RBL_OPT_FUSE, args.fuse)
     m_max = rbl.rbl_gpu.max_steps_for(args.kryl, b)
     spmm_kid = ctx.spmm_kernel_for(b)
+    mat_fmt = ctx.matrix_format()
     spmm_kernel = {1: "gather", 2: "lds-window", 3: "lds-band-mfma", 5: "band-tile-mfma",
                    6: "segmented-gather"}[spmm_kid]
 
@@ -260,7 +265,7 @@ def main():
     # RBL_OPT_FUSE bit 2: the step launches from i = 2 on also apply the local reorth to the Q_i
     # rows they stage (Q_i and Q_{i-1} are read anyway) and write Q_i back: + n b 8 each
     lfused = bool(args.fuse & 4) and spmm_kid == 5 and b == 32 and args.basis_bits == 64 \
-        and os.environ.get("RBL_BT_PACK", "0") != "1"
+        and mat_fmt != 2
     spmm_bytes = (m_max * bytes_step + bytes_start + (m_max - 1) * nloc * b * 8 * lfused) / (m_max + 1)
     spmm_gbs = spmm_bytes / (spmm_ms * 1e-3) / 1e9
     reorth_flops = sum(8.0 * nloc * b * b * (i - 2) for i in range(4, m_max + 1, 2))
@@ -273,8 +278,11 @@ def main():
     try:
         with open(args.traffic_json) as f:
             tj = json.load(f)
-        if (tj.get("config", {}).get("n") == n and tj.get("config", {}).get("b") == b and world == 1
-                and args.basis_bits == 64 and args.matrix == "hashwindow"):
+        tc = tj.get("config", {})
+        fmt_name = {0: "csr", 1: "band tiles", 2: "packed band tiles", 3: "half band tiles", 4: "dense"}[mat_fmt]
+        if (tc.get("n") == n and tc.get("b") == b and world == 1 and args.basis_bits == 64
+                and args.matrix == "hashwindow" and tc.get("fuse") == args.fuse
+                and tc.get("matrix_format") == fmt_name):  # the same kernels as measured
             traffic = tj.get("spmm_hbm_bytes_per_launch")
             traffic_reorth = tj.get("part_reorth_hbm_bytes_per_run")
     except (OSError, ValueError):
@@ -283,7 +291,10 @@ def main():
                  "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(spmm_gbs / HBM_PEAK_GBS, 4),
                  "traffic": None if traffic is None else int(traffic),
                  "algorithmic_bytes_per_launch": int(spmm_bytes),
-                 "streamed_bytes_per_launch": int(streamed_bytes(spmm_kid, nloc, nnz_loc, b, args.halfwidth, m_max)),
+                 "streamed_bytes_per_launch": int(streamed_bytes(spmm_kid, nloc, nnz_loc, b, args.halfwidth, m_max,
+                                                                 mat_fmt)),
+                 "matrix_format": {0: "csr", 1: "band tiles", 2: "packed band tiles", 3: "half band tiles",
+                                   4: "dense"}[mat_fmt],
                  # gather kernels (unbanded patterns) also read one Q row (b * 8 B) per nonzero,
                  # served by L2 / Infinity Cache / HBM: the traffic that bounds them
                  **({"q_row_gather_bytes_per_launch": int(nnz_loc * b * 8),

@@ -82,6 +82,10 @@ struct CsrDev {
   // nonzeros per block: element 0 of the lanes, then element 1; null: the dense tiles `bt`
   const uint64_t* btp_hdr = nullptr;
   const double* btp_val = nullptr;
+  // half band tiles (A symmetric, bt_half): groups NGL..NG-1 of every tile slot, and the
+  // first NGL local tiles whole; replaces `bt`
+  const double* bth = nullptr;
+  const double* bte = nullptr;
   // segmented gather (spmm.hip variant 5): wave tasks (first row, info: > 0 rows of a packed
   // short-row task, < 0 -(slot+1) of a long-row segment), segment slots' first nonzero
   // (slot_k0, nslots + 1 entries), long rows with their first slot (lslot, nlong + 1), and a
@@ -171,6 +175,10 @@ bool spmm_bt(const CsrDev& A, const double* Qin, int64_t col_off, int b, double*
              int* ai_parts = nullptr, const float* Q32 = nullptr, const float* Qprev32 = nullptr);
 // band-tile format of the local CSR: tiles in consumption order (slot (round * grid + wg) * 4
 // + wave), zero-filled `out` of bt_tile_slots(ntiles, tiles_per_wg) * NG * 256 doubles
+// half tiles from the whole ones when the tiles are symmetric bit for bit (0; -1: not
+// symmetric, nothing allocated; > 0: HIP error)
+int bt_half(const double* full, int64_t ntiles, int64_t tpw, int NG, double** half,
+            double** edge, hipStream_t s);
 int64_t bt_tile_slots(int64_t ntiles, int64_t tiles_per_wg);
 void bt_fill(const CsrDev& A, int H, int NG, double* out, hipStream_t s);
 // packed band tiles from the dense ones (NG in {5, 9}): header words per tile slot, and the

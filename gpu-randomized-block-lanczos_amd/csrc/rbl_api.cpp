@@ -42,6 +42,8 @@ struct rbl_ctx {
   double* d_bt = nullptr;      // band-tile kernel: the CSR in MFMA-ordered 16-row band tiles
   int bt_ng = 0;               // its band groups (0: not applicable)
   uint64_t* d_btp_hdr = nullptr;  // the band tiles packed (zeros dropped; replaces d_bt)
+  double* d_bth = nullptr;        // half band tiles (A symmetric; replaces d_bt), and the
+  double* d_bte = nullptr;        //   first (NG-1)/2 local tiles whole
   double* d_btp_val = nullptr;
   double* d_zrow = nullptr;    // 32 zeros: band rows the halo does not hold
   // segmented-gather task table (spmm.hip variant 5; CsrDev::seg_*)
@@ -242,6 +244,8 @@ CsrDev csr(rbl_ctx* ctx) {
   A.row0 = ctx->r0;
   A.band_pos = ctx->d_bpos;
   A.bt = ctx->d_bt;
+  A.bth = ctx->d_bth;
+  A.bte = ctx->d_bte;
   A.bt_ng = ctx->bt_ng;
   A.btp_hdr = ctx->d_btp_hdr;
   A.btp_val = ctx->d_btp_val;
@@ -461,6 +465,22 @@ int prepare_window(rbl_ctx* ctx, const std::vector<int64_t>& rp) {
         if (prc != 0) return prc == (int)hipErrorOutOfMemory ? RBL_ERR_OOM : RBL_ERR_HIP;
         hipFree(ctx->d_bt);
         ctx->d_bt = nullptr;
+      } else {
+        // A symmetric (bit for bit, as Lanczos assumes): store the diagonal group and the
+        // right strip only — 10 of 18.4 KB per tile at H = 64; the kernel transposes the left
+        // groups back from the previous tiles' strips (same U bits).  RBL_BT_HALF = 0: whole.
+        const char* hf = getenv("RBL_BT_HALF");
+        if (!hf || atoi(hf) != 0) {
+          double *half = nullptr, *edge = nullptr;
+          const int hrc = bt_half(ctx->d_bt, nt, ctx->tiles_per_wg, NG, &half, &edge, ctx->stream);
+          if (hrc > 0) return hrc == (int)hipErrorOutOfMemory ? RBL_ERR_OOM : RBL_ERR_HIP;
+          if (hrc == 0) {
+            hipFree(ctx->d_bt);
+            ctx->d_bt = nullptr;
+            ctx->d_bth = half;
+            ctx->d_bte = edge;
+          }
+        }
       }
     }
   }
@@ -1133,6 +1153,8 @@ void free_matrix(rbl_ctx* ctx) {
   hipFree(ctx->d_tinfo); ctx->d_tinfo = nullptr;
   hipFree(ctx->d_bpos); ctx->d_bpos = nullptr;
   hipFree(ctx->d_bt); ctx->d_bt = nullptr;
+  hipFree(ctx->d_bth); ctx->d_bth = nullptr;
+  hipFree(ctx->d_bte); ctx->d_bte = nullptr;
   hipFree(ctx->d_btp_hdr); ctx->d_btp_hdr = nullptr;
   hipFree(ctx->d_btp_val); ctx->d_btp_val = nullptr;
   hipFree(ctx->d_zrow); ctx->d_zrow = nullptr;
@@ -1696,6 +1718,15 @@ int rbl_spmm_kernel_for(rbl_ctx* ctx, int b) {
   if ((v == 0 || v == 2 || v == 3) && win) return 2;
   if ((v == 0 || v == 5) && ctx->seg_ntasks > 0 && (b == 16 || b == 32)) return 6;
   return 1;
+}
+
+int rbl_matrix_format(rbl_ctx* ctx) {
+  if (!ctx || !has_matrix(ctx)) return RBL_ERR_INVALID;
+  if (ctx->dense) return 4;
+  if (ctx->d_bth) return 3;
+  if (ctx->d_btp_hdr) return 2;
+  if (ctx->d_bt) return 1;
+  return 0;
 }
 
 int rbl_apply(rbl_ctx* ctx, int b, const double* X, double* Y) {

@@ -61,7 +61,8 @@ struct Geo {
   static constexpr int kUOff = kBtOff + kBtBytes;
   static constexpr int kLds = kUOff + 4 * kUWave;           // B = 32: 111,104 B; B = 16: 43,008 B
   static constexpr int kCtOff = kLds;                       // VAR bit 10: the -C table
-  static_assert(kLds + 9216 <= 160 * 1024, "LDS budget");
+  static constexpr int kTrOff = kLds + 9216;                // VAR bit 11: per-wave transpose buffers
+  static_assert(kLds + 2 * 9216 <= 160 * 1024, "LDS budget");
 };
 // A_i operand at B = 32: lane reads ring slot pi(l & 15); pi maps the lanes {0-3, 12-15} of
 // each ds_read_b128 lane group to slot classes {0,1} mod 4 and {4-11} to {2,3} mod 4, so rows
@@ -96,6 +97,8 @@ struct BtArgs {
   double* ai_slab;       // AIG: per-workgroup partials of A_i (b x b row-major)
   const uint64_t* hdr;   // VAR bit 7: packed tiles (bt_pack) instead of A
   const double* pv;
+  const double* Ah;      // VAR bit 11: half tiles (bt_half) instead of A, and whole tiles for
+  const double* Ae;      //   the first NGL local tiles
   const double* Cl;      // VAR bit 10: local reorth on staging (ring rows = Q - Qprev Cl),
   double* Qw;            //   interior own rows written back here (CsrDev::lfix_q); only the
   int64_t lf_lo, lf_hi;  //   local rows [lf_lo, lf_hi) are raw, the others already corrected
@@ -110,6 +113,8 @@ struct BtArgs {
 // sequence, so a row has the same bits whichever kernel corrects it.
 constexpr int kCtLd = 36;
 constexpr int kCtBytes = 32 * kCtLd * 8;
+constexpr int kTrLd = 18;                  // half tiles: transpose square, doubles per row
+constexpr int kTrBytes = 16 * kTrLd * 8;   // per wave (4 x 2,304 B <= 9,216)
 __device__ __forceinline__ void lf_loads(const double* rraw, const double* rprev, int lane,
                                          d2v (&raw)[4], d2v (&qa)[4]) {
   const int q = lane >> 4, j = lane & 3;
@@ -263,12 +268,56 @@ void k_spmm_bt(BtArgs a) {
   // at any moment the whole chip sweeps one contiguous stretch of the format
   const int64_t tslot0 = 4 * (int64_t)blockIdx.x;
   const int64_t tslot_r = 4 * (int64_t)gridDim.x;
+  constexpr bool HALF = (VAR & 2048) != 0;
+  constexpr int NGL = (NG - 1) / 2, NGH = NG - NGL;  // left groups / stored groups per tile
+  static_assert(!HALF || !(VAR & 128), "half tiles are dense");
+  // slot of any local tile t (its workgroup's range may be another's): bt_fill's order
+  auto slot_of = [&](int64_t t) -> int64_t {
+    const int64_t w = t / a.tiles_per_wg, lt = t - w * a.tiles_per_wg;
+    return ((lt >> 2) * gridDim.x + w) * 4 + (lt & 3);
+  };
   auto tile_a = [&](int64_t t, int g, int h) -> d2v {
-    const int64_t lt = t - T0;
-    const int64_t ts = (lt >> 2) * tslot_r + tslot0 + (lt & 3);
-    const d2v* p = reinterpret_cast<const d2v*>(a.A + ((((ts * NG + g) * 2 + h) * 64) + lane) * 2);
-    if constexpr (VAR & 1) return __builtin_nontemporal_load(p);
-    return *p;
+    if constexpr (HALF) {
+      // half tiles: tile t's own groups NGL.. (diagonal + right strip); its left group g is
+      // the transpose of group NG-1-g of tile t - NGL + g (stored as that tile's half group
+      // NGL - g, read raw here, transposed by bt_transpose before use); the first NGL local
+      // tiles, whose left groups reach into rows of no local tile, come whole from Ae
+      if (t < NGL) return reinterpret_cast<const d2v*>(a.Ae + ((((t * NG + g) * 2 + h) * 64) + lane) * 2)[0];
+      const int64_t ts = g >= NGL ? slot_of(t) : slot_of(t - NGL + g);
+      const int gh = g >= NGL ? g - NGL : NGL - g;
+      const d2v* p = reinterpret_cast<const d2v*>(a.Ah + ((((ts * NGH + gh) * 2 + h) * 64) + lane) * 2);
+      if constexpr (VAR & 1) {
+        if (g == NGL) return __builtin_nontemporal_load(p);  // the diagonal group: read once
+      }
+      return *p;  // strip groups: read again (transposed) by the next NGL tiles — keep in L2
+    } else {
+      const int64_t lt = t - T0;
+      const int64_t ts = (lt >> 2) * tslot_r + tslot0 + (lt & 3);
+      const d2v* p = reinterpret_cast<const d2v*>(a.A + ((((ts * NG + g) * 2 + h) * 64) + lane) * 2);
+      if constexpr (VAR & 1) return __builtin_nontemporal_load(p);
+      return *p;
+    }
+  };
+  // left group g of a half-format tile: lane holds S[r = l & 15][c = 4u + (l >> 4)] of the
+  // source strip group (u = 0..3 in v[0].x, v[0].y, v[1].x, v[1].y); the tile needs S^T in the
+  // same layout.  Through a wave-private LDS square (row stride kTrLd = 18 doubles: 2-way
+  // banked both ways, the minimum for 64 x 8 B).
+  auto bt_transpose = [&](d2v (&v)[2]) {
+    double* tb = reinterpret_cast<double*>(smem + L::kTrOff + wave * kTrBytes);
+    tb[i16 * kTrLd + q] = v[0].x;
+    tb[i16 * kTrLd + 4 + q] = v[0].y;
+    tb[i16 * kTrLd + 8 + q] = v[1].x;
+    tb[i16 * kTrLd + 12 + q] = v[1].y;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    v[0].x = tb[q * kTrLd + i16];
+    v[0].y = tb[(4 + q) * kTrLd + i16];
+    v[1].x = tb[(8 + q) * kTrLd + i16];
+    v[1].y = tb[(12 + q) * kTrLd + i16];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   };
   auto clamp_t = [&](int64_t t) -> int64_t { return t < T1 ? t : T1 - 1; };
   // packed tiles: header words of tile t (lane w holds word w)
@@ -376,6 +425,12 @@ void k_spmm_bt(BtArgs a) {
     }
 
     if (tw < T1) {  // wave-uniform
+      if constexpr (HALF) {
+        if (tw >= NGL) {
+#pragma unroll
+          for (int g = 0; g < NGL; ++g) bt_transpose(av[g]);
+        }
+      }
       const int64_t tn = clamp_t(tw + 4);
       uint64_t hNN = 0;
       if constexpr (VAR & 128) hNN = hdr_load(clamp_t(tw + 8));
@@ -523,7 +578,7 @@ void k_spmm_bt(BtArgs a) {
 
 template <int B, int NG, bool EPI, bool AIG, int VAR>
 static void launch_bt_v(const BtArgs& a, int grid, hipStream_t s) {
-  constexpr int lds = bt::Geo<B>::kLds + ((VAR & 1024) ? kCtBytes : 0);
+  constexpr int lds = bt::Geo<B>::kLds + ((VAR & 2048) ? 2 * 9216 : (VAR & 1024) ? kCtBytes : 0);
   ensure_lds_attr(reinterpret_cast<const void*>(&k_spmm_bt<B, NG, EPI, AIG, VAR>), lds);
   hipLaunchKernelGGL((k_spmm_bt<B, NG, EPI, AIG, VAR>), dim3(grid), dim3(bt::kThreads), lds, s, a);
 }
@@ -544,6 +599,13 @@ static void launch_bt_t(const BtArgs& a, int grid, hipStream_t s, bool f32) {
     }
     return launch_bt_v<B, NG, EPI, AIG, 3 | 128>(a, grid, s);
   }
+  if (a.Ah) {  // half tiles (bt_half)
+    if (f32) return launch_bt_v<B, NG, EPI, AIG, 3 | 64 | 2048>(a, grid, s);
+    if constexpr (B == 32 && NG == 9 && EPI && AIG) {
+      if (var == 2) return launch_bt_v<B, NG, EPI, AIG, 2 | 2048>(a, grid, s);
+    }
+    return launch_bt_v<B, NG, EPI, AIG, 3 | 2048>(a, grid, s);
+  }
   if (f32) return launch_bt_v<B, NG, EPI, AIG, 3 | 64>(a, grid, s);
   if constexpr (B == 32 && NG == 9 && EPI && AIG) {
     if (var == 0) return launch_bt_v<B, NG, EPI, AIG, 0>(a, grid, s);
@@ -557,12 +619,14 @@ static void launch_bt_t(const BtArgs& a, int grid, hipStream_t s, bool f32) {
 bool spmm_bt(const CsrDev& A, const double* Qin, int64_t col_off, int b, double* U,
              const double* Qprev, const double* Bi, hipStream_t s, double* ai_slab, int* ai_parts,
              const float* Q32, const float* Qprev32) {
-  if ((b != 32 && b != 16) || !(A.bt || A.btp_hdr) || A.ntiles <= 0 || !(A.bt_ng == 5 || A.bt_ng == 9)) return false;
+  if ((b != 32 && b != 16) || !(A.bt || A.bth || A.btp_hdr) || A.ntiles <= 0 || !(A.bt_ng == 5 || A.bt_ng == 9)) return false;
   BtArgs a;
   a.nrows = A.nrows;
   a.ntiles = A.ntiles;
   a.tiles_per_wg = A.bt_tiles_per_wg;
   a.A = A.bt;
+  a.Ah = A.bth;
+  a.Ae = A.bte;
   a.Q = Qin;
   a.col_off = col_off;
   a.q_lo = A.q_lo;
@@ -591,8 +655,13 @@ bool spmm_bt(const CsrDev& A, const double* Qin, int64_t col_off, int b, double*
     if (b != 32 || f32 || a.hdr || !epi || !aig) return false;
     a.lf_lo = A.lfix_lo;
     a.lf_hi = A.lfix_hi;
-    if (A.bt_ng == 9) launch_bt_v<32, 9, true, true, 3 | 1024>(a, grid, s);
-    else launch_bt_v<32, 5, true, true, 3 | 1024>(a, grid, s);
+    if (a.Ah) {
+      if (A.bt_ng == 9) launch_bt_v<32, 9, true, true, 3 | 1024 | 2048>(a, grid, s);
+      else launch_bt_v<32, 5, true, true, 3 | 1024 | 2048>(a, grid, s);
+    } else {
+      if (A.bt_ng == 9) launch_bt_v<32, 9, true, true, 3 | 1024>(a, grid, s);
+      else launch_bt_v<32, 5, true, true, 3 | 1024>(a, grid, s);
+    }
     return true;
   }
   const int key = (b == 32 ? 8 : 0) | (A.bt_ng == 9 ? 4 : 0) | (epi ? 2 : 0) | (aig ? 1 : 0);
@@ -673,7 +742,7 @@ __global__ __launch_bounds__(64) void k_locfix_ranges(double* Q, const double* _
 }
 
 bool spmm_bt_locfix_ok(const CsrDev& A, int b) {
-  return b == 32 && A.bt && !A.btp_hdr && A.ntiles > 0 && (A.bt_ng == 5 || A.bt_ng == 9);
+  return b == 32 && (A.bt || A.bth) && !A.btp_hdr && A.ntiles > 0 && (A.bt_ng == 5 || A.bt_ng == 9);
 }
 
 int spmm_bt_halfwidth(const CsrDev& A) { return 8 * (A.bt_ng - 1); }
@@ -717,6 +786,78 @@ __global__ void k_bt_fill(int64_t nrows, const int64_t* __restrict__ rowptr,
     const int64_t idx = ((((ts * NG + g) * 2 + (u >> 1)) * 64) + 16 * qq + i) * 2 + (u & 1);
     atomicAdd(out + idx, val[e]);
   }
+}
+
+// Half tiles (A symmetric): tile t's left group g equals the transpose of group NG-1-g of tile
+// t - NGL + g bit for bit, so only groups NGL..NG-1 (diagonal + right strip: 10 of 18.4 KB per
+// tile at H = 64) are stored and the kernel transposes the strip groups of the previous NGL
+// tiles back (L2-resident: read NGL tiles earlier).  U is bit-identical to the whole tiles'.
+// k_bt_symcheck: *bad = 1 if any left group of a tile t >= NGL differs from that transpose.
+__global__ void k_bt_symcheck(const double* __restrict__ full, int64_t ntiles, int64_t tpw,
+                              int64_t grid, int NG, int* bad) {
+  const int NGL = (NG - 1) / 2;
+  const int64_t per = (int64_t)NGL * 256;
+  const int64_t total = (ntiles - NGL) * per;
+  auto slot = [&](int64_t t) {
+    const int64_t w = t / tpw, lt = t - w * tpw;
+    return ((lt >> 2) * grid + w) * 4 + (lt & 3);
+  };
+  // element (r, c) of group g of the tile in slot ts: lane r + 16 (c & 3), u = c >> 2
+  auto at = [&](int64_t ts, int g, int r, int c) {
+    const int u = c >> 2;
+    return full[((((ts * NG + g) * 2 + (u >> 1)) * 64) + r + 16 * (c & 3)) * 2 + (u & 1)];
+  };
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t t = NGL + e / per;
+    const int g = (int)((e % per) >> 8), r = (int)(e & 15), c = (int)((e >> 4) & 15);
+    const double x = at(slot(t), g, r, c), y = at(slot(t - NGL + g), NG - 1 - g, c, r);
+    if (__double_as_longlong(x) != __double_as_longlong(y)) *bad = 1;
+  }
+}
+__global__ void k_bt_half(const double* __restrict__ full, int64_t nslots, int NG,
+                          double* __restrict__ half) {
+  const int NGL = (NG - 1) / 2, NGH = NG - NGL;
+  const int64_t total = nslots * NGH * 256;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t ts = e / (NGH * 256);
+    const int64_t rest = e - ts * NGH * 256;
+    half[e] = full[(ts * NG + NGL) * 256 + rest];
+  }
+}
+
+int bt_half(const double* full, int64_t ntiles, int64_t tpw, int NG, double** half,
+            double** edge, hipStream_t s) {
+  const int64_t grid = (ntiles + tpw - 1) / tpw;
+  const int64_t nslots = bt_tile_slots(ntiles, tpw);
+  const int NGL = (NG - 1) / 2, NGH = NG - NGL;
+  *half = *edge = nullptr;
+  int* bad = nullptr;
+  if (hipMalloc(&bad, sizeof(int)) != hipSuccess) return (int)hipErrorOutOfMemory;
+  int hbad = 0;
+  hipMemsetAsync(bad, 0, sizeof(int), s);
+  if (ntiles > NGL)
+    hipLaunchKernelGGL(k_bt_symcheck, dim3(4096), dim3(256), 0, s, full, ntiles, tpw, grid, NG, bad);
+  hipMemcpyAsync(&hbad, bad, sizeof(int), hipMemcpyDeviceToHost, s);
+  hipStreamSynchronize(s);
+  hipFree(bad);
+  if (hbad) return -1;  // not symmetric bit for bit: keep the whole tiles
+  if (hipMalloc(half, (size_t)nslots * NGH * 256 * sizeof(double)) != hipSuccess ||
+      hipMalloc(edge, (size_t)NGL * NG * 256 * sizeof(double)) != hipSuccess) {
+    hipFree(*half);
+    *half = nullptr;
+    return (int)hipErrorOutOfMemory;
+  }
+  hipMemsetAsync(*edge, 0, (size_t)NGL * NG * 256 * sizeof(double), s);
+  hipLaunchKernelGGL(k_bt_half, dim3(4096), dim3(256), 0, s, full, nslots, NG, *half);
+  for (int64_t t = 0; t < NGL && t < ntiles; ++t) {
+    const int64_t w = t / tpw, lt = t - w * tpw;
+    const int64_t ts = ((lt >> 2) * grid + w) * 4 + (lt & 3);
+    hipMemcpyAsync(*edge + t * NG * 256, full + ts * NG * 256, NG * 256 * sizeof(double),
+                   hipMemcpyDeviceToDevice, s);
+  }
+  return (int)hipStreamSynchronize(s);
 }
 
 int64_t bt_tile_slots(int64_t ntiles, int64_t tpw) {

@@ -63,6 +63,7 @@ SIGNATURES = {
     "rbl_get_matrix_csr": (C.c_int, [_p, _pi64, _pi32, _pd]),
     "rbl_apply": (C.c_int, [_p, C.c_int, _pd, _pd]),
     "rbl_spmm_kernel_for": (C.c_int, [_p, C.c_int]),
+    "rbl_matrix_format": (C.c_int, [_p]),
     "rbl_start": (C.c_int, [_p, C.c_int, C.c_int, C.c_int, _pd, _u64]),
     "rbl_step": (C.c_int, [_p, C.c_int, C.c_int, _pd, _pd]),
     "rbl_step_async": (C.c_int, [_p, C.c_int, C.c_int]),

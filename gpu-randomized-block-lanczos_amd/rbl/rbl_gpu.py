@@ -181,6 +181,10 @@ class Context:
         self._check(lib.rbl_apply(self._h, b, dptr(X), dptr(Y)), "rbl_apply")
         return Y
 
+    def matrix_format(self) -> int:
+        """0 CSR only, 1 band tiles, 2 packed band tiles, 3 half band tiles, 4 dense."""
+        return self._check(lib.rbl_matrix_format(self._h), "rbl_matrix_format")
+
     def spmm_kernel_for(self, b: int) -> int:
         """1 = global-gather CSR kernel, 2 = LDS-window CSR kernel."""
         return self._check(lib.rbl_spmm_kernel_for(self._h, b), "rbl_spmm_kernel_for")

@@ -168,6 +168,11 @@ int rbl_apply(rbl_ctx* ctx, int b, const double* X, double* Y);
  * 4 = dense panel GEMM (rbl_set_matrix_dense), 5 = band-tile format on fp64 MFMA,
  * 6 = segmented gather (unstructured patterns, b in {16, 32}). */
 int rbl_spmm_kernel_for(rbl_ctx* ctx, int b);
+/* The device format the matrix is held in: 0 = CSR only, 1 = band tiles (16 x (16 + 2H)
+ * doubles), 2 = packed band tiles (RBL_BT_PACK=1), 3 = half band tiles (A symmetric bit for
+ * bit: diagonal block + right strip, the left part transposed back in the kernel, same
+ * results as 1; RBL_BT_HALF=0 keeps 1), 4 = dense panels. */
+int rbl_matrix_format(rbl_ctx* ctx);
 
 /* ---- Krylov run -----------------------------------------------------------------------
  * rbl_start replaces RBL_gpu.jl:213-214 (`Qg_d = CUDA.randn(n,b); Qg_d = qr(Ag*Qg_d).Q`)

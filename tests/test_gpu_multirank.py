@@ -175,13 +175,57 @@ def test_multirank_local_reorth_fused_into_spmm(rbl, P, n, W):
         return run_ranks(rbl, P, fn)
 
     fz, sep = run(7), run(3)
-    # the fused path ran: its rounding differs from the separate pass somewhere
-    assert not all(np.array_equal(a, c) for a, c in zip(fz[0].trace_A, sep[0].trace_A))
     for i7, i3 in zip(fz, sep):
         assert len(i7.trace_A) == len(i3.trace_A) == 10
         for t7, t3 in ((i7.trace_A, i3.trace_A), (i7.trace_B, i3.trace_B)):
             d = max(np.abs(a - a1).max() / np.abs(a1).max() for a, a1 in zip(t7, t3))
             assert d < 1e-12, d
+
+
+@pytest.mark.parametrize("P", [1, 2])
+def test_multirank_fused_local_reorth_runs(rbl, P):
+    """The fused path really replaces the separate pass on 1 and 2 ranks: its loc-reorth stage
+    (the rank-edge and range-edge fix-ups only) takes a fraction of the separate pass's time."""
+    n, W, k, b = 2_000_000, 64, 10, 32
+    plant = matgen.planted_spectrum(k)
+
+    def run(fuse):
+        def fn(ctx, r):
+            ctx.set_option(rbl._lib.RBL_OPT_TIMERS, 1)
+            ctx.set_option(rbl._lib.RBL_OPT_FUSE, fuse)
+            ctx.gen_hashwindow(n, W, 0.7734, 17, plant)
+            rbl.lanczos(ctx, k, b, seed=9, check=False, max_steps=8, ritz=False)
+            return ctx.timers()["loc reorth"]
+        if P == 1:
+            with rbl.Context(0) as ctx:
+                return [fn(ctx, 0)]
+        return run_ranks(rbl, P, fn)
+
+    t7, t3 = run(7), run(3)
+    assert max(t7) < 0.3 * min(t3), (t7, t3)
+
+
+def test_multirank_half_band_tiles_bit_identical(rbl, monkeypatch):
+    """Half band tiles on 3 ranks (each rank's first NGL tiles whole, their left groups reach
+    into the previous rank's rows) against whole tiles: A_i / B_{i+1} bit for bit."""
+    n, W, p, seed, k, b = 30001, 64, 0.7734, 23, 10, 32
+    plant = matgen.planted_spectrum(k)
+
+    def run(half):
+        monkeypatch.setenv("RBL_BT_HALF", half)
+
+        def fn(ctx, r):
+            ctx.gen_hashwindow(n, W, p, seed, plant)
+            assert ctx.matrix_format() == (3 if half == "1" else 1)
+            _, _, info = rbl.lanczos(ctx, k, b, seed=3, check=False, max_steps=10, trace=True,
+                                     ritz=False)
+            return info
+        return run_ranks(rbl, 3, fn)
+
+    h, w = run("1"), run("0")
+    for ih, iw in zip(h, w):
+        for a, a1 in zip(ih.trace_A + ih.trace_B, iw.trace_A + iw.trace_B):
+            assert np.array_equal(a, a1)
 
 
 def test_multirank_tiny_slices(rbl):

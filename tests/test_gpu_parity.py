@@ -318,8 +318,8 @@ def test_local_reorth_fused_into_spmm(rbl, n, W):
             D, V, info = rbl.lanczos(ctx, k, b, omega=omega, trace=True)
         assert info.converged
         out[fuse] = (np.array(info.trace_A), np.array(info.trace_B), D, V)
+
     assert out[3][0].shape == out[7][0].shape
-    assert not np.array_equal(out[3][0], out[7][0])  # the fused path ran (rounding differs)
     for t in (0, 1):
         d = np.abs(out[7][t] - out[3][t]).max() / np.abs(out[3][t]).max()
         assert d < 1e-12, (t, d)

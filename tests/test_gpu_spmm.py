@@ -153,6 +153,48 @@ def test_spmm_band_tiles_packed_bit_identical(rbl, monkeypatch, n, W, p, b):
         assert np.array_equal(a0, a1)
 
 
+@pytest.mark.parametrize("n,W,b,bits", [(50003, 64, 32, 64), (20001, 32, 32, 64),
+                                         (30000, 64, 16, 64), (12345, 32, 16, 64),
+                                         (40000, 64, 32, 32), (300, 32, 16, 64)])
+def test_spmm_half_band_tiles_bit_identical(rbl, monkeypatch, n, W, b, bits):
+    """Half band tiles (A symmetric: diagonal block + right strip stored, the left groups
+    transposed back in the kernel from the previous tiles' strips) against the whole tiles
+    (RBL_BT_HALF=0): the MFMA operands are the same values in the same order, so U, every
+    Lanczos A_i / B_{i+1} (fused epilogue, A_i partials, fused local reorth, fp32 basis) and
+    the Ritz pairs agree bit for bit.  n = 300: a single workgroup range."""
+    plant = matgen.planted_spectrum(5)
+    A = matgen.hashwindow_csr(n, W, 0.7734, n + 5, plant)
+    X = np.random.default_rng(n + 2).standard_normal((n, b))
+    out = []
+    for half in ("0", "1"):
+        monkeypatch.setenv("RBL_BT_HALF", half)
+        with rbl.Context(0) as ctx:
+            ctx.set_matrix(A)
+            assert ctx.spmm_kernel_for(b) == 5
+            assert ctx.matrix_format() == (3 if half == "1" else 1)
+            Y = ctx.apply(X)
+            D, V, info = rbl.lanczos(ctx, 5, b, seed=2, check=False, max_steps=min(8, n // b),
+                                     trace=True, basis_bits=bits)
+        out.append((Y, info, D, V))
+    _check(A, out[1][0], X)
+    assert np.array_equal(out[0][0], out[1][0])
+    for a0, a1 in zip(out[0][1].trace_A + out[0][1].trace_B, out[1][1].trace_A + out[1][1].trace_B):
+        assert np.array_equal(a0, a1)
+    assert np.array_equal(out[0][2], out[1][2]) and np.array_equal(out[0][3], out[1][3])
+
+
+def test_spmm_half_band_tiles_need_exact_symmetry(rbl):
+    """One nonzero whose mirror differs in the last bit keeps the whole tiles (format 1)."""
+    A = matgen.hashwindow_csr(5000, 64, 0.7734, 3).tolil()
+    A[100, 140] = np.nextafter(A[140, 100], np.inf) if A[140, 100] != 0 else 1.0
+    A = sp.csr_matrix(A)
+    with rbl.Context(0) as ctx:
+        ctx.set_matrix(A)
+        assert ctx.spmm_kernel_for(32) == 5 and ctx.matrix_format() == 1
+        X = np.random.default_rng(0).standard_normal((5000, 32))
+        _check(A, ctx.apply(X), X)
+
+
 @pytest.mark.parametrize("b", [16, 32])
 @pytest.mark.parametrize("variant", [0, 5])
 def test_spmm_segmented_long_rows(rbl, b, variant):

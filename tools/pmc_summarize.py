@@ -62,8 +62,18 @@ def main():
     reo = {k: v for k, v in kern.items() if k.startswith(("k_gram44", "k_tsmm44<32, 64>", "k_tsmm44f"))}
     runs = 1  # bench.py --steps 1 --warmup 0: one 38-step run
     reorth_bytes = sum(v["hbm_bytes_per_launch"] * v["launches"] for v in reo.values()) / runs
+    # the kernels measured: the bench line of the FETCH pass names the fusions and the format
+    extra = {}
+    try:
+        with open(os.path.join(d, "fetch.log")) as fh:
+            j = json.loads([ln for ln in fh if ln.startswith('{"metric"')][0])
+        extra = {"fuse": j["config"].get("fuse", 7),
+                 "matrix_format": j["roofline_secondary"].get("matrix_format")}
+    except (OSError, IndexError, KeyError, ValueError):
+        pass
     res = {
-        "config": {"n": 10_000_000, "b": 32, "workload": "C4a (bench.py defaults), 1 run = 38 steps"},
+        "config": {"n": 10_000_000, "b": 32, "workload": "C4a (bench.py defaults), 1 run = 38 steps",
+                   **extra},
         "calibration": cal,
         "correction_used": {"fetch": fetch_corr, "write": write_corr},
         "spmm_hbm_bytes_per_launch": spmm_bytes,
