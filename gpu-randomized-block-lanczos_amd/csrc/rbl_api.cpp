@@ -468,9 +468,10 @@ int prepare_window(rbl_ctx* ctx, const std::vector<int64_t>& rp) {
       } else {
         // A symmetric (bit for bit, as Lanczos assumes): store the diagonal group and the
         // right strip only — 10 of 18.4 KB per tile at H = 64; the kernel transposes the left
-        // groups back from the previous tiles' strips (same U bits).  RBL_BT_HALF = 0: whole.
+        // groups back from the previous tiles' strips (same U bits).  Opt-in (RBL_BT_HALF = 1)
+        // while it measures slower than the whole tiles.
         const char* hf = getenv("RBL_BT_HALF");
-        if (!hf || atoi(hf) != 0) {
+        if (hf && atoi(hf) == 1) {
           double *half = nullptr, *edge = nullptr;
           const int hrc = bt_half(ctx->d_bt, nt, ctx->tiles_per_wg, NG, &half, &edge, ctx->stream);
           if (hrc > 0) return hrc == (int)hipErrorOutOfMemory ? RBL_ERR_OOM : RBL_ERR_HIP;

@@ -283,9 +283,13 @@ void k_spmm_bt(BtArgs a) {
       // NGL - g, read raw here, transposed by bt_transpose before use); the first NGL local
       // tiles, whose left groups reach into rows of no local tile, come whole from Ae
       if (t < NGL) return reinterpret_cast<const d2v*>(a.Ae + ((((t * NG + g) * 2 + h) * 64) + lane) * 2)[0];
-      const int64_t ts = g >= NGL ? slot_of(t) : slot_of(t - NGL + g);
+      // t is in this workgroup's range; a source tile before it is too unless t is one of the
+      // range's first NGL tiles (then slot_of, with its division)
+      const int64_t lt = t - T0 - (g < NGL ? NGL - g : 0);
+      const int64_t ts = lt >= 0 ? (lt >> 2) * tslot_r + tslot0 + (lt & 3) : slot_of(t - NGL + g);
       const int gh = g >= NGL ? g - NGL : NGL - g;
       const d2v* p = reinterpret_cast<const d2v*>(a.Ah + ((((ts * NGH + gh) * 2 + h) * 64) + lane) * 2);
+      if constexpr (VAR & 4096) return __builtin_nontemporal_load(p);
       if constexpr (VAR & 1) {
         if (g == NGL) return __builtin_nontemporal_load(p);  // the diagonal group: read once
       }
@@ -601,8 +605,9 @@ static void launch_bt_t(const BtArgs& a, int grid, hipStream_t s, bool f32) {
   }
   if (a.Ah) {  // half tiles (bt_half)
     if (f32) return launch_bt_v<B, NG, EPI, AIG, 3 | 64 | 2048>(a, grid, s);
-    if constexpr (B == 32 && NG == 9 && EPI && AIG) {
+    if constexpr (B == 32 && NG == 9 && EPI && AIG) {  // diagnostics: A load policy
       if (var == 2) return launch_bt_v<B, NG, EPI, AIG, 2 | 2048>(a, grid, s);
+      if (var == 4099) return launch_bt_v<B, NG, EPI, AIG, 3 | 2048 | 4096>(a, grid, s);
     }
     return launch_bt_v<B, NG, EPI, AIG, 3 | 2048>(a, grid, s);
   }

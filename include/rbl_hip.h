@@ -171,7 +171,7 @@ int rbl_spmm_kernel_for(rbl_ctx* ctx, int b);
 /* The device format the matrix is held in: 0 = CSR only, 1 = band tiles (16 x (16 + 2H)
  * doubles), 2 = packed band tiles (RBL_BT_PACK=1), 3 = half band tiles (A symmetric bit for
  * bit: diagonal block + right strip, the left part transposed back in the kernel, same
- * results as 1; RBL_BT_HALF=0 keeps 1), 4 = dense panels. */
+ * results as 1; opt-in with RBL_BT_HALF=1), 4 = dense panels. */
 int rbl_matrix_format(rbl_ctx* ctx);
 
 /* ---- Krylov run -----------------------------------------------------------------------

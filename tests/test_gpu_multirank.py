@@ -202,7 +202,7 @@ def test_multirank_fused_local_reorth_runs(rbl, P):
         return run_ranks(rbl, P, fn)
 
     t7, t3 = run(7), run(3)
-    assert max(t7) < 0.3 * min(t3), (t7, t3)
+    assert sum(t7) < 0.5 * sum(t3), (t7, t3)
 
 
 def test_multirank_half_band_tiles_bit_identical(rbl, monkeypatch):

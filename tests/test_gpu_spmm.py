@@ -167,7 +167,7 @@ def test_spmm_half_band_tiles_bit_identical(rbl, monkeypatch, n, W, b, bits):
     X = np.random.default_rng(n + 2).standard_normal((n, b))
     out = []
     for half in ("0", "1"):
-        monkeypatch.setenv("RBL_BT_HALF", half)
+        monkeypatch.setenv("RBL_BT_HALF", half)  # opt-in format
         with rbl.Context(0) as ctx:
             ctx.set_matrix(A)
             assert ctx.spmm_kernel_for(b) == 5
@@ -183,8 +183,9 @@ def test_spmm_half_band_tiles_bit_identical(rbl, monkeypatch, n, W, b, bits):
     assert np.array_equal(out[0][2], out[1][2]) and np.array_equal(out[0][3], out[1][3])
 
 
-def test_spmm_half_band_tiles_need_exact_symmetry(rbl):
+def test_spmm_half_band_tiles_need_exact_symmetry(rbl, monkeypatch):
     """One nonzero whose mirror differs in the last bit keeps the whole tiles (format 1)."""
+    monkeypatch.setenv("RBL_BT_HALF", "1")
     A = matgen.hashwindow_csr(5000, 64, 0.7734, 3).tolil()
     A[100, 140] = np.nextafter(A[140, 100], np.inf) if A[140, 100] != 0 else 1.0
     A = sp.csr_matrix(A)
