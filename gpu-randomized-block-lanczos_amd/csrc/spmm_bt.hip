@@ -62,7 +62,7 @@ struct Geo {
   static constexpr int kLds = kUOff + 4 * kUWave;           // B = 32: 111,104 B; B = 16: 43,008 B
   static constexpr int kCtOff = kLds;                       // VAR bit 10: the -C table
   static constexpr int kTrOff = kLds + 9216;                // VAR bit 11: per-wave transpose buffers
-  static_assert(kLds + 2 * 9216 <= 160 * 1024, "LDS budget");
+  static_assert(kLds + 9216 + 4 * 4 * 2304 <= 160 * 1024, "LDS budget");
 };
 // A_i operand at B = 32: lane reads ring slot pi(l & 15); pi maps the lanes {0-3, 12-15} of
 // each ds_read_b128 lane group to slot classes {0,1} mod 4 and {4-11} to {2,3} mod 4, so rows
@@ -276,19 +276,43 @@ void k_spmm_bt(BtArgs a) {
     const int64_t w = t / a.tiles_per_wg, lt = t - w * a.tiles_per_wg;
     return ((lt >> 2) * gridDim.x + w) * 4 + (lt & 3);
   };
-  auto tile_a = [&](int64_t t, int g, int h) -> d2v {
+  // half tiles: the slots one tile's loads read — its own (groups NGL..NG-1) and, for each left
+  // group g, tile t - NGL + g's (its strip group NG-1-g, stored as half group NGL - g) — worked
+  // out once per tile, outside the MFMA stream (tile_a is then branch-free); the first NGL
+  // local tiles (edge) come whole from Ae
+  struct HalfPlan {
+    int64_t own = 0;
+    int64_t src[NG / 2 > 0 ? NG / 2 : 1] = {};
+    bool edge = false;
+  };
+  auto half_plan = [&](int64_t t) -> HalfPlan {
+    HalfPlan hp;
     if constexpr (HALF) {
-      // half tiles: tile t's own groups NGL.. (diagonal + right strip); its left group g is
-      // the transpose of group NG-1-g of tile t - NGL + g (stored as that tile's half group
-      // NGL - g, read raw here, transposed by bt_transpose before use); the first NGL local
-      // tiles, whose left groups reach into rows of no local tile, come whole from Ae
-      if (t < NGL) return reinterpret_cast<const d2v*>(a.Ae + ((((t * NG + g) * 2 + h) * 64) + lane) * 2)[0];
-      // t is in this workgroup's range; a source tile before it is too unless t is one of the
-      // range's first NGL tiles (then slot_of, with its division)
-      const int64_t lt = t - T0 - (g < NGL ? NGL - g : 0);
-      const int64_t ts = lt >= 0 ? (lt >> 2) * tslot_r + tslot0 + (lt & 3) : slot_of(t - NGL + g);
+      const int64_t lt = t - T0;
+      hp.own = (lt >> 2) * tslot_r + tslot0 + (lt & 3);
+      hp.edge = t < NGL;
+      if (!hp.edge) {
+#pragma unroll
+        for (int g = 0; g < NGL; ++g) {
+          const int64_t ls = lt - NGL + g;
+          hp.src[g] = ls >= 0 ? (ls >> 2) * tslot_r + tslot0 + (ls & 3) : 0;
+        }
+        if (lt < NGL) {  // sources before this workgroup's range (rare: division)
+#pragma unroll
+          for (int g = 0; g < NGL; ++g)
+            if (lt - NGL + g < 0) hp.src[g] = slot_of(t - NGL + g);
+        }
+      }
+    }
+    return hp;
+  };
+  auto tile_a = [&](int64_t t, int g, int h, const HalfPlan& hp) -> d2v {
+    if constexpr (HALF) {
+      const int64_t ts = g >= NGL ? hp.own : hp.src[g < NGL ? g : 0];
       const int gh = g >= NGL ? g - NGL : NGL - g;
-      const d2v* p = reinterpret_cast<const d2v*>(a.Ah + ((((ts * NGH + gh) * 2 + h) * 64) + lane) * 2);
+      const double* ph = a.Ah + ((((ts * NGH + gh) * 2 + h) * 64) + lane) * 2;
+      const double* pe = a.Ae + ((((t * NG + g) * 2 + h) * 64) + lane) * 2;
+      const d2v* p = reinterpret_cast<const d2v*>(hp.edge ? pe : ph);
       if constexpr (VAR & 4096) return __builtin_nontemporal_load(p);
       if constexpr (VAR & 1) {
         if (g == NGL) return __builtin_nontemporal_load(p);  // the diagonal group: read once
@@ -306,19 +330,30 @@ void k_spmm_bt(BtArgs a) {
   // source strip group (u = 0..3 in v[0].x, v[0].y, v[1].x, v[1].y); the tile needs S^T in the
   // same layout.  Through a wave-private LDS square (row stride kTrLd = 18 doubles: 2-way
   // banked both ways, the minimum for 64 x 8 B).
-  auto bt_transpose = [&](d2v (&v)[2]) {
-    double* tb = reinterpret_cast<double*>(smem + L::kTrOff + wave * kTrBytes);
-    tb[i16 * kTrLd + q] = v[0].x;
-    tb[i16 * kTrLd + 4 + q] = v[0].y;
-    tb[i16 * kTrLd + 8 + q] = v[1].x;
-    tb[i16 * kTrLd + 12 + q] = v[1].y;
+  // All NGL left groups in one pass (one square each: one LDS round trip per tile), done as soon
+  // as the next tile's groups are loaded (end of the current tile), so the reads land while the
+  // wave waits at the round barrier.
+  auto bt_transpose = [&](d2v (&v)[NG][2]) {
+    double* tb0 = reinterpret_cast<double*>(smem + L::kTrOff + wave * NGL * kTrBytes);
+#pragma unroll
+    for (int g = 0; g < NGL; ++g) {
+      double* tb = tb0 + g * (kTrBytes / 8);
+      tb[i16 * kTrLd + q] = v[g][0].x;
+      tb[i16 * kTrLd + 4 + q] = v[g][0].y;
+      tb[i16 * kTrLd + 8 + q] = v[g][1].x;
+      tb[i16 * kTrLd + 12 + q] = v[g][1].y;
+    }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    v[0].x = tb[q * kTrLd + i16];
-    v[0].y = tb[(4 + q) * kTrLd + i16];
-    v[1].x = tb[(8 + q) * kTrLd + i16];
-    v[1].y = tb[(12 + q) * kTrLd + i16];
+#pragma unroll
+    for (int g = 0; g < NGL; ++g) {
+      const double* tb = tb0 + g * (kTrBytes / 8);
+      v[g][0].x = tb[q * kTrLd + i16];
+      v[g][0].y = tb[(4 + q) * kTrLd + i16];
+      v[g][1].x = tb[(8 + q) * kTrLd + i16];
+      v[g][1].y = tb[(12 + q) * kTrLd + i16];
+    }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -373,10 +408,14 @@ void k_spmm_bt(BtArgs a) {
     }
     hN = hdr_load(clamp_t(T0 + wave + 4));
   } else {
+    const HalfPlan hp0 = half_plan(clamp_t(T0 + wave));
 #pragma unroll
     for (int g = 0; g < NG; ++g) {
-      av[g][0] = tile_a(clamp_t(T0 + wave), g, 0);
-      av[g][1] = tile_a(clamp_t(T0 + wave), g, 1);
+      av[g][0] = tile_a(clamp_t(T0 + wave), g, 0, hp0);
+      av[g][1] = tile_a(clamp_t(T0 + wave), g, 1, hp0);
+    }
+    if constexpr (HALF) {
+      if (clamp_t(T0 + wave) >= NGL) bt_transpose(av);
     }
   }
   // Q_{i-1} tile rows: lane row i16, columns 8m + 2q + {0,1}
@@ -429,13 +468,8 @@ void k_spmm_bt(BtArgs a) {
     }
 
     if (tw < T1) {  // wave-uniform
-      if constexpr (HALF) {
-        if (tw >= NGL) {
-#pragma unroll
-          for (int g = 0; g < NGL; ++g) bt_transpose(av[g]);
-        }
-      }
       const int64_t tn = clamp_t(tw + 4);
+      const HalfPlan hpn = half_plan(tn);
       uint64_t hNN = 0;
       if constexpr (VAR & 128) hNN = hdr_load(clamp_t(tw + 8));
       const auto rsN = [&] {
@@ -479,8 +513,8 @@ void k_spmm_bt(BtArgs a) {
           av[g][0] = tile_ap(hN, rsN, 2 * g);
           av[g][1] = tile_ap(hN, rsN, 2 * g + 1);
         } else {
-          av[g][0] = tile_a(tn, g, 0);
-          av[g][1] = tile_a(tn, g, 1);
+          av[g][0] = tile_a(tn, g, 0, hpn);
+          av[g][1] = tile_a(tn, g, 1, hpn);
         }
       }
       if constexpr (VAR & 128) hN = hNN;
@@ -542,6 +576,9 @@ void k_spmm_bt(BtArgs a) {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         __builtin_amdgcn_wave_barrier();
       }
+      if constexpr (HALF) {  // the next tile's left groups, loaded during this tile
+        if (tn >= NGL) bt_transpose(av);
+      }
     }
     if constexpr (LF) {
       lf_finish(rn, lraw, lqa);
@@ -582,7 +619,8 @@ void k_spmm_bt(BtArgs a) {
 
 template <int B, int NG, bool EPI, bool AIG, int VAR>
 static void launch_bt_v(const BtArgs& a, int grid, hipStream_t s) {
-  constexpr int lds = bt::Geo<B>::kLds + ((VAR & 2048) ? 2 * 9216 : (VAR & 1024) ? kCtBytes : 0);
+  constexpr int lds = bt::Geo<B>::kLds + ((VAR & 2048) ? 9216 + 4 * ((NG - 1) / 2) * kTrBytes
+                                                      : (VAR & 1024) ? kCtBytes : 0);
   ensure_lds_attr(reinterpret_cast<const void*>(&k_spmm_bt<B, NG, EPI, AIG, VAR>), lds);
   hipLaunchKernelGGL((k_spmm_bt<B, NG, EPI, AIG, VAR>), dim3(grid), dim3(bt::kThreads), lds, s, a);
 }
