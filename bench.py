@@ -292,7 +292,8 @@ def main():
                  "traffic": None if traffic is None else int(traffic),
                  "algorithmic_bytes_per_launch": int(spmm_bytes),
                  "streamed_bytes_per_launch": int(streamed_bytes(spmm_kid, nloc, nnz_loc, b, args.halfwidth, m_max,
-                                                                 mat_fmt)),
+                                                                 mat_fmt)
+                                                  + (m_max - 1) * nloc * b * 8 * lfused / (m_max + 1)),
                  "matrix_format": {0: "csr", 1: "band tiles", 2: "packed band tiles", 3: "half band tiles",
                                    4: "dense"}[mat_fmt],
                  # gather kernels (unbanded patterns) also read one Q row (b * 8 B) per nonzero,
