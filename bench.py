@@ -392,8 +392,6 @@ def main():
                     "host_eig_ms": round(info.eig_ms, 3),
                     "host_ms": {"start": round(info.start_ms, 1), "fetch_wait": round(info.fetch_ms, 1),
                                 "eig": round(info.eig_ms, 1), "ritz_and_d2h": round(info.ritz_ms, 1)},
-               "host_ms": {"start": round(info.start_ms, 1), "fetch_wait": round(info.fetch_ms, 1),
-                           "eig": round(info.eig_ms, 1), "ritz_and_d2h": round(info.ritz_ms, 1)},
                     "stage_ms": {s_: round(v, 3) for s_, v in st_.items()}}
 
     # ---- CPU baseline: the oracle (port of RBL.jl) on a bounded sample, rank 0, N = 1 ----
