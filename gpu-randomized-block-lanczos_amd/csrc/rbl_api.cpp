@@ -15,6 +15,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/rbl_hip.h"
@@ -112,6 +113,8 @@ struct rbl_ctx {
   double* d_small = nullptr;  // R, Rinv, Rtot, Bprev, Ai, G (b x b each)
   int* d_flags = nullptr;     // [need3, skip3, status0, status1]
   double* h_pin = nullptr;    // pinned staging: Ai, Rtot (2 b x b)
+  void* h_d2h[2] = {nullptr, nullptr};  // pinned slots of the staged D2H (d2h_staged)
+  hipEvent_t ev_d2h_slot[2] = {nullptr, nullptr};
   double* h_hist = nullptr;   // rbl_step_async stash: per step i, Ai and Rtot (2 b x b)
   int* h_hflags = nullptr;    //   and the step's 4 flags
   int fetched = 1;            // steps < fetched have been returned by rbl_fetch
@@ -1384,8 +1387,11 @@ int rbl_free(rbl_ctx* ctx) {
   delete ctx->comm;
   if (ctx->stream) hipStreamDestroy(ctx->stream);
   if (ctx->cstream) hipStreamDestroy(ctx->cstream);
-  for (hipEvent_t e : {ctx->ev_fin, ctx->ev_d2h[0], ctx->ev_d2h[1]})
+  for (hipEvent_t e : {ctx->ev_fin, ctx->ev_d2h[0], ctx->ev_d2h[1], ctx->ev_d2h_slot[0],
+                       ctx->ev_d2h_slot[1]})
     if (e) hipEventDestroy(e);
+  for (void* h : ctx->h_d2h)
+    if (h) hipHostFree(h);
   delete ctx;
   return RBL_OK;
 }
@@ -2196,6 +2202,50 @@ int step_impl(rbl_ctx* ctx, int i, int part_reorth, double* A_out, double* B_out
   if (flags[2]) return fail(ctx, RBL_ERR_NUMERIC, "QR breakdown (shifted CholQR failed)");
   return flags[3] ? RBL_WARN_QR_SHIFTED : RBL_OK;
 }
+// Device -> pageable host copy of a large result (the Ritz vectors, RBL_gpu.jl:219 returns them
+// on the host) through two pinned 64 MiB slots: the DMA of piece p runs while host threads copy
+// piece p-1 out of the other slot into the caller's memory.  hipMemcpy into pageable memory goes
+// through the runtime's own bounce buffer on one thread, well under the PCIe rate (§2: 49-56 GB/s
+// pinned).  Every earlier piece's host copy has finished before its slot is refilled.
+// RBL_D2H_DIRECT=1 restores the plain copy (A/B).
+constexpr size_t kD2HPiece = size_t(64) << 20;
+int d2h_staged(rbl_ctx* ctx, void* dst, const void* src, size_t bytes) {
+  if (bytes < 4 * kD2HPiece || std::getenv("RBL_D2H_DIRECT")) {
+    HIPC(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
+    return RBL_OK;
+  }
+  for (int s = 0; s < 2; ++s) {
+    if (!ctx->h_d2h[s]) HIPC(hipHostMalloc(&ctx->h_d2h[s], kD2HPiece, hipHostMallocDefault));
+    if (!ctx->ev_d2h_slot[s]) HIPC(hipEventCreateWithFlags(&ctx->ev_d2h_slot[s], hipEventDisableTiming));
+  }
+  const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+  const int nthr = (int)std::min(8u, hw);
+  auto host_copy = [&](size_t p) {
+    const size_t off = p * kD2HPiece, len = std::min(kD2HPiece, bytes - off);
+    char* d = static_cast<char*>(dst) + off;
+    const char* s = static_cast<const char*>(ctx->h_d2h[p & 1]);
+    const size_t part = ((len + nthr - 1) / nthr + 4095) & ~size_t(4095);
+    std::vector<std::thread> th;
+    for (size_t o = part; o < len; o += part)
+      th.emplace_back([=] { memcpy(d + o, s + o, std::min(part, len - o)); });
+    memcpy(d, s, std::min(part, len));
+    for (auto& t : th) t.join();
+  };
+  const size_t np = (bytes + kD2HPiece - 1) / kD2HPiece;
+  for (size_t p = 0; p <= np; ++p) {
+    if (p < np) {
+      const size_t off = p * kD2HPiece;
+      HIPC(hipMemcpyAsync(ctx->h_d2h[p & 1], static_cast<const char*>(src) + off,
+                          std::min(kD2HPiece, bytes - off), hipMemcpyDeviceToHost, ctx->stream));
+      HIPC(hipEventRecord(ctx->ev_d2h_slot[p & 1], ctx->stream));
+    }
+    if (p > 0) {
+      HIPC(hipEventSynchronize(ctx->ev_d2h_slot[(p - 1) & 1]));
+      host_copy(p - 1);
+    }
+  }
+  return RBL_OK;
+}
 }  // namespace
 
 int rbl_ritz(rbl_ctx* ctx, int nblocks, int k, const double* S, double* V_out) {
@@ -2237,8 +2287,7 @@ int rbl_ritz(rbl_ctx* ctx, int nblocks, int k, const double* S, double* V_out) {
     if (ctx->nloc > 0) rowmajor_to_colmajor(d_V.d(), ctx->nloc, kcp, d_Vcm.d(), ctx->stream);
     HIPC(hipGetLastError());
     if (V_out && ctx->nloc > 0)
-      HIPC(hipMemcpyAsync(V_out + (size_t)c0 * ctx->nloc, d_Vcm.p, ctx->nloc * w * sizeof(double),
-                          hipMemcpyDeviceToHost, ctx->stream));
+      CHK(d2h_staged(ctx, V_out + (size_t)c0 * ctx->nloc, d_Vcm.p, ctx->nloc * w * sizeof(double)));
   }
   HIPC(hipStreamSynchronize(ctx->stream));
   harvest_timers(ctx);

@@ -61,6 +61,42 @@ def dsbev(T: np.ndarray):
     return w, z
 
 
+# The loop needs only the k largest-|lambda| pairs of T (common.jl:50-54 keeps those), which lie
+# among the k lowest and the k highest eigenvalues.  From N = 512 on (and N > 8k) the band is
+# expanded to dense and reduced ONCE to tridiagonal form by the blocked dsytrd (all host
+# threads; the band reduction inside dsbev / dsbevd is sequential), dstemr (MRRR) gives the 2k
+# end pairs of the tridiagonal, and dormqr applies the reflectors to those 2k vectors only.
+# Same eigenvalues as dsbev to ~1e-14 relative; vectors up to sign (tests/test_host_helpers.py).
+# RBL_HOST_EIGEN=dsbev or dsbevd forces the whole-spectrum routine.
+SUBSET_MIN_N = 512
+
+
+def eig_topk(T: np.ndarray, k: int):
+    """sort_eig_abs(*dsbev(T), k) (RBL_gpu.jl:187-188): the k largest-|lambda| eigenpairs of the
+    band T (lower, kd = b), ascending |lambda|."""
+    N = T.shape[1]
+    if _EIGEN != "auto" or N < SUBSET_MIN_N or 8 * k >= N:
+        return sort_eig_abs(*dsbev(T), k)
+    from scipy.linalg import eigh_tridiagonal
+    full = np.zeros((N, N), order="F")
+    for r in range(T.shape[0]):
+        idx = np.arange(N - r)
+        full[idx + r, idx] = T[r, : N - r]
+    c, d, e, tau, info = lapack.dsytrd(full, lower=1, lwork=64 * N, overwrite_a=1)
+    if info != 0:
+        raise np.linalg.LinAlgError(f"dsytrd info={info}")
+    ends = [eigh_tridiagonal(d, e, select="i", select_range=rng, lapack_driver="stemr")
+            for rng in ((0, k - 1), (N - k, N - 1))]
+    Z = np.asfortranarray(np.hstack([ends[0][1], ends[1][1]]))
+    # Q = diag(1, H(1)..H(N-1)): the reflectors sit below the subdiagonal (uplo = 'L')
+    cq, _, info = lapack.dormqr("L", "N", c[1:, : N - 1], tau[: N - 1], Z[1:], lwork=128 * k,
+                                overwrite_c=1)
+    if info != 0:
+        raise np.linalg.LinAlgError(f"dormqr info={info}")
+    Z[1:] = cq
+    return sort_eig_abs(np.concatenate([ends[0][0], ends[1][0]]), Z, k)
+
+
 def sort_eig_abs(D: np.ndarray, V: np.ndarray, k: int):
     """common.jl:50-54 — stable sort by |lambda| (Julia sortperm is stable); keep the top k."""
     perm = np.argsort(np.abs(D), kind="stable")[len(D) - k:]

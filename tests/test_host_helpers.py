@@ -58,3 +58,22 @@ def test_large_band_eigensolve_matches_reference_routine():
     s1 = host.sort_eig_abs(d1, v1, 20)
     s2 = o.sort_eig_abs(d2, v2, 20)
     assert np.abs(s1[0] - s2[0]).max() < 1e-12 * scale
+
+
+def test_topk_eigensolve_matches_reference_selection():
+    """The loop's k largest-|lambda| pairs (rbl.host.eig_topk: dsyevr on the 2k end pairs from
+    N = 512 on) equal the reference's dsbev + sort_eig_abs (common.jl:36-54): eigenvalues to
+    rounding, vectors up to sign, the same convergence decision; both spectrum ends compete."""
+    from rbl import host
+    rng = np.random.default_rng(6)
+    for N, b, k, shift in [(512, 32, 20, 0.0), (640, 16, 20, -40.0), (768, 32, 7, 40.0)]:
+        T = rng.standard_normal((b + 1, N))
+        T[0] += shift * np.sin(np.arange(N))      # large eigenvalues of both signs
+        d1, v1 = host.eig_topk(T, k)
+        d2, v2 = o.sort_eig_abs(*o.dsbev(T), k)
+        scale = np.abs(d2).max()
+        assert np.abs(d1 - d2).max() < 1e-12 * scale
+        assert (1 - np.abs((v1 * v2).sum(axis=0))).max() < 1e-10
+        B = np.triu(rng.standard_normal((b, b)))
+        for tol in (1e-3, 1e2):
+            assert host.check_convergence(B, v1, b, k, tol) == o.check_convergence(B, v2, b, k, tol)
