@@ -6,6 +6,8 @@
 //
 // v_mfma_f32_16x16x4_f32 (cdna_hip_programming.md 'FP32-input MFMA'): lane l holds
 //   A[i = l&15][k = l>>4], B[k = l>>4][j = l&15], D[row 4 (l>>4) + v][col l&15], v = reg 0..3.
+#include <cstdlib>
+
 #include "kernels.hpp"
 
 namespace rbl {
@@ -430,10 +432,71 @@ static void launch_tsmm32(int64_t nrows, const float* Xb, int64_t xstride, int n
                      nX, C, ldc, KY, Y0, Y1, alpha, beta);
 }
 
+// Y += alpha X C for ONE 32-column panel X and 32 output columns (the fp32 local reorth,
+// Q_i -= Q_{i-1} (Q_{i-1}^T Q_i), RBL_gpu.jl:83-93 in FLOAT): a streaming pass, so lanes move
+// whole rows instead of MFMA tiles.  Per 32-row group the workgroup reads X and Y as one
+// contiguous 4 KiB float4 each (thread t: quad t % 8 of row t / 8); X goes through LDS so each
+// lane sees its row, Y stays in the lane's register.  The grid is persistent (C staged once per
+// workgroup as alpha * fp32(C), as k_tsmm32).  The sum runs in k_tsmm32's MFMA order (chunk of
+// 16 k, step s, lane quarter q: k = 16 ch + 4 q + s) as an fmaf chain, then adds Y: the same
+// bits as that kernel (tested).
+__global__ __launch_bounds__(256) void k_upd32_rows(int64_t nrows, const float* __restrict__ X,
+                                                    const double* __restrict__ C, int ldc,
+                                                    float* __restrict__ Y, float alpha) {
+  __shared__ __attribute__((aligned(16))) float cs[32 * 32];
+  __shared__ f4v xs[2][256];
+  for (int i = threadIdx.x; i < 32 * 32; i += 256)
+    cs[i] = alpha * (float)C[(int64_t)(i >> 5) * ldc + (i & 31)];
+  const int t = threadIdx.x, j = t & 7, row = t >> 3;
+  const int64_t ngroups = (nrows + 31) / 32;
+  const f4v* X4 = reinterpret_cast<const f4v*>(X);
+  f4v* Y4 = reinterpret_cast<f4v*>(Y);
+  int buf = 0;
+  for (int64_t g = blockIdx.x; g < ngroups; g += gridDim.x, buf ^= 1) {
+    const int64_t e = g * 256 + t;             // float4 index: row g * 32 + row, quad j
+    const bool ok = g * 32 + row < nrows;
+    xs[buf][t] = ok ? X4[e] : f4v{0.f, 0.f, 0.f, 0.f};
+    f4v y = ok ? Y4[e] : f4v{0.f, 0.f, 0.f, 0.f};
+    __syncthreads();                           // (two buffers: one barrier per group)
+    const f4v* xr = &xs[buf][row * 8];
+    float x[32];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const f4v v = xr[i];
+      x[4 * i] = v[0];
+      x[4 * i + 1] = v[1];
+      x[4 * i + 2] = v[2];
+      x[4 * i + 3] = v[3];
+    }
+    f4v acc = f4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ch = 0; ch < 2; ++ch)
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int k = 16 * ch + 4 * q + s;
+          const f4v c = *reinterpret_cast<const f4v*>(cs + 32 * k + 4 * j);
+#pragma unroll
+          for (int m = 0; m < 4; ++m) acc[m] = fmaf(x[k], c[m], acc[m]);
+        }
+#pragma unroll
+    for (int m = 0; m < 4; ++m) y[m] = acc[m] + y[m];
+    if (ok) Y4[e] = y;
+  }
+}
+
 void tsmm32(int64_t nrows, const float* Xb, int64_t xstride, int nX, int w, const double* C, int ldc,
             float* Y0, float* Y1, int ycount, float alpha, float beta, hipStream_t st) {
   if (nrows <= 0) return;
   const int KY = ycount * w;
+  // the local reorth's shape (one panel, 32 columns, Y += X C); RBL_LOC32_MFMA=1: the tile kernel
+  if (w == 32 && nX == 1 && KY == 32 && beta == 1.f && !std::getenv("RBL_LOC32_MFMA")) {
+    const int64_t groups = (nrows + 31) / 32;
+    const int64_t grid = groups < 8 * (int64_t)window_grid() ? groups : 8 * (int64_t)window_grid();
+    hipLaunchKernelGGL(k_upd32_rows, dim3((unsigned)grid), dim3(256), 0, st, nrows, Xb, C, ldc, Y0, alpha);
+    return;
+  }
   if (w != 16 && w != 32) {
     const int64_t thr = nrows * KY;
     hipLaunchKernelGGL(k_tsmm32_any, dim3((unsigned)((thr + 255) / 256)), dim3(256), 0, st, nrows, Xb,
