@@ -134,6 +134,82 @@ __global__ __launch_bounds__(256) void k_gram32(int64_t nrows, const float* __re
         out[(int64_t)(16 * a + 4 * q + v) * KC + 16 * c + c16] = (double)acc[a][c][v];
 }
 
+// The local-reorth Gram C = Q_{i-1}^T Q_i (one 32-column panel, 32 X columns): k_gram32 gives
+// each wave its own panel, so with one panel three of its four waves only stage X.  Here the
+// four waves take consecutive 16-row slices of a 64-row chunk, load both operands straight
+// from HBM (no LDS, no barrier in the loop; the next slice prefetched), and sum their tiles
+// through LDS in wave order at the end (deterministic).  Same fp32 products; the per-split
+// sum order differs from k_gram32 (rounding level).
+template <int W>
+__global__ __launch_bounds__(256) void k_gram32_one(int64_t nrows, const float* __restrict__ Wp,
+                                                    const float* __restrict__ X,
+                                                    double* __restrict__ slab, int64_t rows_per) {
+  constexpr int T = W / 16;
+  __shared__ f4v red[3][64][T * T];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int q = lane >> 4, c16 = lane & 15;
+  const int64_t s = blockIdx.x;
+  const int64_t r_begin = s * rows_per;
+  const int64_t r_end = r_begin + rows_per < nrows ? r_begin + rows_per : nrows;
+  f4v acc[T][T];
+#pragma unroll
+  for (int a = 0; a < T; ++a)
+#pragma unroll
+    for (int c = 0; c < T; ++c) acc[a][c] = f4v{0.f, 0.f, 0.f, 0.f};
+  auto load = [&](int64_t rb, float (&ar)[4][T], float (&br)[4][T]) {
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const int64_t row = rb + 4 * ks + q;
+      const bool ok = row < r_end;
+      const int64_t rr = ok ? row : (r_end > 0 ? r_end - 1 : 0);
+#pragma unroll
+      for (int a = 0; a < T; ++a) {
+        const float av = Wp[rr * W + c16 + 16 * a];
+        ar[ks][a] = ok ? av : 0.f;
+        br[ks][a] = X[rr * W + c16 + 16 * a];
+      }
+    }
+  };
+  float ac[4][T], bc[4][T], an[4][T], bn[4][T];
+  int64_t rb = r_begin + 16 * wave;
+  if (r_begin < r_end) load(rb, ac, bc);
+  for (; rb < r_end; rb += 64) {
+    load(rb + 64, an, bn);  // clamped past the split: finite values met by zero A
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+      for (int a = 0; a < T; ++a)
+#pragma unroll
+        for (int c = 0; c < T; ++c) acc[a][c] = mfma16(ac[ks][a], bc[ks][c], acc[a][c]);
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+      for (int a = 0; a < T; ++a) {
+        ac[ks][a] = an[ks][a];
+        bc[ks][a] = bn[ks][a];
+      }
+  }
+  if (wave > 0) {
+#pragma unroll
+    for (int a = 0; a < T; ++a)
+#pragma unroll
+      for (int c = 0; c < T; ++c) red[wave - 1][lane][a * T + c] = acc[a][c];
+  }
+  __syncthreads();
+  if (wave != 0) return;
+  double* out = slab + s * (int64_t)W * W;
+#pragma unroll
+  for (int a = 0; a < T; ++a)
+#pragma unroll
+    for (int c = 0; c < T; ++c) {
+      f4v v = acc[a][c];
+#pragma unroll
+      for (int w = 0; w < 3; ++w) v += red[w][lane][a * T + c];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) out[(int64_t)(16 * a + 4 * q + e) * W + 16 * c + c16] = (double)v[e];
+    }
+}
+
 int gram32_splits(int64_t nrows) {
   int64_t s8 = 3 * window_grid() / 8;
   const int64_t max_s8 = (nrows + 8 * 128 - 1) / (8 * 128);
@@ -200,6 +276,13 @@ void gram32_partial(int64_t nrows, const float* Wb, int64_t wstride, int nW, int
     const int64_t rows_per = (nrows + splits - 1) / splits;
     hipLaunchKernelGGL(k_gram32_any, dim3((unsigned)((len + 255) / 256), (unsigned)splits), dim3(256), 0,
                        st, nrows, Wb, wstride, nW, w, X0, X1, xcount, slab, rows_per);
+    return;
+  }
+  if (w == 32 && nW == 1 && xcount == 1 && !std::getenv("RBL_LOC32_MFMA")) {
+    int64_t rows_per = (nrows + splits - 1) / splits;
+    rows_per = (rows_per + 63) / 64 * 64;
+    hipLaunchKernelGGL(k_gram32_one<32>, dim3((unsigned)splits), dim3(256), 0, st, nrows, Wb, X0, slab,
+                       rows_per);
     return;
   }
   if (w == 32) {

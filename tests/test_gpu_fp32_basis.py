@@ -176,10 +176,10 @@ def test_fp32_basis_tiny_slices(rbl):
 
 @pytest.mark.parametrize("dense", [False, True])
 def test_fp32_local_reorth_row_kernel_matches_tile_kernel(rbl, dense, monkeypatch):
-    """b = 32: the fp32 local-reorth update runs as a row-streaming kernel (k_upd32_rows) that
-    sums in k_tsmm32's MFMA k order; RBL_LOC32_MFMA=1 restores the tile kernel.  Traces and
-    every basis block agree to fp32 rounding (bit-identical where the MFMA's internal order is
-    the documented fmaf chain)."""
+    """b = 32: the fp32 local reorth runs its Gram on four waves per split (k_gram32_one) and
+    its update as a row-streaming kernel (k_upd32_rows, k_tsmm32's MFMA k order);
+    RBL_LOC32_MFMA=1 restores both tile kernels.  Traces and every basis block agree to fp32
+    rounding (the Gram's per-split sum order differs)."""
     b, steps = 32, 8
     A = (matgen.hashwindow_csr(6000, 64, 0.7734, 7, matgen.planted_spectrum(10)) if dense
          else c1_matrix(5000, 10))
