@@ -2219,7 +2219,8 @@ int d2h_staged(rbl_ctx* ctx, void* dst, const void* src, size_t bytes) {
     if (!ctx->ev_d2h_slot[s]) HIPC(hipEventCreateWithFlags(&ctx->ev_d2h_slot[s], hipEventDisableTiming));
   }
   const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-  const int nthr = (int)std::min(8u, hw);
+  const char* envt = std::getenv("RBL_D2H_THREADS");
+  const int nthr = (int)std::min(envt ? std::max(1u, (unsigned)atoi(envt)) : 8u, hw);
   auto host_copy = [&](size_t p) {
     const size_t off = p * kD2HPiece, len = std::min(kD2HPiece, bytes - off);
     char* d = static_cast<char*>(dst) + off;

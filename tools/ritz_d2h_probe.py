@@ -15,8 +15,10 @@ with rbl.Context(0) as ctx:
     rbl.lanczos(ctx, k, b, check=False, ritz=False, max_steps=8)
     S = np.asfortranarray(np.random.default_rng(0).standard_normal((8 * b, k)))
     for kind, direct in [("zeros", 1), ("zeros", 0), ("touched", 1), ("touched", 0),
-                         ("zeros", 1), ("zeros", 0), ("empty", 0)]:
-        if direct:
+                         ("zeros", 1), ("zeros", 0), ("empty", 0)] + [("zeros", -t) for t in (4, 8, 12, 16)] * 2:
+        if direct < 0:
+            os.environ["RBL_D2H_THREADS"] = str(-direct)
+        if direct > 0:
             os.environ["RBL_D2H_DIRECT"] = "1"
         else:
             os.environ.pop("RBL_D2H_DIRECT", None)
