@@ -63,12 +63,18 @@ def dsbev(T: np.ndarray):
 
 # The loop needs only the k largest-|lambda| pairs of T (common.jl:50-54 keeps those), which lie
 # among the k lowest and the k highest eigenvalues.  From N = 512 on (and N > 8k) the band is
-# expanded to dense and reduced ONCE to tridiagonal form by the blocked dsytrd (all host
-# threads; the band reduction inside dsbev / dsbevd is sequential), dstemr (MRRR) gives the 2k
+# expanded to dense and reduced ONCE to tridiagonal form by the blocked dsytrd (the band
+# reduction inside dsbev / dsbevd is unblocked), dstemr (MRRR) gives the 2k
 # end pairs of the tridiagonal, and dormqr applies the reflectors to those 2k vectors only.
 # Same eigenvalues as dsbev to ~1e-14 relative; vectors up to sign (tests/test_host_helpers.py).
-# RBL_HOST_EIGEN=dsbev or dsbevd forces the whole-spectrum routine.
+# RBL_HOST_EIGEN=dsbev or dsbevd forces the whole-spectrum routine.  At these sizes one BLAS
+# thread is fastest on the MI355X box's host (tools/host_topk_probe.py, N = 896: 31.6 ms on 1
+# thread, 35-41 ms on 2-16), so the solve runs under a one-thread limit when threadpoolctl exists.
 SUBSET_MIN_N = 512
+try:
+    from threadpoolctl import threadpool_limits as _tp_limits
+except ImportError:  # pragma: no cover - the image ships it
+    _tp_limits = None
 
 
 def eig_topk(T: np.ndarray, k: int):
@@ -77,6 +83,14 @@ def eig_topk(T: np.ndarray, k: int):
     N = T.shape[1]
     if _EIGEN != "auto" or N < SUBSET_MIN_N or 8 * k >= N:
         return sort_eig_abs(*dsbev(T), k)
+    if _tp_limits is not None:
+        with _tp_limits(limits=1, user_api="blas"):
+            return _eig_topk_dense(T, k)
+    return _eig_topk_dense(T, k)
+
+
+def _eig_topk_dense(T: np.ndarray, k: int):
+    N = T.shape[1]
     from scipy.linalg import eigh_tridiagonal
     full = np.zeros((N, N), order="F")
     for r in range(T.shape[0]):
