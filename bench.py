@@ -64,9 +64,18 @@ def parse():
                          "bulk, as the reference's slow_dec suite, so convergence takes ~24 steps)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     ap.add_argument("--spmm-kernel", type=int, default=0)
-    ap.add_argument("--matrix", default="hashwindow", choices=("hashwindow", "rmat"),
-                    help="rmat: BASELINE config 4's power-law pattern (SURVEY §8(d) C4b)")
+    ap.add_argument("--matrix", default="hashwindow", choices=("hashwindow", "rmat", "circuit"),
+                    help="rmat: BASELINE config 4's power-law pattern (SURVEY §8(d) C4b); "
+                         "circuit: BASELINE config 3's shape (G3_circuit-like SPD Laplacian, "
+                         "scattered; use --n 1585478 --b 16)")
+    ap.add_argument("--c3-steps", type=int, default=3,
+                    help="timed runs of the C3 circuit sub-record that follows a hash-window run "
+                         "(n = 1,585,478, b = 16, k = 20: BASELINE config 3's shape; 0 skips it)")
     ap.add_argument("--rmat-scale", type=int, default=24)
+    ap.add_argument("--rmat-steps", type=int, default=2,
+                    help="timed runs of the C4b R-MAT sub-record that follows a hash-window "
+                         "run (BASELINE config 4 in the same job; 0 skips it)")
+    ap.add_argument("--rmat-warmup", type=int, default=1)
     ap.add_argument("--rmat-edges", type=int, default=0,
                     help="R-MAT draws (0: 0.66 n x 100: ~1e9 nonzeros at n = 1e7 after merging)")
     ap.add_argument("--device-blocks", type=int, default=0,
@@ -91,8 +100,8 @@ def streamed_bytes(kid, nloc, nnz_loc, b, halfwidth, m_max, fmt=1):
     streams 16 x (16 + 2H) dense doubles per 16-row tile instead of 12 B per nonzero; the
     LDS-band kernel (3) 8 B value + 2 B position per nonzero plus the row pointers.  Packed
     band tiles (RBL_BT_PACK=1; dense by default) stream the nonzeros and a header of 24
-    (H = 32) or 42 (H = 64) 8-B words per tile; half band tiles (format 3, the default for a
-    symmetric A) the diagonal block and the right strip, 16 x (16 + H) doubles per tile (the
+    (H = 32) or 42 (H = 64) 8-B words per tile; half band tiles (format 3, opt-in with
+    RBL_BT_HALF=1 for a symmetric A; measured no faster) the diagonal block and the right strip, 16 x (16 + H) doubles per tile (the
     left part is the previous tiles' strips again, read back through L2)."""
     vec = (m_max * 3 + 2) / (m_max + 1) * nloc * b * 8
     if kid == 5:
@@ -108,10 +117,37 @@ def streamed_bytes(kid, nloc, nnz_loc, b, halfwidth, m_max, fmt=1):
     return nnz_loc * 12 + (nloc + 1) * 8 + vec
 
 
+def gpu_count_sysfs():
+    """GPUs this process may use, without touching the HIP runtime: the visible-devices list
+    if one is set, else the KFD topology nodes with a GPU (gfx_target_version != 0).  None when
+    neither is readable (then the ranks find out themselves)."""
+    for var in ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            return len([x for x in v.split(",") if x.strip() != ""])
+    base = "/sys/class/kfd/kfd/topology/nodes"
+    try:
+        nodes = os.listdir(base)
+    except OSError:
+        return None
+    count = 0
+    for nd in nodes:
+        try:
+            with open(os.path.join(base, nd, "properties")) as f:
+                for line in f:
+                    key, _, val = line.partition(" ")
+                    if key == "gfx_target_version" and int(val) != 0:
+                        count += 1
+                        break
+        except (OSError, ValueError):
+            continue
+    return count
+
+
 def launch_ranks(args) -> None:
-    """`--gpus N` outside torch.distributed.run: check the GPUs exist, then run this script
-    under torch.distributed.run with N processes (this process never touches the GPU;
-    torch.cuda.device_count() does not initialise it) and exit with its status."""
+    """`--gpus N` outside torch.distributed.run: check the GPUs exist (KFD sysfs, no HIP call:
+    this launcher process never initialises the GPU runtime), then run this script under
+    torch.distributed.run with N processes and exit with its status."""
     env_world = os.environ.get("WORLD_SIZE")
     if env_world is not None:
         if args.gpus is not None and args.gpus != int(env_world):
@@ -121,9 +157,8 @@ def launch_ranks(args) -> None:
         return
     import subprocess
     import socket
-    import torch
-    have = torch.cuda.device_count()
-    if have < args.gpus:
+    have = gpu_count_sysfs()
+    if have is not None and have < args.gpus:
         sys.exit(f"bench.py: --gpus {args.gpus} needs {args.gpus} GPUs, this node has {have}")
     with socket.socket() as sk:
         sk.bind(("127.0.0.1", 0))
@@ -136,6 +171,9 @@ def launch_ranks(args) -> None:
 
 def workload_name(args) -> str:
     """BASELINE.json config this run measures, by its shape."""
+    if args.matrix == "circuit":
+        return ("C3-shaped circuit SpMM-Lanczos" if (args.n, args.b) == (1_585_478, 16)
+                else "circuit-like SpMM-Lanczos")
     if args.matrix == "rmat":
         return "C4b R-MAT SpMM-Lanczos" if args.n == 10_000_000 and args.b == 32 else "R-MAT SpMM-Lanczos"
     if args.basis_bits == 32 and args.n == 50_000_000 and args.b == 32:
@@ -155,6 +193,140 @@ def metric_name(args, nnz: int) -> str:
     return (f"RBL iters/sec + time-to-k={args.k} eigenpairs, n={args.n:.0e} "
             f"nnz/row={nnz / args.n:.0f} b={args.b}" + (" fp32 basis" if args.basis_bits == 32 else "")
             + f" ({args.matrix})")
+
+
+def measure(ctx, args, matrix, K, W, nloc, nnz_loc, world, barrier, allmax):
+    """W untimed + K timed fixed-length runs (rbl_start + m_max block steps, convergence checks
+    off) on the matrix the context holds; the max over ranks of the timed region, the stage
+    times (hipEvents) and the SpMM / partial-reorth rooflines priced from them."""
+    import rbl
+    from rbl import _lib
+    n, b, k = args.n, args.b, args.k
+    m_max = rbl.rbl_gpu.max_steps_for(args.kryl, b)
+    spmm_kid = ctx.spmm_kernel_for(b)
+    mat_fmt = ctx.matrix_format()
+    spmm_kernel = {1: "gather", 2: "lds-window", 3: "lds-band-mfma", 5: "band-tile-mfma",
+                   6: "segmented-gather"}[spmm_kid]
+
+    def one_run():
+        rbl.lanczos(ctx, k, b, kryl_sz=args.kryl, seed=args.seed + 1, check=False, ritz=False,
+                    basis_bits=args.basis_bits)
+
+    for _ in range(W):
+        one_run()
+    barrier()
+    ctx.synchronize()
+    ctx.reset_timers()
+    ctx.comm_stats(reset=True)
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(K):
+        one_run()
+    ctx.synchronize()
+    barrier()
+    elapsed = allmax(time.perf_counter() - t0)
+    stage = ctx.timers()
+    comm = ctx.comm_stats()
+    iters = K * m_max
+    value = iters / elapsed
+    stage_per_run = {s: v / K for s, v in stage.items()}
+
+    # ---- roofline: SpMM (HBM) and partial reorth (fp64 MFMA), live from HIP events ----
+    spmm_launches = K * (m_max + 1)               # rbl_start + one per block step
+    spmm_ms = stage["AQ"] / spmm_launches
+    # algorithmic bytes (SURVEY §8(d)): nnz*(8+4) + (n+1)*8 + read Q + write U
+    # (+ read Q_{i-1} for the fused 3-term epilogue on the m_max step launches)
+    bytes_step = nnz_loc * 12 + (nloc + 1) * 8 + 3 * nloc * b * 8
+    bytes_start = nnz_loc * 12 + (nloc + 1) * 8 + 2 * nloc * b * 8
+    # RBL_OPT_FUSE bit 2: the step launches from i = 2 on also apply the local reorth to the Q_i
+    # rows they stage (Q_i and Q_{i-1} are read anyway) and write Q_i back: + n b 8 each
+    lfused = bool(args.fuse & 4) and spmm_kid == 5 and b == 32 and args.basis_bits == 64 \
+        and mat_fmt != 2
+    spmm_bytes = (m_max * bytes_step + bytes_start + (m_max - 1) * nloc * b * 8 * lfused) / (m_max + 1)
+    spmm_gbs = spmm_bytes / (spmm_ms * 1e-3) / 1e9
+    reorth_flops = sum(8.0 * nloc * b * b * (i - 2) for i in range(4, m_max + 1, 2))
+    reorth_ms = stage_per_run["part reorth"]
+    reorth_tf = reorth_flops / (reorth_ms * 1e-3) / 1e12 if reorth_ms > 0 else 0.0
+    # HBM bytes from PMC counters (tools/pmc_traffic.sh -> tools/pmc_summarize.py; separate
+    # FETCH_SIZE / WRITE_SIZE passes, gfx950 per-width calibration): a committed measurement of
+    # the same kernels on the same config, used only when the config matches
+    traffic = traffic_reorth = None
+    fmt_name = {0: "csr", 1: "band tiles", 2: "packed band tiles", 3: "half band tiles", 4: "dense"}[mat_fmt]
+    try:
+        with open(args.traffic_json) as f:
+            tj = json.load(f)
+        for rec in [tj] + list(tj.get("workloads", [])):
+            tc = rec.get("config", {})
+            if (tc.get("n") == n and tc.get("b") == b and world == 1 and args.basis_bits == 64
+                    and tc.get("matrix", "hashwindow") == matrix and tc.get("fuse") == args.fuse
+                    and tc.get("matrix_format") == fmt_name):  # the same kernels as measured
+                traffic = rec.get("spmm_hbm_bytes_per_launch")
+                traffic_reorth = rec.get("part_reorth_hbm_bytes_per_run")
+                break
+    except (OSError, ValueError):
+        pass
+    roof_spmm = {"kernel": f"spmm {spmm_kernel} (AQ stage)", "bound": "hbm", "achieved": round(spmm_gbs, 1),
+                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(spmm_gbs / HBM_PEAK_GBS, 4),
+                 "traffic": None if traffic is None else int(traffic),
+                 "algorithmic_bytes_per_launch": int(spmm_bytes),
+                 "streamed_bytes_per_launch": int(streamed_bytes(spmm_kid, nloc, nnz_loc, b, args.halfwidth, m_max,
+                                                                 mat_fmt)
+                                                  + (m_max - 1) * nloc * b * 8 * lfused / (m_max + 1)),
+                 "matrix_format": fmt_name,
+                 # gather kernels (unbanded patterns) also read one Q row (b * 8 B) per nonzero,
+                 # served by L2 / Infinity Cache / HBM: the traffic that bounds them
+                 **({"q_row_gather_bytes_per_launch": int(nnz_loc * b * 8),
+                     "gbs_incl_q_row_gathers": round((spmm_bytes + nnz_loc * b * 8) / (spmm_ms * 1e-3) / 1e9, 1)}
+                    if spmm_kid in (1, 6) else {}),
+                 "fused_local_reorth": lfused,
+                 "ms_per_launch": round(spmm_ms, 4)}
+    mfma_peak = FP64_MFMA_PEAK_TF if args.basis_bits == 64 else FP32_MFMA_PEAK_TF
+    # the clock the chip holds under these kernels (profiles/pmc_clock.json: GRBM_GUI_ACTIVE
+    # / 8 / wall, MI355X_MICROARCH.md 'DVFS give-back'): the spec peak assumes 2.4 GHz
+    held = None
+    try:
+        with open(os.path.join(ROOT, "profiles", "pmc_clock.json")) as f:
+            kc = json.load(f)["kernels"]
+        # the partial-reorth kernels at b = 32 (the Gram and the 64-column update, any variant)
+        ks = [v for k_, v in kc.items() if k_.startswith(("k_gram44<32, 2", "k_tsmm44f<32"))]
+        if ks and args.basis_bits == 64 and b == 32:
+            held = sum(k["clock_ghz"] * k["avg_us"] for k in ks) / sum(k["avg_us"] for k in ks)
+    except (OSError, ValueError, KeyError):
+        pass
+    # SURVEY §8(d) a7: bytes (2m + 6) B_blk per even step (the basis read by the Gram and by the
+    # update, plus the pair read / written); below the ridge (b = 16: AI ~ b/2) the stage is
+    # HBM-bound and priced against the HBM peak instead
+    s_basis = 8 if args.basis_bits == 64 else 4
+    reorth_bytes = sum((2 * (i - 2) + 6) * nloc * b * s_basis for i in range(4, m_max + 1, 2))
+    ai = reorth_flops / reorth_bytes if reorth_bytes else 0.0
+    ridge = mfma_peak * 1e12 / (HBM_PEAK_GBS * 1e9)
+    reorth_gbs = reorth_bytes / (reorth_ms * 1e-3) / 1e9 if reorth_ms > 0 else 0.0
+    mbound = ai >= ridge
+    roof_reorth = {"kernel": "partial reorth (gram+update)" + ("" if args.basis_bits == 64 else ", fp32"),
+                   "bound": "mfma" if mbound else "hbm",
+                   "achieved": round(reorth_tf, 2) if mbound else round(reorth_gbs, 1),
+                   "peak": mfma_peak if mbound else HBM_PEAK_GBS,
+                   "unit": "TFLOP/s" if mbound else "GB/s",
+                   "frac": round(reorth_tf / mfma_peak if mbound else reorth_gbs / HBM_PEAK_GBS, 4),
+                   "arithmetic_intensity": round(ai, 2), "ridge": round(ridge, 2),
+                   "algorithmic_bytes_per_run": int(reorth_bytes),
+                   "tflops": round(reorth_tf, 2),
+                   "traffic": None if traffic_reorth is None else int(traffic_reorth),
+                   "traffic_unit": f"HBM bytes per run (gram + update, {len(range(4, m_max + 1, 2))} launches each)",
+                   "algorithmic_flops_per_run": reorth_flops, "ms_per_run": round(reorth_ms, 3),
+                   **({"held_clock_ghz": round(held, 3),
+                       "frac_of_peak_at_held_clock": round(reorth_tf / (mfma_peak * held / 2.4), 4)}
+                      if held and mbound else {})}
+    if stage["part reorth"] > stage["AQ"]:
+        roofline, roofline2 = roof_reorth, roof_spmm
+    else:
+        roofline, roofline2 = roof_spmm, roof_reorth
+    # collectives per block step on this rank (all-reduces, grouped send/recv), from the library
+    steps_timed = K * (m_max + 1)
+    comm_per_step = {key: round(v / steps_timed, 3) for key, v in comm.items()}
+    return {"elapsed": elapsed, "stage": stage, "value": value, "roofline": roofline,
+            "roofline_secondary": roofline2, "spmm_kernel": spmm_kernel,
+            "comm_per_step": comm_per_step, "m_max": m_max}
 
 
 def main():
@@ -217,6 +389,8 @@ def main():
         if not args.rmat_edges:
             args.rmat_edges = int(0.66 * 100 * n)
         ctx.gen_rmat(n, args.rmat_scale, args.rmat_edges, args.seed, plant)
+    elif args.matrix == "circuit":
+        ctx.gen_circuit(n, args.seed, plant)
     else:
         ctx.gen_hashwindow(n, args.halfwidth, args.density, args.seed, plant)
     gen_s = time.perf_counter() - t0
@@ -228,122 +402,12 @@ def main():
     ctx.set_option(_lib.RBL_OPT_DEVICE_BLOCKS, args.device_blocks)
     ctx.set_option(_lib.RBL_OPT_FUSE, args.fuse)
     m_max = rbl.rbl_gpu.max_steps_for(args.kryl, b)
-    spmm_kid = ctx.spmm_kernel_for(b)
-    mat_fmt = ctx.matrix_format()
-    spmm_kernel = {1: "gather", 2: "lds-window", 3: "lds-band-mfma", 5: "band-tile-mfma",
-                   6: "segmented-gather"}[spmm_kid]
-
-    def one_run():
-        rbl.lanczos(ctx, k, b, kryl_sz=args.kryl, seed=args.seed + 1, check=False, ritz=False,
-                    basis_bits=args.basis_bits)
-
-    for _ in range(args.warmup):
-        one_run()
-    barrier()
-    ctx.synchronize()
-    ctx.reset_timers()
-    barrier()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        one_run()
-    ctx.synchronize()
-    barrier()
-    elapsed = allmax(time.perf_counter() - t0)
-    stage = ctx.timers()
+    meas = measure(ctx, args, args.matrix, args.steps, args.warmup, nloc, nnz_loc, world,
+                   barrier, allmax)
     K = args.steps
-    iters = K * m_max
-    value = iters / elapsed
+    elapsed, stage, value = meas["elapsed"], meas["stage"], meas["value"]
     stage_per_run = {s: v / K for s, v in stage.items()}
-
-    # ---- roofline: SpMM (HBM) and partial reorth (fp64 MFMA), live from HIP events ----
-    spmm_launches = K * (m_max + 1)               # rbl_start + one per block step
-    spmm_ms = stage["AQ"] / spmm_launches
-    # algorithmic bytes: nnz*(8+4) + (n+1)*8 + read Q + write U
-    # (+ read Q_{i-1} for the fused 3-term epilogue on the m_max step launches)
-    bytes_step = nnz_loc * 12 + (nloc + 1) * 8 + 3 * nloc * b * 8
-    bytes_start = nnz_loc * 12 + (nloc + 1) * 8 + 2 * nloc * b * 8
-    # RBL_OPT_FUSE bit 2: the step launches from i = 2 on also apply the local reorth to the Q_i
-    # rows they stage (Q_i and Q_{i-1} are read anyway) and write Q_i back: + n b 8 each
-    lfused = bool(args.fuse & 4) and spmm_kid == 5 and b == 32 and args.basis_bits == 64 \
-        and mat_fmt != 2
-    spmm_bytes = (m_max * bytes_step + bytes_start + (m_max - 1) * nloc * b * 8 * lfused) / (m_max + 1)
-    spmm_gbs = spmm_bytes / (spmm_ms * 1e-3) / 1e9
-    reorth_flops = sum(8.0 * nloc * b * b * (i - 2) for i in range(4, m_max + 1, 2))
-    reorth_ms = stage_per_run["part reorth"]
-    reorth_tf = reorth_flops / (reorth_ms * 1e-3) / 1e12 if reorth_ms > 0 else 0.0
-    # HBM bytes from PMC counters (tools/pmc_traffic.sh -> tools/pmc_summarize.py; separate
-    # FETCH_SIZE / WRITE_SIZE passes, gfx950 per-width calibration): a committed measurement of
-    # the same kernels on the same config, used only when the config matches
-    traffic = traffic_reorth = None
-    try:
-        with open(args.traffic_json) as f:
-            tj = json.load(f)
-        tc = tj.get("config", {})
-        fmt_name = {0: "csr", 1: "band tiles", 2: "packed band tiles", 3: "half band tiles", 4: "dense"}[mat_fmt]
-        if (tc.get("n") == n and tc.get("b") == b and world == 1 and args.basis_bits == 64
-                and args.matrix == "hashwindow" and tc.get("fuse") == args.fuse
-                and tc.get("matrix_format") == fmt_name):  # the same kernels as measured
-            traffic = tj.get("spmm_hbm_bytes_per_launch")
-            traffic_reorth = tj.get("part_reorth_hbm_bytes_per_run")
-    except (OSError, ValueError):
-        pass
-    roof_spmm = {"kernel": f"spmm {spmm_kernel} (AQ stage)", "bound": "hbm", "achieved": round(spmm_gbs, 1),
-                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(spmm_gbs / HBM_PEAK_GBS, 4),
-                 "traffic": None if traffic is None else int(traffic),
-                 "algorithmic_bytes_per_launch": int(spmm_bytes),
-                 "streamed_bytes_per_launch": int(streamed_bytes(spmm_kid, nloc, nnz_loc, b, args.halfwidth, m_max,
-                                                                 mat_fmt)
-                                                  + (m_max - 1) * nloc * b * 8 * lfused / (m_max + 1)),
-                 "matrix_format": {0: "csr", 1: "band tiles", 2: "packed band tiles", 3: "half band tiles",
-                                   4: "dense"}[mat_fmt],
-                 # gather kernels (unbanded patterns) also read one Q row (b * 8 B) per nonzero,
-                 # served by L2 / Infinity Cache / HBM: the traffic that bounds them
-                 **({"q_row_gather_bytes_per_launch": int(nnz_loc * b * 8),
-                     "gbs_incl_q_row_gathers": round((spmm_bytes + nnz_loc * b * 8) / (spmm_ms * 1e-3) / 1e9, 1)}
-                    if spmm_kid in (1, 6) else {}),
-                 "fused_local_reorth": lfused,
-                 "ms_per_launch": round(spmm_ms, 4)}
-    mfma_peak = FP64_MFMA_PEAK_TF if args.basis_bits == 64 else FP32_MFMA_PEAK_TF
-    # the clock the chip holds under these kernels (profiles/pmc_clock.json: GRBM_GUI_ACTIVE
-    # / 8 / wall, MI355X_MICROARCH.md 'DVFS give-back'): the spec peak assumes 2.4 GHz
-    held = None
-    try:
-        with open(os.path.join(ROOT, "profiles", "pmc_clock.json")) as f:
-            kc = json.load(f)["kernels"]
-        # the partial-reorth kernels at b = 32 (the Gram and the 64-column update, any variant)
-        ks = [v for k_, v in kc.items() if k_.startswith(("k_gram44<32, 2", "k_tsmm44f<32"))]
-        if ks and args.basis_bits == 64 and b == 32:
-            held = sum(k["clock_ghz"] * k["avg_us"] for k in ks) / sum(k["avg_us"] for k in ks)
-    except (OSError, ValueError, KeyError):
-        pass
-    # bytes (2m + 6) B_blk per even step (the basis read by the Gram and by the
-    # update, plus the pair read / written); below the ridge (b = 16: AI ~ b/2) the stage is
-    # HBM-bound and priced against the HBM peak instead
-    s_basis = 8 if args.basis_bits == 64 else 4
-    reorth_bytes = sum((2 * (i - 2) + 6) * nloc * b * s_basis for i in range(4, m_max + 1, 2))
-    ai = reorth_flops / reorth_bytes if reorth_bytes else 0.0
-    ridge = mfma_peak * 1e12 / (HBM_PEAK_GBS * 1e9)
-    reorth_gbs = reorth_bytes / (reorth_ms * 1e-3) / 1e9 if reorth_ms > 0 else 0.0
-    mbound = ai >= ridge
-    roof_reorth = {"kernel": "partial reorth (gram+update)" + ("" if args.basis_bits == 64 else ", fp32"),
-                   "bound": "mfma" if mbound else "hbm",
-                   "achieved": round(reorth_tf, 2) if mbound else round(reorth_gbs, 1),
-                   "peak": mfma_peak if mbound else HBM_PEAK_GBS,
-                   "unit": "TFLOP/s" if mbound else "GB/s",
-                   "frac": round(reorth_tf / mfma_peak if mbound else reorth_gbs / HBM_PEAK_GBS, 4),
-                   "arithmetic_intensity": round(ai, 2), "ridge": round(ridge, 2),
-                   "algorithmic_bytes_per_run": int(reorth_bytes),
-                   "tflops": round(reorth_tf, 2),
-                   "traffic": None if traffic_reorth is None else int(traffic_reorth),
-                   "traffic_unit": f"HBM bytes per run (gram + update, {len(range(4, m_max + 1, 2))} launches each)",
-                   "algorithmic_flops_per_run": reorth_flops, "ms_per_run": round(reorth_ms, 3),
-                   **({"held_clock_ghz": round(held, 3),
-                       "frac_of_peak_at_held_clock": round(reorth_tf / (mfma_peak * held / 2.4), 4)}
-                      if held and mbound else {})}
-    if stage["part reorth"] > stage["AQ"]:
-        roofline, roofline2 = roof_reorth, roof_spmm
-    else:
-        roofline, roofline2 = roof_spmm, roof_reorth
+    roofline, roofline2 = meas["roofline"], meas["roofline_secondary"]
 
     # ---- time-to-k (convergence on, start -> converged Ritz vectors) ----
     ttk = None
@@ -394,6 +458,17 @@ def main():
                                 "eig": round(info.eig_ms, 1), "ritz_and_d2h": round(info.ritz_ms, 1)},
                     "stage_ms": {s_: round(v, 3) for s_, v in st_.items()}}
 
+    # ---- BASELINE config 4 (C4b): the R-MAT pattern at the same n, b, k, same ranks ----
+    rmat_rec = None
+    if args.matrix == "hashwindow" and args.rmat_steps > 0 and args.basis_bits == 64:
+        rmat_rec = rmat_subrecord(ctx, args, plant, world, barrier, allmax, allsum,
+                                  allgather_i64)
+
+    # ---- BASELINE config 3's shape: the circuit-like matrix at G3_circuit's n, b = 16 ----
+    c3_rec = None
+    if args.matrix == "hashwindow" and args.c3_steps > 0 and args.basis_bits == 64:
+        c3_rec = c3_subrecord(ctx, args, world, barrier, allmax, allsum, allgather_i64)
+
     # ---- CPU baseline: the oracle (port of RBL.jl) on a bounded sample, rank 0, N = 1 ----
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -420,7 +495,8 @@ def main():
                        **({"halfwidth": args.halfwidth, "density": args.density}
                           if args.matrix == "hashwindow" else
                           {"rmat_scale": args.rmat_scale, "rmat_edges": args.rmat_edges,
-                           "rmat_abcd": [0.57, 0.19, 0.19, 0.05]}),
+                           "rmat_abcd": [0.57, 0.19, 0.19, 0.05]} if args.matrix == "rmat" else
+                          {"circuit_width": 1259, "circuit_p_edge": 0.95873}),
                        "block_steps_per_run": m_max, "parallelism": f"rows{world}",
                        "transport": comm["transport"], "transport_ranks": comm["nranks"],
                        "nnz_per_rank": nnz_ranks,
@@ -434,11 +510,103 @@ def main():
             "time_to_k_slow_spectrum": ttk_slow,
             "matrix_gen_s": round(gen_s, 3),
             "cpu_baseline": cpu,
+            "comm_per_step": meas["comm_per_step"],
+            "c4b_rmat": rmat_rec,
+            "c3_circuit": c3_rec,
         }
         print(json.dumps(line), flush=True)
     ctx.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def rmat_subrecord(ctx, args, plant, world, barrier, allmax, allsum, allgather_i64):
+    """BASELINE config 4 in the same driver run: the seeded R-MAT matrix
+    ((a,b,c,d) = (0.57,0.19,0.19,0.05), scale 24, 0.66 n x 100 draws: ~1e9 nonzeros at n = 1e7)
+    generated on the device in place of the headline matrix, nnz-balanced over the ranks; the
+    same fixed-length runs (`args.rmat_warmup` untimed + `args.rmat_steps` timed, max over
+    ranks), the SpMM priced on SURVEY's CSR bytes and on the Q-row gathers that bound it, and
+    a time-to-k on its planted spectrum."""
+    import copy
+    import rbl
+    ra = copy.copy(args)
+    ra.matrix = "rmat"
+    edges = args.rmat_edges or int(0.66 * 100 * args.n)
+    t0 = time.perf_counter()
+    ctx.gen_rmat(args.n, args.rmat_scale, edges, args.seed, plant)
+    gen_s = time.perf_counter() - t0
+    _, r0, r1, nnz_loc = ctx.matrix_info()
+    nloc = r1 - r0
+    nnz = allsum(nnz_loc)
+    meas = measure(ctx, ra, "rmat", args.rmat_steps, args.rmat_warmup, nloc, nnz_loc, world,
+                   barrier, allmax)
+    K = args.rmat_steps
+    barrier()
+    ctx.synchronize()
+    ctx.reset_timers()
+    t0 = time.perf_counter()
+    D, V, info = rbl.lanczos(ctx, args.k, args.b, kryl_sz=args.kryl, seed=args.seed + 2,
+                             check=True, ritz=True)
+    ctx.synchronize()
+    barrier()
+    ttk_s = allmax(time.perf_counter() - t0)
+    return {"workload": "C4b R-MAT SpMM-Lanczos" if (args.n, args.b) == (10_000_000, 32)
+            else "R-MAT SpMM-Lanczos",
+            "metric": f"RBL iters/sec, n={args.n:.0e} nnz/row={nnz / args.n:.0f} b={args.b} (rmat)",
+            "value": round(meas["value"], 3), "unit": "block iterations/s",
+            "steps": K, "warmup": args.rmat_warmup,
+            "ms_per_step": round(meas["elapsed"] / K * 1e3, 3),
+            "n": args.n, "nnz": nnz, "rmat_scale": args.rmat_scale, "rmat_edges": edges,
+            "rmat_abcd": [0.57, 0.19, 0.19, 0.05], "nnz_per_rank": allgather_i64(nnz_loc),
+            "roofline": meas["roofline"], "roofline_secondary": meas["roofline_secondary"],
+            "stage_ms_per_run": {s_: round(v / K, 3) for s_, v in meas["stage"].items()},
+            "comm_per_step": meas["comm_per_step"],
+            "time_to_k": {"seconds": round(ttk_s, 4), "iters": info.iters,
+                          "converged": info.converged, "k": args.k,
+                          "top_eigenvalues": [round(float(x), 6) for x in D[:3]]},
+            "matrix_gen_s": round(gen_s, 3)}
+
+
+def c3_subrecord(ctx, args, world, barrier, allmax, allsum, allgather_i64):
+    """BASELINE config 3's shape in the same driver run: the seeded
+    circuit-like SPD matrix of G3_circuit's size (n = 1,585,478, 7.66 M nonzeros, scattered: no
+    band; the real G3_circuit is not in the image) generated on the device, b = 16, k = 20; the
+    same fixed-length runs (m_max = 75 steps at b = 16) and a time-to-k."""
+    import copy
+    import rbl
+    ra = copy.copy(args)
+    ra.matrix, ra.n, ra.b, ra.k = "circuit", 1_585_478, 16, 20
+    plant = np.array([100.0 * (2 * ra.k + 1 - l) for l in range(1, 2 * ra.k + 1)])
+    t0 = time.perf_counter()
+    ctx.gen_circuit(ra.n, ra.seed, plant)
+    gen_s = time.perf_counter() - t0
+    _, r0, r1, nnz_loc = ctx.matrix_info()
+    nloc = r1 - r0
+    nnz = allsum(nnz_loc)
+    K = args.c3_steps
+    meas = measure(ctx, ra, "circuit", K, 1, nloc, nnz_loc, world, barrier, allmax)
+    barrier()
+    ctx.synchronize()
+    ctx.reset_timers()
+    t0 = time.perf_counter()
+    D, V, info = rbl.lanczos(ctx, ra.k, ra.b, kryl_sz=ra.kryl, seed=ra.seed + 2, check=True,
+                             ritz=True)
+    ctx.synchronize()
+    barrier()
+    ttk_s = allmax(time.perf_counter() - t0)
+    return {"workload": "C3-shaped circuit SpMM-Lanczos (G3_circuit's n and nnz, synthetic)",
+            "metric": f"RBL iters/sec, n={ra.n} nnz/row={nnz / ra.n:.2f} b={ra.b} (circuit)",
+            "value": round(meas["value"], 3), "unit": "block iterations/s",
+            "steps": K, "warmup": 1, "ms_per_step": round(meas["elapsed"] / K * 1e3, 3),
+            "n": ra.n, "nnz": nnz, "b": ra.b, "k": ra.k, "block_steps_per_run": meas["m_max"],
+            "nnz_per_rank": allgather_i64(nnz_loc),
+            "roofline": meas["roofline"], "roofline_secondary": meas["roofline_secondary"],
+            "stage_ms_per_run": {s_: round(v / K, 3) for s_, v in meas["stage"].items()},
+            "comm_per_step": meas["comm_per_step"],
+            "time_to_k": {"seconds": round(ttk_s, 4), "iters": info.iters,
+                          "converged": info.converged, "k": ra.k,
+                          "top_eigenvalues": [round(float(x), 6) for x in D[:3]]},
+            "matrix_gen_s": round(gen_s, 3)}
 
 
 def cpu_model() -> str:
@@ -470,6 +638,8 @@ def cpu_baseline(args, m_max, plant):
     if args.matrix == "rmat":  # same draw density per row, ids scaled down with n
         sc = max(1, int(math.ceil(math.log2(ns))))
         A = matgen.rmat_csr(ns, sc, int(args.rmat_edges * ns / args.n), args.seed, plant)
+    elif args.matrix == "circuit":
+        A = matgen.circuit_like_csr(ns, args.seed, plant)
     else:
         A = matgen.hashwindow_csr(ns, args.halfwidth, args.density, args.seed, plant)
     omega = np.random.default_rng(0).standard_normal((ns, args.b))

@@ -66,6 +66,99 @@ void hw_fill(int64_t n, int64_t W, double p, uint64_t seed, int64_t r0, int64_t 
                      r0, r1, rowptr, nplant, plant_dev, col, val);
 }
 
+// ---- circuit-like SPD matrix of G3_circuit's shape (BASELINE config 3; oracle/matgen.py
+// circuit_like_csr): a weighted Laplacian on a 5-point stencil over rows of `width` nodes, each
+// edge (lo, hi) kept iff u53(h) < p_edge (h = pair_hash(seed, lo, hi)), weight
+// 0.5 + u53(mix64(h ^ K)); diagonal 0.01 + the kept weights in the order right, down, left, up
+// (+ plant[l] at node l * floor(n / nplant)); node i becomes row / column scatter(i).  Row r of
+// the result is node scatter_inv(r): at most 5 nonzeros, columns sorted in registers.
+constexpr uint64_t kCircK = 0x9FB21C651E98DF25ull;
+
+struct CircNb {
+  int64_t node[4];
+  double w[4];
+  int cnt;
+};
+
+__device__ inline CircNb circ_neighbours(int64_t i, int64_t n, int64_t width, double p,
+                                         uint64_t seed) {
+  CircNb nb;
+  nb.cnt = 0;
+  // (lo, hi, other node) for right, down, left, up
+  const int64_t lo[4] = {i, i, i - 1, i - width};
+  const int64_t hi[4] = {i + 1, i + width, i, i};
+  const bool ok[4] = {(i % width) != width - 1 && i + 1 < n, i + width < n,
+                      (i % width) != 0, i - width >= 0};
+  for (int d = 0; d < 4; ++d) {
+    if (!ok[d]) continue;
+    const uint64_t h = pair_hash(seed, lo[d], hi[d]);
+    if (!(u53(h) < p)) continue;
+    nb.node[nb.cnt] = lo[d] == i ? hi[d] : lo[d];
+    nb.w[nb.cnt] = 0.5 + u53(mix64(h ^ kCircK));
+    ++nb.cnt;
+  }
+  return nb;
+}
+
+__global__ void k_circ_count(int64_t n, int64_t width, double p, uint64_t seed, Scatter sc,
+                             int64_t r0, int64_t r1, int32_t* counts) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t r = r0 + t;
+  if (r >= r1) return;
+  const int64_t i = scatter_inv(sc, r);
+  counts[t] = 1 + circ_neighbours(i, n, width, p, seed).cnt;
+}
+
+__global__ void k_circ_fill(int64_t n, int64_t width, double p, uint64_t seed, Scatter sc,
+                            int64_t r0, int64_t r1, const int64_t* __restrict__ rowptr, int nplant,
+                            const double* __restrict__ plant, int32_t* col, double* val) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t r = r0 + t;
+  if (r >= r1) return;
+  const int64_t i = scatter_inv(sc, r);
+  const CircNb nb = circ_neighbours(i, n, width, p, seed);
+  double diag = 0.01;
+  for (int d = 0; d < nb.cnt; ++d) diag += nb.w[d];
+  const int64_t stride = nplant > 0 ? n / nplant : 0;
+  if (stride > 0 && i % stride == 0 && i / stride < nplant) diag += plant[i / stride];
+  int64_t c[5];
+  double v[5];
+  const int m = nb.cnt + 1;
+  c[0] = r;
+  v[0] = diag;
+  for (int d = 0; d < nb.cnt; ++d) {
+    c[d + 1] = scatter(sc, nb.node[d]);
+    v[d + 1] = -nb.w[d];
+  }
+  for (int a = 1; a < m; ++a)  // insertion sort by column (<= 5 entries)
+    for (int b2 = a; b2 > 0 && c[b2 - 1] > c[b2]; --b2) {
+      const int64_t tc = c[b2]; c[b2] = c[b2 - 1]; c[b2 - 1] = tc;
+      const double tv = v[b2]; v[b2] = v[b2 - 1]; v[b2 - 1] = tv;
+    }
+  const int64_t e = rowptr[t];
+  for (int a = 0; a < m; ++a) {
+    col[e + a] = (int32_t)c[a];
+    val[e + a] = v[a];
+  }
+}
+
+void circ_count(int64_t n, int64_t width, double p, uint64_t seed, int64_t r0, int64_t r1,
+                int32_t* counts, hipStream_t s) {
+  const int64_t m = r1 - r0;
+  if (m <= 0) return;
+  hipLaunchKernelGGL(k_circ_count, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, n, width,
+                     p, seed, make_scatter(n, seed), r0, r1, counts);
+}
+
+void circ_fill(int64_t n, int64_t width, double p, uint64_t seed, int64_t r0, int64_t r1,
+               const int64_t* rowptr, int nplant, const double* plant_dev, int32_t* col,
+               double* val, hipStream_t s) {
+  const int64_t m = r1 - r0;
+  if (m <= 0) return;
+  hipLaunchKernelGGL(k_circ_fill, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, n, width, p,
+                     seed, make_scatter(n, seed), r0, r1, rowptr, nplant, plant_dev, col, val);
+}
+
 __global__ void k_randn(double* Q, int64_t nrows, int b, int64_t r0, uint64_t seed) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= nrows * b) return;

@@ -66,8 +66,9 @@ struct CsrDev {
   // fails if another kernel would run with qloc set.
   const void* qloc = nullptr;
   int64_t loc_lo = 0, loc_hi = 0;
-  // local reorth fused into the band-tile SpMM (RBL_OPT_FUSE bit 2, one rank, b = 32, dense
-  // tiles): the kernel stages every Q ring row as Q_i - Q_{i-1} C (C = lfix_c, b x b on the
+  // local reorth fused into the band-tile SpMM (RBL_OPT_FUSE bit 2, b = 32, dense tiles; one
+  // rank or several — then each rank's edge rows are corrected before the halo exchange, by
+  // spmm_bt_locfix_edges, and the SpMM leaves them as read): the kernel stages every Q ring row as Q_i - Q_{i-1} C (C = lfix_c, b x b on the
   // device; Q_{i-1} = the SpMM's Qprev) and writes the corrected own rows back into lfix_q
   // (the block Q_i) except the first and last H rows of each workgroup's range, which
   // neighbours read raw — spmm_bt_locfix_rest corrects those after the SpMM
@@ -288,6 +289,13 @@ void col_footprint(const int32_t* col, int64_t nnz, const int64_t* bounds_dev, i
 
 // --- gen.hip ---------------------------------------------------------------------------
 // Hash-window matrix rows [r0,r1): counts per row, then fill given rowptr (0-based, local).
+// circuit-like matrix (gen.hip; oracle/matgen.py circuit_like_csr): rows [r0, r1) of the
+// scattered index space, counts then CSR fill (columns sorted)
+void circ_count(int64_t n, int64_t width, double p, uint64_t seed, int64_t r0, int64_t r1,
+                int32_t* counts, hipStream_t s);
+void circ_fill(int64_t n, int64_t width, double p, uint64_t seed, int64_t r0, int64_t r1,
+               const int64_t* rowptr, int nplant, const double* plant_dev, int32_t* col,
+               double* val, hipStream_t s);
 void hw_count(int64_t n, int64_t W, double p, uint64_t seed, int64_t r0, int64_t r1,
               int32_t* counts, hipStream_t s);
 void hw_fill(int64_t n, int64_t W, double p, uint64_t seed, int64_t r0, int64_t r1,

@@ -135,6 +135,9 @@ struct rbl_ctx {
   bool cloc_final = false;    // formed after this step's reorth (valid whatever its flags)
   std::vector<int> step_flags;  // part_reorth flags per step (the fusion's schedule guess)
   double stage_ms[RBL_NUM_STAGES] = {0};
+  // collectives issued by this rank since the last reset (rbl_comm_stats): all-reduce calls and
+  // bytes, grouped halo exchanges and the bytes sent / received in them
+  int64_t comm_stats[RBL_COMM_NSTATS] = {0};
   struct Mark { int stage; hipEvent_t a, b; };
   std::vector<Mark> marks;
   std::vector<hipEvent_t> ev_pool;
@@ -570,7 +573,17 @@ int allreduce(rbl_ctx* ctx, double* buf, size_t count) {
   if (ctx->nranks == 1) return RBL_OK;
   StageScope t(ctx, RBL_STAGE_COMM);
   COMMC(ctx->comm->allreduce_sum(buf, count, ctx->stream, &ctx->err));
+  ctx->comm_stats[RBL_COMM_ALLREDUCE_CALLS] += 1;
+  ctx->comm_stats[RBL_COMM_ALLREDUCE_BYTES] += (int64_t)(count * sizeof(double));
   return RBL_OK;
+}
+
+void count_exchange(rbl_ctx* ctx, const std::vector<Comm::Xfer>& x) {
+  ctx->comm_stats[RBL_COMM_EXCHANGE_CALLS] += 1;
+  for (const auto& t : x) {
+    ctx->comm_stats[RBL_COMM_SEND_BYTES] += (int64_t)(t.nsend * sizeof(double));
+    ctx->comm_stats[RBL_COMM_RECV_BYTES] += (int64_t)(t.nrecv * sizeof(double));
+  }
 }
 
 // Gram C = W^T X over all ranks.  C layout [nW*w][X.count*X.w].
@@ -651,6 +664,29 @@ int rowop(rbl_ctx* ctx, const double* X, const double* C, double* Y, double alph
   reduce_slab(ctx->d_slab, grid, (int64_t)b * b, G, skip, ctx->stream);
   HIPC(hipGetLastError());
   return allreduce(ctx, G, (size_t)b * b);
+}
+
+// Gram slab of a run (doubles): the largest Gram is the partial-reorth one, (max_blocks-1)
+// panels x 2b per split; also the row ops' partials, the partial-reorth update's local-reorth
+// Gram partials and the fp32 Grams.  rbl_start allocates it; the automatic device-block plan
+// (RBL_OPT_DEVICE_BLOCKS < 0) budgets it — one formula for both.
+size_t gram_slab_elems(const rbl_ctx* ctx, int b, int max_blocks, int basis_bits) {
+  size_t slab = 0;
+  for (int nW = 1; nW <= std::max(1, max_blocks - 1); ++nW)
+    for (int xc : {b, 2 * b}) {
+      const size_t sp = (size_t)gram_splits(ctx->nloc, nW, b, xc);
+      slab = std::max(slab, sp * nW * b * xc);
+    }
+  slab = std::max(slab, (size_t)2 * rowgram_grid(ctx->nloc, kRowgramMaxPerCu) * b * b);  // rowop partials (+ cross Gram)
+  // the partial-reorth update's local-reorth Gram partials (one b x b per 128-row tile:
+  // n_local b^2 / 128 doubles, a quarter of a block at b = 32)
+  if (b == 32 && basis_bits == 64 && (ctx->fuse & 2)) {
+    const int xg = tsmm44_xg_grid(ctx->nloc);
+    slab = std::max(slab, (size_t)(xg + reduce_scratch_splits(xg)) * b * b);
+  }
+  if (basis_bits == 32)  // fp32 Grams: up to (max_blocks-1) panels x 2b per split
+    slab = std::max(slab, (size_t)gram32_splits(ctx->nloc) * std::max(1, max_blocks - 1) * b * 2 * b);
+  return slab;
 }
 
 bool has_matrix(const rbl_ctx* ctx) { return ctx->d_rowptr || ctx->dense; }
@@ -1074,6 +1110,7 @@ int halo_exchange(rbl_ctx* ctx, const double* Q, const double** Qin, int64_t* of
     }
   }
   COMMC(ctx->comm->exchange(x, ctx->stream, &ctx->err));
+  count_exchange(ctx, x);
   *Qin = ext;
   *off = ctx->ext_lo;
   return RBL_OK;
@@ -1109,6 +1146,7 @@ int halo_exchange32(rbl_ctx* ctx, const float* Q, const float** Qin, int64_t* of
     }
   }
   COMMC(ctx->comm->exchange(x, ctx->stream, &ctx->err));
+  count_exchange(ctx, x);
   *Qin = ext;
   *off = ctx->ext_lo;
   return RBL_OK;
@@ -1267,6 +1305,37 @@ int upload_csr(rbl_ctx* ctx, int64_t n, int64_t r0, int64_t r1, const int64_t* r
   }
   CHK(prepare_window(ctx, rp));
   return setup_halo(ctx);
+}
+
+// The halo of an unbanded local CSR (R-MAT, circuit): for every other rank q, the contiguous
+// range of q's rows the local columns reference (col_footprint on the device).
+int halo_from_footprint(rbl_ctx* ctx) {
+  const int P = ctx->nranks;
+  const int64_t nnz = ctx->nnz;
+  ctx->need_lo.assign(P, 0);
+  ctx->need_hi.assign(P, 0);
+  if (P > 1 && nnz > 0) {
+    int64_t* d_b = nullptr;
+    unsigned long long* d_lh = nullptr;
+    HIPC(hipMalloc(&d_b, (P + 1) * sizeof(int64_t)));
+    HIPC(hipMalloc(&d_lh, 2 * P * sizeof(unsigned long long)));
+    std::vector<unsigned long long> lh(2 * P);
+    for (int q = 0; q < P; ++q) { lh[q] = ~0ull; lh[P + q] = 0ull; }
+    HIPC(hipMemcpy(d_b, ctx->bounds.data(), (P + 1) * sizeof(int64_t), hipMemcpyHostToDevice));
+    HIPC(hipMemcpy(d_lh, lh.data(), 2 * P * sizeof(unsigned long long), hipMemcpyHostToDevice));
+    col_footprint(ctx->d_col, nnz, d_b, P, d_lh, d_lh + P, ctx->stream);
+    HIPC(hipGetLastError());
+    HIPC(hipMemcpyAsync(lh.data(), d_lh, 2 * P * sizeof(unsigned long long), hipMemcpyDeviceToHost, ctx->stream));
+    HIPC(hipStreamSynchronize(ctx->stream));
+    hipFree(d_b);
+    hipFree(d_lh);
+    for (int q = 0; q < P; ++q) {
+      if (q == ctx->rank || lh[P + q] == 0ull) continue;
+      ctx->need_lo[q] = (int64_t)lh[q];
+      ctx->need_hi[q] = (int64_t)lh[P + q];
+    }
+  }
+  return RBL_OK;
 }
 
 }  // namespace
@@ -1428,8 +1497,12 @@ int rbl_set_option(rbl_ctx* ctx, int option, int64_t value) {
       ctx->dev_blocks_opt = (int)value;
       return RBL_OK;
     case RBL_OPT_SPMM_KERNEL:
-      if (value < 0 || value > 5) return fail(ctx, RBL_ERR_INVALID, "spmm kernel must be 0..5");
-      ctx->spmm_variant = (int)value;
+      // option values are the kernel ids rbl_spmm_kernel_for reports (4, the dense panel GEMM,
+      // follows from rbl_set_matrix_dense and is not selectable); internally the band tiles
+      // are variant 4 and the segmented gather variant 5 (spmm.hip)
+      if (value < 0 || value > 6 || value == 4)
+        return fail(ctx, RBL_ERR_INVALID, "spmm kernel must be 0 (auto) or a kernel id 1, 2, 3, 5, 6");
+      ctx->spmm_variant = value == 5 ? 4 : value == 6 ? 5 : (int)value;
       return RBL_OK;
     case RBL_OPT_SPLIT_HALO: ctx->split_halo = value != 0; return RBL_OK;
     case RBL_OPT_KEEP_CSR: ctx->keep_csr = value != 0; return RBL_OK;
@@ -1600,6 +1673,54 @@ int rbl_gen_matrix_hashwindow(rbl_ctx* ctx, int64_t n, int64_t halfwidth, double
   return setup_halo(ctx);
 }
 
+int rbl_gen_matrix_circuit(rbl_ctx* ctx, int64_t n, int64_t width, double p_edge, uint64_t seed,
+                           int nplant, const double* plant) {
+  if (!ctx || n < 1 || width < 1 || nplant < 0 || (nplant > 0 && !plant) || n > INT32_MAX ||
+      !(p_edge >= 0.0 && p_edge <= 1.0))
+    return fail(ctx, RBL_ERR_INVALID, "rbl_gen_matrix_circuit: bad arguments");
+  HIPC(hipSetDevice(ctx->device));
+  free_run(ctx);
+  free_matrix(ctx);
+  const int P = ctx->nranks;
+  ctx->bounds.assign(P + 1, 0);
+  for (int q = 0; q <= P; ++q) ctx->bounds[q] = n * q / P;  // <= 5 nonzeros per row: uniform
+  const int64_t r0 = ctx->bounds[ctx->rank], r1 = ctx->bounds[ctx->rank + 1], m = r1 - r0;
+  ctx->n = n;
+  ctx->r0 = r0;
+  ctx->r1 = r1;
+  ctx->nloc = m;
+  int32_t* d_cnt = nullptr;
+  HIPC(hipMalloc(&d_cnt, std::max<int64_t>(m, 1) * sizeof(int32_t)));
+  circ_count(n, width, p_edge, seed, r0, r1, d_cnt, ctx->stream);
+  HIPC(hipGetLastError());
+  std::vector<int32_t> cnt(m);
+  HIPC(hipMemcpyAsync(cnt.data(), d_cnt, m * sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
+  HIPC(hipStreamSynchronize(ctx->stream));
+  hipFree(d_cnt);
+  std::vector<int64_t> rp(m + 1, 0);
+  for (int64_t i = 0; i < m; ++i) rp[i + 1] = rp[i] + cnt[i];
+  ctx->nnz = rp[m];
+  HIPC(hipMalloc(&ctx->d_rowptr, (m + 1) * sizeof(int64_t)));
+  HIPC(hipMalloc(&ctx->d_col, (ctx->nnz + kCsrPad) * sizeof(int32_t)));
+  HIPC(hipMalloc(&ctx->d_val, (ctx->nnz + kCsrPad) * sizeof(double)));
+  HIPC(hipMemset(ctx->d_col + ctx->nnz, 0, kCsrPad * sizeof(int32_t)));
+  HIPC(hipMemset(ctx->d_val + ctx->nnz, 0, kCsrPad * sizeof(double)));
+  HIPC(hipMemcpy(ctx->d_rowptr, rp.data(), (m + 1) * sizeof(int64_t), hipMemcpyHostToDevice));
+  double* d_plant = nullptr;
+  if (nplant > 0) {
+    HIPC(hipMalloc(&d_plant, nplant * sizeof(double)));
+    HIPC(hipMemcpy(d_plant, plant, nplant * sizeof(double), hipMemcpyHostToDevice));
+  }
+  circ_fill(n, width, p_edge, seed, r0, r1, ctx->d_rowptr, nplant, d_plant, ctx->d_col,
+            ctx->d_val, ctx->stream);
+  HIPC(hipGetLastError());
+  HIPC(hipStreamSynchronize(ctx->stream));
+  hipFree(d_plant);
+  CHK(halo_from_footprint(ctx));
+  CHK(prepare_window(ctx, rp));
+  return setup_halo(ctx);
+}
+
 int rbl_gen_matrix_rmat(rbl_ctx* ctx, int64_t n, int scale, int64_t edges, double a, double b,
                         double c, uint64_t seed, int nplant, const double* plant) {
   if (!ctx || n < 1 || scale < 1 || scale > 31 || ((int64_t)1 << scale) < n || edges < 0 ||
@@ -1661,29 +1782,7 @@ int rbl_gen_matrix_rmat(rbl_ctx* ctx, int64_t n, int scale, int64_t edges, doubl
   ctx->nnz = nnz;
   std::vector<int64_t> rp(m + 1);
   HIPC(hipMemcpy(rp.data(), ctx->d_rowptr, (m + 1) * sizeof(int64_t), hipMemcpyDeviceToHost));
-  ctx->need_lo.assign(P, 0);
-  ctx->need_hi.assign(P, 0);
-  if (P > 1 && nnz > 0) {
-    int64_t* d_b = nullptr;
-    unsigned long long* d_lh = nullptr;
-    HIPC(hipMalloc(&d_b, (P + 1) * sizeof(int64_t)));
-    HIPC(hipMalloc(&d_lh, 2 * P * sizeof(unsigned long long)));
-    std::vector<unsigned long long> lh(2 * P);
-    for (int q = 0; q < P; ++q) { lh[q] = ~0ull; lh[P + q] = 0ull; }
-    HIPC(hipMemcpy(d_b, ctx->bounds.data(), (P + 1) * sizeof(int64_t), hipMemcpyHostToDevice));
-    HIPC(hipMemcpy(d_lh, lh.data(), 2 * P * sizeof(unsigned long long), hipMemcpyHostToDevice));
-    col_footprint(ctx->d_col, nnz, d_b, P, d_lh, d_lh + P, ctx->stream);
-    HIPC(hipGetLastError());
-    HIPC(hipMemcpyAsync(lh.data(), d_lh, 2 * P * sizeof(unsigned long long), hipMemcpyDeviceToHost, ctx->stream));
-    HIPC(hipStreamSynchronize(ctx->stream));
-    hipFree(d_b);
-    hipFree(d_lh);
-    for (int q = 0; q < P; ++q) {
-      if (q == ctx->rank || lh[P + q] == 0ull) continue;
-      ctx->need_lo[q] = (int64_t)lh[q];
-      ctx->need_hi[q] = (int64_t)lh[P + q];
-    }
-  }
+  CHK(halo_from_footprint(ctx));
   CHK(prepare_window(ctx, rp));
   return setup_halo(ctx);
 }
@@ -1808,7 +1907,7 @@ int rbl_start(rbl_ctx* ctx, int b, int max_blocks, int basis_bits, const double*
       // when the SpMM cannot read fp32), one staging block, the Gram slab
       const double work = 2.0 + (ctx->nranks > 1 ? 1.0 : 0.0) +
                           (basis_bits == 32 ? 1.0 + (direct32_ok(ctx, b) ? 0.0 : 1.0) : 0.0);
-      const double other = work * blk64 + blk + (double)(max_blocks + 1) * b * 2 * b * 8.0 * 64;
+      const double other = work * blk64 + blk + 8.0 * (double)gram_slab_elems(ctx, b, max_blocks, basis_bits);
       g = (int)std::max(3.0, std::floor((0.8 * ((double)fr + mine) - other) / blk));
     }
     dev_slots = std::min(dev_slots, std::max(3, g));
@@ -1876,22 +1975,7 @@ int rbl_start(rbl_ctx* ctx, int b, int max_blocks, int basis_bits, const double*
     HIPC(hipMalloc(&ctx->d_qext, std::max<int64_t>(ctx->ext_hi - ctx->ext_lo, 1) * b * sizeof(double)));
     HIPC(hipMemsetAsync(ctx->d_qext, 0, std::max<int64_t>(ctx->ext_hi - ctx->ext_lo, 1) * b * sizeof(double), ctx->stream));
   }
-  // Gram slab: the largest Gram is the partial-reorth one, (max_blocks-1) panels x 2b
-  size_t slab = 0;
-  for (int nW = 1; nW <= std::max(1, max_blocks - 1); ++nW)
-    for (int xc : {b, 2 * b}) {
-      const size_t sp = (size_t)gram_splits(ctx->nloc, nW, b, xc);
-      slab = std::max(slab, sp * nW * b * xc);
-    }
-  slab = std::max(slab, (size_t)2 * rowgram_grid(ctx->nloc, kRowgramMaxPerCu) * b * b);  // rowop partials (+ cross Gram)
-  // the partial-reorth update's local-reorth Gram partials (one b x b per 128-row tile:
-  // n_local b^2 / 128 doubles, a quarter of a block at b = 32)
-  if (b == 32 && basis_bits == 64 && (ctx->fuse & 2)) {
-    const int xg = tsmm44_xg_grid(ctx->nloc);
-    slab = std::max(slab, (size_t)(xg + reduce_scratch_splits(xg)) * b * b);
-  }
-  if (basis_bits == 32)  // fp32 Grams: up to (max_blocks-1) panels x 2b per split
-    slab = std::max(slab, (size_t)gram32_splits(ctx->nloc) * std::max(1, max_blocks - 1) * b * 2 * b);
+  const size_t slab = gram_slab_elems(ctx, b, max_blocks, basis_bits);
   ctx->slab_elems = slab;
   HIPC(hipMalloc(&ctx->d_slab, slab * sizeof(double)));
   ctx->C_elems = (size_t)std::max(1, max_blocks) * b * 2 * b;
@@ -2275,10 +2359,12 @@ int rbl_ritz(rbl_ctx* ctx, int nblocks, int k, const double* S, double* V_out) {
   std::vector<double> srm((size_t)rows * kcp);
   for (int c0 = 0; c0 < k; c0 += kc) {
     const int w = std::min(kc, k - c0);
+    // the previous chunk's copy may still read srm (HIP does not promise a pageable source is
+    // consumed when hipMemcpyAsync returns): wait for it before refilling
+    HIPC(hipStreamSynchronize(ctx->stream));
     // S columns [c0, c0 + w) (column-major, ld = rows) -> row-major rows x kcp, zero-padded
     for (int64_t r = 0; r < rows; ++r)
       for (int c = 0; c < kcp; ++c) srm[(size_t)r * kcp + c] = c < w ? S[(size_t)(c0 + c) * rows + r] : 0.0;
-    HIPC(hipStreamSynchronize(ctx->stream));  // srm is reused by the next chunk
     HIPC(hipMemcpyAsync(d_S.p, srm.data(), rows * kcp * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
     {
       StageScope t(ctx, RBL_STAGE_RITZ);
@@ -2400,6 +2486,15 @@ int rbl_timers(rbl_ctx* ctx, double* ms, int nstages) {
   for (int s = 0; s < nstages && s < RBL_NUM_STAGES; ++s) ms[s] = ctx->stage_ms[s];
   return RBL_OK;
 }
+int rbl_comm_stats(rbl_ctx* ctx, int64_t* out, int nstats, int reset) {
+  if (!ctx || nstats < 0 || (nstats > 0 && !out)) return RBL_ERR_INVALID;
+  for (int i = 0; i < nstats && i < RBL_COMM_NSTATS; ++i) out[i] = ctx->comm_stats[i];
+  for (int i = RBL_COMM_NSTATS; i < nstats; ++i) out[i] = 0;
+  if (reset)
+    for (int64_t& v : ctx->comm_stats) v = 0;
+  return RBL_OK;
+}
+
 int rbl_reset_timers(rbl_ctx* ctx) {
   if (!ctx) return RBL_ERR_INVALID;
   for (double& v : ctx->stage_ms) v = 0.0;

@@ -33,6 +33,53 @@ __host__ __device__ inline double hw_value(uint64_t seed, int64_t lo, int64_t hi
   return (u + u) - 1.0;
 }
 
+// Seeded bijection of [0, n) (the circuit generator's node scatter; oracle/matgen.py
+// scatter_perm): a 4-round Feistel network on 2*half-bit words, 2^(2 half) >= n, cycle-walked
+// back into [0, n) (at most 4 rounds of walking on average: 2^(2 half) < 4n).
+struct Scatter {
+  uint64_t key = 0, mask = 0;
+  int half = 1;
+  int64_t n = 0;
+};
+inline Scatter make_scatter(int64_t n, uint64_t seed) {
+  Scatter s;
+  while ((int64_t(1) << (2 * s.half)) < n) ++s.half;
+  s.mask = (uint64_t(1) << s.half) - 1;
+  s.key = mix64(seed ^ 0xA0761D6478BD642Full);
+  s.n = n;
+  return s;
+}
+__host__ __device__ inline uint64_t feistel_fwd(const Scatter& s, uint64_t x) {
+  uint64_t L = x >> s.half, R = x & s.mask;
+  for (int r = 0; r < 4; ++r) {
+    const uint64_t F = mix64(s.key ^ ((uint64_t)r << 56) ^ R) & s.mask;
+    const uint64_t nl = R;
+    R = L ^ F;
+    L = nl;
+  }
+  return (L << s.half) | R;
+}
+__host__ __device__ inline uint64_t feistel_inv(const Scatter& s, uint64_t x) {
+  uint64_t L = x >> s.half, R = x & s.mask;
+  for (int r = 3; r >= 0; --r) {
+    const uint64_t pr = L;
+    const uint64_t pl = R ^ (mix64(s.key ^ ((uint64_t)r << 56) ^ pr) & s.mask);
+    L = pl;
+    R = pr;
+  }
+  return (L << s.half) | R;
+}
+__host__ __device__ inline int64_t scatter(const Scatter& s, int64_t i) {
+  uint64_t x = (uint64_t)i;
+  do { x = feistel_fwd(s, x); } while (x >= (uint64_t)s.n);
+  return (int64_t)x;
+}
+__host__ __device__ inline int64_t scatter_inv(const Scatter& s, int64_t r) {
+  uint64_t x = (uint64_t)r;
+  do { x = feistel_inv(s, x); } while (x >= (uint64_t)s.n);
+  return (int64_t)x;
+}
+
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
 // ----------------------------------------------------------------------------------------

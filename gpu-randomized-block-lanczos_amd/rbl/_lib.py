@@ -57,6 +57,7 @@ SIGNATURES = {
     "rbl_set_matrix_csr_rows": (C.c_int, [_p, _i64, _i64, _i64, _pi64, _pi64, _pd, C.c_int]),
     "rbl_set_matrix_dense": (C.c_int, [_p, _i64, _i64, _i64, _pd, _i64]),
     "rbl_gen_matrix_hashwindow": (C.c_int, [_p, _i64, _i64, C.c_double, _u64, C.c_int, _pd]),
+    "rbl_gen_matrix_circuit": (C.c_int, [_p, _i64, _i64, C.c_double, _u64, C.c_int, _pd]),
     "rbl_gen_matrix_rmat": (C.c_int, [_p, _i64, C.c_int, _i64, C.c_double, C.c_double, C.c_double,
                                       _u64, C.c_int, _pd]),
     "rbl_matrix_info": (C.c_int, [_p, _pi64, _pi64, _pi64, _pi64]),
@@ -81,6 +82,7 @@ SIGNATURES = {
     "rbl_stage_name": (C.c_char_p, [C.c_int]),
     "rbl_timers": (C.c_int, [_p, _pd, C.c_int]),
     "rbl_reset_timers": (C.c_int, [_p]),
+    "rbl_comm_stats": (C.c_int, [_p, _pi64, C.c_int, C.c_int]),
     "rbl_synchronize": (C.c_int, [_p]),
     "rbl_plan_row_partition": (C.c_int, [_i64, _pi64, C.c_int, _pi64]),
     "rbl_plan_halo": (C.c_int, [_i64, _pi64, _pi64, C.c_int, C.c_int, _pi64, _pi64, _pi64]),

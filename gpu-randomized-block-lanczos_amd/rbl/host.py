@@ -6,7 +6,11 @@ Restates Julia/common.jl:9-65 for the product's host loop:
                       (RBL_gpu.jl:185);
   * ``dsbev``       — LAPACK dsbev(jobz='V', uplo='L') (common.jl:28-48), via SciPy's LAPACK
                       (dsbevd, the same eigenpairs to rounding, from N = 256 on: see below);
-  * ``sort_eig_abs``  (common.jl:50-54) and ``check_convergence`` (common.jl:56-65).
+  * ``sort_eig_abs``  (common.jl:50-54) and ``check_convergence`` (common.jl:56-65);
+  * ``fix_signs``   — not in the reference: each Ritz coefficient column's sign fixed so its
+                      largest-magnitude entry is positive.  An eigenvector's sign is whatever
+                      the LAPACK routine returns (dsbev, dsbevd and the top-k path may differ),
+                      so V = [Q_1..Q_m] S is made deterministic whichever solver ran.
 """
 from __future__ import annotations
 
@@ -121,3 +125,14 @@ def check_convergence(B: np.ndarray, V: np.ndarray, b: int, k: int, tol: float) 
     """common.jl:56-65 — every ||B_{i+1} S[end-b+1:end, l]||_2 <= tol (absolute)."""
     Y = B @ V[V.shape[0] - b:, :k]
     return bool(np.all(np.linalg.norm(Y, axis=0) <= tol))
+
+
+def fix_signs(S: np.ndarray) -> np.ndarray:
+    """Flip each column of S so that its largest-|.| entry (the first, on ties) is positive.
+    V = [Q] S inherits the choice, so the Ritz vectors no longer depend on the eigensolver's
+    sign convention (the reference returns whatever dsbev gives, common.jl:36-48)."""
+    if S.size == 0:
+        return S
+    idx = np.argmax(np.abs(S), axis=0)
+    sgn = np.where(S[idx, np.arange(S.shape[1])] < 0, -1.0, 1.0)
+    return S * sgn

@@ -9,7 +9,10 @@ Semantics follow the GPU reference loop (RBL_gpu.jl:134-203):
   * max Krylov size 1200 (RBL_gpu.jl:211), step i runs while i*b < kryl_sz (:162);
   * partial reorth at even i (:164), local reorth every step (:167);
   * eigensolve + convergence test when i*b > k and i % 4 == 0 (:186-191), absolute 1e-7;
-  * D returned in descending |lambda| (:202), V = [Q_1..Q_m] S in fp64 (RBL.jl:61-71, P3).
+  * D returned in descending |lambda| (:202), V = [Q_1..Q_m] S in fp64 (RBL.jl:61-71, P3);
+    each column of S (so each Ritz vector) signed so its largest coefficient is positive —
+    LAPACK's eigenvector signs are arbitrary and differ between dsbev, dsbevd and the top-k
+    path, so this makes V independent of the host eigensolver (parity is up to sign anyway).
 Non-convergence (the reference's BoundsError) returns the last Ritz pairs
 with ``info.converged = False`` and status RBL_WARN_NOT_CONVERGED.
 """
@@ -24,7 +27,7 @@ import scipy.sparse as sp
 
 from . import _lib
 from ._lib import RBLError, dptr, i32ptr, i64ptr, lib, u8ptr
-from .host import TBand, check_convergence, dsbev, eig_topk, sort_eig_abs
+from .host import TBand, check_convergence, dsbev, eig_topk, fix_signs, sort_eig_abs
 
 KRYL_SZ_GPU = 1200          # RBL_gpu.jl:211
 RESIDUAL_TOL = 1e-7         # RBL_gpu.jl:189
@@ -157,6 +160,15 @@ class Context:
                                             dptr(plant) if plant.size else None),
                     "rbl_gen_matrix_rmat")
 
+    def gen_circuit(self, n: int = 1_585_478, seed: int = 20261015, plant=None,
+                    width: int = 1259, p_edge: float = 0.95873) -> None:
+        """Seeded circuit-like SPD matrix of G3_circuit's shape (BASELINE config 3), generated
+        on the device (rbl_gen_matrix_circuit); the defaults give n and nnz of G3_circuit."""
+        plant = np.ascontiguousarray(plant if plant is not None else np.zeros(0), np.float64)
+        self._check(lib.rbl_gen_matrix_circuit(self._h, n, width, p_edge, seed, plant.size,
+                                               dptr(plant) if plant.size else None),
+                    "rbl_gen_matrix_circuit")
+
     def matrix_info(self):
         v = [np.zeros(1, np.int64) for _ in range(4)]
         self._check(lib.rbl_matrix_info(self._h, *[i64ptr(x) for x in v]), "rbl_matrix_info")
@@ -186,7 +198,9 @@ class Context:
         return self._check(lib.rbl_matrix_format(self._h), "rbl_matrix_format")
 
     def spmm_kernel_for(self, b: int) -> int:
-        """1 = global-gather CSR kernel, 2 = LDS-window CSR kernel."""
+        """The SpMM kernel rbl_step runs at block size b: 1 global-gather CSR, 2 LDS-window CSR,
+        3 LDS-densified band, 4 dense panels, 5 band tiles, 6 segmented gather (the same ids
+        RBL_OPT_SPMM_KERNEL takes)."""
         return self._check(lib.rbl_spmm_kernel_for(self._h, b), "rbl_spmm_kernel_for")
 
     # -- Krylov run -------------------------------------------------------------------------
@@ -274,6 +288,14 @@ class Context:
         buf = C.create_string_buffer(32)
         self._check(lib.rbl_comm_info(self._h, C.byref(n), C.byref(r), buf, 32), "rbl_comm_info")
         return {"nranks": n.value, "rank": r.value, "transport": buf.value.decode()}
+
+    def comm_stats(self, reset: bool = False) -> dict:
+        """Collectives this rank issued since the last reset (rbl_comm_stats): all-reduce
+        calls / bytes, halo exchanges, bytes sent / received."""
+        out = np.zeros(5, np.int64)
+        self._check(lib.rbl_comm_stats(self._h, i64ptr(out), 5, int(reset)), "rbl_comm_stats")
+        return dict(zip(("allreduce_calls", "allreduce_bytes", "exchange_calls", "send_bytes",
+                         "recv_bytes"), (int(x) for x in out)))
 
     def synchronize(self) -> None:
         self._check(lib.rbl_synchronize(self._h), "rbl_synchronize")
@@ -390,7 +412,9 @@ def lanczos(ctx: Context, k: int, b: int, *, kryl_sz: int = KRYL_SZ_GPU, omega=N
     info.iters = i
     info.nblocks = i                               # Q_1..Q_i (length(Q))
     D = D[::-1].copy()
-    S = S[:, ::-1].copy()
+    # each Ritz vector's sign: its coefficient column's largest entry positive (host.fix_signs;
+    # the eigensolvers disagree on signs, the reference returns dsbev's)
+    S = fix_signs(S[:, ::-1])
     info.status = _lib.RBL_OK if info.converged else _lib.RBL_WARN_NOT_CONVERGED
     V = None
     if ritz and S.size:

@@ -63,12 +63,14 @@ extern "C" {
                                    * memory, streamed back over PCIe for partial reorth and
                                    * Ritz.  fp64 or fp32 basis (the reference's buffer is typed
                                    * FLOAT, RBL_gpu.jl:59-81); set before rbl_start.            */
-#define RBL_OPT_SPMM_KERNEL   2   /* 0: auto; 1: global-gather CSR; 2: LDS-window CSR (DPP);
-                                   * 3: LDS-densified band on fp64 MFMA; 4: band-tile format
-                                   * (CSR densified once into MFMA operand order, b = 32,
-                                   * |c - r| <= 64); each falls back 4 -> 3 -> 2 -> 1 when
-                                   * the matrix does not fit the kernel's limits; 5: segmented
-                                   * gather (power-law rows split / packed, b in {16, 32})     */
+#define RBL_OPT_SPMM_KERNEL   2   /* 0: auto; otherwise the kernel id rbl_spmm_kernel_for reports:
+                                   * 1 global-gather CSR; 2 LDS-window CSR (DPP); 3 LDS-densified
+                                   * band on fp64 MFMA; 5 band-tile format (CSR densified once
+                                   * into MFMA operand order, b in {16, 32}, |c - r| <= 64);
+                                   * 6 segmented gather (power-law rows split / packed, b in
+                                   * {16, 32}).  Each falls back 5 -> 3 -> 2 -> 1 when the matrix
+                                   * does not fit the kernel's limits.  4 (dense panels) follows
+                                   * from rbl_set_matrix_dense and is rejected here.           */
 #define RBL_OPT_SPLIT_HALO    4   /* several ranks, band-tile SpMM: 1 (default) the kernel reads
                                    * the own rows from the block and the halo buffer holds only
                                    * the neighbours' rows; 0 the own block is copied into the
@@ -80,16 +82,20 @@ extern "C" {
                                    * (n = 5e7: 60 GB).  Then only b in {16, 32} can run and
                                    * rbl_get_matrix_csr fails.  Set before the matrix.          */
 #define RBL_OPT_FUSE          6   /* pass fusions of the memory-bound b x b stages (b in {16, 32},
-                                   * fp64 basis); bits 0 and 1 give the same results bit for
-                                   * bit, bits 1 and 2 to rounding: bit 0 (default
-                                   * on) CholQR2 in 3 passes over the block instead of 4 (Q1 is
-                                   * recomputed, never stored); bit 1 (default on) the next
-                                   * step's local-reorth Gram Q_i^T Q_{i+1} formed while the QR
-                                   * writes Q_{i+1}, used when that step runs no partial reorth;
-                                   * bit 2 (default on) the local-reorth update
-                                   * Q_i -= Q_{i-1} C applied by the SpMM as it stages Q_i's
-                                   * rows (one rank, band tiles, b = 32; rounding differs from
-                                   * the separate pass at the 1e-16 level, not bit for bit) */
+                                   * fp64 basis; default 7, all on):
+                                   * bit 0: CholQR2 in 3 passes over the block instead of 4 (Q1
+                                   *   recomputed, never stored) — bit for bit the same results;
+                                   * bit 1: the next step's local-reorth Gram Q_i^T Q_{i+1} formed
+                                   *   while the QR writes Q_{i+1} (used when that step runs no
+                                   *   partial reorth), and Q_{i-1}^T Q_i by the last partial-
+                                   *   reorth update — same results to rounding (1e-12);
+                                   * bit 2: the local-reorth update Q_i -= Q_{i-1} C applied by
+                                   *   the band-tile SpMM as it stages Q_i's rows (b = 32) — same
+                                   *   results to rounding.  Works on several ranks: each rank
+                                   *   corrects its first and last H rows (the rows its
+                                   *   neighbours receive) before the halo exchange.  The
+                                   *   several-rank form is tested with in-process ranks on one
+                                   *   GPU; it has no run on several GPUs yet.               */
 
 typedef struct rbl_ctx rbl_ctx;
 
@@ -155,6 +161,16 @@ int rbl_gen_matrix_hashwindow(rbl_ctx* ctx, int64_t n, int64_t halfwidth, double
  * split over the ranks by nonzeros.  NumPy restatement: oracle/matgen.py rmat_csr. */
 int rbl_gen_matrix_rmat(rbl_ctx* ctx, int64_t n, int scale, int64_t edges, double a, double b,
                         double c, uint64_t seed, int nplant, const double* plant);
+/* Device-side generator of a circuit-like SPD matrix of SuiteSparse G3_circuit's shape
+ * (BASELINE config 3; the real file is not shipped): a weighted graph Laplacian on a 5-point
+ * stencil over rows of `width` nodes, each edge (lo,hi) kept iff hash(seed,lo,hi) < p_edge,
+ * weight 0.5 + uniform[0,1) from the same hash; diagonal 0.01 + the kept weights (+ plant[l]
+ * at node l*floor(n/nplant)); node i is scattered to row/column scatter(i), a seeded Feistel
+ * bijection of [0,n), so the pattern has no band (the gather SpMM runs).  n = 1,585,478,
+ * width 1259, p_edge 0.95873 give G3_circuit's 7.66 M nonzeros.  Rows split uniformly over
+ * the ranks.  NumPy restatement: oracle/matgen.py circuit_like_csr. */
+int rbl_gen_matrix_circuit(rbl_ctx* ctx, int64_t n, int64_t width, double p_edge, uint64_t seed,
+                           int nplant, const double* plant);
 int rbl_matrix_info(rbl_ctx* ctx, int64_t* n, int64_t* row_begin, int64_t* row_end,
                     int64_t* nnz_local);
 /* Download the local CSR (0-based) — test/inspection only. */
@@ -179,7 +195,7 @@ int rbl_matrix_format(rbl_ctx* ctx);
  * and the buffer planning of RBL_gpu.jl:95-104 (the whole basis lives in HBM).
  * `omega` is the local n_local x b column-major start block, or NULL for a device
  * counter-based N(0,1) draw from `seed`.  basis_bits: 64 (fp64 basis) or 32 (the mixed
- * mode of RBL_gpu.jl with FLOAT = Float32, b in {16, 32}: Krylov blocks and their partial /
+ * mode of RBL_gpu.jl with FLOAT = Float32, any b: Krylov blocks and their partial /
  * local reorthogonalisation in fp32 on fp32 MFMA; A Q, the 3-term update, QR, A_i, B_i and
  * the Ritz projection in fp64 from the widened blocks). */
 int rbl_start(rbl_ctx* ctx, int b, int max_blocks, int basis_bits, const double* omega,
@@ -239,6 +255,18 @@ int rbl_reset_timers(rbl_ctx* ctx);
  * "qr", "part reorth", "loc reorth", "Ritz vectors") plus "comm" (halo + all-reduce).
  * rbl_synchronize waits for the context's stream and folds finished events into them. */
 int rbl_synchronize(rbl_ctx* ctx);
+
+/* Collectives this rank issued since the last reset (no reference equivalent: the reference is
+ * single-GPU).  out[RBL_COMM_*] for the first nstats counters; reset != 0 zeroes them after the
+ * read.  All-reduces are the b x b / (m b) x 2b Gram sums; exchanges the grouped halo
+ * send/recv of Q rows before each SpMM (one rank: all zero). */
+#define RBL_COMM_ALLREDUCE_CALLS 0
+#define RBL_COMM_ALLREDUCE_BYTES 1
+#define RBL_COMM_EXCHANGE_CALLS  2
+#define RBL_COMM_SEND_BYTES      3
+#define RBL_COMM_RECV_BYTES      4
+#define RBL_COMM_NSTATS          5
+int rbl_comm_stats(rbl_ctx* ctx, int64_t* out, int nstats, int reset);
 
 /* ---- host-only planning (callable without a GPU) -------------------------------------- */
 /* nnz-balanced contiguous row partition: bounds_out[0..nranks] (bounds_out[0]=0). */

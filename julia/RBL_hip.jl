@@ -1,21 +1,33 @@
 # RBL_hip.jl — drop-in for `RBL_gpu(A, k, b)` (Julia/RBL_gpu.jl:205-221) on AMD MI355X.
 #
-# A maintainer adds this file next to Julia/common.jl in the reference repository.  The
-# host keeps the reference's block-tridiagonal assembly and eigensolve (insertA!, insertB!,
-# dsbev, sort_eig_abs, check_convergence from common.jl:9-65); the device work of every
-# block step (RBL_gpu.jl:164-184) is one `ccall` into librbl_hip.so (include/rbl_hip.h).
-#
-# Untested here: Julia is not installed in the build container (SURVEY §8(c)).  The same
-# loop, in Python over ctypes, is gpu-randomized-block-lanczos_amd/rbl/rbl_gpu.py:lanczos and
-# is what the parity tests run.
+# A maintainer adds this file next to Julia/common.jl in the reference repository and
+# includes it instead of RBL_gpu.jl.  The host keeps the reference's block-tridiagonal
+# assembly and eigensolve (insertA!, insertB!, dsbev, sort_eig_abs, check_convergence from
+# common.jl:9-65); the device work of every block step (RBL_gpu.jl:164-184) is one `ccall`
+# into librbl_hip.so (include/rbl_hip.h).
 #
 #   include("common.jl"); include("RBL_hip.jl")
-#   D, V = RBL_hip(A, k, b)              # A::SparseMatrixCSC{Float64,Int64} or Matrix{Float64}
-#   D, V = RBL_hip(A, k, b; basis_bits = 32)   # FLOAT = Float32 mode (common.jl:5)
-#   D, V = RBL_hip(A, k, b; device_blocks = -1)  # hybrid buffer: what fits in HBM, rest on host
+#   to = TimerOutput()                   # the caller's global, as benchmark.jl:56 / test.jl:7
+#   D, V = RBL_gpu(A, k, b)              # the reference's own signature and return values
+#   show(to)                             # "AQ", "3-term", "qr", "part reorth", "loc reorth",
+#                                        # "eig", "Ritz vectors" as RBL_gpu.jl:152-219 records
+#   D, V = RBL_hip(A, k, b; basis_bits = 32)      # FLOAT = Float32 mode (common.jl:5)
+#   D, V = RBL_hip(A, k, b; device_blocks = -1)   # hybrid buffer: what fits in HBM, rest on host
 #   D, V = RBL_hip_restarted(A, k)       # restarted.jl:106 (RBL_gpu_restarted)
+#
+# Untested here: Julia is not installed in the build container (SURVEY §8(c)).  Every ccall
+# below is checked against include/rbl_hip.h by tests/test_julia_binding.py (argument count
+# and types), and the loop is the one gpu-randomized-block-lanczos_amd/rbl/rbl_gpu.py:lanczos
+# runs in the parity tests and the benchmark: steps are enqueued with rbl_step_async and their
+# A_i / B_{i+1} fetched with rbl_fetch only where the host needs the T band (a convergence check,
+# RBL_gpu.jl:186, or the last step), so the GPU never waits for the host between steps.
 
 const librbl_hip = get(ENV, "RBL_HIP_LIB", "librbl_hip.so")
+
+# rbl_hip.h option ids
+const RBL_OPT_TIMERS = Cint(0)
+const RBL_OPT_DEVICE_BLOCKS = Cint(3)
+const RBL_WARN_QR_SHIFTED = Cint(2)
 
 struct RblError <: Exception
     code::Cint
@@ -30,12 +42,19 @@ function rbl_check(ctx::Ptr{Cvoid}, st::Cint, what::String)
     return st
 end
 
-# Ag = adapt(CuArray, A) (RBL_gpu.jl:209): Julia's 1-based CSC arrays as-is, or the dense
-# column-major matrix (RBL_gpu(A::Matrix{Float64})) as-is
-set_matrix!(ctx, A::SparseMatrixCSC{Float64,Int64}) =
+# Ag = adapt(CuArray, A) (RBL_gpu.jl:209).  librbl_hip takes CSR arrays; a symmetric A's CSC
+# arrays are its CSR arrays (passed as-is, 1-based), any other A is transposed first so the
+# device multiplies by A itself, as cuSPARSE does (benchmark.jl:58 passes an unsymmetric
+# sprandn).  A dense A (RBL_gpu(A::Matrix{Float64})) goes over column-major as-is.
+function set_matrix!(ctx, A::SparseMatrixCSC{Float64})
+    C = issymmetric(A) ? A : SparseMatrixCSC(transpose(A))
+    colptr = Vector{Int64}(C.colptr)
+    rowval = Vector{Int64}(C.rowval)
     rbl_check(ctx, ccall((:rbl_set_matrix_csc, librbl_hip), Cint,
                          (Ptr{Cvoid}, Int64, Int64, Ptr{Int64}, Ptr{Int64}, Ptr{Float64}, Cint),
-                         ctx, size(A, 2), nnz(A), A.colptr, A.rowval, A.nzval, 1), "rbl_set_matrix_csc")
+                         ctx, size(C, 2), nnz(C), colptr, rowval, C.nzval, Cint(1)),
+              "rbl_set_matrix_csc")
+end
 set_matrix!(ctx, A::Matrix{Float64}) =
     rbl_check(ctx, ccall((:rbl_set_matrix_dense, librbl_hip), Cint,
                          (Ptr{Cvoid}, Int64, Int64, Int64, Ptr{Float64}, Int64),
@@ -43,70 +62,145 @@ set_matrix!(ctx, A::Matrix{Float64}) =
 
 function rbl_context(device::Int)
     hr = Ref{Ptr{Cvoid}}(C_NULL)
-    st = ccall((:rbl_create, librbl_hip), Cint, (Ref{Ptr{Cvoid}}, Cint), hr, device)
+    st = ccall((:rbl_create, librbl_hip), Cint, (Ref{Ptr{Cvoid}}, Cint), hr, Cint(device))
     rbl_check(hr[], st, "rbl_create")
     return hr[]
 end
 
-function RBL_hip(A::Union{SparseMatrixCSC{Float64,Int64},Matrix{Float64}}, k::Int64, b::Int64;
+# The device stage times (hipEvents, ms) folded into the caller's TimerOutput under the
+# reference's labels (RBL_gpu.jl:152-187, 219), one call per label per run.  TimerOutputs has
+# no public call to add an externally measured time, so this writes the section's
+# accumulated data; if that internal layout ever changes, the times are printed instead.
+function fold_device_timers!(to, ctx::Ptr{Cvoid})
+    ns = ccall((:rbl_num_stages, librbl_hip), Cint, ())
+    ms = zeros(Float64, ns)
+    rbl_check(ctx, ccall((:rbl_timers, librbl_hip), Cint, (Ptr{Cvoid}, Ptr{Float64}, Cint),
+                         ctx, ms, ns), "rbl_timers")
+    for s in 0:ns-1
+        ms[s+1] > 0 || continue
+        label = unsafe_string(ccall((:rbl_stage_name, librbl_hip), Cstring, (Cint,), Cint(s)))
+        try
+            node = get!(to.inner_timers, label) do
+                TimerOutputs.TimerOutput(label)
+            end
+            node.accumulated_data.time += round(Int64, ms[s+1] * 1e6)   # ns
+            node.accumulated_data.ncalls += 1
+        catch
+            @info "RBL_gpu device time" label ms = ms[s+1]
+        end
+    end
+end
+
+function RBL_hip(A::Union{SparseMatrixCSC{Float64},Matrix{Float64}}, k::Int64, b::Int64;
                  device::Int = 0, seed::UInt64 = rand(UInt64), kryl_sz::Int64 = 1200,
-                 basis_bits::Int = 64, device_blocks::Int = 0)
+                 basis_bits::Int = (FLOAT == Float32 ? 32 : 64), device_blocks::Int = 0,
+                 timer = nothing)
     n = size(A, 2)
     ctx = rbl_context(device)
     try
         set_matrix!(ctx, A)
-        # RBL_OPT_DEVICE_BLOCKS = 3: the hybrid GPU/host Krylov buffer (RBL_gpu.jl:24-27, 59-81)
+        # RBL_OPT_DEVICE_BLOCKS: the hybrid GPU/host Krylov buffer (RBL_gpu.jl:24-27, 59-81)
         rbl_check(ctx, ccall((:rbl_set_option, librbl_hip), Cint, (Ptr{Cvoid}, Cint, Int64),
-                             ctx, 3, device_blocks), "rbl_set_option")
+                             ctx, RBL_OPT_DEVICE_BLOCKS, device_blocks), "rbl_set_option")
+        rbl_check(ctx, ccall((:rbl_set_option, librbl_hip), Cint, (Ptr{Cvoid}, Cint, Int64),
+                             ctx, RBL_OPT_TIMERS, timer === nothing ? 0 : 1), "rbl_set_option")
         # Qg_d = qr(Ag * randn(n, b)).Q (RBL_gpu.jl:213-214); the basis lives in HBM
         m_max = cld(kryl_sz, b)
         rbl_check(ctx, ccall((:rbl_start, librbl_hip), Cint,
                              (Ptr{Cvoid}, Cint, Cint, Cint, Ptr{Float64}, UInt64),
-                             ctx, b, m_max, basis_bits, C_NULL, seed), "rbl_start")
-        Ai = zeros(Float64, b, b)
-        Bi = zeros(Float64, b, b)
-        step!(i, part) = rbl_check(ctx, ccall((:rbl_step, librbl_hip), Cint,
-                                              (Ptr{Cvoid}, Cint, Cint, Ptr{Float64}, Ptr{Float64}),
-                                              ctx, i, part, Ai, Bi), "rbl_step")
-        # first loop (RBL_gpu.jl:149-161)
-        step!(1, 0)
-        T = insertA!(copy(Ai), b)
-        insertB!(copy(Bi), T, b, 1)
+                             ctx, Cint(b), Cint(m_max), Cint(basis_bits), C_NULL, seed), "rbl_start")
+        enqueued = 0
+        function enqueue!(upto)
+            while enqueued < upto
+                enqueued += 1
+                part = (enqueued >= 2 && mod(enqueued, 2) == 0) ? 1 : 0   # RBL_gpu.jl:164
+                rbl_check(ctx, ccall((:rbl_step_async, librbl_hip), Cint, (Ptr{Cvoid}, Cint, Cint),
+                                     ctx, Cint(enqueued), Cint(part)), "rbl_step_async")
+            end
+        end
+        # A_j, B_{j+1} of steps i0..i1-1, column-major b x b each
+        function fetch!(i0, i1)
+            m = i1 - i0
+            Ah = zeros(Float64, b, b, m)
+            Bh = zeros(Float64, b, b, m)
+            sts = zeros(Cint, m)
+            rbl_check(ctx, ccall((:rbl_fetch, librbl_hip), Cint,
+                                 (Ptr{Cvoid}, Cint, Cint, Ptr{Float64}, Ptr{Float64}, Ptr{Cint}),
+                                 ctx, Cint(i0), Cint(i1), Ah, Bh, sts), "rbl_fetch")
+            return Ah, Bh
+        end
+        T = zeros(Float64, b + 1, 0)
         D = zeros(Float64)
         V = zeros(Float64)
         converged = false
-        i = 1
-        while i * b < kryl_sz                                   # RBL_gpu.jl:162
-            i += 1
-            step!(i, mod(i, 2) == 0 ? 1 : 0)                    # :164-184
-            T = [T insertA!(copy(Ai), b)]                       # :185
-            if (i * b > k) && (mod(i, 4) == 0)                  # :186
-                D, V = dsbev('V', 'L', T)                       # :187
-                D, V = sort_eig_abs(D, V, k)                    # :188
-                if check_convergence(copy(Bi), V, b, k, 1e-7)   # :189
-                    converged = true
-                    break
+        first = 1
+        i = 0
+        while true
+            i += 1                                                 # step 1: :149-161; then :162
+            is_check = i >= 2 && (i * b > k) && (mod(i, 4) == 0)   # :186
+            is_last = !(i * b < kryl_sz && i < m_max)              # :162
+            (is_check || is_last) || continue
+            enqueue!(i)
+            Ah, Bh = fetch!(first, i + 1)
+            for (jj, j) in enumerate(first:i)
+                Ai = Ah[:, :, jj]
+                Bi = Bh[:, :, jj]
+                T = j == 1 ? insertA!(Ai, b) : [T insertA!(Ai, b)]  # :160, :185
+                if j == i && is_check
+                    if timer === nothing
+                        D, V = dsbev('V', 'L', T)                    # :187
+                    else
+                        @timeit timer "eig" D, V = dsbev('V', 'L', T)
+                    end
+                    D, V = sort_eig_abs(D, V, k)                    # :188
+                    if check_convergence(Bi, V, b, k, 1e-7)         # :189
+                        converged = true
+                        break
+                    end
                 end
+                insertB!(Bi, T, b, j)                               # :161, :193
             end
-            insertB!(copy(Bi), T, b, i)                         # :193
+            first = i + 1
+            (converged || is_last) && break
         end
         if ndims(D) == 0
             # P6: no eigensolve ran; the reference would fail in recover_eigvec
-            throw(RblError(1, "RBL_hip: no Ritz values (loop ended before the first check)"))
+            throw(RblError(1, "RBL_gpu: no Ritz values (loop ended before the first check)"))
         end
-        converged || @warn "RBL_hip: not converged within kryl_sz=$kryl_sz (best effort)"
-        D = D[end:-1:1]                                         # :202
+        converged || @warn "RBL_gpu: not converged within kryl_sz=$kryl_sz (best effort)"
+        println("Iterations: $i and kryl_sz: $(i * b)")            # :195
+        D = D[end:-1:1]                                             # :202
         S = Matrix{Float64}(V[:, end:-1:1])
+        # each Ritz vector's sign: its largest coefficient positive (as the Python host,
+        # rbl/host.py fix_signs), so V does not depend on LAPACK's sign choice
+        for c in 1:size(S, 2)
+            p = argmax(abs.(S[:, c]))
+            S[p, c] < 0 && (S[:, c] .*= -1)
+        end
         nblocks = size(S, 1) ÷ b
         Vout = zeros(Float64, n, k)
         # recover_eigvec (RBL_gpu.jl:219, :106-132) in fp64 on the device
         rbl_check(ctx, ccall((:rbl_ritz, librbl_hip), Cint,
                              (Ptr{Cvoid}, Cint, Cint, Ptr{Float64}, Ptr{Float64}),
-                             ctx, nblocks, k, S, Vout), "rbl_ritz")
+                             ctx, Cint(nblocks), Cint(k), S, Vout), "rbl_ritz")
+        if timer !== nothing
+            rbl_check(ctx, ccall((:rbl_synchronize, librbl_hip), Cint, (Ptr{Cvoid},), ctx),
+                      "rbl_synchronize")
+            fold_device_timers!(timer, ctx)
+        end
         return D, Vout
     finally
         ccall((:rbl_free, librbl_hip), Cint, (Ptr{Cvoid},), ctx)
     end
+end
+
+# The reference's entry point, same signature and results (RBL_gpu.jl:205-221): D, the k
+# largest-|lambda| eigenvalues in descending |lambda|, and V (n x k, columns aligned with D).
+# Like the reference it records its stages in the caller's global `to` (test.jl:7,
+# benchmark.jl:56) when one is defined.
+function RBL_gpu(A::Union{SparseMatrixCSC{DOUBLE},Matrix{DOUBLE}}, k::Int64, b::Int64)
+    timer = isdefined(Main, :to) ? Main.to : nothing
+    return RBL_hip(A, k, b; timer = timer)
 end
 
 # restarted.jl:106-146 (RBL_gpu_restarted): b = 1 cycles with locking.  The cycle
@@ -114,7 +208,7 @@ end
 # locked reorth), rbl_reorth_last, then dsbev on the host; locked vectors and the restart
 # block stay on the device (rbl_lock / rbl_restart).  V: the locked Ritz vectors (the
 # reference returns zeros(n, k)).
-function RBL_hip_restarted(A::Union{SparseMatrixCSC{Float64,Int64},Matrix{Float64}}, k::Int64;
+function RBL_hip_restarted(A::Union{SparseMatrixCSC{Float64},Matrix{Float64}}, k::Int64;
                            device::Int = 0, seed::UInt64 = rand(UInt64), kryl0::Int64 = 100,
                            max_cycles::Int64 = 60)
     n = size(A, 2)
@@ -124,12 +218,13 @@ function RBL_hip_restarted(A::Union{SparseMatrixCSC{Float64,Int64},Matrix{Float6
         set_matrix!(ctx, A)
         rbl_check(ctx, ccall((:rbl_start, librbl_hip), Cint,
                              (Ptr{Cvoid}, Cint, Cint, Cint, Ptr{Float64}, UInt64),
-                             ctx, b, kryl0 + 10 * max_cycles, 64, C_NULL, seed), "rbl_start")
+                             ctx, Cint(b), Cint(kryl0 + 10 * max_cycles), Cint(64), C_NULL, seed),
+                  "rbl_start")
         Ai = zeros(Float64, b, b)
         Bi = zeros(Float64, b, b)
         step!(i, flags) = rbl_check(ctx, ccall((:rbl_step, librbl_hip), Cint,
                                                (Ptr{Cvoid}, Cint, Cint, Ptr{Float64}, Ptr{Float64}),
-                                               ctx, i, flags, Ai, Bi), "rbl_step")
+                                               ctx, Cint(i), Cint(flags), Ai, Bi), "rbl_step")
         D = Float64[]
         count = 0
         kryl = kryl0
@@ -147,7 +242,7 @@ function RBL_hip_restarted(A::Union{SparseMatrixCSC{Float64,Int64},Matrix{Float6
             end
             m = i - 1
             rbl_check(ctx, ccall((:rbl_reorth_last, librbl_hip), Cint, (Ptr{Cvoid}, Cint, Cint),
-                                 ctx, m, 3), "rbl_reorth_last")  # :100-102
+                                 ctx, Cint(m), Cint(3)), "rbl_reorth_last")  # :100-102
             d, v = dsbev('V', 'L', T)                            # :103
             conv = Bi * v[end-b+1:end, end:-1:1]                 # :104
             d = d[end:-1:1]
@@ -160,7 +255,8 @@ function RBL_hip_restarted(A::Union{SparseMatrixCSC{Float64,Int64},Matrix{Float6
                     ncomp += 1
                     s = Matrix{Float64}(v[:, j:j])
                     rbl_check(ctx, ccall((:rbl_lock, librbl_hip), Cint,
-                                         (Ptr{Cvoid}, Cint, Cint, Ptr{Float64}), ctx, m, 1, s), "rbl_lock")
+                                         (Ptr{Cvoid}, Cint, Cint, Ptr{Float64}),
+                                         ctx, Cint(m), Cint(1), s), "rbl_lock")
                     push!(D, d[j])
                 else
                     restart = Matrix{Float64}(v[:, j:j])
@@ -171,7 +267,7 @@ function RBL_hip_restarted(A::Union{SparseMatrixCSC{Float64,Int64},Matrix{Float6
                 restart = zeros(Float64, m * b, b); restart[1, 1] = 1.0
             end
             rbl_check(ctx, ccall((:rbl_restart, librbl_hip), Cint, (Ptr{Cvoid}, Cint, Ptr{Float64}),
-                                 ctx, m, restart), "rbl_restart")
+                                 ctx, Cint(m), restart), "rbl_restart")
             kryl += 10
             count += ncomp
             cycles += 1

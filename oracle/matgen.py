@@ -120,6 +120,42 @@ def planted_spectrum(k: int, scale: float = 100.0):
 
 
 _CIRC_K = np.uint64(0x9FB21C651E98DF25)
+_SCATTER_K = np.uint64(0xA0761D6478BD642F)
+
+
+def _feistel_half(n: int) -> int:
+    h = 1
+    while (1 << (2 * h)) < n:
+        h += 1
+    return h
+
+
+def _feistel(x, key, half, inverse=False):
+    """4-round Feistel network on 2*half-bit words (rbl_common.hpp scatter_round)."""
+    mask = np.uint64((1 << half) - 1)
+    L = x >> np.uint64(half)
+    R = x & mask
+    rounds = range(3, -1, -1) if inverse else range(4)
+    for r in rounds:
+        rk = key ^ (np.uint64(r) << np.uint64(56))
+        if inverse:
+            L, R = R ^ (mix64(rk ^ L) & mask), L
+        else:
+            L, R = R, L ^ (mix64(rk ^ R) & mask)
+    return (L << np.uint64(half)) | R
+
+
+def scatter_perm(n: int, seed: int, idx, inverse=False):
+    """Seeded bijection of [0, n) (gen.hip scatter / scatter_inv): the Feistel network above on
+    the smallest even bit width covering n, cycle-walked back into [0, n)."""
+    half = _feistel_half(n)
+    key = mix64(np.uint64(seed) ^ _SCATTER_K)
+    x = np.asarray(idx, dtype=np.uint64).copy()
+    todo = np.ones(x.shape, bool)
+    while todo.any():
+        x[todo] = _feistel(x[todo], key, half, inverse)
+        todo = x >= np.uint64(n)
+    return x.astype(np.int64)
 G3_CIRCUIT_N = 1_585_478          # SuiteSparse G3_circuit (BASELINE config 3): n
 G3_CIRCUIT_NNZ = 7_660_826        #   and stored nonzeros, both triangles (4.83 per row)
 
@@ -131,8 +167,10 @@ def circuit_like_csr(n: int = G3_CIRCUIT_N, seed: int = 20261015, plant=None, wi
     rows of `width` nodes (nodes i, i+1 in one row; i, i+width), each edge kept iff
     u53(h(seed, lo, hi)) < p_edge (so ~4.83 nonzeros per row at the defaults, like
     G3_circuit's 7.66 M over 1.59 M rows), weight 0.5 + u53(mix64(h ^ K)); diagonal = the row's
-    weight sum + 0.01 (+ plant[l] at node l * floor(n / len(plant))).  Then a seeded symmetric
-    permutation scatters the pattern over the whole index range, as circuit matrices are: no
+    weight sum + 0.01 (+ plant[l] at node l * floor(n / len(plant))), summed in the order
+    0.01, right, down, left, up neighbour.  Then a seeded symmetric permutation (scatter_perm:
+    a Feistel bijection, so the device generator rbl_gen_matrix_circuit builds the same bits
+    row by row) scatters the pattern over the whole index range, as circuit matrices are: no
     band, so the gather SpMM runs, not the band tiles.  Returns SciPy CSR (n x n)."""
     i = np.arange(n, dtype=np.int64)
     lo_h = i[(i % width) != width - 1]
@@ -151,8 +189,9 @@ def circuit_like_csr(n: int = G3_CIRCUIT_N, seed: int = 20261015, plant=None, wi
         plant = np.asarray(plant, dtype=np.float64)
         stride = n // len(plant)
         diag[np.arange(len(plant)) * stride] += plant
-    # seeded symmetric permutation (node i -> perm[i])
-    perm = np.random.default_rng(seed).permutation(n).astype(np.int64)
+    # seeded symmetric permutation (node i -> perm[i]): a hash bijection the device generator
+    # (gen.hip k_circ_fill) computes per row
+    perm = scatter_perm(n, seed, np.arange(n, dtype=np.int64))
     R = np.concatenate([perm[lo], perm[hi], perm])
     C = np.concatenate([perm[hi], perm[lo], perm])
     V = np.concatenate([-w, -w, diag])

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Full-size eigenvalue fixtures for BASELINE configs 2 and 3 (committed; regenerate from the
-repo root with ``python tests/golden/make_fullsize.py [c2|c3]``; ~2-10 min each on 8 cores).
+repo root with ``python tests/golden/make_fullsize.py [c2|c3|c4b]``; ~2-10 min each on 8 cores).
 
 The expected outputs come from the oracle (oracle/rbl_oracle.py: the CPU restatement of
 RBL.jl:74-142 with the GPU driver's bounds, RBL_gpu.jl:134-219, and the HIP path's choices —
@@ -13,6 +13,12 @@ Fixtures are data only: the generator parameters, Omega's seed, and the outputs.
                  SuiteSparse G3_circuit (BASELINE config 3; the real file is not in this image
                  and is not fetched), SPD weighted Laplacian, scattered by a symmetric
                  permutation (no band), planted top spectrum; b = 16, k = 20.
+
+  golden_c4b.npz BASELINE config 4's R-MAT pattern at n = 1e6: matgen.rmat_csr with
+                 (a,b,c,d) = (0.57,0.19,0.19,0.05), scale 20, 0.66 n x 100 draws (the bench's
+                 C4b draw density: ~100 nnz/row after symmetrising and merging; hub rows of
+                 ~1e5 nonzeros, so the segmented gather splits them), planted top spectrum;
+                 b = 32, k = 20.  The device generator (gen_rmat.hip) builds the same bits.
 
 Each holds D (k, descending |lambda|), the iteration count, and per Ritz vector its 16
 largest-magnitude entries (row ids + values) — enough to compare vectors up to sign without
@@ -33,6 +39,7 @@ from oracle import rbl_oracle as o  # noqa: E402
 
 C2 = dict(n=1_000_000, halfwidth=32, density=0.7734, seed=20261015, b=16, k=20, omega_seed=2)
 C3 = dict(n=matgen.G3_CIRCUIT_N, seed=20261015, b=16, k=20, omega_seed=3)
+C4B = dict(n=1_000_000, scale=20, edges=66_000_000, seed=20261015, b=32, k=20, omega_seed=4)
 TOP = 16
 
 
@@ -43,6 +50,11 @@ def c2_matrix():
 
 def c3_matrix():
     return matgen.circuit_like_csr(C3["n"], C3["seed"], matgen.planted_spectrum(C3["k"]))
+
+
+def c4b_matrix():
+    return matgen.rmat_csr(C4B["n"], C4B["scale"], C4B["edges"], C4B["seed"],
+                           matgen.planted_spectrum(C4B["k"]))
 
 
 def omega_for(cfg):
@@ -72,7 +84,9 @@ def main(which):
         run("c2", C2, c2_matrix())
     if "c3" in which:
         run("c3", C3, c3_matrix())
+    if "c4b" in which:
+        run("c4b", C4B, c4b_matrix())
 
 
 if __name__ == "__main__":
-    main(sys.argv[1:] or ["c2", "c3"])
+    main(sys.argv[1:] or ["c2", "c3", "c4b"])

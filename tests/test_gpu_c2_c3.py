@@ -8,7 +8,11 @@ GPU driver's bounds — ran at these sizes in the build container):
     Laplacian with no band (the segmented-gather SpMM runs) — written to a Matrix Market file
     and read back through rbl.io.load_matrix (the reference's `mmread` path,
     Julia/benchmark.jl:21-28) before RBL_gpu runs on it.  The real G3_circuit runs too when a
-    copy is staged at $RBL_G3_CIRCUIT (never fetched): residual properties only.
+    copy is staged at $RBL_G3_CIRCUIT (never fetched): residual properties only;
+  * C4b at n = 1e6: BASELINE config 4's R-MAT pattern (scale 20, the bench's draw density,
+    ~115 nnz/row, hub rows of ~1e5 nonzeros that the segmented gather cuts into segments),
+    generated on the device (bit-exact with the oracle's matgen.rmat_csr,
+    test_gpu_rmat::test_rmat_generator_bit_exact), b = 32, k = 20.
 
 Tolerances: eigenvalues |dlambda| / |lambda| < 1e-10 (north star); the same
 number of block steps to convergence; each Ritz vector's 16 largest entries within 1e-6 of the
@@ -105,3 +109,36 @@ def test_real_g3_circuit_if_staged(rbl):
     if info.converged:
         assert _residual(A, D, V).max() < RES_TOL
     assert np.all(np.diff(np.abs(D)) <= 0)
+
+
+def test_c4b_rmat_1e6_vs_oracle(rbl):
+    """BASELINE config 4's pattern at n = 1e6 against the oracle's full run (golden_c4b.npz):
+    the segmented-gather SpMM with hub rows split into segments (k_seg_fixup), b = 32."""
+    import scipy.sparse as sp
+    g, cfg = _fixture("c4b")
+    k, b = cfg["k"], cfg["b"]
+    with rbl.Context(0) as ctx:
+        ctx.gen_rmat(cfg["n"], cfg["scale"], cfg["edges"], cfg["seed"], matgen.planted_spectrum(k))
+        assert ctx.matrix_info()[3] == int(g["nnz"])
+        assert ctx.spmm_kernel_for(b) == 6
+        rp, col, val = ctx.get_matrix_csr()
+        assert np.diff(rp).max() > 4 * 4096          # hub rows: several segments each
+        D, V, info = rbl.lanczos(ctx, k, b, omega=_omega(cfg))
+    assert info.converged
+    _compare(g, D, V, info.iters)
+    A = sp.csr_matrix((val, col, rp), shape=(cfg["n"], cfg["n"]))
+    assert _residual(A, D, V).max() < RES_TOL
+
+
+def test_c3_device_generator_vs_oracle(rbl):
+    """The C3 shape generated on the device (rbl_gen_matrix_circuit, bit-exact with the oracle's
+    matgen.circuit_like_csr: test_gpu_circuit.py) gives the oracle fixture's eigenpairs: the
+    bench's `c3_circuit` workload."""
+    g, cfg = _fixture("c3")
+    k, b = cfg["k"], cfg["b"]
+    with rbl.Context(0) as ctx:
+        ctx.gen_circuit(cfg["n"], cfg["seed"], matgen.planted_spectrum(k))
+        assert ctx.matrix_info()[3] == int(g["nnz"])
+        D, V, info = rbl.lanczos(ctx, k, b, omega=_omega(cfg))
+    assert info.converged
+    _compare(g, D, V, info.iters)

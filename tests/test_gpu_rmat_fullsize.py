@@ -1,0 +1,109 @@
+"""GPU: BASELINE config 4 at full size (C4b: R-MAT scale 24, n = 1e7, ~1e9 nonzeros, b = 32,
+k = 20 — the bench's `c4b_rmat` workload), checked through size-independent properties, since
+the oracle cannot run at this size in a test (it ran at n = 1e6: test_gpu_c2_c3.py
+test_c4b_rmat_1e6_vs_oracle):
+
+  * SpMM (`rbl_apply`: the segmented gather + long-row fixup the bench runs) on sampled rows
+    against SciPy's product of the same CSR rows downloaded from the device: the 64 highest-
+    degree rows (hubs of up to ~1e6 nonzeros, cut into 4,096-nonzero segments whose partial rows
+    k_seg_fixup sums), 32 windows of 256 rows spread over [0, n) (packed short-row tasks), and
+    the last rows; every element within 1e-13 * (|A| |X|) (the kernel only reorders the fp64
+    sums; same bound as test_gpu_spmm);
+  * linearity of the SpMM: A (X1 + 2 X2) = A X1 + 2 A X2 within 3x that bound;
+  * RBL_gpu to convergence (RBL_gpu.jl:134-219 semantics): every Ritz pair's residual
+    ||A v - lambda v|| / |lambda| < 1e-7 (A v by SciPy over all 1e9 nonzeros), Ritz vectors
+    orthonormal (|V^T V - I| < 1e-9), Rayleigh quotients equal to lambda within 1e-10
+    relative, D sorted by descending |lambda| (P11).
+
+Host memory: ~12 GB for the downloaded CSR, ~8 GB of n x 32 blocks; device: the context's
+~125 GB (basis of 39 fp64 blocks + matrix)."""
+import time
+
+import numpy as np
+import pytest
+import scipy.sparse as sp
+
+pytestmark = pytest.mark.gpu
+
+N, SCALE, EDGES, SEED, B, K = 10_000_000, 24, 660_000_000, 20261015, 32, 20
+T0 = time.perf_counter()
+SPMM_TOL = 1e-13
+RES_TOL = 1e-7
+ORTH_TOL = 1e-9
+RAYLEIGH_TOL = 1e-10
+SEG_LEN = 4096          # kernels.hpp kSegLen: nonzeros per long-row segment
+
+
+def _log(msg):
+    print(f"[c4b fullsize] {msg} {time.perf_counter() - T0:.1f} s", flush=True)
+
+
+@pytest.fixture(scope="module")
+def full():
+    """One context with the bench's C4b matrix generated on the device, and its CSR on the host."""
+    import rbl
+    plant = np.array([100.0 * (2 * K + 1 - l) for l in range(1, 2 * K + 1)])
+    ctx = rbl.Context(0)
+    ctx.gen_rmat(N, SCALE, EDGES, SEED, plant)
+    n, r0, r1, nnz = ctx.matrix_info()
+    assert (n, r0, r1) == (N, 0, N) and 0.95e9 < nnz < 1.05e9
+    _log(f"generated {nnz} nonzeros")
+    rowptr, col, val = ctx.get_matrix_csr()
+    _log("CSR downloaded")
+    A = sp.csr_matrix((val, col, rowptr.astype(np.int32)), shape=(N, N))
+    yield rbl, ctx, A
+    ctx.close()
+
+
+def _row_sets(A):
+    deg = np.diff(A.indptr)
+    hubs = np.sort(np.argsort(-deg)[:64])
+    assert deg[hubs].max() > 100 * SEG_LEN        # the top hub spans > 100 segments
+    assert (deg[hubs] > SEG_LEN).sum() >= 32      # and most sampled hubs are segmented
+    starts = np.linspace(1024, N - 2048, 32).astype(np.int64)
+    return [hubs] + [np.arange(s, s + 256) for s in starts] + [np.arange(N - 300, N)]
+
+
+def test_c4b_fullsize_spmm_sampled_rows_and_linearity(full):
+    rbl, ctx, A = full
+    assert ctx.spmm_kernel_for(B) == 6            # the segmented gather of the bench line
+    rows = _row_sets(A)
+    rng = np.random.default_rng(7)
+    X1 = rng.standard_normal((N, B))
+    Y1 = ctx.apply(X1)
+    _log("A X1")
+    aX = np.abs(X1)
+    for r in rows:
+        As = A[r]
+        ref = As @ X1
+        bound = (abs(As) @ aX) * SPMM_TOL + 1e-300
+        err = np.abs(Y1[r] - ref)
+        assert np.all(err <= bound), (int(r[0]), float(np.max(err / bound)))
+    _log("sampled rows checked")
+    X2 = rng.standard_normal((N, B))
+    Y2 = ctx.apply(X2)
+    X1 += 2.0 * X2
+    Y3 = ctx.apply(X1)
+    Y1 += 2.0 * Y2
+    aX = np.abs(X1)
+    aX += 4.0 * np.abs(X2)
+    for r in rows:
+        bound = 3 * SPMM_TOL * (abs(A[r]) @ aX)
+        assert np.all(np.abs(Y3[r] - Y1[r]) <= bound + 1e-300), int(r[0])
+    _log("linearity checked")
+
+
+def test_c4b_fullsize_rbl_gpu(full):
+    rbl, ctx, A = full
+    D, V, info = rbl.lanczos(ctx, K, B, seed=SEED + 2, check=True, ritz=True)
+    _log(f"RBL_gpu: {info.iters} steps")
+    assert info.converged and D.shape == (K,) and V.shape == (N, K)
+    assert np.all(np.diff(np.abs(D)) <= 0)                        # P11
+    AV = A @ V
+    _log("A V on the host")
+    res = np.linalg.norm(AV - V * D, axis=0) / np.abs(D)
+    assert res.max() < RES_TOL, res
+    G = V.T @ V
+    assert np.abs(G - np.eye(K)).max() < ORTH_TOL, np.abs(G - np.eye(K)).max()
+    rq = np.einsum("ij,ij->j", V, AV) / np.einsum("ij,ij->j", V, V)
+    assert np.all(np.abs(rq - D) <= RAYLEIGH_TOL * np.abs(D)), np.abs(rq - D) / np.abs(D)

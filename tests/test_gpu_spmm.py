@@ -33,10 +33,11 @@ def _rand_sym(n, density, seed, empty_rows=()):
 
 
 @pytest.mark.parametrize("b", [1, 5, 8, 16, 32, 64])
-@pytest.mark.parametrize("variant", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("variant", [0, 1, 2, 3, 5])
 def test_spmm_hashwindow(rbl, b, variant):
-    """variant 1 = gather, 2 = LDS window (DPP), 3 = LDS-densified band on MFMA, 4 = band
-    tiles (MFMA operand order, spmm_bt.hip; kernel id 5), 0 = auto."""
+    """RBL_OPT_SPMM_KERNEL takes the kernel ids rbl_spmm_kernel_for reports: 1 = gather,
+    2 = LDS window (DPP), 3 = LDS-densified band on MFMA, 5 = band tiles (MFMA operand order,
+    spmm_bt.hip), 0 = auto."""
     A = matgen.hashwindow_csr(7000, 64, 0.7734, 5, matgen.planted_spectrum(10))
     X = np.random.default_rng(b).standard_normal((A.shape[0], b))
     with rbl.Context(0) as ctx:
@@ -44,7 +45,7 @@ def test_spmm_hashwindow(rbl, b, variant):
         ctx.set_option(2, variant)
         k = ctx.spmm_kernel_for(b)
         if b in (16, 32):
-            assert k == {0: 5, 1: 1, 2: 2, 3: 3, 4: 5}[variant]   # the kernel under test runs
+            assert k == {0: 5, 1: 1, 2: 2, 3: 3, 5: 5}[variant]   # the kernel under test runs
         else:
             assert k == 1
         Y = ctx.apply(X)
@@ -71,7 +72,7 @@ def test_spmm_window_ragged_and_partial_tiles(rbl, b):
 
 
 @pytest.mark.parametrize("b", [16, 32])
-@pytest.mark.parametrize("variant", [2, 3, 4])
+@pytest.mark.parametrize("variant", [2, 3, 5])
 def test_spmm_window_kernels_ragged(rbl, b, variant):
     """Both LDS kernels forced, on ragged tiles / narrow and wide bands / dense bands."""
     for n, W, p in [(1001, 3, 0.9), (333, 60, 0.5), (4099, 64, 1.0), (17, 8, 0.5), (2000, 30, 0.2)]:
@@ -101,7 +102,7 @@ def test_spmm_window_and_gather_agree_in_lanczos(rbl):
     """The whole block step is insensitive to the SpMM kernel choice (1e-12 on A_i)."""
     A = matgen.hashwindow_csr(6000, 64, 0.7734, 9, matgen.planted_spectrum(10))
     out = []
-    for variant in (1, 2, 3, 4):
+    for variant in (1, 2, 3, 5):
         with rbl.Context(0) as ctx:
             ctx.set_matrix(A)
             ctx.set_option(2, variant)
@@ -197,9 +198,9 @@ def test_spmm_half_band_tiles_need_exact_symmetry(rbl, monkeypatch):
 
 
 @pytest.mark.parametrize("b", [16, 32])
-@pytest.mark.parametrize("variant", [0, 5])
+@pytest.mark.parametrize("variant", [0, 6])
 def test_spmm_segmented_long_rows(rbl, b, variant):
-    """Segmented gather (variant 5, kernel id 6): an arrow matrix whose 3 hub rows/columns
+    """Segmented gather (kernel id 6): an arrow matrix whose 3 hub rows/columns
     touch every row (20,000 nonzeros each: 5 segments of 4,096 each, summed in order by the
     fixup kernel) beside short random rows, empty rows and the fused 3-term epilogue path
     through a short Lanczos trace."""
@@ -228,7 +229,7 @@ def test_spmm_segmented_and_gather_agree_in_lanczos(rbl):
     A = mg.rmat_csr(16000, 14, 1_200_000, 3, mg.planted_spectrum(5))
     assert np.diff(A.indptr).max() > 4096     # long rows present
     out = []
-    for variant in (1, 5):
+    for variant in (1, 6):
         with rbl.Context(0) as ctx:
             ctx.set_matrix(A)
             ctx.set_option(2, variant)

@@ -77,3 +77,23 @@ def test_topk_eigensolve_matches_reference_selection():
         B = np.triu(rng.standard_normal((b, b)))
         for tol in (1e-3, 1e2):
             assert host.check_convergence(B, v1, b, k, tol) == o.check_convergence(B, v2, b, k, tol)
+
+
+def test_fix_signs_makes_ritz_coefficients_solver_independent():
+    """The top-k path and dsbev may return eigenvectors of opposite signs; after fix_signs the
+    coefficient columns (hence V = [Q] S) agree entry for entry."""
+    from rbl.host import eig_topk, fix_signs, sort_eig_abs
+    from scipy.linalg import lapack
+    rng = np.random.default_rng(11)
+    b, N, k = 8, 640, 10
+    T = rng.standard_normal((b + 1, N))
+    T[0] += np.linspace(-50, 60, N)
+    w, z, info = lapack.dsbev(T, compute_v=1, lower=1)
+    D1, S1 = sort_eig_abs(w, z, k)
+    D2, S2 = eig_topk(T, k)
+    assert np.allclose(D1, D2, rtol=1e-12, atol=0)
+    F1, F2 = fix_signs(S1), fix_signs(S2)
+    assert np.abs(F1 - F2).max() < 1e-9
+    assert np.all(F1[np.argmax(np.abs(F1), axis=0), np.arange(k)] > 0)
+    neg = fix_signs(-S1)
+    assert np.array_equal(neg, F1)
