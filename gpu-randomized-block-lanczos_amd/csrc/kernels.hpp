@@ -99,7 +99,30 @@ struct CsrDev {
   const int64_t* seg_lrow = nullptr;
   const int64_t* seg_lslot = nullptr;
   double* seg_scratch = nullptr;
+  // column tiers of the segmented gather (RBL_SEG_TIERS; one rank): the nonzeros split by the
+  // degree rank of their column into up to kMaxSegTiers CSRs of the same rows, each with its
+  // own task table; the SpMM sweeps them in order, accumulating into U, so each sweep's Q-row
+  // gathers come from a set that fits a cache level (hot rows: an XCD's L2)
+  int seg_ntiers = 0;
+  // several ranks: two tiers, the own columns [loc_lo, loc_hi) (tier 0, gathered from `qloc`,
+  // the block itself, when set) and the halo columns (tier 1, from Qin): tier 0 runs while the
+  // halo exchange is in flight; the stream waits for `seg_wait` (if set) before tier 1
+  bool seg_split = false;
+  hipEvent_t seg_wait = nullptr;
+  struct Tier {
+    const int64_t* rowptr = nullptr;
+    const int32_t* col = nullptr;
+    const double* val = nullptr;
+    int64_t ntasks = 0, nlong = 0;
+    const int64_t* trow = nullptr;
+    const int32_t* tinfo = nullptr;
+    const int64_t* slot_k0 = nullptr;
+    const int64_t* lrow = nullptr;
+    const int64_t* lslot = nullptr;
+    double* scratch = nullptr;
+  } seg_tier[3];
 };
+constexpr int kMaxSegTiers = 3;
 constexpr int64_t kSegLen = 4096;   // nonzeros per long-row segment
 constexpr int64_t kSegPack = 512;   // nonzeros per packed short-row task (<= 64 rows)
 
@@ -150,6 +173,13 @@ int spmm(const CsrDev& A, const double* Qin, int64_t col_off, int b, double* U,
          double* ai_slab = nullptr);
 
 bool spmm_seg_ok(const CsrDev& A, int b);
+// column tiers (CsrDev::seg_tier): per row, the nonzeros of each tier (tier_of[col], uint8)
+// counted into cnt[t * m + r], then copied in column order into the tier CSRs
+void seg_tier_count(int64_t m, const int64_t* rowptr, const int32_t* col, const uint8_t* tier_of,
+                    int ntiers, int32_t* cnt, hipStream_t s);
+void seg_tier_fill(int64_t m, const int64_t* rowptr, const int32_t* col, const double* val,
+                   const uint8_t* tier_of, int ntiers, int64_t* const* trp, int32_t* const* tcol,
+                   double* const* tval, hipStream_t s);
 // spmm_window.hip: persistent LDS-window kernel (b in {16,32}); false if not applicable.
 bool spmm_window(const CsrDev& A, const double* Qin, int64_t col_off, int b, double* U,
                  const double* Qprev, const double* Bi, hipStream_t s);

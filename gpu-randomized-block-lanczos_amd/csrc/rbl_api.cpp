@@ -55,6 +55,26 @@ struct rbl_ctx {
   int64_t* d_seg_lrow = nullptr;
   int64_t* d_seg_lslot = nullptr;
   double* d_seg_scratch = nullptr;
+  // column tiers of the segmented gather (RBL_SEG_TIERS, one rank; CsrDev::seg_tier): each a
+  // CSR of the same rows holding the nonzeros of one column-degree tier, with its task table
+  struct SegTierBuf {
+    int64_t* rowptr = nullptr;
+    int32_t* col = nullptr;
+    double* val = nullptr;
+    int64_t ntasks = 0, nlong = 0;
+    int64_t* trow = nullptr;
+    int32_t* tinfo = nullptr;
+    int64_t* slot_k0 = nullptr;
+    int64_t* lrow = nullptr;
+    int64_t* lslot = nullptr;
+    double* scratch = nullptr;
+  };
+  int seg_ntiers = 0;
+  SegTierBuf seg_tier[3];
+  bool seg_split = false;             // several ranks: tiers = own / halo columns
+  bool halo_overlap = true;           // RBL_OPT_HALO_OVERLAP
+  hipStream_t hstream = nullptr;      // the overlapped halo exchange
+  hipEvent_t ev_qready = nullptr, ev_halo = nullptr;
   // dense A (RBL_gpu(A::Matrix{Float64})): local rows in 32-column row-major panels
   // (panel p = columns [32p, 32p+32), zero past n), multiplied by tsmm44 against d_qfull
   // (all n rows of Q, zero-padded to 32 * dense_panels rows, b <= 64 columns)
@@ -267,14 +287,31 @@ CsrDev csr(rbl_ctx* ctx) {
   A.seg_lrow = ctx->d_seg_lrow;
   A.seg_lslot = ctx->d_seg_lslot;
   A.seg_scratch = ctx->d_seg_scratch;
+  A.seg_ntiers = ctx->seg_ntiers;
+  A.seg_split = ctx->seg_split;
+  for (int t = 0; t < ctx->seg_ntiers; ++t) {
+    const auto& T = ctx->seg_tier[t];
+    auto& D = A.seg_tier[t];
+    D.rowptr = T.rowptr;
+    D.col = T.col;
+    D.val = T.val;
+    D.ntasks = T.ntasks;
+    D.nlong = T.nlong;
+    D.trow = T.trow;
+    D.tinfo = T.tinfo;
+    D.slot_k0 = T.slot_k0;
+    D.lrow = T.lrow;
+    D.lslot = T.lslot;
+    D.scratch = T.scratch;
+  }
   return A;
 }
 
 // Task table of the segmented gather (spmm.hip variant 5): short rows packed into tasks of
 // <= kSegPack nonzeros and <= 64 rows, rows over kSegLen nonzeros cut into segments.
-int prepare_segments(rbl_ctx* ctx, const std::vector<int64_t>& rp) {
-  const int64_t m = ctx->nloc;
-  if (m <= 0 || ctx->nnz <= 0) return RBL_OK;
+int build_seg(rbl_ctx* ctx, const std::vector<int64_t>& rp, rbl_ctx::SegTierBuf& out) {
+  const int64_t m = (int64_t)rp.size() - 1;
+  if (m <= 0) return RBL_OK;
   std::vector<int64_t> trow, slot_k0, lrow, lslot;
   std::vector<int32_t> tinfo;
   int64_t cur_r0 = 0, cur_nnz = 0;
@@ -308,27 +345,171 @@ int prepare_segments(rbl_ctx* ctx, const std::vector<int64_t>& rp) {
   flush();
   lslot.push_back((int64_t)slot_k0.size());
   slot_k0.push_back(INT64_MAX);
-  ctx->seg_ntasks = (int64_t)trow.size();
-  ctx->seg_nlong = (int64_t)lrow.size();
-  HIPC(hipMalloc(&ctx->d_seg_trow, trow.size() * sizeof(int64_t)));
-  HIPC(hipMalloc(&ctx->d_seg_tinfo, tinfo.size() * sizeof(int32_t)));
-  HIPC(hipMalloc(&ctx->d_seg_slot_k0, slot_k0.size() * sizeof(int64_t)));
-  HIPC(hipMalloc(&ctx->d_seg_lslot, lslot.size() * sizeof(int64_t)));
-  HIPC(hipMalloc(&ctx->d_seg_lrow, std::max<size_t>(lrow.size(), 1) * sizeof(int64_t)));
-  HIPC(hipMalloc(&ctx->d_seg_scratch, std::max<size_t>(slot_k0.size() - 1, 1) * 32 * sizeof(double)));
-  HIPC(hipMemcpy(ctx->d_seg_trow, trow.data(), trow.size() * sizeof(int64_t), hipMemcpyHostToDevice));
-  HIPC(hipMemcpy(ctx->d_seg_tinfo, tinfo.data(), tinfo.size() * sizeof(int32_t), hipMemcpyHostToDevice));
-  HIPC(hipMemcpy(ctx->d_seg_slot_k0, slot_k0.data(), slot_k0.size() * sizeof(int64_t), hipMemcpyHostToDevice));
-  HIPC(hipMemcpy(ctx->d_seg_lslot, lslot.data(), lslot.size() * sizeof(int64_t), hipMemcpyHostToDevice));
+  out.ntasks = (int64_t)trow.size();
+  out.nlong = (int64_t)lrow.size();
+  HIPC(hipMalloc(&out.trow, trow.size() * sizeof(int64_t)));
+  HIPC(hipMalloc(&out.tinfo, tinfo.size() * sizeof(int32_t)));
+  HIPC(hipMalloc(&out.slot_k0, slot_k0.size() * sizeof(int64_t)));
+  HIPC(hipMalloc(&out.lslot, lslot.size() * sizeof(int64_t)));
+  HIPC(hipMalloc(&out.lrow, std::max<size_t>(lrow.size(), 1) * sizeof(int64_t)));
+  HIPC(hipMalloc(&out.scratch, std::max<size_t>(slot_k0.size() - 1, 1) * 32 * sizeof(double)));
+  HIPC(hipMemcpy(out.trow, trow.data(), trow.size() * sizeof(int64_t), hipMemcpyHostToDevice));
+  HIPC(hipMemcpy(out.tinfo, tinfo.data(), tinfo.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+  HIPC(hipMemcpy(out.slot_k0, slot_k0.data(), slot_k0.size() * sizeof(int64_t), hipMemcpyHostToDevice));
+  HIPC(hipMemcpy(out.lslot, lslot.data(), lslot.size() * sizeof(int64_t), hipMemcpyHostToDevice));
   if (!lrow.empty())
-    HIPC(hipMemcpy(ctx->d_seg_lrow, lrow.data(), lrow.size() * sizeof(int64_t), hipMemcpyHostToDevice));
+    HIPC(hipMemcpy(out.lrow, lrow.data(), lrow.size() * sizeof(int64_t), hipMemcpyHostToDevice));
+  return RBL_OK;
+}
+
+void free_seg(rbl_ctx::SegTierBuf& T, bool with_csr) {
+  if (with_csr) {
+    hipFree(T.rowptr);
+    hipFree(T.col);
+    hipFree(T.val);
+  }
+  hipFree(T.trow);
+  hipFree(T.tinfo);
+  hipFree(T.slot_k0);
+  hipFree(T.lrow);
+  hipFree(T.lslot);
+  hipFree(T.scratch);
+  T = rbl_ctx::SegTierBuf();
+}
+
+void free_tiers(rbl_ctx* ctx) {
+  for (auto& T : ctx->seg_tier) free_seg(T, true);
+  ctx->seg_ntiers = 0;
+  ctx->seg_split = false;
+}
+
+int prepare_segments(rbl_ctx* ctx, const std::vector<int64_t>& rp) {
+  if (ctx->nloc <= 0 || ctx->nnz <= 0) return RBL_OK;
+  rbl_ctx::SegTierBuf T;
+  const int st = build_seg(ctx, rp, T);
+  ctx->seg_ntasks = T.ntasks;
+  ctx->seg_nlong = T.nlong;
+  ctx->d_seg_trow = T.trow;
+  ctx->d_seg_tinfo = T.tinfo;
+  ctx->d_seg_slot_k0 = T.slot_k0;
+  ctx->d_seg_lrow = T.lrow;
+  ctx->d_seg_lslot = T.lslot;
+  ctx->d_seg_scratch = T.scratch;
+  return st;
+}
+
+int build_tiers(rbl_ctx* ctx, const std::vector<uint8_t>& tier_of, int nt);
+
+// Column tiers of the segmented gather (RBL_SEG_TIERS="h[,w]": the h highest-degree columns,
+// then the next w, then the rest; one rank, A symmetric so a column's degree is its row's).
+// The SpMM sweeps the tiers in order; each sweep's gathers hit a Q-row set sized for one cache
+// level.  Results differ from the one-sweep SpMM only in the order of each row's sum.
+// Several ranks (unbanded A, the segmented gather): two tiers instead, the own columns
+// [r0, r1) and the halo columns, so the own part of the SpMM runs while the halo exchange is in
+// flight (step_impl); the sum order per row is the same with or without the overlap.
+int prepare_tiers(rbl_ctx* ctx, const std::vector<int64_t>& rp) {
+  free_tiers(ctx);
+  if (ctx->seg_ntasks == 0 || ctx->nnz == 0) return RBL_OK;
+  if (ctx->nranks > 1) {
+    if (ctx->bt_ng || ctx->band_ok16 || ctx->band_ok32 || ctx->window_ok16 || ctx->window_ok32 ||
+        ctx->dense)
+      return RBL_OK;  // a banded kernel runs: its halo is a few rows
+    std::vector<uint8_t> tier_of(ctx->n, 1);
+    for (int64_t c = ctx->r0; c < ctx->r1; ++c) tier_of[c] = 0;
+    CHK(build_tiers(ctx, tier_of, 2));
+    ctx->seg_split = true;
+    return RBL_OK;
+  }
+  const char* e = std::getenv("RBL_SEG_TIERS");
+  if (!e || ctx->nloc != ctx->n) return RBL_OK;
+  std::vector<int64_t> sz;
+  for (const char* p = e; *p;) {
+    char* end = nullptr;
+    const long long v = std::strtoll(p, &end, 10);
+    if (end == p) break;
+    if (v > 0) sz.push_back(v);
+    p = *end == ',' ? end + 1 : end;
+    if (sz.size() == kMaxSegTiers - 1) break;
+  }
+  if (sz.empty()) return RBL_OK;
+  const int nt = (int)sz.size() + 1;
+  const int64_t n = ctx->n, m = ctx->nloc;
+  std::vector<int64_t> order(n);
+  for (int64_t c = 0; c < n; ++c) order[c] = c;
+  std::stable_sort(order.begin(), order.end(), [&](int64_t a, int64_t b2) {
+    return rp[a + 1] - rp[a] > rp[b2 + 1] - rp[b2];
+  });
+  std::vector<uint8_t> tier_of(n, (uint8_t)(nt - 1));
+  int64_t rank = 0;
+  for (int t = 0; t < nt - 1; ++t)
+    for (int64_t k = 0; k < sz[t] && rank < n; ++k) tier_of[order[rank++]] = (uint8_t)t;
+  (void)m;
+  return build_tiers(ctx, tier_of, nt);
+}
+
+// The tier CSRs and task tables for a column -> tier map (tier_of: n entries, < nt).
+int build_tiers(rbl_ctx* ctx, const std::vector<uint8_t>& tier_of, int nt) {
+  const int64_t n = ctx->n, m = ctx->nloc;
+  uint8_t* d_tier = nullptr;
+  int32_t* d_cnt = nullptr;
+  HIPC(hipMalloc(&d_tier, n));
+  HIPC(hipMalloc(&d_cnt, (size_t)nt * m * sizeof(int32_t)));
+  HIPC(hipMemcpy(d_tier, tier_of.data(), n, hipMemcpyHostToDevice));
+  seg_tier_count(m, ctx->d_rowptr, ctx->d_col, d_tier, nt, d_cnt, ctx->stream);
+  HIPC(hipGetLastError());
+  std::vector<int32_t> cnt((size_t)nt * m);
+  HIPC(hipMemcpyAsync(cnt.data(), d_cnt, cnt.size() * sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
+  HIPC(hipStreamSynchronize(ctx->stream));
+  std::vector<std::vector<int64_t>> trp(nt, std::vector<int64_t>(m + 1, 0));
+  int64_t* rpp[kMaxSegTiers] = {nullptr, nullptr, nullptr};
+  int32_t* colp[kMaxSegTiers] = {nullptr, nullptr, nullptr};
+  double* valp[kMaxSegTiers] = {nullptr, nullptr, nullptr};
+  for (int t = 0; t < nt; ++t) {
+    for (int64_t r = 0; r < m; ++r) trp[t][r + 1] = trp[t][r] + cnt[(size_t)t * m + r];
+    auto& T = ctx->seg_tier[t];
+    const int64_t nz = trp[t][m];
+    HIPC(hipMalloc(&T.rowptr, (m + 1) * sizeof(int64_t)));
+    HIPC(hipMalloc(&T.col, (nz + kCsrPad) * sizeof(int32_t)));
+    HIPC(hipMalloc(&T.val, (nz + kCsrPad) * sizeof(double)));
+    HIPC(hipMemset(T.col + nz, 0, kCsrPad * sizeof(int32_t)));
+    HIPC(hipMemset(T.val + nz, 0, kCsrPad * sizeof(double)));
+    HIPC(hipMemcpy(T.rowptr, trp[t].data(), (m + 1) * sizeof(int64_t), hipMemcpyHostToDevice));
+    rpp[t] = T.rowptr;
+    colp[t] = T.col;
+    valp[t] = T.val;
+  }
+  ctx->seg_ntiers = nt;  // (free_tiers releases partial state on a later failure)
+  seg_tier_fill(m, ctx->d_rowptr, ctx->d_col, ctx->d_val, d_tier, nt, rpp, colp, valp, ctx->stream);
+  HIPC(hipGetLastError());
+  HIPC(hipStreamSynchronize(ctx->stream));
+  hipFree(d_tier);
+  hipFree(d_cnt);
+  for (int t = 0; t < nt; ++t) {
+    auto& T = ctx->seg_tier[t];
+    int64_t* rp_keep = T.rowptr;
+    int32_t* col_keep = T.col;
+    double* val_keep = T.val;
+    CHK(build_seg(ctx, trp[t], T));
+    T.rowptr = rp_keep;
+    T.col = col_keep;
+    T.val = val_keep;
+  }
   return RBL_OK;
 }
 
 // Per-16-row-tile column footprint for the LDS-window SpMM and the checks that every tile
 // fits its ring (spmm_window.hip): columns sorted per row, footprints non-decreasing, a
 // tile's nonzeros <= 2048, ring rows: 256 (b=32) / 512 (b=16), new rows per tile <= 32 / 64.
+int prepare_window_formats(rbl_ctx* ctx, const std::vector<int64_t>& rp);
+// Every SpMM format of a freshly set CSR: the segmented-gather table, the window / band /
+// band-tile formats, then (unbanded only) the column tiers.
 int prepare_window(rbl_ctx* ctx, const std::vector<int64_t>& rp) {
+  CHK(prepare_window_formats(ctx, rp));
+  if (!ctx->csr_dropped) CHK(prepare_tiers(ctx, rp));
+  return RBL_OK;
+}
+
+int prepare_window_formats(rbl_ctx* ctx, const std::vector<int64_t>& rp) {
   CHK(prepare_segments(ctx, rp));
   ctx->window_ok16 = ctx->window_ok32 = false;
   ctx->band_ok16 = ctx->band_ok32 = false;
@@ -502,6 +683,7 @@ int prepare_window(rbl_ctx* ctx, const std::vector<int64_t>& rp) {
     hipFree(ctx->d_seg_lslot); ctx->d_seg_lslot = nullptr;
     hipFree(ctx->d_seg_scratch); ctx->d_seg_scratch = nullptr;
     ctx->seg_ntasks = ctx->seg_nlong = 0;
+    free_tiers(ctx);
     ctx->window_ok16 = ctx->window_ok32 = false;
     ctx->band_ok16 = ctx->band_ok32 = false;
     ctx->band_gram = ctx->band_pair = false;
@@ -534,18 +716,19 @@ struct StageScope {
   hipEvent_t a = nullptr;
   // every stage is also a roctx range named like the reference's TimerOutputs labels
   // (RBL_gpu.jl:152-187: "AQ", "3-term", ...): `rocprofv3 --marker-trace` shows them
-  StageScope(rbl_ctx* c, int s) : ctx(c), stage(s) {
+  hipStream_t st;
+  StageScope(rbl_ctx* c, int s, hipStream_t on = nullptr) : ctx(c), stage(s), st(on ? on : c->stream) {
     roctxRangePushA(kStageNames[s]);
     if (ctx->timers) {
       a = next_event(ctx);
-      if (a) hipEventRecord(a, ctx->stream);
+      if (a) hipEventRecord(a, st);
     }
   }
   ~StageScope() {
     if (ctx->timers && a) {
       hipEvent_t b = next_event(ctx);
       if (b) {
-        hipEventRecord(b, ctx->stream);
+        hipEventRecord(b, st);
         ctx->marks.push_back({stage, a, b});
       }
     }
@@ -711,7 +894,7 @@ int ensure_qm64(rbl_ctx* ctx) {
 int apply_A(rbl_ctx* ctx, const double* Qin, int64_t off, int b, double* U, const double* Qprev,
             const double* Bi, double* slab, const double* qloc = nullptr,
             const double* lfix_c = nullptr, double* lfix_q = nullptr, int64_t lf_lo = 0,
-            int64_t lf_hi = 0) {
+            int64_t lf_hi = 0, hipEvent_t seg_wait = nullptr) {
   if (ctx->nloc <= 0) return 0;
   if (ctx->csr_dropped && rbl_spmm_kernel_for(ctx, b) != 5)
     return fail(ctx, RBL_ERR_STATE, "the CSR was released (RBL_OPT_KEEP_CSR = 0): only the band-tile "
@@ -723,6 +906,7 @@ int apply_A(rbl_ctx* ctx, const double* Qin, int64_t off, int b, double* U, cons
       A.loc_lo = ctx->r0;
       A.loc_hi = ctx->r0 + ctx->nloc;
     }
+    A.seg_wait = seg_wait;  // own/halo column tiers: the halo tier waits for the exchange
     if (lfix_c) {  // local reorth fused into the SpMM's staging (RBL_OPT_FUSE bit 2)
       A.lfix_c = lfix_c;
       A.lfix_q = lfix_q;
@@ -1083,18 +1267,19 @@ int tsqr(rbl_ctx* ctx, const double* U, double* Qout, bool g1_ready = false, flo
 // false: only the neighbours' rows land there (the band-tile SpMM reads the own rows from Q
 // itself, CsrDev::qloc), saving a read + write of the whole local block per step.
 int halo_exchange(rbl_ctx* ctx, const double* Q, const double** Qin, int64_t* off,
-                  bool copy_local = true) {
+                  bool copy_local = true, hipStream_t st = nullptr) {
   if (ctx->nranks == 1) {
     *Qin = Q;
     *off = 0;
     return RBL_OK;
   }
-  StageScope t(ctx, RBL_STAGE_COMM);
+  if (!st) st = ctx->stream;
+  StageScope t(ctx, RBL_STAGE_COMM, st);
   const int b = ctx->b;
   double* ext = ctx->d_qext;
   if (copy_local)
     HIPC(hipMemcpyAsync(ext + (ctx->r0 - ctx->ext_lo) * b, Q, ctx->nloc * b * sizeof(double),
-                        hipMemcpyDeviceToDevice, ctx->stream));
+                        hipMemcpyDeviceToDevice, st));
   std::vector<Comm::Xfer> x(ctx->nranks);
   for (int q = 0; q < ctx->nranks; ++q) {
     if (q == ctx->rank) continue;
@@ -1109,7 +1294,7 @@ int halo_exchange(rbl_ctx* ctx, const double* Q, const double** Qin, int64_t* of
       x[q].nrecv = (size_t)(nh - nl) * b;
     }
   }
-  COMMC(ctx->comm->exchange(x, ctx->stream, &ctx->err));
+  COMMC(ctx->comm->exchange(x, st, &ctx->err));
   count_exchange(ctx, x);
   *Qin = ext;
   *off = ctx->ext_lo;
@@ -1208,6 +1393,7 @@ void free_matrix(rbl_ctx* ctx) {
   hipFree(ctx->d_seg_lslot); ctx->d_seg_lslot = nullptr;
   hipFree(ctx->d_seg_scratch); ctx->d_seg_scratch = nullptr;
   ctx->seg_ntasks = ctx->seg_nlong = 0;
+  free_tiers(ctx);
   hipFree(ctx->d_dense); ctx->d_dense = nullptr;
   hipFree(ctx->d_qfull); ctx->d_qfull = nullptr; ctx->qfull_cols = 0;
   ctx->dense = false;
@@ -1448,6 +1634,7 @@ int rbl_free(rbl_ctx* ctx) {
   if (!ctx) return RBL_OK;
   hipSetDevice(ctx->device);
   if (ctx->stream) hipStreamSynchronize(ctx->stream);
+  if (ctx->hstream) hipStreamSynchronize(ctx->hstream);
   free_run(ctx);
   free_matrix(ctx);
   for (auto e : ctx->ev_pool) hipEventDestroy(e);
@@ -1456,8 +1643,9 @@ int rbl_free(rbl_ctx* ctx) {
   delete ctx->comm;
   if (ctx->stream) hipStreamDestroy(ctx->stream);
   if (ctx->cstream) hipStreamDestroy(ctx->cstream);
+  if (ctx->hstream) hipStreamDestroy(ctx->hstream);
   for (hipEvent_t e : {ctx->ev_fin, ctx->ev_d2h[0], ctx->ev_d2h[1], ctx->ev_d2h_slot[0],
-                       ctx->ev_d2h_slot[1]})
+                       ctx->ev_d2h_slot[1], ctx->ev_qready, ctx->ev_halo})
     if (e) hipEventDestroy(e);
   for (void* h : ctx->h_d2h)
     if (h) hipHostFree(h);
@@ -1505,6 +1693,7 @@ int rbl_set_option(rbl_ctx* ctx, int option, int64_t value) {
       ctx->spmm_variant = value == 5 ? 4 : value == 6 ? 5 : (int)value;
       return RBL_OK;
     case RBL_OPT_SPLIT_HALO: ctx->split_halo = value != 0; return RBL_OK;
+    case RBL_OPT_HALO_OVERLAP: ctx->halo_overlap = value != 0; return RBL_OK;
     case RBL_OPT_KEEP_CSR: ctx->keep_csr = value != 0; return RBL_OK;
     case RBL_OPT_FUSE:
       if (value < 0 || value > 7) return fail(ctx, RBL_ERR_INVALID, "RBL_OPT_FUSE is a 3-bit mask");
@@ -2195,10 +2384,31 @@ int step_impl(rbl_ctx* ctx, int i, int part_reorth, double* A_out, double* B_out
     int64_t off = 0;
     // several ranks with the band-tile kernel: the halo buffer takes only the neighbours'
     // rows; the kernel reads the own rows from the block (no per-step local copy)
+    const int kid = rbl_spmm_kernel_for(ctx, b);
+    const bool seg_split = !direct32 && kid == 6 && ctx->seg_split;
     const bool split = ctx->nranks > 1 && !ctx->dense &&
-                       (direct32 || rbl_spmm_kernel_for(ctx, b) == 5) && ctx->split_halo;
-    if (direct32) CHK(halo_exchange32(ctx, Qi32, &Qin32, &off, !split));
-    else CHK(halo_exchange(ctx, Qi, &Qin, &off, !split));
+                       (direct32 || kid == 5 || seg_split) && ctx->split_halo;
+    // unbanded A on several ranks (the halo is most of Q_i): the exchange runs on a side
+    // stream while the SpMM's own-column tier runs; the halo tier waits for it
+    // (RBL_OPT_HALO_OVERLAP; the same sums in the same order either way)
+    const bool overlap = split && seg_split && ctx->halo_overlap;
+    hipEvent_t halo_ev = nullptr;
+    if (overlap) {
+      if (!ctx->hstream) {
+        HIPC(hipStreamCreateWithFlags(&ctx->hstream, hipStreamNonBlocking));
+        HIPC(hipEventCreateWithFlags(&ctx->ev_qready, hipEventDisableTiming));
+        HIPC(hipEventCreateWithFlags(&ctx->ev_halo, hipEventDisableTiming));
+      }
+      HIPC(hipEventRecord(ctx->ev_qready, ctx->stream));  // Q_i final (local reorth done)
+      HIPC(hipStreamWaitEvent(ctx->hstream, ctx->ev_qready, 0));
+      CHK(halo_exchange(ctx, Qi, &Qin, &off, false, ctx->hstream));
+      HIPC(hipEventRecord(ctx->ev_halo, ctx->hstream));
+      halo_ev = ctx->ev_halo;
+    } else if (direct32) {
+      CHK(halo_exchange32(ctx, Qi32, &Qin32, &off, !split));
+    } else {
+      CHK(halo_exchange(ctx, Qi, &Qin, &off, !split));
+    }
     StageScope t(ctx, RBL_STAGE_AQ);
     // the band kernel can also form the partials of A_i = Q_i^T U while U is in registers
     if (direct32) {
@@ -2213,7 +2423,7 @@ int step_impl(rbl_ctx* ctx, int i, int part_reorth, double* A_out, double* B_out
         return fail(ctx, RBL_ERR_INVALID, "internal: fp32 band-tile SpMM not applicable");
     } else {
       ai_parts = apply_A(ctx, Qin, off, b, ctx->d_U, Qm, i >= 2 ? smallp(ctx, S_BPREV) : nullptr,
-                         ctx->d_slab, split ? Qi : nullptr, Cloc, Qi, lf_lo, lf_hi);
+                         ctx->d_slab, split ? Qi : nullptr, Cloc, Qi, lf_lo, lf_hi, halo_ev);
     }
     if (ai_parts < 0) return ai_parts;
     HIPC(hipGetLastError());

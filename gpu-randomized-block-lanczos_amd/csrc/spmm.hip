@@ -77,7 +77,7 @@ __global__ __launch_bounds__(256) void k_spmm_seg(
     const int64_t* __restrict__ rowptr, const int32_t* __restrict__ col,
     const double* __restrict__ val, const double* __restrict__ Q, int64_t col_off,
     double* __restrict__ U, double* __restrict__ scratch, const int64_t* __restrict__ slot_k0,
-    const double* __restrict__ Qprev, const double* __restrict__ Bi) {
+    const double* __restrict__ Qprev, const double* __restrict__ Bi, bool accum) {
   constexpr int R = kWave / BP;
   const int lane = threadIdx.x & 63;
   const int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -120,6 +120,7 @@ __global__ __launch_bounds__(256) void k_spmm_seg(
     for (int rr = h; rr < info; rr += R) {  // lane-group-uniform row loop
       const int64_t row = r0 + rr;
       double acc = dot(rowptr[row], rowptr[row + 1], BP);
+      if (accum) acc += U[row * BP + c];  // a later column tier: add to the earlier sweeps
       if (Qprev) {
         const double qv = Qprev[row * BP + c];
 #pragma unroll
@@ -145,7 +146,7 @@ __global__ __launch_bounds__(256) void k_seg_fixup(int64_t nlong, const int64_t*
                                                   const double* __restrict__ scratch,
                                                   double* __restrict__ U,
                                                   const double* __restrict__ Qprev,
-                                                  const double* __restrict__ Bi) {
+                                                  const double* __restrict__ Bi, bool accum) {
   constexpr int R = kWave / BP;
   const int lane = threadIdx.x & 63;
   const int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / BP;
@@ -155,6 +156,7 @@ __global__ __launch_bounds__(256) void k_seg_fixup(int64_t nlong, const int64_t*
   const int64_t row = lrow[i];
   double acc = 0.0;
   for (int64_t sl = lslot[i]; sl < lslot[i + 1]; ++sl) acc += scratch[sl * BP + c];
+  if (accum) acc += U[row * BP + c];
   if (Qprev) {
     for (int u = 0; u < BP; ++u) acc = fma(-Qprev[row * BP + u], Bi[c * BP + u], acc);
   }
@@ -162,17 +164,106 @@ __global__ __launch_bounds__(256) void k_seg_fixup(int64_t nlong, const int64_t*
 }
 
 template <int BP>
-static void launch_seg(const CsrDev& A, const double* Q, int64_t off, double* U,
-                       const double* Qprev, const double* Bi, hipStream_t s) {
-  const int64_t blocks = (A.seg_ntasks + 3) / 4;
-  hipLaunchKernelGGL((k_spmm_seg<BP>), dim3((unsigned)blocks), dim3(256), 0, s, A.seg_ntasks,
-                     A.seg_trow, A.seg_tinfo, A.rowptr, A.col, A.val, Q, off, U, A.seg_scratch,
-                     A.seg_slot_k0, Qprev, Bi);
-  if (A.seg_nlong > 0) {
-    const int64_t th = A.seg_nlong * BP;
+static void launch_seg(const CsrDev::Tier& T, const double* Q, int64_t off, double* U,
+                       const double* Qprev, const double* Bi, bool accum, hipStream_t s) {
+  if (T.ntasks <= 0) return;
+  const int64_t blocks = (T.ntasks + 3) / 4;
+  hipLaunchKernelGGL((k_spmm_seg<BP>), dim3((unsigned)blocks), dim3(256), 0, s, T.ntasks,
+                     T.trow, T.tinfo, T.rowptr, T.col, T.val, Q, off, U, T.scratch,
+                     T.slot_k0, Qprev, Bi, accum);
+  if (T.nlong > 0) {
+    const int64_t th = T.nlong * BP;
     hipLaunchKernelGGL((k_seg_fixup<BP>), dim3((unsigned)((th + 255) / 256)), dim3(256), 0, s,
-                       A.seg_nlong, A.seg_lrow, A.seg_lslot, A.seg_scratch, U, Qprev, Bi);
+                       T.nlong, T.lrow, T.lslot, T.scratch, U, Qprev, Bi, accum);
   }
+}
+
+// the whole matrix as one tier, or (CsrDev::seg_ntiers) the column tiers in order: the first
+// writes U, the others add to it, the last applies the 3-term epilogue
+template <int BP>
+static void launch_seg_all(const CsrDev& A, const double* Q, int64_t off, double* U,
+                           const double* Qprev, const double* Bi, hipStream_t s) {
+  if (A.seg_ntiers > 0) {
+    for (int t = 0; t < A.seg_ntiers; ++t) {
+      const bool last = t == A.seg_ntiers - 1;
+      const double* Qt = Q;
+      int64_t ot = off;
+      if (A.seg_split && t == 0 && A.qloc) {  // own columns straight from the block
+        Qt = static_cast<const double*>(A.qloc);
+        ot = A.loc_lo;
+      }
+      if (A.seg_split && t == 1 && A.seg_wait) hipStreamWaitEvent(s, A.seg_wait, 0);
+      launch_seg<BP>(A.seg_tier[t], Qt, ot, U, last ? Qprev : nullptr, Bi, t > 0, s);
+    }
+    return;
+  }
+  CsrDev::Tier T;
+  T.rowptr = A.rowptr;
+  T.col = A.col;
+  T.val = A.val;
+  T.ntasks = A.seg_ntasks;
+  T.nlong = A.seg_nlong;
+  T.trow = A.seg_trow;
+  T.tinfo = A.seg_tinfo;
+  T.slot_k0 = A.seg_slot_k0;
+  T.lrow = A.seg_lrow;
+  T.lslot = A.seg_lslot;
+  T.scratch = A.seg_scratch;
+  launch_seg<BP>(T, Q, off, U, Qprev, Bi, false, s);
+}
+
+// ---- column tiers: count, then fill (one thread per row; a one-off per matrix) ----
+__global__ void k_seg_tier_count(int64_t m, const int64_t* __restrict__ rowptr,
+                                 const int32_t* __restrict__ col, const uint8_t* __restrict__ tier_of,
+                                 int ntiers, int32_t* __restrict__ cnt) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= m) return;
+  int c3[kMaxSegTiers] = {0, 0, 0};
+  for (int64_t k = rowptr[r]; k < rowptr[r + 1]; ++k) ++c3[tier_of[col[k]]];
+  for (int t = 0; t < ntiers; ++t) cnt[t * m + r] = c3[t];
+}
+
+struct TierPtrs {
+  int64_t* rp[kMaxSegTiers];
+  int32_t* col[kMaxSegTiers];
+  double* val[kMaxSegTiers];
+};
+
+__global__ void k_seg_tier_fill(int64_t m, const int64_t* __restrict__ rowptr,
+                                const int32_t* __restrict__ col, const double* __restrict__ val,
+                                const uint8_t* __restrict__ tier_of, TierPtrs tp) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= m) return;
+  int64_t pos[kMaxSegTiers];
+  for (int t = 0; t < kMaxSegTiers; ++t) pos[t] = tp.rp[t] ? tp.rp[t][r] : 0;
+  for (int64_t k = rowptr[r]; k < rowptr[r + 1]; ++k) {
+    const int c = col[k];
+    const int t = tier_of[c];
+    tp.col[t][pos[t]] = c;
+    tp.val[t][pos[t]] = val[k];
+    ++pos[t];
+  }
+}
+
+void seg_tier_count(int64_t m, const int64_t* rowptr, const int32_t* col, const uint8_t* tier_of,
+                    int ntiers, int32_t* cnt, hipStream_t s) {
+  if (m <= 0) return;
+  hipLaunchKernelGGL(k_seg_tier_count, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, m,
+                     rowptr, col, tier_of, ntiers, cnt);
+}
+
+void seg_tier_fill(int64_t m, const int64_t* rowptr, const int32_t* col, const double* val,
+                   const uint8_t* tier_of, int ntiers, int64_t* const* trp, int32_t* const* tcol,
+                   double* const* tval, hipStream_t s) {
+  if (m <= 0) return;
+  TierPtrs tp;
+  for (int t = 0; t < kMaxSegTiers; ++t) {
+    tp.rp[t] = t < ntiers ? trp[t] : nullptr;
+    tp.col[t] = t < ntiers ? tcol[t] : nullptr;
+    tp.val[t] = t < ntiers ? tval[t] : nullptr;
+  }
+  hipLaunchKernelGGL(k_seg_tier_fill, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, m,
+                     rowptr, col, val, tier_of, tp);
 }
 
 bool spmm_seg_ok(const CsrDev& A, int b) { return A.seg_ntasks > 0 && (b == 16 || b == 32); }
@@ -195,7 +286,9 @@ int spmm(const CsrDev& A, const double* Qin, int64_t col_off, int b, double* U,
   if ((variant == 0 || variant == 4) &&
       spmm_bt(A, Qin, col_off, b, U, Qprev, Bi, s, ai_slab, &parts))
     return parts;
-  if (A.qloc || A.lfix_c) return -2;  // band-tile kernel only (caller bug)
+  // split sources: the band-tile kernel, or the own/halo column tiers of the segmented gather
+  if (A.lfix_c) return -2;
+  if (A.qloc && !(A.seg_split && (variant == 0 || variant == 5) && spmm_seg_ok(A, b))) return -2;
   if ((variant == 0 || variant == 3 || variant == 4) &&
       spmm_band(A, Qin, col_off, b, U, Qprev, Bi, s, ai_slab, &parts))
     return parts;
@@ -203,8 +296,8 @@ int spmm(const CsrDev& A, const double* Qin, int64_t col_off, int b, double* U,
       spmm_window(A, Qin, col_off, b, U, Qprev, Bi, s))
     return 0;
   if ((variant == 0 || variant == 5) && spmm_seg_ok(A, b)) {
-    if (b == 32) launch_seg<32>(A, Qin, col_off, U, Qprev, Bi, s);
-    else launch_seg<16>(A, Qin, col_off, U, Qprev, Bi, s);
+    if (b == 32) launch_seg_all<32>(A, Qin, col_off, U, Qprev, Bi, s);
+    else launch_seg_all<16>(A, Qin, col_off, U, Qprev, Bi, s);
     return 0;
   }
   if (b <= 1) launch_gather<1>(A, Qin, col_off, b, U, Qprev, Bi, s);

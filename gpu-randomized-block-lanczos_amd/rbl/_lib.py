@@ -31,6 +31,7 @@ RBL_OPT_DEVICE_BLOCKS = 3
 RBL_OPT_SPLIT_HALO = 4
 RBL_OPT_KEEP_CSR = 5
 RBL_OPT_FUSE = 6
+RBL_OPT_HALO_OVERLAP = 7
 
 _p = C.c_void_p
 _i64 = C.c_int64

@@ -97,6 +97,12 @@ extern "C" {
                                    *   several-rank form is tested with in-process ranks on one
                                    *   GPU; it has no run on several GPUs yet.               */
 
+#define RBL_OPT_HALO_OVERLAP  7   /* several ranks, unbanded A (the segmented gather, whose halo is
+                                   * most of Q_i): 1 (default) the halo exchange runs on a side
+                                   * stream while the SpMM multiplies the own-column part of
+                                   * each row, the halo-column part after it lands; 0 the same
+                                   * two parts after the exchange (same results, bit for bit) */
+
 typedef struct rbl_ctx rbl_ctx;
 
 int rbl_abi_version(void);

@@ -188,7 +188,8 @@ def circuit_like_csr(n: int = G3_CIRCUIT_N, seed: int = 20261015, plant=None, wi
     if plant is not None and len(plant):
         plant = np.asarray(plant, dtype=np.float64)
         stride = n // len(plant)
-        diag[np.arange(len(plant)) * stride] += plant
+        if stride > 0:  # (n < len(plant): no plant, as the device generator)
+            diag[np.arange(len(plant)) * stride] += plant
     # seeded symmetric permutation (node i -> perm[i]): a hash bijection the device generator
     # (gen.hip k_circ_fill) computes per row
     perm = scatter_perm(n, seed, np.arange(n, dtype=np.int64))

@@ -111,3 +111,67 @@ def test_rmat_multirank_lanczos(rbl):
             assert np.abs(a - a1).max() <= 1e-9 * np.abs(a1).max()
         for bb, bb1 in zip(info.trace_B, info1.trace_B):
             assert np.abs(bb - bb1).max() <= 1e-9 * np.abs(bb1).max()
+
+
+@pytest.mark.parametrize("tiers", ["64", "64,1024"])
+def test_rmat_column_tiers(rbl, tiers, monkeypatch):
+    """Column-tiered segmented gather (RBL_SEG_TIERS: the highest-degree columns swept first,
+    each tier its own CSR + task table, accumulated into U): the SpMM within 1e-13 |A||X| of
+    SciPy, and a fixed-step Lanczos trace equal to the one-sweep kernel's to 1e-12 (only each
+    row's sum order differs)."""
+    A = matgen.rmat_csr(CASE["n"], CASE["scale"], CASE["edges"], CASE["seed"],
+                        matgen.planted_spectrum(5))
+    X = np.random.default_rng(11).standard_normal((A.shape[0], 32))
+    infos = []
+    for env in (None, tiers):
+        if env is None:
+            monkeypatch.delenv("RBL_SEG_TIERS", raising=False)
+        else:
+            monkeypatch.setenv("RBL_SEG_TIERS", env)
+        with rbl.Context(0) as ctx:
+            ctx.gen_rmat(CASE["n"], CASE["scale"], CASE["edges"], CASE["seed"],
+                         matgen.planted_spectrum(5))
+            Y = ctx.apply(X)
+            _, _, info = rbl.lanczos(ctx, 5, 32, seed=9, check=False, max_steps=8, trace=True,
+                                     ritz=False)
+            infos.append(info)
+        bound = (abs(A) @ np.abs(X)) * 1e-13 + 1e-300
+        assert np.all(np.abs(Y - A @ X) <= bound)
+    for a0, a1 in zip(infos[0].trace_A, infos[1].trace_A):
+        assert np.abs(a0 - a1).max() <= 1e-12 * np.abs(a0).max()
+
+
+@pytest.mark.parametrize("P", [2, 3])
+def test_rmat_multirank_halo_overlap_bit_identical(rbl, P):
+    """Several ranks on an unbanded matrix: each rank's SpMM runs as two column tiers, the own
+    columns (gathered from the block itself while the halo exchange is in flight on a side
+    stream) and the halo columns (after the exchange lands).  RBL_OPT_HALO_OVERLAP only moves
+    the exchange off the SpMM's stream, so A_i / B_i are bit-identical with it on and off, and
+    equal the single-rank run to rounding; the collective counters see one exchange per SpMM."""
+    from rbl import _lib
+    plant = matgen.planted_spectrum(5)
+    steps = 8
+
+    def run(overlap):
+        def fn(ctx, r):
+            ctx.set_option(_lib.RBL_OPT_HALO_OVERLAP, overlap)
+            ctx.gen_rmat(CASE["n"], CASE["scale"], CASE["edges"], CASE["seed"], plant)
+            ctx.comm_stats(reset=True)
+            _, _, info = rbl.lanczos(ctx, 5, 32, seed=9, check=False, max_steps=steps,
+                                     trace=True, ritz=False)
+            return info, ctx.comm_stats()
+        return run_ranks(rbl, P, fn)
+
+    on, off = run(1), run(0)
+    with rbl.Context(0) as ctx:
+        ctx.gen_rmat(CASE["n"], CASE["scale"], CASE["edges"], CASE["seed"], plant)
+        _, _, single = rbl.lanczos(ctx, 5, 32, seed=9, check=False, max_steps=steps, trace=True,
+                                   ritz=False)
+    for (i_on, st_on), (i_off, st_off) in zip(on, off):
+        for a, a0 in zip(i_on.trace_A + i_on.trace_B, i_off.trace_A + i_off.trace_B):
+            assert np.array_equal(a, a0)
+        for a, a1 in zip(i_on.trace_A, single.trace_A):
+            assert np.abs(a - a1).max() <= 1e-9 * np.abs(a1).max()
+        assert st_on == st_off
+        assert st_on["exchange_calls"] == steps + 1      # rbl_start + one per block step
+        assert st_on["recv_bytes"] > 0 and st_on["allreduce_calls"] >= 4 * (steps - 1)

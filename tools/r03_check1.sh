@@ -4,7 +4,7 @@ set -u
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 timeout -k 10 900 python -u -m pytest -x -v -s --timeout 400 --timeout-method thread \
-  tests/test_gpu_spmm.py tests/test_gpu_rmat.py tests/test_gpu_c2_c3.py::test_c4b_rmat_1e6_vs_oracle \
+  tests/test_gpu_spmm.py tests/test_gpu_rmat.py tests/test_gpu_circuit.py tests/test_gpu_c2_c3.py \
   tests/test_gpu_rmat_fullsize.py \
   > gpurun_out/r03_t1.log 2>&1; rc=$?
 echo "tests rc=$rc"; tail -8 gpurun_out/r03_t1.log
