@@ -54,8 +54,9 @@ def parse():
     ap.add_argument("--kryl", type=int, default=1200)
     ap.add_argument("--cpu-sample-n", type=int, default=100_000,
                     help="rows of the CPU baseline's sample (same generator, same block steps)")
-    ap.add_argument("--cpu-one-thread", action="store_true",
-                    help="also time the CPU baseline with 1 BLAS thread (benchmark.jl:49)")
+    ap.add_argument("--no-cpu-one-thread", action="store_true",
+                    help="skip the CPU baseline's second timing at 1 BLAS thread (benchmark.jl:49 "
+                         "sets BLAS.set_num_threads(1); on by default)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-ttk", action="store_true")
     ap.add_argument("--no-ttk-slow", action="store_true",
@@ -208,12 +209,19 @@ def measure(ctx, args, matrix, K, W, nloc, nnz_loc, world, barrier, allmax):
     spmm_kernel = {1: "gather", 2: "lds-window", 3: "lds-band-mfma", 5: "band-tile-mfma",
                    6: "segmented-gather"}[spmm_kid]
 
+    host = {"start": 0.0, "enqueue": 0.0, "fetch_wait": 0.0}
+
     def one_run():
-        rbl.lanczos(ctx, k, b, kryl_sz=args.kryl, seed=args.seed + 1, check=False, ritz=False,
-                    basis_bits=args.basis_bits)
+        _, _, info = rbl.lanczos(ctx, k, b, kryl_sz=args.kryl, seed=args.seed + 1, check=False,
+                                 ritz=False, basis_bits=args.basis_bits)
+        host["start"] += info.start_ms
+        host["enqueue"] += info.enqueue_ms
+        host["fetch_wait"] += info.fetch_ms
 
     for _ in range(W):
         one_run()
+    for key in host:
+        host[key] = 0.0
     barrier()
     ctx.synchronize()
     ctx.reset_timers()
@@ -324,7 +332,11 @@ def measure(ctx, args, matrix, K, W, nloc, nnz_loc, world, barrier, allmax):
     # collectives per block step on this rank (all-reduces, grouped send/recv), from the library
     steps_timed = K * (m_max + 1)
     comm_per_step = {key: round(v / steps_timed, 3) for key, v in comm.items()}
+    # the host side of a run (rbl.lanczos): rbl_start (blocks until A Omega + QR are done),
+    # enqueueing the steps, and waiting in rbl_fetch for the last one
+    host_ms = {key: round(v / K, 1) for key, v in host.items()}
     return {"elapsed": elapsed, "stage": stage, "value": value, "roofline": roofline,
+            "host_ms_per_run": host_ms,
             "roofline_secondary": roofline2, "spmm_kernel": spmm_kernel,
             "comm_per_step": comm_per_step, "m_max": m_max}
 
@@ -506,6 +518,7 @@ def main():
             "roofline": roofline,
             "roofline_secondary": roofline2,
             "stage_ms_per_run": {s: round(v, 3) for s, v in stage_per_run.items()},
+            "host_ms_per_run": meas["host_ms_per_run"],
             "time_to_k": ttk,
             "time_to_k_slow_spectrum": ttk_slow,
             "matrix_gen_s": round(gen_s, 3),
@@ -661,10 +674,14 @@ def cpu_baseline(args, m_max, plant):
                      f"(nnz={A.nnz}) for the same {m_max} block steps: {t:.2f} s measured, i.e. "
                      f"{m_max / t:.4f} iters/s at n={ns}; value = that per-iteration time scaled "
                      f"x{scale:.0f} to n={args.n}",
+           "cross_check": "the same port at n = 1e6 (129 s on the box, profiles/r02_bench_cpu1e6.json) "
+                          "gave 0.0294 iters/s scaled to n = 1e7, ~10 % below this n = 1e5 "
+                          "extrapolation: the baseline is stated from the smaller sample to keep "
+                          "the default run within minutes",
            "sample_n": ns, "sample_seconds": round(t, 3),
            "sample_iters_per_s": round(m_max / t, 5),
            "host_cpus": os.cpu_count(), "cpu_model": cpu_model()}
-    if args.cpu_one_thread and threadpool_limits is not None:
+    if not args.no_cpu_one_thread and threadpool_limits is not None:
         with threadpool_limits(limits=1):
             t1 = timed()
         out.update({"value_1thread": round(m_max / (t1 * scale), 5),

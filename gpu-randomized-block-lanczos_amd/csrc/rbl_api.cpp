@@ -167,7 +167,7 @@ struct rbl_ctx {
 namespace {
 
 const char* kStageNames[RBL_NUM_STAGES] = {"AQ", "3-term", "qr", "part reorth", "loc reorth",
-                                           "Ritz vectors", "comm"};
+                                           "Ritz vectors", "comm", "spill wait"};
 
 int fail(rbl_ctx* c, int code, const std::string& msg) {
   if (c) c->err = msg;
@@ -2447,6 +2447,7 @@ int step_impl(rbl_ctx* ctx, int i, int part_reorth, double* A_out, double* B_out
   }
   // Q_{i+1} B_{i+1} = qr(U)   (RBL_gpu.jl:180-184)
   if (ctx->d2h_pending[i & 1]) {  // the working slot's previous block is on the host
+    StageScope t(ctx, RBL_STAGE_SPILL_WAIT);  // the stream stalls here until that copy is done
     HIPC(hipStreamWaitEvent(ctx->stream, ctx->ev_d2h[i & 1], 0));
     ctx->d2h_pending[i & 1] = false;
   }

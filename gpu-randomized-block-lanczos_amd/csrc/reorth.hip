@@ -58,6 +58,9 @@ constexpr int kG44Waves = 4;
 #ifndef RBL_G44_PF
 #define RBL_G44_PF 2
 #endif
+#ifndef RBL_G44_W16
+#define RBL_G44_W16 1
+#endif
 constexpr int kG44Rows = RBL_G44_ROWS;
 
 // PAIR (B = 16): a wave's "panel" j is the pair of basis panels 2j, 2j+1 (32 columns, as one
@@ -98,8 +101,12 @@ __device__ __forceinline__ void gram44_body(int64_t r_begin, int64_t r_end, int6
   const int xe0 = tid * EPT;
   const int xrow = xe0 / KC, xcol = xe0 % KC;
   const double* xsl = X.ptr[xcol / B] + (xcol % B) + (int64_t)xrow * B;
-  // column group ag of the wave's panel (PAIR: ag = the pair member)
-  const double* wl = W.base + (int64_t)(PAIR ? 2 * j : j) * W.stride + (lane & 15) + q * B;
+  // column group ag of the wave's panel (PAIR: ag = the pair member).  W16 (b = 32): lane
+  // column 2 (lane & 15) + ag, both ag in one 16-B load (W16 = 0: columns (lane & 15) + 16 ag,
+  // two 8-B loads); the MFMAs see the same operands per output, only C's row order differs
+  constexpr bool W16 = RBL_G44_W16 && !PAIR && AG == 2;
+  const double* wl = W.base + (int64_t)(PAIR ? 2 * j : j) * W.stride +
+                     (W16 ? 2 * (lane & 15) : (lane & 15)) + q * B;
   const int64_t wag = PAIR ? W.stride : 16;
   auto shift = [&](int64_t rc0) -> int64_t { return rc0 < r_end - kG44Rows ? rc0 : r_end - kG44Rows; };
   auto load_x = [&](int64_t rc0, double (&xr)[EPT]) {
@@ -115,10 +122,19 @@ __device__ __forceinline__ void gram44_body(int64_t r_begin, int64_t r_end, int6
   };
   auto load_a = [&](int64_t rc0, double (&ar)[KS][AG]) {
     const double* p = wl + shift(rc0) * B;
+    if constexpr (W16) {
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks)
+      for (int ks = 0; ks < KS; ++ks) {
+        const d2v v = ldw(reinterpret_cast<const d2v*>(p + 4 * ks * B));
+        ar[ks][0] = v.x;
+        ar[ks][AG - 1] = v.y;
+      }
+    } else {
 #pragma unroll
-      for (int ag = 0; ag < AG; ++ag) ar[ks][ag] = ldw(p + 4 * ks * B + wag * ag);
+      for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+        for (int ag = 0; ag < AG; ++ag) ar[ks][ag] = ldw(p + 4 * ks * B + wag * ag);
+    }
   };
 
   const int64_t nchunks = r_end > r_begin ? (r_end - r_begin + kG44Rows - 1) / kG44Rows : 0;
@@ -208,7 +224,7 @@ __device__ __forceinline__ void gram44_body(int64_t r_begin, int64_t r_end, int6
   for (int ag = 0; ag < AG; ++ag)
 #pragma unroll
     for (int cg = 0; cg < CGP; ++cg) {
-      const int a = 16 * ag + 4 * g + (lane >> 4);
+      const int a = W16 ? 2 * (4 * g + (lane >> 4)) + ag : 16 * ag + 4 * g + (lane >> 4);
       const int cc = 4 * cg + (lane & 3);
       out[(int64_t)a * KC + cc] = acc[ag][cg];
     }

@@ -6,6 +6,9 @@
 //
 // Q blocks are row-major n x b: the gather of Q[c,:] is one contiguous b*8-byte segment.
 // Memory-bound: algorithmic bytes nnz*(8+4) + (n+1)*8 + 2*n*b*8 per call.
+#include <algorithm>
+#include <cstdlib>
+
 #include "kernels.hpp"
 
 namespace rbl {

@@ -312,6 +312,7 @@ class RBLInfo:
     fetch_ms: float = 0.0        # host waits in rbl_fetch (the GPU finishing enqueued steps)
     ritz_ms: float = 0.0         # host wall time of rbl_ritz (device work + D2H of V)
     start_ms: float = 0.0        # host wall time of rbl_start (A Omega + QR)
+    enqueue_ms: float = 0.0      # host time inside rbl_step_async (enqueueing the steps)
     trace_A: list = field(default_factory=list)
     trace_B: list = field(default_factory=list)
 
@@ -360,9 +361,11 @@ def lanczos(ctx: Context, k: int, b: int, *, kryl_sz: int = KRYL_SZ_GPU, omega=N
 
     def enqueue(upto):
         nonlocal enq
+        t0 = time.perf_counter()
         while enq < upto:
             enq += 1
             ctx.step_async(enq, enq >= 2 and enq % 2 == 0)   # :164-184
+        info.enqueue_ms += (time.perf_counter() - t0) * 1e3
 
     first = 1                                      # first unfetched step
     i = 0

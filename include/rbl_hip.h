@@ -49,7 +49,9 @@ extern "C" {
 #define RBL_STAGE_LOC_REORTH  4   /* "loc reorth"    RBL_gpu.jl:167                               */
 #define RBL_STAGE_RITZ        5   /* "Ritz vectors"  RBL_gpu.jl:219                               */
 #define RBL_STAGE_COMM        6   /* halo exchange + all-reduce (no reference equivalent)         */
-#define RBL_NUM_STAGES        7
+#define RBL_STAGE_SPILL_WAIT  7   /* "spill wait": host spill, the step's QR waiting for the D2H
+                                   * copy-out of a finished block that shares its working slot  */
+#define RBL_NUM_STAGES        8
 
 /* Options for rbl_set_option(). */
 #define RBL_OPT_TIMERS        0   /* 1: record per-stage hipEvents (adds event records)         */
@@ -258,7 +260,8 @@ int rbl_timers(rbl_ctx* ctx, double* ms, int nstages);
 int rbl_reset_timers(rbl_ctx* ctx);
 /* Stage times accumulate (ms, hipEvents on the context stream) while RBL_OPT_TIMERS is
  * set; names are the reference's TimerOutputs labels (RBL_gpu.jl:153-186: "AQ", "3-term",
- * "qr", "part reorth", "loc reorth", "Ritz vectors") plus "comm" (halo + all-reduce).
+ * "qr", "part reorth", "loc reorth", "Ritz vectors") plus "comm" (halo + all-reduce) and
+ * "spill wait" (host spill: the stall on a block's copy-out).
  * rbl_synchronize waits for the context's stream and folds finished events into them. */
 int rbl_synchronize(rbl_ctx* ctx);
 

@@ -34,7 +34,7 @@ def test_abi_version_and_stage_names():
     from rbl import _lib
     assert _lib.lib.rbl_abi_version() == 1
     assert _lib.stage_names() == ["AQ", "3-term", "qr", "part reorth", "loc reorth",
-                                  "Ritz vectors", "comm"]
+                                  "Ritz vectors", "comm", "spill wait"]
 
 
 @pytest.mark.parametrize("W,p,seed", [(0, 0.5, 1), (3, 0.9, 2), (64, 0.7734, 20261015)])

@@ -5,7 +5,7 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 timeout -k 10 900 python -u -m pytest -x -v -s --timeout 400 --timeout-method thread \
   tests/test_gpu_circuit.py tests/test_gpu_rmat.py tests/test_gpu_c2_c3.py \
-  tests/test_gpu_rmat_fullsize.py tests/test_gpu_multirank.py \
+  tests/test_gpu_rmat_fullsize.py tests/test_gpu_multirank.py tests/test_gpu_parity.py tests/test_lib_host.py \
   > gpurun_out/r03_t2.log 2>&1; rc=$?
 echo "tests rc=$rc"; tail -8 gpurun_out/r03_t2.log
 [ $rc -ne 0 ] && exit $rc
