@@ -107,6 +107,7 @@ struct rbl_ctx {
   // j >= resident in working slot resident + (j & 1) while among the two newest, and in
   // pinned host slot j - resident once final (copied during step j + 2)
   int dev_blocks_opt = 0;
+  bool auto_planned = false;  // the current basis plan came from RBL_OPT_DEVICE_BLOCKS = -1
   int resident = INT32_MAX;
   // pinned host slots of the spilled blocks (block j at h_spill[j - resident]), pinned when
   // the block is first written out: host memory grows with the blocks a run really spills
@@ -2079,7 +2080,17 @@ int rbl_start(rbl_ctx* ctx, int b, int max_blocks, int basis_bits, const double*
   // per run costs more than the run itself at n = 1e7)
   // device slots of the basis (RBL_OPT_DEVICE_BLOCKS; RBL_gpu.jl:95-104 gpu_buffer_size)
   int dev_slots = max_blocks + 1;
-  if (ctx->dev_blocks_opt != 0) {
+  // the shape of the current plan matches: the automatic plan (G = -1) keeps its slot count
+  // instead of re-deriving it from the free memory its own buffers now occupy — re-planning
+  // frees and re-allocates the basis and unpins / re-pins every host spill slot (C5: ~40 s per
+  // run on the host, hipHostMalloc / hipHostFree of ~80 GB)
+  const bool same_shape = (ctx->d_basis || ctx->d_basis32) && ctx->b == b &&
+                          ctx->max_blocks == max_blocks && ctx->slot == ctx->nloc * b &&
+                          ctx->basis_bits == basis_bits;
+  const int cur_slots = ctx->resident == INT32_MAX ? ctx->max_blocks + 1 : ctx->resident + 2;
+  if (ctx->dev_blocks_opt < 0 && same_shape && ctx->auto_planned) {
+    dev_slots = cur_slots;
+  } else if (ctx->dev_blocks_opt != 0) {
     int g = ctx->dev_blocks_opt;
     if (g < 0) {
       size_t fr = 0, tot = 0;
@@ -2101,10 +2112,7 @@ int rbl_start(rbl_ctx* ctx, int b, int max_blocks, int basis_bits, const double*
     }
     dev_slots = std::min(dev_slots, std::max(3, g));
   }
-  const bool reuse = (ctx->d_basis || ctx->d_basis32) && ctx->b == b &&
-                     ctx->max_blocks == max_blocks && ctx->slot == ctx->nloc * b &&
-                     ctx->basis_bits == basis_bits &&
-                     (ctx->resident == INT32_MAX ? max_blocks + 1 : ctx->resident + 2) == dev_slots;
+  const bool reuse = same_shape && cur_slots == dev_slots;
   ctx->nlock = 0;  // a new problem: no locked vectors
   ctx->cloc_step = 0;
   ctx->step_flags.clear();
@@ -2120,6 +2128,7 @@ int rbl_start(rbl_ctx* ctx, int b, int max_blocks, int basis_bits, const double*
   ctx->slot = ctx->nloc * b;
   const int64_t nl = std::max<int64_t>(ctx->nloc, 1);
   ctx->basis_bits = basis_bits;
+  ctx->auto_planned = ctx->dev_blocks_opt < 0;
   if (basis_bits == 64) {
     HIPC(hipMalloc(&ctx->d_basis, (size_t)dev_slots * nl * b * sizeof(double)));
     if (dev_slots < max_blocks + 1) {  // host spill: pinned slots for blocks resident..max_blocks

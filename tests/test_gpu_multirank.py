@@ -259,3 +259,33 @@ def test_rccl_transport_selftest(rbl):
     st = _lib.lib.rbl_comm_selftest(0, msg, 256)
     assert st == _lib.RBL_OK, msg.value.decode()
     assert msg.value.decode() == "ok: rccl"
+
+
+def test_multirank_matrix_sequence_like_bench(rbl):
+    """bench.py's sequence on one context per rank: the hash-window run, then the R-MAT and the
+    circuit sub-records, each matrix generated in place of the last (every plan — halo, tiers,
+    basis — rebuilt).  On 2 in-process ranks each fixed-step trace equals the single-rank one."""
+    from oracle import matgen
+    plant = matgen.planted_spectrum(5)
+    gens = [lambda c: c.gen_hashwindow(3000, 64, 0.7734, 5, plant),
+            lambda c: c.gen_rmat(6000, 13, 120_000, 7, plant),
+            lambda c: c.gen_circuit(5000, 5, plant, width=71)]
+    shapes = [(32, 6), (32, 6), (16, 6)]
+
+    def run(ctx):
+        out = []
+        for g, (b, steps) in zip(gens, shapes):
+            g(ctx)
+            _, _, info = rbl.lanczos(ctx, 5, b, seed=3, check=False, max_steps=steps, trace=True,
+                                     ritz=False)
+            out.append(info)
+        return out
+
+    with rbl.Context(0) as ctx:
+        single = run(ctx)
+    for per_rank in run_ranks(rbl, 2, lambda ctx, r: run(ctx)):
+        for info, ref in zip(per_rank, single):
+            for a, a1 in zip(info.trace_A, ref.trace_A):
+                assert np.abs(a - a1).max() <= 1e-9 * np.abs(a1).max()
+            for bb, bb1 in zip(info.trace_B, ref.trace_B):
+                assert np.abs(bb - bb1).max() <= 1e-9 * np.abs(bb1).max()
