@@ -1,0 +1,49 @@
+#!/usr/bin/env python3
+"""Collectives per block step at P in-process ranks (LocalGroup on one GPU): the counts and
+bytes rbl_comm_stats reports for the bench's three patterns at a reduced n (the counts per step
+do not depend on n; the halo bytes scale with n and are extrapolated to the bench's n below).
+Usage: python tools/r03_comm_counts.py [P]"""
+import json
+import os
+import sys
+import threading
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "gpu-randomized-block-lanczos_amd")]
+import numpy as np  # noqa: E402
+import rbl  # noqa: E402
+
+P = int(sys.argv[1]) if len(sys.argv) > 1 else 8
+plant = np.array([100.0 * (41 - l) for l in range(1, 41)])
+cases = {
+    "hashwindow (C4a pattern)": (lambda c: c.gen_hashwindow(400_000, 64, 0.7734, 20261015, plant), 32, 400_000, 10_000_000),
+    "rmat (C4b pattern)": (lambda c: c.gen_rmat(400_000, 19, int(0.66 * 100 * 400_000), 20261015, plant), 32, 400_000, 10_000_000),
+    "circuit (C3 shape)": (lambda c: c.gen_circuit(1_585_478, 20261015, plant), 16, 1_585_478, 1_585_478),
+}
+out = {}
+for name, (gen, b, n, n_bench) in cases.items():
+    steps = 38 if b == 32 else 75
+    res = [None] * P
+    group = rbl.LocalGroup(P)
+
+    def worker(r):
+        with rbl.Context(0, group=group, rank=r) as ctx:
+            gen(ctx)
+            ctx.comm_stats(reset=True)
+            rbl.lanczos(ctx, 20, b, seed=3, check=False, ritz=False)
+            res[r] = ctx.comm_stats()
+
+    th = [threading.Thread(target=worker, args=(r,)) for r in range(P)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(600)
+    group.close()
+    spmm = steps + 1
+    per = {k: [round(s[k] / spmm, 2) for s in res] for k in res[0]}
+    scale = n_bench / n
+    out[name] = {"P": P, "b": b, "n_measured": n, "block_steps": steps,
+                 "per_spmm_step_by_rank": per,
+                 "recv_bytes_per_step_max_rank_at_bench_n": max(per["recv_bytes"]) * scale}
+    print(name, json.dumps(out[name]), flush=True)
+json.dump(out, open(os.path.join(ROOT, "gpurun_out", f"r03_comm_counts_P{P}.json"), "w"), indent=1)

@@ -19,4 +19,7 @@ timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun
   python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-ttk --rmat-steps 1 --c3-steps 1 \
   > gpurun_out/r03_prof_main.log 2>&1; rc=$?
 echo "prof rc=$rc"
+[ $rc -ne 0 ] && exit $rc
+timeout -k 10 600 python tools/r03_comm_counts.py 8 > gpurun_out/r03_comm_counts.log 2>&1; rc=$?
+echo "comm counts rc=$rc"; tail -3 gpurun_out/r03_comm_counts.log | cut -c1-400
 exit $rc
