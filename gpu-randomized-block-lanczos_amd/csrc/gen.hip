@@ -159,6 +159,46 @@ void circ_fill(int64_t n, int64_t width, double p, uint64_t seed, int64_t r0, in
                      seed, make_scatter(n, seed), r0, r1, rowptr, nplant, plant_dev, col, val);
 }
 
+// ---- indexed halo (several ranks, unbanded A): pack the rows peers asked for, mark the
+// columns a rank references outside its rows, renumber the halo tier's columns ----
+__global__ void k_gather_rows(const double* __restrict__ Q, const int32_t* __restrict__ idx,
+                              int64_t nrows, int b, double* __restrict__ out) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= nrows * b) return;
+  const int64_t i = e / b;
+  const int c = (int)(e - i * b);
+  out[e] = Q[(int64_t)idx[i] * b + c];
+}
+void gather_rows(const double* Q, const int32_t* idx, int64_t nrows, int b, double* out,
+                 hipStream_t s) {
+  const int64_t m = nrows * b;
+  if (m <= 0) return;
+  hipLaunchKernelGGL(k_gather_rows, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, Q, idx,
+                     nrows, b, out);
+}
+__global__ void k_mark_cols(const int32_t* __restrict__ col, int64_t nnz, int64_t r0, int64_t r1,
+                            uint8_t* mark) {
+  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < nnz;
+       k += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t c = col[k];
+    if (c < r0 || c >= r1) mark[c] = 1;  // idempotent byte stores: no atomics needed
+  }
+}
+void mark_cols(const int32_t* col, int64_t nnz, int64_t r0, int64_t r1, uint8_t* mark,
+               hipStream_t s) {
+  if (nnz <= 0) return;
+  hipLaunchKernelGGL(k_mark_cols, dim3(4096), dim3(256), 0, s, col, nnz, r0, r1, mark);
+}
+__global__ void k_remap_cols(int32_t* col, int64_t nnz, const int32_t* __restrict__ map) {
+  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < nnz;
+       k += (int64_t)gridDim.x * blockDim.x)
+    col[k] = map[col[k]];
+}
+void remap_cols(int32_t* col, int64_t nnz, const int32_t* map, hipStream_t s) {
+  if (nnz <= 0) return;
+  hipLaunchKernelGGL(k_remap_cols, dim3(4096), dim3(256), 0, s, col, nnz, map);
+}
+
 __global__ void k_randn(double* Q, int64_t nrows, int b, int64_t r0, uint64_t seed) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= nrows * b) return;

@@ -326,6 +326,13 @@ void circ_count(int64_t n, int64_t width, double p, uint64_t seed, int64_t r0, i
 void circ_fill(int64_t n, int64_t width, double p, uint64_t seed, int64_t r0, int64_t r1,
                const int64_t* rowptr, int nplant, const double* plant_dev, int32_t* col,
                double* val, hipStream_t s);
+// indexed halo (several ranks, unbanded A): out[i] = Q[idx[i]] (rows of b doubles); mark[c] = 1
+// for every column c outside [r0, r1); col[k] = map[col[k]]
+void gather_rows(const double* Q, const int32_t* idx, int64_t nrows, int b, double* out,
+                 hipStream_t s);
+void mark_cols(const int32_t* col, int64_t nnz, int64_t r0, int64_t r1, uint8_t* mark,
+               hipStream_t s);
+void remap_cols(int32_t* col, int64_t nnz, const int32_t* map, hipStream_t s);
 void hw_count(int64_t n, int64_t W, double p, uint64_t seed, int64_t r0, int64_t r1,
               int32_t* counts, hipStream_t s);
 void hw_fill(int64_t n, int64_t W, double p, uint64_t seed, int64_t r0, int64_t r1,

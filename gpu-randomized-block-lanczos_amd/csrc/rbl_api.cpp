@@ -72,6 +72,15 @@ struct rbl_ctx {
   int seg_ntiers = 0;
   SegTierBuf seg_tier[3];
   bool seg_split = false;             // several ranks: tiers = own / halo columns
+  // indexed halo (with seg_split): the halo tier's columns renumbered to ghost slots
+  // [0, n_ghost) in d_qext, grouped by owning rank; each step every rank packs the rows its
+  // peers asked for (d_send_idx, local row ids grouped by peer) and sends only those
+  bool ghost = false;
+  int64_t n_ghost = 0, n_send = 0;
+  std::vector<int64_t> ghost_cnt, ghost_off, send_cnt, send_off;
+  int32_t* d_send_idx = nullptr;
+  double* d_sendbuf = nullptr;        // n_send x b, per run
+  const double* ghost_local = nullptr;  // the block the last exchange sent from
   bool halo_overlap = true;           // RBL_OPT_HALO_OVERLAP
   hipStream_t hstream = nullptr;      // the overlapped halo exchange
   hipEvent_t ev_qready = nullptr, ev_halo = nullptr;
@@ -382,6 +391,9 @@ void free_tiers(rbl_ctx* ctx) {
   for (auto& T : ctx->seg_tier) free_seg(T, true);
   ctx->seg_ntiers = 0;
   ctx->seg_split = false;
+  hipFree(ctx->d_send_idx); ctx->d_send_idx = nullptr;
+  ctx->ghost = false;
+  ctx->n_ghost = ctx->n_send = 0;
 }
 
 int prepare_segments(rbl_ctx* ctx, const std::vector<int64_t>& rp) {
@@ -401,6 +413,87 @@ int prepare_segments(rbl_ctx* ctx, const std::vector<int64_t>& rp) {
 
 int build_tiers(rbl_ctx* ctx, const std::vector<uint8_t>& tier_of, int nt);
 
+// nonzeros of tier t (its row pointer's last entry)
+int64_t tier_nnz(rbl_ctx* ctx, int t) {
+  int64_t v = 0;
+  if (ctx->seg_tier[t].rowptr && ctx->nloc > 0)
+    (void)hipMemcpy(&v, ctx->seg_tier[t].rowptr + ctx->nloc, sizeof(int64_t), hipMemcpyDeviceToHost);
+  return v;
+}
+
+// Indexed halo: the columns this rank references outside its rows become ghost slots (sorted by
+// global id, so grouped by owner); the ranks exchange how many rows, then which rows, each asks
+// of each; *d_map (device, n int32) maps a ghost column to its slot (caller frees).
+int build_ghosts(rbl_ctx* ctx, int32_t** d_map) {
+  const int P = ctx->nranks, me = ctx->rank;
+  const int64_t n = ctx->n;
+  uint8_t* d_mark = nullptr;
+  HIPC(hipMalloc(&d_mark, std::max<int64_t>(n, 1)));
+  HIPC(hipMemsetAsync(d_mark, 0, n, ctx->stream));
+  mark_cols(ctx->d_col, ctx->nnz, ctx->r0, ctx->r1, d_mark, ctx->stream);
+  HIPC(hipGetLastError());
+  std::vector<uint8_t> mark(n);
+  HIPC(hipMemcpyAsync(mark.data(), d_mark, n, hipMemcpyDeviceToHost, ctx->stream));
+  HIPC(hipStreamSynchronize(ctx->stream));
+  hipFree(d_mark);
+  std::vector<int32_t> map(n, 0);
+  std::vector<int64_t> req;  // global ids of the ghost rows, ascending
+  ctx->ghost_cnt.assign(P, 0);
+  ctx->ghost_off.assign(P, 0);
+  for (int q = 0; q < P; ++q) {
+    ctx->ghost_off[q] = (int64_t)req.size();
+    if (q == me) continue;
+    for (int64_t c = ctx->bounds[q]; c < ctx->bounds[q + 1]; ++c)
+      if (mark[c]) {
+        map[c] = (int32_t)req.size();
+        req.push_back(c);
+      }
+    ctx->ghost_cnt[q] = (int64_t)req.size() - ctx->ghost_off[q];
+  }
+  ctx->n_ghost = (int64_t)req.size();
+  // what each peer asks of me: row `me` of the all-gathered count table, column by column
+  std::vector<int64_t> all((size_t)P * P);
+  COMMC(ctx->comm->allgather_host(ctx->ghost_cnt.data(), all.data(), P, ctx->stream, &ctx->err));
+  ctx->send_cnt.assign(P, 0);
+  ctx->send_off.assign(P, 0);
+  int64_t ns = 0;
+  for (int q = 0; q < P; ++q) {
+    ctx->send_off[q] = ns;
+    ctx->send_cnt[q] = q == me ? 0 : all[(size_t)q * P + me];
+    ns += ctx->send_cnt[q];
+  }
+  ctx->n_send = ns;
+  // the request lists themselves, int64 ids carried as 8-byte words by the halo transport
+  DevBuf d_req, d_got;
+  HIPC(hipMalloc(&d_req.p, std::max<int64_t>(ctx->n_ghost, 1) * sizeof(int64_t)));
+  HIPC(hipMalloc(&d_got.p, std::max<int64_t>(ns, 1) * sizeof(int64_t)));
+  if (ctx->n_ghost)
+    HIPC(hipMemcpy(d_req.p, req.data(), ctx->n_ghost * sizeof(int64_t), hipMemcpyHostToDevice));
+  std::vector<Comm::Xfer> x(P);
+  for (int q = 0; q < P; ++q) {
+    if (q == me) continue;
+    x[q].send = d_req.d() + ctx->ghost_off[q];
+    x[q].nsend = (size_t)ctx->ghost_cnt[q];
+    x[q].recv = d_got.d() + ctx->send_off[q];
+    x[q].nrecv = (size_t)ctx->send_cnt[q];
+  }
+  COMMC(ctx->comm->exchange(x, ctx->stream, &ctx->err));
+  std::vector<int64_t> got(std::max<int64_t>(ns, 1));
+  HIPC(hipMemcpyAsync(got.data(), d_got.p, ns * sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
+  HIPC(hipStreamSynchronize(ctx->stream));
+  std::vector<int32_t> idx(std::max<int64_t>(ns, 1), 0);
+  for (int64_t i = 0; i < ns; ++i) {
+    const int64_t g = got[i] - ctx->r0;
+    if (g < 0 || g >= ctx->nloc) return fail(ctx, RBL_ERR_INVALID, "indexed halo: a peer asked for a row I do not own");
+    idx[i] = (int32_t)g;
+  }
+  HIPC(hipMalloc(&ctx->d_send_idx, std::max<int64_t>(ns, 1) * sizeof(int32_t)));
+  if (ns) HIPC(hipMemcpy(ctx->d_send_idx, idx.data(), ns * sizeof(int32_t), hipMemcpyHostToDevice));
+  HIPC(hipMalloc(d_map, std::max<int64_t>(n, 1) * sizeof(int32_t)));
+  HIPC(hipMemcpy(*d_map, map.data(), n * sizeof(int32_t), hipMemcpyHostToDevice));
+  return RBL_OK;
+}
+
 // Column tiers of the segmented gather (RBL_SEG_TIERS="h[,w]": the h highest-degree columns,
 // then the next w, then the rest; one rank, A symmetric so a column's degree is its row's).
 // The SpMM sweeps the tiers in order; each sweep's gathers hit a Q-row set sized for one cache
@@ -412,13 +505,28 @@ int prepare_tiers(rbl_ctx* ctx, const std::vector<int64_t>& rp) {
   free_tiers(ctx);
   if (ctx->seg_ntasks == 0 || ctx->nnz == 0) return RBL_OK;
   if (ctx->nranks > 1) {
-    if (ctx->bt_ng || ctx->band_ok16 || ctx->band_ok32 || ctx->window_ok16 || ctx->window_ok32 ||
-        ctx->dense)
-      return RBL_OK;  // a banded kernel runs: its halo is a few rows
+    // every rank must take the same branch (the setup below runs collectives)
+    const int64_t banded = (ctx->bt_ng || ctx->band_ok16 || ctx->band_ok32 || ctx->window_ok16 ||
+                            ctx->window_ok32 || ctx->dense) ? 1 : 0;
+    std::vector<int64_t> all(ctx->nranks);
+    COMMC(ctx->comm->allgather_host(&banded, all.data(), 1, ctx->stream, &ctx->err));
+    for (int64_t v : all)
+      if (v) return RBL_OK;  // a banded kernel runs: its halo is a few rows
     std::vector<uint8_t> tier_of(ctx->n, 1);
     for (int64_t c = ctx->r0; c < ctx->r1; ++c) tier_of[c] = 0;
-    CHK(build_tiers(ctx, tier_of, 2));
+    int32_t* d_map = nullptr;
+    CHK(build_ghosts(ctx, &d_map));
+    const int st = build_tiers(ctx, tier_of, 2);
+    if (st == RBL_OK) {
+      remap_cols(ctx->seg_tier[1].col, ctx->seg_tier[1].ntasks > 0 ? tier_nnz(ctx, 1) : 0, d_map,
+                 ctx->stream);
+      HIPC(hipGetLastError());
+      HIPC(hipStreamSynchronize(ctx->stream));
+    }
+    hipFree(d_map);
+    CHK(st);
     ctx->seg_split = true;
+    ctx->ghost = true;
     return RBL_OK;
   }
   const char* e = std::getenv("RBL_SEG_TIERS");
@@ -902,6 +1010,8 @@ int apply_A(rbl_ctx* ctx, const double* Qin, int64_t off, int b, double* U, cons
                                     "SpMM (b in {16, 32}) can run");
   if (!ctx->dense) {
     CsrDev A = csr(ctx);
+    // indexed halo: the own-column tier always reads the block the exchange sent from
+    if (!qloc && ctx->ghost && ctx->nranks > 1) qloc = ctx->ghost_local;
     if (qloc) {  // own rows from the block itself (halo_exchange without the local copy)
       A.qloc = qloc;
       A.loc_lo = ctx->r0;
@@ -1278,6 +1388,24 @@ int halo_exchange(rbl_ctx* ctx, const double* Q, const double** Qin, int64_t* of
   StageScope t(ctx, RBL_STAGE_COMM, st);
   const int b = ctx->b;
   double* ext = ctx->d_qext;
+  if (ctx->ghost) {  // indexed halo: pack the asked-for rows, receive into the ghost slots
+    gather_rows(Q, ctx->d_send_idx, ctx->n_send, b, ctx->d_sendbuf, st);
+    HIPC(hipGetLastError());
+    std::vector<Comm::Xfer> x(ctx->nranks);
+    for (int q = 0; q < ctx->nranks; ++q) {
+      if (q == ctx->rank) continue;
+      x[q].send = ctx->d_sendbuf + ctx->send_off[q] * b;
+      x[q].nsend = (size_t)ctx->send_cnt[q] * b;
+      x[q].recv = ext + ctx->ghost_off[q] * b;
+      x[q].nrecv = (size_t)ctx->ghost_cnt[q] * b;
+    }
+    COMMC(ctx->comm->exchange(x, st, &ctx->err));
+    count_exchange(ctx, x);
+    ctx->ghost_local = Q;
+    *Qin = ext;
+    *off = 0;
+    return RBL_OK;
+  }
   if (copy_local)
     HIPC(hipMemcpyAsync(ext + (ctx->r0 - ctx->ext_lo) * b, Q, ctx->nloc * b * sizeof(double),
                         hipMemcpyDeviceToDevice, st));
@@ -1355,6 +1483,7 @@ void free_run(rbl_ctx* ctx) {
   hipFree(ctx->d_U); ctx->d_U = nullptr;
   hipFree(ctx->d_T); ctx->d_T = nullptr;
   hipFree(ctx->d_qext); ctx->d_qext = nullptr;
+  hipFree(ctx->d_sendbuf); ctx->d_sendbuf = nullptr;
   hipFree(ctx->d_slab); ctx->d_slab = nullptr;
   hipFree(ctx->d_C); ctx->d_C = nullptr;
   hipFree(ctx->d_small); ctx->d_small = nullptr;
@@ -2040,17 +2169,22 @@ int rbl_apply(rbl_ctx* ctx, int b, const double* X, double* Y) {
   colmajor_to_rowmajor(x.d(), ctx->nloc, b, xr.d(), ctx->stream);
   const double* Qin = xr.d();
   int64_t off = 0;
+  DevBuf sendbuf;
   if (ctx->nranks > 1) {  // halo exchange through a private extended buffer
-    const int64_t ext_rows = std::max<int64_t>(ctx->ext_hi - ctx->ext_lo, 1);
+    const int64_t ext_rows = std::max<int64_t>(ctx->ghost ? ctx->n_ghost : ctx->ext_hi - ctx->ext_lo, 1);
     HIPC(hipMalloc(&ext.p, ext_rows * b * sizeof(double)));
     // rows between the received ranges stay finite (band-tile kernel multiplies them by 0)
     HIPC(hipMemsetAsync(ext.p, 0, ext_rows * b * sizeof(double), ctx->stream));
+    if (ctx->ghost) HIPC(hipMalloc(&sendbuf.p, std::max<int64_t>(ctx->n_send, 1) * b * sizeof(double)));
     double* keep_ext = ctx->d_qext;
+    double* keep_send = ctx->d_sendbuf;
     const int keep_b = ctx->b;
     ctx->d_qext = ext.d();
+    ctx->d_sendbuf = sendbuf.d();
     ctx->b = b;
     const int st = halo_exchange(ctx, xr.d(), &Qin, &off);
     ctx->d_qext = keep_ext;
+    ctx->d_sendbuf = keep_send;
     ctx->b = keep_b;
     if (st < 0) return st;
   }
@@ -2170,8 +2304,11 @@ int rbl_start(rbl_ctx* ctx, int b, int max_blocks, int basis_bits, const double*
   ctx->T_cols = b;
   HIPC(hipMalloc(&ctx->d_T, nl * b * sizeof(double)));
   if (ctx->nranks > 1) {
-    HIPC(hipMalloc(&ctx->d_qext, std::max<int64_t>(ctx->ext_hi - ctx->ext_lo, 1) * b * sizeof(double)));
-    HIPC(hipMemsetAsync(ctx->d_qext, 0, std::max<int64_t>(ctx->ext_hi - ctx->ext_lo, 1) * b * sizeof(double), ctx->stream));
+    const int64_t ext_rows = std::max<int64_t>(ctx->ghost ? ctx->n_ghost : ctx->ext_hi - ctx->ext_lo, 1);
+    HIPC(hipMalloc(&ctx->d_qext, ext_rows * b * sizeof(double)));
+    HIPC(hipMemsetAsync(ctx->d_qext, 0, ext_rows * b * sizeof(double), ctx->stream));
+    if (ctx->ghost)
+      HIPC(hipMalloc(&ctx->d_sendbuf, std::max<int64_t>(ctx->n_send, 1) * b * sizeof(double)));
   }
   const size_t slab = gram_slab_elems(ctx, b, max_blocks, basis_bits);
   ctx->slab_elems = slab;

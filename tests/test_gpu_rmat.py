@@ -145,7 +145,8 @@ def test_rmat_column_tiers(rbl, tiers, monkeypatch):
 def test_rmat_multirank_halo_overlap_bit_identical(rbl, P):
     """Several ranks on an unbanded matrix: each rank's SpMM runs as two column tiers, the own
     columns (gathered from the block itself while the halo exchange is in flight on a side
-    stream) and the halo columns (after the exchange lands).  RBL_OPT_HALO_OVERLAP only moves
+    stream) and the halo columns (after the exchange lands), renumbered to the ghost rows the
+    indexed halo delivers — only the rows a rank's columns reference.  RBL_OPT_HALO_OVERLAP only moves
     the exchange off the SpMM's stream, so A_i / B_i are bit-identical with it on and off, and
     equal the single-rank run to rounding; the collective counters see one exchange per SpMM."""
     from rbl import _lib
@@ -156,10 +157,13 @@ def test_rmat_multirank_halo_overlap_bit_identical(rbl, P):
         def fn(ctx, r):
             ctx.set_option(_lib.RBL_OPT_HALO_OVERLAP, overlap)
             ctx.gen_rmat(CASE["n"], CASE["scale"], CASE["edges"], CASE["seed"], plant)
+            _, r0, r1, _ = ctx.matrix_info()
+            _, col, _ = ctx.get_matrix_csr()
+            ghosts = np.unique(col[(col < r0) | (col >= r1)]).size
             ctx.comm_stats(reset=True)
             _, _, info = rbl.lanczos(ctx, 5, 32, seed=9, check=False, max_steps=steps,
                                      trace=True, ritz=False)
-            return info, ctx.comm_stats()
+            return info, ctx.comm_stats(), ghosts
         return run_ranks(rbl, P, fn)
 
     on, off = run(1), run(0)
@@ -167,11 +171,52 @@ def test_rmat_multirank_halo_overlap_bit_identical(rbl, P):
         ctx.gen_rmat(CASE["n"], CASE["scale"], CASE["edges"], CASE["seed"], plant)
         _, _, single = rbl.lanczos(ctx, 5, 32, seed=9, check=False, max_steps=steps, trace=True,
                                    ritz=False)
-    for (i_on, st_on), (i_off, st_off) in zip(on, off):
+    for (i_on, st_on, ghosts), (i_off, st_off, _) in zip(on, off):
         for a, a0 in zip(i_on.trace_A + i_on.trace_B, i_off.trace_A + i_off.trace_B):
             assert np.array_equal(a, a0)
         for a, a1 in zip(i_on.trace_A, single.trace_A):
             assert np.abs(a - a1).max() <= 1e-9 * np.abs(a1).max()
         assert st_on == st_off
         assert st_on["exchange_calls"] == steps + 1      # rbl_start + one per block step
-        assert st_on["recv_bytes"] > 0 and st_on["allreduce_calls"] >= 4 * (steps - 1)
+        # indexed halo: each exchange receives exactly the rows the rank's columns reference
+        assert st_on["recv_bytes"] == (steps + 1) * ghosts * 32 * 8 > 0
+        assert st_on["allreduce_calls"] >= 4 * (steps - 1)
+
+
+def test_rmat_indexed_halo_small_and_ragged(rbl):
+    """The indexed halo at the edges: n = 700 on 4 ranks (a hub-heavy first rank with few
+    rows, peers that need nothing from some ranks), b = 16 and b = 32; the fixed-step traces
+    equal the single-rank ones, and rbl_apply through the ghost exchange matches SciPy."""
+    plant = matgen.planted_spectrum(3)
+    n, scale, edges, seed = 700, 10, 30_000, 13
+    A = matgen.rmat_csr(n, scale, edges, seed, plant)
+    X = np.random.default_rng(5).standard_normal((n, 16))
+    for b in (16, 32):
+        def run(ctx):
+            ctx.gen_rmat(n, scale, edges, seed, plant)
+            _, _, info = rbl.lanczos(ctx, 3, b, seed=2, check=False, max_steps=6, trace=True,
+                                     ritz=False)
+            return info
+
+        with rbl.Context(0) as ctx:
+            ref = run(ctx)
+
+        def fn(ctx, r):
+            info = run(ctx)
+            _, r0, r1, _ = ctx.matrix_info()
+            return info, r0, r1
+
+        out = run_ranks(rbl, 4, fn)
+        for info, _, _ in out:
+            for a, a1 in zip(info.trace_A, ref.trace_A):
+                assert np.abs(a - a1).max() <= 1e-9 * np.abs(a1).max()
+
+    def fa(ctx, r):
+        ctx.gen_rmat(n, scale, edges, seed, plant)
+        _, r0, r1, _ = ctx.matrix_info()
+        return r0, ctx.apply(X[r0:r1])
+
+    parts = sorted(run_ranks(rbl, 4, fa), key=lambda t: t[0])
+    Y = np.vstack([y for _, y in parts])
+    bound = (abs(A) @ np.abs(X)) * 1e-13 + 1e-300
+    assert np.all(np.abs(Y - A @ X) <= bound)
