@@ -61,11 +61,34 @@ constexpr int kG44Waves = 4;
 #ifndef RBL_G44_W16
 #define RBL_G44_W16 1
 #endif
+#ifndef RBL_G44_GLDS
+#define RBL_G44_GLDS 1
+#endif
 constexpr int kG44Rows = RBL_G44_ROWS;
+typedef __attribute__((address_space(3))) void* lds_vptr;
+typedef __attribute__((address_space(1))) void* glb_vptr;
+constexpr int kLine = 136;  // doubles per LDS-DMA line: 1 KiB + 64 B pad
+
+// GL (k_gram44): the X chunk (16 rows x KC, KC = 32 or 64) is staged by LDS-DMA
+// (global_load_lds_dwordx4) into 1-KiB lines padded to 1088 B, row R at line
+// (R & 3) + 4 ((R >> 2) / RPL), slot (R >> 2) % RPL: the rows 4ks + q (q = 0..3) one
+// ds_read_b128 touches sit in 4 lines (conflict-free, lane offset q * 1088 + 16 (lane & 3)).
+// Columns in natural order: lane (lane & 3) reads columns 8cp + 2(lane & 3) + {0, 1} (the
+// register path stores perm8 order), which changes only the accumulator -> column map.  The
+// rows of a shifted last chunk below rc0 are zeroed in LDS after the DMA lands.
+template <int KC>
+struct G44Lines {
+  static constexpr int RPL = 1024 / (8 * KC);
+  static constexpr int NL = kG44Rows * KC * 8 / 1024;  // lines per chunk
+  __host__ __device__ static constexpr int off(int R) {
+    return ((R & 3) + 4 * ((R >> 2) / RPL)) * kLine + ((R >> 2) % RPL) * KC;
+  }
+  __host__ __device__ static constexpr int row(int L, int s) { return 4 * (s + RPL * (L >> 2)) + (L & 3); }
+};
 
 // PAIR (B = 16): a wave's "panel" j is the pair of basis panels 2j, 2j+1 (32 columns, as one
 // B = 32 panel: the same registers and MFMAs per chunk), so b = 16 runs the b = 32 tile shape
-template <int B, int NX, int NPH, bool PAIR = false>
+template <int B, int NX, int NPH, bool PAIR = false, bool GL = false>
 __device__ __forceinline__ void gram44_body(int64_t r_begin, int64_t r_end, int64_t s, int pg,
                                             int r, const PanelRun& W, const Panels& X,
                                             double* slab, double* xs_base) {
@@ -78,7 +101,10 @@ __device__ __forceinline__ void gram44_body(int64_t r_begin, int64_t r_end, int6
   constexpr int EPT = kG44Rows * KC / (kG44Waves * 64);
   constexpr int KS = kG44Rows / 4;
   static_assert(CGP >= 2 && CGP % 2 == 0, "column split");
-  double(*xs)[kG44Rows * LD] = reinterpret_cast<double(*)[kG44Rows * LD]>(xs_base);
+  using GLn = G44Lines<KC>;
+  static_assert(!GL || ((KC == 32 || KC == 64) && kG44Rows == 16 && GLn::NL % kG44Waves == 0), "GL shape");
+  constexpr int XB = GL ? GLn::NL * kLine : kG44Rows * LD;  // doubles per X buffer
+  double(*xs)[XB] = reinterpret_cast<double(*)[XB]>(xs_base);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int q = lane >> 4;
   const int j = pg * kG44Waves + wave % r;  // panel
@@ -120,6 +146,23 @@ __device__ __forceinline__ void gram44_body(int64_t r_begin, int64_t r_end, int6
 #pragma unroll
     for (int v = 0; v < EPT; ++v) xs[buf][xrow * LD + perm8(xcol + v)] = ok ? xr[v] : 0.0;
   };
+  // GL: this wave's lines of the chunk; lane -> slot lane / (KC / 2), column 2 (lane % (KC / 2))
+  const double* gl_src[GL ? GLn::NL / kG44Waves : 1];
+  if constexpr (GL) {
+    const int col = 2 * (lane % (KC / 2));
+    const double* xp = col >= B ? X.ptr[NX - 1] : X.ptr[0];
+#pragma unroll
+    for (int i = 0; i < GLn::NL / kG44Waves; ++i)
+      gl_src[i] = xp + (int64_t)GLn::row(wave * (GLn::NL / kG44Waves) + i, lane / (KC / 2)) * B + col % B;
+  }
+  auto dma_x = [&](int buf, int64_t rc0) {
+    const int64_t rb = shift(rc0) * B;
+#pragma unroll
+    for (int i = 0; i < GLn::NL / kG44Waves; ++i)
+      __builtin_amdgcn_global_load_lds((glb_vptr)(gl_src[i] + rb),
+                                       (lds_vptr)(xs[buf] + (wave * (GLn::NL / kG44Waves) + i) * kLine),
+                                       16, 0, 0);
+  };
   auto load_a = [&](int64_t rc0, double (&ar)[KS][AG]) {
     const double* p = wl + shift(rc0) * B;
     if constexpr (W16) {
@@ -137,39 +180,49 @@ __device__ __forceinline__ void gram44_body(int64_t r_begin, int64_t r_end, int6
     }
   };
 
-  const int64_t nchunks = r_end > r_begin ? (r_end - r_begin + kG44Rows - 1) / kG44Rows : 0;
+  auto mma = [&](const double* xbuf, const double (&acur)[KS][AG]) {
+    const double* xb = GL ? xbuf + 8 * cp0 + q * kLine + 2 * (lane & 3) : xbuf + 8 * cp0;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+#pragma unroll
+      for (int cp = 0; cp < CGP / 2; ++cp) {  // column groups 2cp, 2cp+1 in one 16-B read
+        const d2v bf = GL ? *reinterpret_cast<const d2v*>(xb + GLn::off(4 * ks) + 8 * cp)
+                          : *reinterpret_cast<const d2v*>(xb + (4 * ks + q) * LD + 8 * cp + 2 * (lane & 3));
+#pragma unroll
+        for (int ag = 0; ag < AG; ++ag) {
+          acc[ag][2 * cp] = mfma4(acur[ks][ag], bf.x, acc[ag][2 * cp]);
+          acc[ag][2 * cp + 1] = mfma4(acur[ks][ag], bf.y, acc[ag][2 * cp + 1]);
+        }
+      }
+    }
+  };
+
+  // GL: the loop covers whole chunks only; a last partial chunk (shifted back, rows below
+  // rc0 zeroed) goes through the register path after it
+  const int64_t nchunks = r_end > r_begin ? (r_end - r_begin + (GL ? 0 : kG44Rows - 1)) / kG44Rows : 0;
   double xr[EPT];
 #if RBL_G44_PF >= 2
   // basis operands two chunks ahead in three rotating register sets (no copies: a copy of a
   // landing prefetch would make the wave wait for it one chunk early)
   double a0[KS][AG], a1[KS][AG], a2[KS][AG];
   if (nchunks > 0) {
-    load_x(r_begin, xr);
-    store_x(0, r_begin, xr);
+    if constexpr (GL) {
+      dma_x(0, r_begin);
+    } else {
+      load_x(r_begin, xr);
+      store_x(0, r_begin, xr);
+    }
     load_a(r_begin, a0);
     load_a(r_begin + kG44Rows, a1);
   }
   __syncthreads();
   auto step = [&](int64_t c, const double (&acur)[KS][AG], double (&afut)[KS][AG]) {
     const int64_t rc0 = r_begin + c * kG44Rows;
-    load_x(rc0 + kG44Rows, xr);
+    if constexpr (GL) dma_x((int)((c + 1) & 1), rc0 + kG44Rows);
+    else load_x(rc0 + kG44Rows, xr);
     load_a(rc0 + 2 * kG44Rows, afut);
-    const double* xb = xs[c & 1] + 8 * cp0;
-    if (active && c < nchunks) {  // no loads inside: the vmcnt bookkeeping is unaffected
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) {
-#pragma unroll
-        for (int cp = 0; cp < CGP / 2; ++cp) {
-          const d2v bf = *reinterpret_cast<const d2v*>(xb + (4 * ks + q) * LD + 8 * cp + 2 * (lane & 3));
-#pragma unroll
-          for (int ag = 0; ag < AG; ++ag) {
-            acc[ag][2 * cp] = mfma4(acur[ks][ag], bf.x, acc[ag][2 * cp]);
-            acc[ag][2 * cp + 1] = mfma4(acur[ks][ag], bf.y, acc[ag][2 * cp + 1]);
-          }
-        }
-      }
-    }
-    store_x((int)((c + 1) & 1), rc0 + kG44Rows, xr);
+    if (active && c < nchunks) mma(xs[c & 1], acur);  // no loads inside: vmcnt bookkeeping unaffected
+    if constexpr (!GL) store_x((int)((c + 1) & 1), rc0 + kG44Rows, xr);
     __syncthreads();
   };
   for (int64_t c = 0; c < nchunks; c += 3) {
@@ -177,7 +230,22 @@ __device__ __forceinline__ void gram44_body(int64_t r_begin, int64_t r_end, int6
     step(c + 1, a1, a0);
     step(c + 2, a2, a1);
   }
+  if constexpr (GL) {
+    const int64_t rc0 = r_begin + nchunks * kG44Rows;
+    if (rc0 < r_end) {  // every DMA has landed (closing barrier of the last step)
+      load_x(rc0, xr);
+      load_a(rc0, a0);
+#pragma unroll
+      for (int v = 0; v < EPT; ++v) {
+        const int64_t row = shift(rc0) + xrow;
+        xs[0][GLn::off(xrow) + xcol + v] = row >= rc0 ? xr[v] : 0.0;
+      }
+      __syncthreads();
+      if (active) mma(xs[0], a0);
+    }
+  }
 #else
+  static_assert(!GL, "GL: PF = 2 only");
   double acur[KS][AG], anext[KS][AG];
   if (nchunks > 0) {
     load_x(r_begin, xr);
@@ -191,21 +259,7 @@ __device__ __forceinline__ void gram44_body(int64_t r_begin, int64_t r_end, int6
     // waitcnt pass merge a no-load path and drain the prefetch before the MFMAs
     load_x(rc0 + kG44Rows, xr);
     if (!(RBL_REORTH_ABL & 1)) load_a(rc0 + kG44Rows, anext);
-    const double* xb = xs[c & 1] + 8 * cp0;
-    if (active) {  // idle waves (a 3-panel group) only help stage X
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) {
-#pragma unroll
-        for (int cp = 0; cp < CGP / 2; ++cp) {  // column groups 2cp, 2cp+1 in one 16-B read
-          const d2v bf = *reinterpret_cast<const d2v*>(xb + (4 * ks + q) * LD + 8 * cp + 2 * (lane & 3));
-#pragma unroll
-          for (int ag = 0; ag < AG; ++ag) {
-            acc[ag][2 * cp] = mfma4(acur[ks][ag], bf.x, acc[ag][2 * cp]);
-            acc[ag][2 * cp + 1] = mfma4(acur[ks][ag], bf.y, acc[ag][2 * cp + 1]);
-          }
-        }
-      }
-    }
+    if (active) mma(xs[c & 1], acur);  // idle waves (a 3-panel group) only help stage X
     // unconditional as well: a consumer under `if (more)` lets LLVM sink the loads into it
     // (after the MFMAs); on the last chunk this writes the dead spare buffer
     if (!(RBL_REORTH_ABL & 4)) store_x((int)((c + 1) & 1), rc0 + kG44Rows, xr);
@@ -225,12 +279,12 @@ __device__ __forceinline__ void gram44_body(int64_t r_begin, int64_t r_end, int6
 #pragma unroll
     for (int cg = 0; cg < CGP; ++cg) {
       const int a = W16 ? 2 * (4 * g + (lane >> 4)) + ag : 16 * ag + 4 * g + (lane >> 4);
-      const int cc = 4 * cg + (lane & 3);
+      const int cc = GL ? 8 * (cg >> 1) + 2 * (lane & 3) + (cg & 1) : 4 * cg + (lane & 3);
       out[(int64_t)a * KC + cc] = acc[ag][cg];
     }
 }
 
-template <int B, int NX, bool PAIR = false>
+template <int B, int NX, bool PAIR = false, bool GL = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RBL_G44_WPE))) void k_gram44(
     int64_t nrows, PanelRun W, Panels X, double* slab, int npg, int64_t rows_per, const int* skip) {
   if (skip && *skip) return;
@@ -238,7 +292,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RBL_G44_WPE
   constexpr int CG = KC / 4;
   constexpr int NPH2 = CG / 2 >= 2 ? 2 : 1;
   constexpr int NPH4 = CG / 2 >= 4 ? 4 : NPH2;
-  __shared__ __attribute__((aligned(16))) double xs[2 * kG44Rows * (KC + 8)];
+  constexpr int XS = GL ? 2 * G44Lines<KC>::NL * kLine : 2 * kG44Rows * (KC + 8);
+  __shared__ __attribute__((aligned(16))) double xs[XS];
   // XCD-aware mapping: the npg workgroups of one row split share blockIdx % 8 (one XCD under
   // round-robin dispatch) and are consecutive there, so X is fetched once per XCD L2.
   const int bid = blockIdx.x;
@@ -249,9 +304,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RBL_G44_WPE
   const int64_t r_end = r_begin + rows_per < nrows ? r_begin + rows_per : nrows;
   const int rem = (PAIR ? W.count / 2 : W.count) - pg * kG44Waves;
   const int r = rem < kG44Waves ? rem : kG44Waves;  // panels in this group (workgroup-uniform)
-  if (r >= 3) gram44_body<B, NX, 1, PAIR>(r_begin, r_end, s, pg, r, W, X, slab, xs);
-  else if (r == 2) gram44_body<B, NX, NPH2, PAIR>(r_begin, r_end, s, pg, r, W, X, slab, xs);
-  else gram44_body<B, NX, NPH4, PAIR>(r_begin, r_end, s, pg, r, W, X, slab, xs);
+  if (r >= 3) gram44_body<B, NX, 1, PAIR, GL>(r_begin, r_end, s, pg, r, W, X, slab, xs);
+  else if (r == 2) gram44_body<B, NX, NPH2, PAIR, GL>(r_begin, r_end, s, pg, r, W, X, slab, xs);
+  else gram44_body<B, NX, NPH4, PAIR, GL>(r_begin, r_end, s, pg, r, W, X, slab, xs);
 }
 
 bool gram44_ok(int64_t nrows, int nW, int w, int xcount, int xw) {
@@ -277,8 +332,15 @@ static void launch_gram44(int64_t nrows, const PanelRun& W, const Panels& X, dou
   const int npg = (units + kG44Waves - 1) / kG44Waves;
   int64_t rows_per = (nrows + splits - 1) / splits;
   rows_per = (rows_per + kG44Rows - 1) / kG44Rows * kG44Rows;
-  hipLaunchKernelGGL((k_gram44<B, NX, PAIR>), dim3(npg * splits), dim3(256), 0, st, nrows, W, X, slab,
-                     npg, rows_per, skip);
+  constexpr bool kGL = RBL_G44_GLDS && RBL_G44_PF >= 2 && kG44Rows == 16 && (NX * B == 32 || NX * B == 64);
+  bool gl = kGL;
+  for (int t = 0; t < X.count; ++t) gl &= reinterpret_cast<uintptr_t>(X.ptr[t]) % 16 == 0;
+  if (gl)
+    hipLaunchKernelGGL((k_gram44<B, NX, PAIR, kGL>), dim3(npg * splits), dim3(256), 0, st, nrows, W, X,
+                       slab, npg, rows_per, skip);
+  else
+    hipLaunchKernelGGL((k_gram44<B, NX, PAIR, false>), dim3(npg * splits), dim3(256), 0, st, nrows, W, X,
+                       slab, npg, rows_per, skip);
 }
 
 void gram44_partial(int64_t nrows, const PanelRun& W, const Panels& X, double* slab, int splits,
@@ -305,7 +367,12 @@ void gram44_partial(int64_t nrows, const PanelRun& W, const Panels& X, double* s
 // A operands read 2 k per 16-B load (k permuted consistently in A and B), next chunk's A
 // prefetched while the current one computes.
 // ----------------------------------------------------------------------------------------
-constexpr int kT44Rows = 32;   // rows per wave
+constexpr int kT44Rows = 32;   // rows per wave (k_tsmm44)
+#ifndef RBL_T44_NRT
+#define RBL_T44_NRT 2
+#endif
+constexpr int kT44fNrt = RBL_T44_NRT;      // 16-row tiles per wave (k_tsmm44f)
+constexpr int kT44fRows = 16 * kT44fNrt;   // rows per wave (k_tsmm44f)
 constexpr int kT44K = 32;      // k per chunk
 
 template <int B, int KYP, bool F32X = false>
@@ -475,8 +542,35 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
 // final rows (16x16x4 MFMAs from the output stage) into xslab[blockIdx] (one 32 x 32 partial
 // per 128-row tile) — the local-reorth coefficient of the same step (RBL_gpu.jl:87), formed
 // while the partial-reorth update writes the blocks instead of in another pass over both.
-template <int B, int KC = RBL_T44_KC, int PF = RBL_T44_PF, bool XG = false, int KYP = 64>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k_tsmm44f(
+// GL: the C chunk is staged by LDS-DMA (global_load_lds_dwordx4: no VGPRs, no ds_write) into
+// 1-KiB lines padded to 1088 B; a C row (KYP doubles) lies whole in one line slot, rows placed
+// so that the 4 rows one ds_read_b128 touches (k = 8h + v + 2q, q = 0..3) sit in 4 lines:
+// conflict-free reads with a lane offset q * 1088 + 16 (lane & 3) and compile-time rest.  Lane
+// (lane & 3) then reads columns 8cp + 2(lane & 3) + {0, 1} (GL = false: perm8 order, columns
+// 4(2cp) + (lane & 3) and 4(2cp+1) + (lane & 3)); only the accumulator -> column map differs,
+// every output sums the same products in the same order.  Needs C 16-B aligned, ldc even.
+// Off by default: bit-identical, VALU per MFMA 0.273 -> 0.220, but MFMA busy 0.827 -> 0.802 and
+// 0.8 % slower over 5 alternating probe reps (profiles/r03_pmc_reorth_glds.txt)
+#ifndef RBL_T44_GLDS
+#define RBL_T44_GLDS 0
+#endif
+template <int KYP>
+struct T44Lines {
+  static constexpr int RPL = 1024 / (8 * KYP);  // C rows per 1-KiB line (2 or 4)
+  static constexpr int LINE = kLine;            // doubles per padded line (1088 B)
+  // row R = 8h + v + 2q of a chunk -> (line, slot); inverse for the DMA writer
+  __device__ static constexpr int line(int R) {
+    return RPL == 2 ? R >> 1 : 4 * (R >> 4) + ((R >> 1) & 3);
+  }
+  __device__ static constexpr int slot(int R) { return RPL == 2 ? R & 1 : (R & 1) + 2 * ((R >> 3) & 1); }
+  __device__ static constexpr int row(int L, int s) {
+    return RPL == 2 ? 2 * L + s : 16 * (L >> 2) + 2 * (L & 3) + (s & 1) + 8 * (s >> 1);
+  }
+  __device__ static constexpr int off(int R) { return line(R) * LINE + slot(R) * KYP; }
+};
+
+template <int B, int KC = RBL_T44_KC, int PF = RBL_T44_PF, bool XG = false, int KYP = 64, bool GL = false>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kT44fNrt == 2 ? 3 : 2))) void k_tsmm44f(
     int64_t nrows, PanelRun X, const double* __restrict__ C, int ldc, Panels Y, double alpha,
     double beta, const int* skip, double* __restrict__ xslab) {
   if (skip && *skip) return;
@@ -484,15 +578,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
   constexpr int YW = KYP / 2, NT = YW / 16;  // XG: Y = [Q_i | Q_{i-1}], YW columns each
   constexpr int NH = KC / 8;  // 16-B A loads per row tile per chunk
   constexpr int CEPT = KC * KYP / 256;
-  constexpr int CS = 2 * KC * LDC > 4 * 16 * KYP ? 2 * KC * LDC : 4 * 16 * KYP;  // + epilogue stage
+  using TL = T44Lines<KYP>;
+  constexpr int NL = KC / TL::RPL;  // GL: lines per chunk
+  static_assert(!GL || (NL % 4 == 0 && KC % 16 == 0), "GL chunk shape");
+  constexpr int CB = GL ? NL * TL::LINE : KC * LDC;  // doubles per C buffer
+  constexpr int CS = 2 * CB > 4 * 16 * KYP ? 2 * CB : 4 * 16 * KYP;  // + epilogue stage
   __shared__ __attribute__((aligned(16))) double cs_raw[CS];
-  double(*cs)[KC * LDC] = reinterpret_cast<double(*)[KC * LDC]>(cs_raw);
+  double(*cs)[CB] = reinterpret_cast<double(*)[CB]>(cs_raw);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int q = lane >> 4;
   const int nch = X.count * B / KC;
-  const int64_t ntiles = (nrows + 4 * kT44Rows - 1) / (4 * kT44Rows);
-  // one 128-row tile per workgroup, or (XG) persistent over tiles
+    // one 128-row tile per workgroup, or (XG) persistent over tiles
   auto tile_body = [&](int64_t tile) {
   typedef double d4x __attribute__((ext_vector_type(4)));
   d4x gx[XG ? NT : 1][XG ? NT : 1];
@@ -502,25 +599,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
 #pragma unroll
       for (int jt = 0; jt < NT; ++jt) gx[it][jt] = d4x{0.0, 0.0, 0.0, 0.0};
   }
-  const int64_t r0 = (tile * 4 + wave) * kT44Rows;
-  const int64_t rw = r0 + kT44Rows <= nrows ? r0 : nrows - kT44Rows;  // wave-uniform
+  constexpr int NRT = kT44fNrt;
+  const int64_t r0 = (tile * 4 + wave) * kT44fRows;
+  const int64_t rw = r0 + kT44fRows <= nrows ? r0 : nrows - kT44fRows;  // wave-uniform
 
-  double acc[2][CG];
+  double acc[NRT][CG];
 #pragma unroll
-  for (int rt = 0; rt < 2; ++rt)
+  for (int rt = 0; rt < NRT; ++rt)
 #pragma unroll
     for (int cg = 0; cg < CG; ++cg) acc[rt][cg] = 0.0;
 
   // A: rows rw + 16 rt + (lane&15), k = KC ch + 8 h + 2 q + v
-  const int aoff0 = (lane & 15) * B + 2 * q, aoff1 = aoff0 + 16 * B;
-  auto load_a = [&](int ch, d2v (&ar)[2][NH]) {
+  const int aoff0 = (lane & 15) * B + 2 * q;
+  auto load_a = [&](int ch, d2v (&ar)[NRT][NH]) {
     const int chc = ch < nch ? ch : nch - 1;
 #pragma unroll
     for (int h = 0; h < NH; ++h) {
       const int kk = KC * chc + 8 * h;
       const double* xb = X.base + (int64_t)(kk / B) * X.stride + rw * B + (kk % B);
-      ar[0][h] = *reinterpret_cast<const d2v*>(xb + aoff0);
-      ar[1][h] = *reinterpret_cast<const d2v*>(xb + aoff1);
+#pragma unroll
+      for (int rt = 0; rt < NRT; ++rt) ar[rt][h] = *reinterpret_cast<const d2v*>(xb + aoff0 + 16 * rt * B);
     }
   };
   // C chunk element tid + 256 v: row KC chc + tid / KYP + (256 / KYP) v, column tid % KYP
@@ -536,17 +634,35 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
 #pragma unroll
     for (int v = 0; v < CEPT; ++v) cs[buf][cso + CRS * v * LDC] = cr[v];
   };
-  auto mfmas = [&](int ch, const d2v (&acur)[2][NH]) {
-    const double* cb = cs[ch & 1] + 2 * q * LDC + 2 * (lane & 3);
+  // GL: this wave's NL / 4 lines of chunk ch; lane -> slot lane / (KYP / 2), pair lane % (KYP / 2)
+  // (lane offsets are loop-invariant: a uniform chunk base plus a 32-bit lane offset per line)
+  int gl_off[GL ? NL / 4 : 1];
+  if constexpr (GL) {
+    const int gl_slot = lane / (KYP / 2), gl_pair = lane % (KYP / 2);
+#pragma unroll
+    for (int i = 0; i < NL / 4; ++i) gl_off[i] = TL::row(wave * (NL / 4) + i, gl_slot) * ldc + 2 * gl_pair;
+  }
+  auto dma_c = [&](int buf, int ch) {
+    const int chc = ch < nch ? ch : nch - 1;
+    const double* cbase = C + (int64_t)KC * chc * ldc;
+#pragma unroll
+    for (int i = 0; i < NL / 4; ++i) {
+      const int L = wave * (NL / 4) + i;
+      __builtin_amdgcn_global_load_lds((glb_vptr)(cbase + gl_off[i]), (lds_vptr)(cs[buf] + L * TL::LINE), 16, 0, 0);
+    }
+  };
+  auto mfmas = [&](int ch, const d2v (&acur)[NRT][NH]) {
+    const double* cb = GL ? cs[ch & 1] + q * TL::LINE + 2 * (lane & 3)
+                          : cs[ch & 1] + 2 * q * LDC + 2 * (lane & 3);
 #pragma unroll
     for (int hv = 0; hv < 2 * NH; ++hv) {
       const int h = hv >> 1, v = hv & 1;
-      const double* cr0 = cb + (8 * h + v) * LDC;
+      const double* cr0 = cb + (GL ? TL::off(8 * h + v) : (8 * h + v) * LDC);
 #pragma unroll
       for (int cp = 0; cp < CG / 2; ++cp) {
         const d2v bf = *reinterpret_cast<const d2v*>(cr0 + 8 * cp);
 #pragma unroll
-        for (int rt = 0; rt < 2; ++rt) {
+        for (int rt = 0; rt < NRT; ++rt) {
           acc[rt][2 * cp] = mfma4(acur[rt][h][v], bf.x, acc[rt][2 * cp]);
           acc[rt][2 * cp + 1] = mfma4(acur[rt][h][v], bf.y, acc[rt][2 * cp + 1]);
         }
@@ -555,14 +671,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
   };
 
   double cr[CEPT];
-  load_c(0, cr);
-  store_c(0, cr);
+  if constexpr (GL) {
+    dma_c(0, 0);
+  } else {
+    load_c(0, cr);
+    store_c(0, cr);
+  }
   if constexpr (PF >= 2) {
-    d2v a0[2][NH], a1[2][NH], a2[2][NH];
+    static_assert(!GL, "GL: PF = 1 only");
+    d2v a0[NRT][NH], a1[NRT][NH], a2[NRT][NH];
     load_a(0, a0);
     load_a(1, a1);
     __syncthreads();
-    auto step = [&](int ch, const d2v (&acur)[2][NH], d2v (&afut)[2][NH]) {
+    auto step = [&](int ch, const d2v (&acur)[NRT][NH], d2v (&afut)[NRT][NH]) {
       load_c(ch + 1, cr);
       load_a(ch + 2, afut);
       if (ch < nch) mfmas(ch, acur);  // no loads inside: the vmcnt bookkeeping is unaffected
@@ -574,8 +695,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
       step(ch + 1, a1, a0);
       step(ch + 2, a2, a1);
     }
+  } else if constexpr (GL) {
+    // two register sets swapped by a 2-unrolled loop (no copies); the DMA into the other
+    // buffer (last read before the previous barrier) lands by the vmcnt(0) of this step's
+    // closing barrier, before any wave reads it
+    d2v a0[NRT][NH], a1[NRT][NH];
+    load_a(0, a0);
+    __syncthreads();
+    auto step = [&](int ch, const d2v (&acur)[NRT][NH], d2v (&anext)[NRT][NH]) {
+      dma_c((ch + 1) & 1, ch + 1);
+      load_a(ch + 1, anext);
+      if (ch < nch) mfmas(ch, acur);  // no loads inside: the vmcnt bookkeeping is unaffected
+      __syncthreads();
+    };
+    for (int ch = 0; ch < nch; ch += 2) {
+      step(ch, a0, a1);
+      step(ch + 1, a1, a0);
+    }
   } else {
-    d2v acur[2][NH], anext[2][NH];
+    d2v acur[NRT][NH], anext[NRT][NH];
     load_a(0, acur);
     __syncthreads();
     for (int ch = 0; ch < nch; ++ch) {
@@ -584,7 +722,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
       mfmas(ch, acur);
       if (!(RBL_REORTH_ABL & 4)) store_c((ch + 1) & 1, cr);
 #pragma unroll
-      for (int rt = 0; rt < 2; ++rt)
+      for (int rt = 0; rt < NRT; ++rt)
 #pragma unroll
         for (int h = 0; h < NH; ++h) acur[rt][h] = anext[rt][h];
       if (!(RBL_REORTH_ABL & 2)) __syncthreads();
@@ -596,10 +734,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k
   const int g = (lane >> 2) & 3;
   constexpr int kYPer = 16 * KYP / 128;
 #pragma unroll
-  for (int rt = 0; rt < 2; ++rt) {
+  for (int rt = 0; rt < NRT; ++rt) {
+    if constexpr (GL) {
+      // acc[rt][2cp + x] holds column 8cp + 2(lane & 3) + x
 #pragma unroll
-    for (int cg = 0; cg < CG; ++cg)
-      ot[(4 * g + q) * KYP + ((4 * cg + (lane & 3)) ^ (4 * g))] = alpha * acc[rt][cg];
+      for (int cp = 0; cp < CG / 2; ++cp)
+        *reinterpret_cast<d2v*>(ot + (4 * g + q) * KYP + ((8 * cp + 2 * (lane & 3)) ^ (4 * g))) =
+            d2v{alpha * acc[rt][2 * cp], alpha * acc[rt][2 * cp + 1]};
+    } else {
+#pragma unroll
+      for (int cg = 0; cg < CG; ++cg)
+        ot[(4 * g + q) * KYP + ((4 * cg + (lane & 3)) ^ (4 * g))] = alpha * acc[rt][cg];
+    }
 #pragma unroll
     for (int m = 0; m < kYPer; ++m) {
       const int e = 2 * lane + 128 * m, row = e / KYP, c = e % KYP;
@@ -685,8 +831,8 @@ void tsmm44_f32x(int64_t nrows, const PanelRun& X, const double* C, int ldc, con
 }
 
 int tsmm44_xg_grid(int64_t nrows) {
-  // one partial per 128-row tile
-  return (int)((nrows + 4 * kT44Rows - 1) / (4 * kT44Rows));
+  // one partial per workgroup tile of k_tsmm44f (4 waves x kT44fRows rows)
+  return (int)((nrows + 4 * kT44fRows - 1) / (4 * kT44fRows));
 }
 
 void tsmm44(int64_t nrows, const PanelRun& X, const double* C, int ldc, const Panels& Y,
@@ -705,14 +851,24 @@ void tsmm44(int64_t nrows, const PanelRun& X, const double* C, int ldc, const Pa
   // (KYP = 32 builds but stays off: at b = 16 the update is HBM-bound and the generic kernel
   // ran 4 % faster on C2, its cross-Gram form 6 % slower than the Gram pass it replaces —
   // tools/r02_c2_ab.sh)
-  if (fast_ok && KY == 64 && (X.count * X.w) % kT44K == 0 && nrows >= kT44Rows &&
+  if (fast_ok && KY == 64 && (X.count * X.w) % kT44K == 0 && nrows >= kT44fRows &&
       Y.w % 2 == 0 && !alias) {
-    const int64_t wgs = (nrows + 4 * kT44Rows - 1) / (4 * kT44Rows);
+    const int64_t wgs = (nrows + 4 * kT44fRows - 1) / (4 * kT44fRows);
     const bool xg = xslab && Y.count == 2 && 2 * Y.w == KY;
     if (xg) *xgrid = (int)wgs;
+    // LDS-DMA staging of C: 16-B aligned rows
+    const bool gl = RBL_T44_GLDS && RBL_T44_PF == 1 && ldc % 2 == 0 &&
+                    reinterpret_cast<uintptr_t>(C) % 16 == 0;
 #define RBL_T44F(BB, XGG, KK)                                                                      \
-  hipLaunchKernelGGL((k_tsmm44f<BB, RBL_T44_KC, RBL_T44_PF, XGG, KK>), dim3((unsigned)wgs), dim3(256), 0, \
-                     st, nrows, X, C, ldc, Y, alpha, beta, skip, XGG ? xslab : nullptr)
+  do {                                                                                              \
+    if (gl)                                                                                         \
+      hipLaunchKernelGGL((k_tsmm44f<BB, RBL_T44_KC, RBL_T44_PF, XGG, KK, RBL_T44_GLDS && RBL_T44_PF == 1>), \
+                         dim3((unsigned)wgs), dim3(256), 0, st, nrows, X, C, ldc, Y, alpha, beta, skip, \
+                         XGG ? xslab : nullptr);                                                    \
+    else                                                                                            \
+      hipLaunchKernelGGL((k_tsmm44f<BB, RBL_T44_KC, RBL_T44_PF, XGG, KK, false>), dim3((unsigned)wgs), \
+                         dim3(256), 0, st, nrows, X, C, ldc, Y, alpha, beta, skip, XGG ? xslab : nullptr); \
+  } while (0)
     if (KY == 64) {
       if (X.w == 32) { if (xg) RBL_T44F(32, true, 64); else RBL_T44F(32, false, 64); }
       else { if (xg) RBL_T44F(16, true, 64); else RBL_T44F(16, false, 64); }
