@@ -733,6 +733,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kT44fNrt ==
   double* ot = cs_raw + wave * 16 * KYP;
   const int g = (lane >> 2) & 3;
   constexpr int kYPer = 16 * KYP / 128;
+  // a lane's stage column ce is the same for every m (128 % KYP == 0): its Y panel, column and
+  // row base are hoisted (no per-store division or 64-bit multiply); rows r < nrows always
+  // (rw + kT44fRows <= nrows), so "own" is row-in-tile >= r0 - rw
+  constexpr int kRowStep = 128 / KYP;
+  const int ce = (2 * lane) % KYP, rl = (2 * lane) / KYP;
+  const int yt = ce >= Y.w ? 1 : 0;
+  double* yb = const_cast<double*>(yt ? Y.ptr[Panels::kMax - 1] : Y.ptr[0]) + (ce - yt * Y.w) +
+               (rw + rl) * Y.w;
+  const int dskip = (int)(r0 - rw);
+  const bool has_beta = beta != 0.0;
 #pragma unroll
   for (int rt = 0; rt < NRT; ++rt) {
     if constexpr (GL) {
@@ -748,18 +758,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kT44fNrt ==
     }
 #pragma unroll
     for (int m = 0; m < kYPer; ++m) {
-      const int e = 2 * lane + 128 * m, row = e / KYP, c = e % KYP;
-      const int64_t r = rw + 16 * rt + row;
-      d2v v = *reinterpret_cast<const d2v*>(ot + row * KYP + (c ^ (4 * ((row >> 2) & 3))));
-      const bool own = r >= r0 && r < nrows;
+      const int row = rl + kRowStep * m;
+      d2v v = *reinterpret_cast<const d2v*>(ot + row * KYP + (ce ^ (4 * ((row >> 2) & 3))));
+      const bool own = 16 * rt + row >= dskip;
       if (own) {
-        const int t = c / Y.w;
-        d2v* yp = reinterpret_cast<d2v*>(const_cast<double*>(Y.ptr[t]) + r * Y.w + (c - t * Y.w));
-        if (beta != 0.0) v += beta * *yp;
+        d2v* yp = reinterpret_cast<d2v*>(yb + (int64_t)((16 * rt + kRowStep * m) * Y.w));
+        if (has_beta) v += beta * *yp;
         *yp = v;
       }
       if constexpr (XG)  // final values back into the stage (0 for rows this wave does not own)
-        *reinterpret_cast<d2v*>(ot + row * KYP + (c ^ (4 * ((row >> 2) & 3)))) = own ? v : d2v{0.0, 0.0};
+        *reinterpret_cast<d2v*>(ot + row * KYP + (ce ^ (4 * ((row >> 2) & 3)))) = own ? v : d2v{0.0, 0.0};
     }
     if constexpr (XG) {
       // (Q_{i-1}^T Q_i)[16 it + .][16 jt + .] += sum over the 16 rows; row 4 s4 + q sits at
