@@ -135,9 +135,11 @@ int rowgram_grid(int64_t nrows, int per_cu = 2);
 constexpr int kRowgramMaxPerCu = 4;  // rowgram_ex's grids stay <= rowgram_grid(nrows, this)
 // X32 (optional): X read from fp32 instead (widened exactly).  Y32 (optional): Y' written to
 // Y32 rounded to fp32 instead of Y — unless f64flag is non-null and *f64flag != 0 (device).
+// tri: C is upper triangular (zeros below the diagonal), X fp64 — all-zero MFMA blocks skipped.
 void rowgram(int64_t nrows, int b, const double* X, const double* C, int ldc, double* Y,
              double alpha, double beta, double* slab, int grid, const int* skip, hipStream_t s,
-             const float* X32 = nullptr, float* Y32 = nullptr, const int* f64flag = nullptr);
+             const float* X32 = nullptr, float* Y32 = nullptr, const int* f64flag = nullptr,
+             bool tri = false);
 // The CholQR forms of the fused row op (b in {16, 32}, X fp64):
 //   mode 1: slab <- Gram of X C (no store);  mode 2: Y = (X C) C2 (slab must be null);
 //   Z != null (modes 0 and 2): slab2 <- per-workgroup partials of Z^T Y (grid x b x b).
@@ -159,6 +161,7 @@ struct RowOpArgs {
   double* slab2 = nullptr;
   int mode = 0;
   int* grid_out = nullptr;  // rowgram_ex with grid <= 0: the grid it chose (per-CU occupancy)
+  bool tri = false;         // C (and C2) upper triangular: all-zero MFMA blocks skipped (exact)
 };
 bool rowgram_ex(int64_t nrows, int b, const RowOpArgs& a, int grid, hipStream_t s);
 

@@ -939,7 +939,7 @@ int tsmm_checked(rbl_ctx* ctx, const PanelRun& X, const double* C, int ldc, cons
 // G = Y^T Y over all ranks.  b in {16, 32}.
 int rowop(rbl_ctx* ctx, const double* X, const double* C, double* Y, double alpha, double beta,
           double* G, const int* skip, const float* X32 = nullptr, float* Y32 = nullptr,
-          const int* f64flag = nullptr) {
+          const int* f64flag = nullptr, bool tri = false) {
   const int b = ctx->b;
   const int grid = rowgram_grid(ctx->nloc);
   if (G && (size_t)grid * b * b > ctx->slab_elems)
@@ -947,7 +947,7 @@ int rowop(rbl_ctx* ctx, const double* X, const double* C, double* Y, double alph
   if (ctx->nloc > 0) {
     // without a Gram the grid follows the kernel's occupancy (no partials to count)
     rowgram(ctx->nloc, b, X, C, b, Y, alpha, beta, G ? ctx->d_slab : nullptr, G ? grid : 0, skip,
-            ctx->stream, X32, Y32, f64flag);
+            ctx->stream, X32, Y32, f64flag, tri && !X32);
     HIPC(hipGetLastError());
   } else if (G) {  // no rows on this rank: its share of the Gram is zero (the all-reduce still runs)
     HIPC(hipMemsetAsync(ctx->d_slab, 0, (size_t)grid * b * b * sizeof(double), ctx->stream));
@@ -1311,6 +1311,7 @@ int tsqr(rbl_ctx* ctx, const double* U, double* Qout, bool g1_ready = false, flo
     a1.C = smallp(ctx, S_RINV);
     a1.ldc = b;
     a1.mode = 1;
+    a1.tri = true;  // R^-1
     CHK(rowop_ex(ctx, a1, G, nullptr, false));
     copy_small(smallp(ctx, S_RINV), smallp(ctx, S_RINV1), (int64_t)b * b, ctx->stream);
     chol_step(G, b, ctx->n, 1, smallp(ctx, S_R), smallp(ctx, S_RINV), smallp(ctx, S_RTOT), need3,
@@ -1320,6 +1321,7 @@ int tsqr(rbl_ctx* ctx, const double* U, double* Qout, bool g1_ready = false, flo
     a2.C = smallp(ctx, S_RINV1);
     a2.C2 = smallp(ctx, S_RINV);
     a2.ldc = b;
+    a2.tri = true;  // R1^-1, R2^-1
     a2.Y = Qout;
     a2.Y32 = Qout32;
     a2.f64flag = Qout32 ? need3 : nullptr;
@@ -1334,6 +1336,7 @@ int tsqr(rbl_ctx* ctx, const double* U, double* Qout, bool g1_ready = false, flo
     a3.X = Qout;
     a3.C = smallp(ctx, S_RINV);
     a3.ldc = b;
+    a3.tri = true;
     a3.Y = Qout;
     a3.skip = skip3;
     a3.Y32 = Qout32;
@@ -1345,7 +1348,7 @@ int tsqr(rbl_ctx* ctx, const double* U, double* Qout, bool g1_ready = false, flo
   }
   if (Zloc) return fail(ctx, RBL_ERR_INVALID, "internal: local-reorth Gram fusion needs the 3-pass QR");
   if (fused) {
-    CHK(rowop(ctx, U, smallp(ctx, S_RINV), Qout, 1.0, 0.0, G, nullptr));
+    CHK(rowop(ctx, U, smallp(ctx, S_RINV), Qout, 1.0, 0.0, G, nullptr, nullptr, nullptr, nullptr, true));
   } else {
     CHK(tsmm_checked(ctx, run1(U, b), smallp(ctx, S_RINV), b, pan1(Qout, b), 1.0, 0.0, nullptr));
     CHK(gram(ctx, run1(Qout, b), pan1(Qout, b), G, nullptr));
@@ -1356,7 +1359,7 @@ int tsqr(rbl_ctx* ctx, const double* U, double* Qout, bool g1_ready = false, flo
   if (fused) {  // in place; the Gram feeds pass 3 when a shifted first pass asked for it
     // (fp32 basis: the result goes straight to Qout32 unless pass 3 follows)
     CHK(rowop(ctx, Qout, smallp(ctx, S_RINV), Qout, 1.0, 0.0, G, nullptr, nullptr, Qout32,
-              Qout32 ? need3 : nullptr));
+              Qout32 ? need3 : nullptr, true));
   } else {
     CHK(apply_inplace(nullptr));
     CHK(gram(ctx, run1(Qout, b), pan1(Qout, b), G, skip3));
@@ -1365,7 +1368,8 @@ int tsqr(rbl_ctx* ctx, const double* U, double* Qout, bool g1_ready = false, flo
   chol_step(G, b, ctx->n, 1, smallp(ctx, S_R), smallp(ctx, S_RINV), smallp(ctx, S_RTOT), need3,
             status, skip3, ctx->stream, smallp(ctx, S_CHS0));
   if (fused) {
-    CHK(rowop(ctx, Qout, smallp(ctx, S_RINV), Qout, 1.0, 0.0, nullptr, skip3, nullptr, Qout32));
+    CHK(rowop(ctx, Qout, smallp(ctx, S_RINV), Qout, 1.0, 0.0, nullptr, skip3, nullptr, Qout32,
+              nullptr, true));
   } else {
     CHK(apply_inplace(skip3));
     if (Qout32) cvt_f64_to_f32(Qout, Qout32, ctx->nloc * b, ctx->stream);

@@ -19,6 +19,9 @@
 //   MODE 2: Y' = (X C) C2: pass 2 recomputes Q1 = U R1^-1 bit for bit (same operands, same
 //           MFMA order) and applies R2^-1 in the same pass, so Q1 never goes to HBM (3 passes
 //           over n x b per QR instead of 4; the same bits as the 4-pass form).
+// TRI: C (and C2) upper triangular (CholQR's R^-1): an MFMA whose four k rows of C are all
+// zero in its four columns (k > c throughout) adds exact zeros and is skipped — 24 of the 64
+// per 16-row tile at b = 32 (the k-interleave 8h + 2q + v keeps the order of every other MFMA).
 // XG: the cross Gram Z^T Y' of another block Z (v_mfma_f64_16x16x4f64, Z read in its A layout,
 // Y' from the output stage): the next step's local-reorth coefficient Q_{i}^T Q_{i+1}
 // (RBL_gpu.jl:87) formed while Q_{i+1} is written.
@@ -56,10 +59,29 @@ __device__ __forceinline__ void stnt(d2v v, d2v* p) {
   else *p = v;
 }
 
+// acc[cg] += a * C[k][4cg + j] for the k rows k0 + 2q (q = 0..3) of one MFMA, columns in perm8
+// order (column groups 2cp, 2cp+1 in one 16-B read); TRI: column groups with 4cg + 3 < k0 are
+// all zero in C and skipped (compile-time: k0 and cg are unrolled constants)
+template <bool TRI, int CG>
+__device__ __forceinline__ void mfma_row(const int k0, double a, const double* cb, double (&acc)[CG]) {
+#pragma unroll
+  for (int cp = 0; cp < CG / 2; ++cp) {
+    const bool z0 = TRI && k0 > 8 * cp + 3, z1 = TRI && k0 > 8 * cp + 7;
+    if (z0 && z1) continue;
+    const d2v bf = *reinterpret_cast<const d2v*>(cb + 8 * cp);
+    if (!z0) acc[2 * cp] = mfma4r(a, bf.x, acc[2 * cp]);
+    if (!z1) acc[2 * cp + 1] = mfma4r(a, bf.y, acc[2 * cp + 1]);
+  }
+  if constexpr (CG % 2) {
+    if (!(TRI && k0 > 4 * (CG - 1) + 3)) acc[CG - 1] = mfma4r(a, cb[8 * (CG / 2)], acc[CG - 1]);
+  }
+}
+
 // XF: X is read from X32 (fp32, widened exactly); YF: Y' goes to Y32 rounded to fp32 (as
 // cvt_f64_to_f32) unless *f64flag is set, then to Y in fp64 — the fp32-basis step's QR
 // (RBL_gpu.jl:182 `Qg = FLOAT(Qg_d)`) without a separate narrowing pass.
-template <int B, bool GRAM, bool XF = false, bool YF = false, int MODE = 0, bool XG = false>
+template <int B, bool GRAM, bool XF = false, bool YF = false, int MODE = 0, bool XG = false,
+          bool TRI = false>
 __global__ __launch_bounds__(kRowThreads) __attribute__((amdgpu_waves_per_eu(GRAM || XG ? 2 : 3))) void k_rowgram(int64_t nrows, const double* X,  // X may alias Y (in-place apply)
                                                          const double* __restrict__ C, int ldc,
                                                          double* Y, double alpha, double beta,
@@ -192,15 +214,7 @@ __global__ __launch_bounds__(kRowThreads) __attribute__((amdgpu_waves_per_eu(GRA
         for (int v = 0; v < 2; ++v) {
           const double a = v ? xa[rt][h].y : xa[rt][h].x;
           const double* cb = cs + (8 * h + 2 * q + v) * LDC + 2 * j;
-#pragma unroll
-          for (int cp = 0; cp < CG / 2; ++cp) {
-            const d2v bf = *reinterpret_cast<const d2v*>(cb + 8 * cp);
-            acc[rt][2 * cp] = mfma4r(a, bf.x, acc[rt][2 * cp]);
-            acc[rt][2 * cp + 1] = mfma4r(a, bf.y, acc[rt][2 * cp + 1]);
-          }
-          if constexpr (CG % 2) {
-            acc[rt][CG - 1] = mfma4r(a, cb[8 * (CG / 2)], acc[rt][CG - 1]);
-          }
+          mfma_row<TRI>(8 * h + v, a, cb, acc[rt]);
         }
       if constexpr (TWO) {
         // Q1 tile (D layout) -> the wave's LDS stage -> A layout; acc = Q1 C2, the same MFMA
@@ -218,15 +232,7 @@ __global__ __launch_bounds__(kRowThreads) __attribute__((amdgpu_waves_per_eu(GRA
           for (int v = 0; v < 2; ++v) {
             const double a = v ? x2[h].y : x2[h].x;
             const double* cb = cs2 + (8 * h + 2 * q + v) * LDC + 2 * j;
-#pragma unroll
-            for (int cp = 0; cp < CG / 2; ++cp) {
-              const d2v bf = *reinterpret_cast<const d2v*>(cb + 8 * cp);
-              acc[rt][2 * cp] = mfma4r(a, bf.x, acc[rt][2 * cp]);
-              acc[rt][2 * cp + 1] = mfma4r(a, bf.y, acc[rt][2 * cp + 1]);
-            }
-            if constexpr (CG % 2) {
-              acc[rt][CG - 1] = mfma4r(a, cb[8 * (CG / 2)], acc[rt][CG - 1]);
-            }
+            mfma_row<TRI>(8 * h + v, a, cb, acc[rt]);
           }
       }
       const int64_t rbase = blk * kBlockRows + 16 * rt;
@@ -330,13 +336,13 @@ __global__ __launch_bounds__(kRowThreads) __attribute__((amdgpu_waves_per_eu(GRA
 // workgroups per CU the instantiation holds (its VGPRs), cached; the persistent grid is this
 // many per CU, capped at kMaxPerCu, so every workgroup is resident from the start
 constexpr int kMaxPerCu = 4;
-template <int B, bool GRAM, bool XF, bool YF, int MODE, bool XG>
+template <int B, bool GRAM, bool XF, bool YF, int MODE, bool XG, bool TRI>
 int rg_per_cu() {
   static std::atomic<int> per{0};
   int v = per.load(std::memory_order_relaxed);
   if (v == 0) {
     int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_rowgram<B, GRAM, XF, YF, MODE, XG>,
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_rowgram<B, GRAM, XF, YF, MODE, XG, TRI>,
                                                      kRowThreads, 0) != hipSuccess || nb < 1)
       nb = 2;
     v = nb < kMaxPerCu ? nb : kMaxPerCu;
@@ -345,13 +351,21 @@ int rg_per_cu() {
   return v;
 }
 
+template <int B, bool GRAM, bool XF, bool YF, int MODE, bool XG, bool TRI>
+void launch_rg_t(const RowOpArgs& a, int64_t nrows, int grid, hipStream_t s) {
+  if (grid <= 0) grid = rowgram_grid(nrows, rg_per_cu<B, GRAM, XF, YF, MODE, XG, TRI>());
+  if (a.grid_out) *a.grid_out = grid;
+  hipLaunchKernelGGL((k_rowgram<B, GRAM, XF, YF, MODE, XG, TRI>), dim3(grid), dim3(kRowThreads), 0, s,
+                     nrows, a.X, a.C, a.ldc, a.Y, a.alpha, a.beta, a.slab, a.skip, a.X32, a.Y32,
+                     a.f64flag, a.C2, a.Z, a.slab2);
+}
+// the triangular form for the fp64-X instantiations (CholQR's applies); fp32-X stays general
 template <int B, bool GRAM, bool XF, bool YF, int MODE, bool XG>
 void launch_rg(const RowOpArgs& a, int64_t nrows, int grid, hipStream_t s) {
-  if (grid <= 0) grid = rowgram_grid(nrows, rg_per_cu<B, GRAM, XF, YF, MODE, XG>());
-  if (a.grid_out) *a.grid_out = grid;
-  hipLaunchKernelGGL((k_rowgram<B, GRAM, XF, YF, MODE, XG>), dim3(grid), dim3(kRowThreads), 0, s, nrows,
-                     a.X, a.C, a.ldc, a.Y, a.alpha, a.beta, a.slab, a.skip, a.X32, a.Y32, a.f64flag,
-                     a.C2, a.Z, a.slab2);
+  if constexpr (!XF) {
+    if (a.tri) return launch_rg_t<B, GRAM, XF, YF, MODE, XG, true>(a, nrows, grid, s);
+  }
+  launch_rg_t<B, GRAM, XF, YF, MODE, XG, false>(a, nrows, grid, s);
 }
 
 template <int B>
@@ -418,8 +432,9 @@ bool rowgram_ex(int64_t nrows, int b, const RowOpArgs& a, int grid, hipStream_t 
 
 void rowgram(int64_t nrows, int b, const double* X, const double* C, int ldc, double* Y,
              double alpha, double beta, double* slab, int grid, const int* skip, hipStream_t s,
-             const float* X32, float* Y32, const int* f64flag) {
+             const float* X32, float* Y32, const int* f64flag, bool tri) {
   RowOpArgs a;
+  a.tri = tri;
   a.X = X;
   a.C = C;
   a.ldc = ldc;
