@@ -12,7 +12,7 @@ pids=""
 for s in $srcs; do
   o=$out/obj/${s%.*}.o
   if [ "${s##*.}" = "cpp" ]; then x="-x hip"; else x=""; fi
-  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wno-unused-result $defs $x -c $s -o $o &
+  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wno-unused-result -Wno-unused-value $defs $x -c $s -o $o &
   pids="$pids $!"
 done
 for p in $pids; do wait $p; done
