@@ -253,7 +253,7 @@ void tsmm(int64_t nrows, const PanelRun& X, const double* C, int ldc, const Pane
 // --- reorth.hip: v_mfma_f64_4x4x4f64 fast paths (panel widths 16 / 32), selected by
 // gram_splits / gram_partial / tsmm above when applicable.
 bool gram44_ok(int64_t nrows, int nW, int w, int xcount, int xw);
-int gram44_splits(int64_t nrows, int nW);
+int gram44_splits(int64_t nrows, int nW, int w = 32);
 void gram44_partial(int64_t nrows, const PanelRun& W, const Panels& X, double* slab, int splits,
                     const int* skip, hipStream_t s);
 bool tsmm44_ok(int xw, int ky, int yw);

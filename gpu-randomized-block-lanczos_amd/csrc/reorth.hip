@@ -14,6 +14,7 @@
 // With the 4 blocks on 4 consecutive row-quads, the A operand of a wave is
 //   M[r0 + (lane&15)][k0 + (lane>>4)]  (Gram: W^T -> W[r0+(lane>>4)][a0+(lane&15)]),
 // i.e. 16 consecutive doubles per k — coalesced 128-B segments.
+#include <algorithm>
 #include <cstdlib>
 
 #include "kernels.hpp"
@@ -314,11 +315,19 @@ bool gram44_ok(int64_t nrows, int nW, int w, int xcount, int xw) {
          (xcount == 1 || xcount == 2);
 }
 
-int gram44_splits(int64_t nrows, int nW) {
+// RBL_G44_SPLITS: splits per resident workgroup slot (diagnostics).  Capping the splits at two
+// full waves of workgroups (a smaller partial slab, less reduction) made the Gram 6 % slower
+// at n = 1e7 and at 1.25e6 rows (profiles/r03_gram_splits_ab.log): short workgroups balance
+// the tail of the launch better than the slab costs.
+#ifndef RBL_G44_SPLITS
+#define RBL_G44_SPLITS 1
+#endif
+int gram44_splits(int64_t nrows, int nW, int w) {
   (void)nW;
+  (void)w;
   // three 4-wave workgroups per CU: 3 x CUs splits, a multiple of 8 (XCD mapping), each
   // split >= 128 rows
-  int64_t s8 = RBL_G44_WPE * window_grid() / 8;
+  int64_t s8 = (int64_t)RBL_G44_SPLITS * RBL_G44_WPE * window_grid() / 8;
   const int64_t max_s8 = (nrows + 8 * 128 - 1) / (8 * 128);
   if (s8 > max_s8) s8 = max_s8;
   if (s8 < 1) s8 = 1;

@@ -115,7 +115,7 @@ static int tiles16(int x) { return (x + 15) / 16; }
 static int pick_at(int w) { int t = tiles16(w); return t <= 1 ? 1 : (t <= 2 ? 2 : 4); }
 
 int gram_splits(int64_t nrows, int nW, int w, int xcols) {
-  if (xcols % w == 0 && gram44_ok(nrows, nW, w, xcols / w, w)) return gram44_splits(nrows, nW);
+  if (xcols % w == 0 && gram44_ok(nrows, nW, w, xcols / w, w)) return gram44_splits(nrows, nW, w);
   const int ctt = tiles16(xcols);
   const int ct = ctt <= 1 ? 1 : (ctt <= 2 ? 2 : 4);
   const int ncg = (ctt + ct - 1) / ct;

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <algorithm>
 #include <cstdlib>
 #include <vector>
 
@@ -32,8 +33,10 @@ int main(int argc, char** argv) {
   fill(W, n * b * nWmax, 1);
   fill(X0, n * b, 2);
   fill(X1, n * b, 3);
-  const int smax = rbl::gram44_splits(n, nWmax);
-  (void)hipMalloc(&slab, (size_t)smax * nWmax * b * 64 * 8);
+  size_t slab_elems = 0;  // the split count may depend on nW: size for the largest product
+  for (int nW = 2; nW <= nWmax; nW += 2)
+    slab_elems = std::max(slab_elems, (size_t)rbl::gram44_splits(n, nW) * nW * b * 64);
+  (void)hipMalloc(&slab, slab_elems * 8);
   (void)hipMalloc(&C, (size_t)nWmax * b * 64 * 8);
   fill(C, nWmax * b * 64, 4);
   (void)hipMalloc(&Cg, (size_t)nWmax * b * 64 * 8);
@@ -77,7 +80,7 @@ int main(int argc, char** argv) {
       }
     }
     const double f = 2.0 * n * nW * b * 64;
-    printf("nW=%2d  gram %7.3f ms %5.1f TF   tsmm %7.3f ms %5.1f TF\n", nW, bg, f / bg / 1e9, bt,
+    printf("nW=%2d  splits %4d  gram %7.3f ms %5.1f TF   tsmm %7.3f ms %5.1f TF\n", nW, splits, bg, f / bg / 1e9, bt,
            f / bt / 1e9);
     tg += bg;
     tt += bt;
