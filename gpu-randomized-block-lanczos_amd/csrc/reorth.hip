@@ -315,20 +315,22 @@ bool gram44_ok(int64_t nrows, int nW, int w, int xcount, int xw) {
          (xcount == 1 || xcount == 2);
 }
 
-// RBL_G44_SPLITS: splits per resident workgroup slot (diagnostics).  Capping the splits at two
-// full waves of workgroups (a smaller partial slab, less reduction) made the Gram 6 % slower
-// at n = 1e7 and at 1.25e6 rows (profiles/r03_gram_splits_ab.log): short workgroups balance
-// the tail of the launch better than the slab costs.
-#ifndef RBL_G44_SPLITS
-#define RBL_G44_SPLITS 1
+// Splits: between one and two per resident workgroup slot (3 x CUs .. 6 x CUs), at most one
+// per RBL_G44_SPLIT_ROWS rows.  Short splits balance the launch's tail; below a few thousand
+// rows each, the per-split partial (slab write + reduction) costs more than that saves.
+// Measured (tools/reorth_probe, profiles/r03_gram_splits_ab.log): 6 x CUs splits -1.2 % at
+// n = 1e7 (6.5 k rows each), but 976 splits at n = 4e6 (4.1 k rows) +1.7 % and 6 x CUs at
+// 1.25e6 +2.3 %; a cap at two waves of workgroups +6 %.  So >= 6 k rows per split.
+#ifndef RBL_G44_SPLIT_ROWS
+#define RBL_G44_SPLIT_ROWS 6144
 #endif
 int gram44_splits(int64_t nrows, int nW, int w) {
   (void)nW;
   (void)w;
-  // three 4-wave workgroups per CU: 3 x CUs splits, a multiple of 8 (XCD mapping), each
-  // split >= 128 rows
-  int64_t s8 = (int64_t)RBL_G44_SPLITS * RBL_G44_WPE * window_grid() / 8;
-  const int64_t max_s8 = (nrows + 8 * 128 - 1) / (8 * 128);
+  const int64_t slots8 = (int64_t)RBL_G44_WPE * window_grid() / 8;  // XCD mapping: multiples of 8
+  int64_t s8 = nrows / (8 * (int64_t)RBL_G44_SPLIT_ROWS);
+  s8 = std::min(std::max(s8, slots8), 2 * slots8);
+  const int64_t max_s8 = (nrows + 8 * 128 - 1) / (8 * 128);  // each split >= 128 rows
   if (s8 > max_s8) s8 = max_s8;
   if (s8 < 1) s8 = 1;
   return (int)(s8 * 8);
