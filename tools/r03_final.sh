@@ -4,6 +4,9 @@
 set -u
 mkdir -p gpurun_out
 export TMPDIR=/tmp
+timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_fullsize.py \
+  tests/test_gpu_golden.py tests/test_gpu_parity.py > gpurun_out/r03f_tests.log 2>&1 || { echo "tests failed"; tail -5 gpurun_out/r03f_tests.log; exit 1; }
+tail -1 gpurun_out/r03f_tests.log
 bash tools/pmc_traffic.sh > gpurun_out/r03f_pmc.log 2>&1 || { echo "pmc failed"; tail -5 gpurun_out/r03f_pmc.log; exit 1; }
 python tools/pmc_summarize.py gpurun_out/pmc gpurun_out/pmc_traffic_r03.json > gpurun_out/r03f_pmc_summary.txt || exit 1
 cat gpurun_out/r03f_pmc_summary.txt
