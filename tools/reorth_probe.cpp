@@ -53,7 +53,9 @@ int main(int argc, char** argv) {
   for (int nW = 2; nW <= nWmax; nW += 2) {
     rbl::PanelRun Wr;
     Wr.base = W;
-    Wr.stride = n * b;
+    // PROBE_W0=1: every panel aliases panel 0 (same instruction stream and MFMAs, the basis
+    // served from L2 / Infinity Cache instead of HBM) — separates data movement from MFMA issue
+    Wr.stride = (getenv("PROBE_W0") && atoi(getenv("PROBE_W0"))) ? 0 : n * b;
     Wr.count = nW;
     Wr.w = b;
     rbl::Panels X;
