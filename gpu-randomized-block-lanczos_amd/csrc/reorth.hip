@@ -132,8 +132,10 @@ __device__ __forceinline__ void gram44_body(int64_t r_begin, int64_t r_end, int6
   // column 2 (lane & 15) + ag, both ag in one 16-B load (W16 = 0: columns (lane & 15) + 16 ag,
   // two 8-B loads); the MFMAs see the same operands per output, only C's row order differs
   constexpr bool W16 = RBL_G44_W16 && !PAIR && AG == 2;
-  const double* wl = W.base + (int64_t)(PAIR ? 2 * j : j) * W.stride +
-                     (W16 ? 2 * (lane & 15) : (lane & 15)) + q * B;
+  // the basis loads: a wave-uniform base (the panel, the chunk's rows) plus an unsigned 32-bit
+  // lane offset, so they can issue in the saddr form without per-load 64-bit address VALU
+  const double* wpan = W.base + (int64_t)__builtin_amdgcn_readfirstlane(PAIR ? 2 * j : j) * W.stride;
+  const unsigned wlo = (unsigned)((W16 ? 2 * (lane & 15) : (lane & 15)) + q * B);
   const int64_t wag = PAIR ? W.stride : 16;
   auto shift = [&](int64_t rc0) -> int64_t { return rc0 < r_end - kG44Rows ? rc0 : r_end - kG44Rows; };
   auto load_x = [&](int64_t rc0, double (&xr)[EPT]) {
@@ -165,11 +167,11 @@ __device__ __forceinline__ void gram44_body(int64_t r_begin, int64_t r_end, int6
                                        16, 0, 0);
   };
   auto load_a = [&](int64_t rc0, double (&ar)[KS][AG]) {
-    const double* p = wl + shift(rc0) * B;
+    const double* p = wpan + shift(rc0) * B;  // uniform
     if constexpr (W16) {
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
-        const d2v v = ldw(reinterpret_cast<const d2v*>(p + 4 * ks * B));
+        const d2v v = ldw(reinterpret_cast<const d2v*>(p + (wlo + (unsigned)(4 * ks * B))));
         ar[ks][0] = v.x;
         ar[ks][AG - 1] = v.y;
       }
@@ -177,7 +179,7 @@ __device__ __forceinline__ void gram44_body(int64_t r_begin, int64_t r_end, int6
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
-        for (int ag = 0; ag < AG; ++ag) ar[ks][ag] = ldw(p + 4 * ks * B + wag * ag);
+        for (int ag = 0; ag < AG; ++ag) ar[ks][ag] = ldw(p + wag * ag + (wlo + (unsigned)(4 * ks * B)));
     }
   };
 
@@ -621,7 +623,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kT44fNrt ==
     for (int cg = 0; cg < CG; ++cg) acc[rt][cg] = 0.0;
 
   // A: rows rw + 16 rt + (lane&15), k = KC ch + 8 h + 2 q + v
-  const int aoff0 = (lane & 15) * B + 2 * q;
+  // every load is a wave-uniform base (SGPRs) plus an unsigned 32-bit lane offset, so it can
+  // issue in the saddr form with no per-load 64-bit address VALU
+  const unsigned aoff0 = (unsigned)((lane & 15) * B + 2 * q);
   auto load_a = [&](int ch, d2v (&ar)[NRT][NH]) {
     const int chc = ch < nch ? ch : nch - 1;
 #pragma unroll
@@ -629,16 +633,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kT44fNrt ==
       const int kk = KC * chc + 8 * h;
       const double* xb = X.base + (int64_t)(kk / B) * X.stride + rw * B + (kk % B);
 #pragma unroll
-      for (int rt = 0; rt < NRT; ++rt) ar[rt][h] = *reinterpret_cast<const d2v*>(xb + aoff0 + 16 * rt * B);
+      for (int rt = 0; rt < NRT; ++rt)
+        ar[rt][h] = *reinterpret_cast<const d2v*>(xb + (aoff0 + (unsigned)(16 * rt * B)));
     }
   };
   // C chunk element tid + 256 v: row KC chc + tid / KYP + (256 / KYP) v, column tid % KYP
   constexpr int CRS = 256 / KYP;
+  const unsigned coff = (unsigned)((tid / KYP) * ldc + tid % KYP);
   auto load_c = [&](int ch, double (&cr)[CEPT]) {
     const int chc = ch < nch ? ch : nch - 1;
-    const double* cb = C + (int64_t)(KC * chc + tid / KYP) * ldc + tid % KYP;
 #pragma unroll
-    for (int v = 0; v < CEPT; ++v) cr[v] = cb[(int64_t)(CRS * v) * ldc];
+    for (int v = 0; v < CEPT; ++v) {
+      const double* cb = C + (int64_t)(KC * chc + CRS * v) * ldc;  // uniform
+      cr[v] = cb[coff];
+    }
   };
   const int cso = (tid / KYP) * LDC + perm8(tid % KYP);
   auto store_c = [&](int buf, const double (&cr)[CEPT]) {
