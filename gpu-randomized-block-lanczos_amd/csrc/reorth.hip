@@ -877,11 +877,15 @@ void tsmm44(int64_t nrows, const PanelRun& X, const double* C, int ldc, const Pa
     alias |= Y.ptr[t] >= X.base && Y.ptr[t] < X.base + (int64_t)X.count * X.stride;
   // (KYP = 32 builds but stays off: at b = 16 the update is HBM-bound and the generic kernel
   // ran 4 % faster on C2, its cross-Gram form 6 % slower than the Gram pass it replaces —
-  // tools/r02_c2_ab.sh)
-  if (fast_ok && KY == 64 && (X.count * X.w) % kT44K == 0 && nrows >= kT44fRows &&
-      Y.w % 2 == 0 && !alias) {
+  // tools/r02_c2_ab.sh; round 3 again 3 % faster on C2 and C3, profiles/r03_tsmm_fast32_ab.log)
+  static const bool fast32 = [] {  // RBL_TSMM44_FAST32=1: the 32-column form too (A/B)
+    const char* e = getenv("RBL_TSMM44_FAST32");
+    return e && atoi(e) != 0;
+  }();
+  if (fast_ok && (KY == 64 || (KY == 32 && fast32)) && (X.count * X.w) % kT44K == 0 &&
+      nrows >= kT44fRows && Y.w % 2 == 0 && !alias) {
     const int64_t wgs = (nrows + 4 * kT44fRows - 1) / (4 * kT44fRows);
-    const bool xg = xslab && Y.count == 2 && 2 * Y.w == KY;
+    const bool xg = xslab && KY == 64 && Y.count == 2 && 2 * Y.w == KY;
     if (xg) *xgrid = (int)wgs;
     // LDS-DMA staging of C: 16-B aligned rows
     const bool gl = RBL_T44_GLDS && RBL_T44_PF == 1 && ldc % 2 == 0 &&
