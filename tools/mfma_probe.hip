@@ -46,6 +46,35 @@ __global__ __launch_bounds__(256) void k_valu(double* out, int iters, double a0)
   for (int i = 0; i < NACC; ++i) s += acc[i];
   out[blockIdx.x * blockDim.x + threadIdx.x] = s;
 }
+typedef float f4p __attribute__((ext_vector_type(4)));
+typedef float f16p __attribute__((ext_vector_type(16)));
+template <int NACC>
+__global__ __launch_bounds__(256) void k_mfma32(double* out, int iters, float a0) {
+  f4p acc[NACC];
+  for (int i = 0; i < NACC; ++i) acc[i] = f4p{0, 0, 0, 0};
+  float a = a0 + threadIdx.x * 1e-3f, b = 1.0f - threadIdx.x * 1e-4f;
+  for (int it = 0; it < iters; ++it) {
+#pragma unroll
+    for (int i = 0; i < NACC; ++i) acc[i] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc[i], 0, 0, 0);
+  }
+  float s = 0;
+  for (int i = 0; i < NACC; ++i) s += acc[i][0] + acc[i][1] + acc[i][2] + acc[i][3];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+template <int NACC>
+__global__ __launch_bounds__(256) void k_mfma32x(double* out, int iters, float a0) {
+  f16p acc[NACC];
+  for (int i = 0; i < NACC; ++i)
+    for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
+  float a = a0 + threadIdx.x * 1e-3f, b = 1.0f - threadIdx.x * 1e-4f;
+  for (int it = 0; it < iters; ++it) {
+#pragma unroll
+    for (int i = 0; i < NACC; ++i) acc[i] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc[i], 0, 0, 0);
+  }
+  float s = 0;
+  for (int i = 0; i < NACC; ++i) s += acc[i][0] + acc[i][15];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
 __global__ void k_read(const double2* __restrict__ x, size_t n2, double* out) {
   double s = 0;
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n2; i += (size_t)gridDim.x * blockDim.x) {
@@ -92,6 +121,23 @@ int main() {
     (void)hipEventSynchronize(e1);
     (void)hipEventElapsedTime(&ms, e0, e1);
     printf("valu v_fma_f64: %.2f TFLOP/s\n", (double)wgs * 256 * iters * 16 * 2.0 / ms / 1e9);
+  }
+  {
+    const int wgs = 2048, iters = 2000;
+    hipLaunchKernelGGL(k_mfma32<8>, dim3(wgs), dim3(256), 0, 0, out, 10, 0.5f);
+    (void)hipEventRecord(e0);
+    hipLaunchKernelGGL(k_mfma32<8>, dim3(wgs), dim3(256), 0, 0, out, iters, 0.5f);
+    (void)hipEventRecord(e1);
+    (void)hipEventSynchronize(e1);
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    printf("mfma_f32_16x16x4: %.2f TFLOP/s\n", (double)wgs * 4 * iters * 8 * 2048.0 / ms / 1e9);
+    hipLaunchKernelGGL(k_mfma32x<4>, dim3(wgs), dim3(256), 0, 0, out, 10, 0.5f);
+    (void)hipEventRecord(e0);
+    hipLaunchKernelGGL(k_mfma32x<4>, dim3(wgs), dim3(256), 0, 0, out, iters, 0.5f);
+    (void)hipEventRecord(e1);
+    (void)hipEventSynchronize(e1);
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    printf("mfma_f32_32x32x2: %.2f TFLOP/s\n", (double)wgs * 4 * iters * 4 * 4096.0 / ms / 1e9);
   }
   const size_t bytes = 8ull << 30;
   double2 *x, *y;

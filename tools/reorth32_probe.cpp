@@ -47,10 +47,12 @@ int main(int argc, char** argv) {
     float bg = 1e30f, bt = 1e30f;
     for (int rep = 0; rep < 3; ++rep) {
       (void)hipEventRecord(e0);
-      rbl::gram32_partial(n, W, n * b, nW, b, X0, X1, 2, slab, splits, 0);
+      // PROBE_W0=1: every panel aliases panel 0 (basis from cache, same instructions)
+      const int64_t ws = (getenv("PROBE_W0") && atoi(getenv("PROBE_W0"))) ? 0 : n * b;
+      rbl::gram32_partial(n, W, ws, nW, b, X0, X1, 2, slab, splits, 0);
       rbl::reduce_slab(slab, splits, (int64_t)nW * b * 64, Cg, nullptr, 0);
       (void)hipEventRecord(e1);
-      rbl::tsmm32(n, W, n * b, nW, b, C, 64, X0, X1, 2, -1.f, 1.f, 0);
+      rbl::tsmm32(n, W, ws, nW, b, C, 64, X0, X1, 2, -1.f, 1.f, 0);
       (void)hipEventRecord(e2);
       (void)hipEventSynchronize(e2);
       float g, t;
