@@ -27,6 +27,9 @@ struct PanelRun {
 // writes carries kRowPad spare rows: the band kernel's loads and stores run unguarded.
 constexpr int64_t kCsrPad = 256;
 constexpr int64_t kRowPad = 16;
+// zeroed rows past the fp32 basis slots and the fp32 staging slot: the fp32 Gram's shifted
+// chunks (reorth32.hip, up to this many rows) may read them when a slice has fewer rows
+constexpr int64_t kRowPad32 = 32;
 
 struct CsrDev {
   int64_t nrows = 0;

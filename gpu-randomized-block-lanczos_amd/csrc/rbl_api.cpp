@@ -2282,17 +2282,17 @@ int rbl_start(rbl_ctx* ctx, int b, int max_blocks, int basis_bits, const double*
       }
     }
   } else {
-    // + 16 zeroed pad rows, and every slot zeroed once: the fp32 Gram kernel's shifted chunks
-    // may read rows past a tiny slice (reorth32.hip), which must be finite
-    const size_t bytes32 = ((size_t)dev_slots * nl + 16) * b * sizeof(float);
+    // + kRowPad32 zeroed pad rows, and every slot zeroed once: the fp32 Gram kernel's shifted
+    // chunks may read rows past a tiny slice (reorth32.hip), which must be finite
+    const size_t bytes32 = ((size_t)dev_slots * nl + kRowPad32) * b * sizeof(float);
     HIPC(hipMalloc(&ctx->d_basis32, bytes32));
     HIPC(hipMemsetAsync(ctx->d_basis32, 0, bytes32, ctx->stream));
     if (dev_slots < max_blocks + 1) {  // host spill of the FLOAT basis (RBL_gpu.jl:59-81)
       ctx->resident = dev_slots - 2;
       ctx->h_spill.assign(max_blocks + 1 - ctx->resident, nullptr);
-      // + 16 zero rows like the slots (the Gram's shifted chunks)
-      HIPC(hipMalloc(&ctx->d_stage32, ((size_t)nl + 16) * b * sizeof(float)));
-      HIPC(hipMemsetAsync(ctx->d_stage32, 0, ((size_t)nl + 16) * b * sizeof(float), ctx->stream));
+      // + kRowPad32 zero rows like the slots (the Gram's shifted chunks)
+      HIPC(hipMalloc(&ctx->d_stage32, ((size_t)nl + kRowPad32) * b * sizeof(float)));
+      HIPC(hipMemsetAsync(ctx->d_stage32, 0, ((size_t)nl + kRowPad32) * b * sizeof(float), ctx->stream));
       if (!ctx->cstream) {
         HIPC(hipStreamCreateWithFlags(&ctx->cstream, hipStreamNonBlocking));
         HIPC(hipEventCreateWithFlags(&ctx->ev_fin, hipEventDisableTiming));

@@ -25,7 +25,16 @@ __device__ __forceinline__ f4v mfma16(float a, float b, f4v c) {
 // ds_read_b128 hands a lane its B operand for all four 16-column tiles.
 // ----------------------------------------------------------------------------------------
 constexpr int kG32Waves = 4;
-constexpr int kG32Rows = 16;
+// rows per X chunk (one barrier per chunk): 16 or 32
+#ifndef RBL_G32_ROWS
+#define RBL_G32_ROWS 32
+#endif
+constexpr int kG32Rows = RBL_G32_ROWS;
+// basis operand prefetch depth in chunks (1 or 2)
+#ifndef RBL_G32_PF
+#define RBL_G32_PF 1
+#endif
+static_assert((kG32Rows == 16 || kG32Rows == 32) && kG32Rows <= kRowPad32, "fp32 Gram chunk rows");
 
 template <int W, int NX>
 __global__ __launch_bounds__(256) void k_gram32(int64_t nrows, const float* __restrict__ Wb,
@@ -35,6 +44,8 @@ __global__ __launch_bounds__(256) void k_gram32(int64_t nrows, const float* __re
   constexpr int KC = NX * W;        // X columns
   constexpr int CT = KC / 16;       // 16-column tiles of X (1..4)
   constexpr int AT = W / 16;        // 16-column tiles of the panel (1..2)
+  constexpr int KS = kG32Rows / 4;  // k steps (4 rows each) per chunk
+  constexpr int XR = kG32Rows / 16; // X rows staged per thread per chunk
   __shared__ __attribute__((aligned(16))) float xs[2][kG32Rows * 64];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int q = lane >> 4, c16 = lane & 15;
@@ -57,8 +68,9 @@ __global__ __launch_bounds__(256) void k_gram32(int64_t nrows, const float* __re
   // X staging: thread (row = tid / 16, cc = tid % 16) moves X[row][cc + 16 ct] (ct < CT).
   // A partial last chunk is shifted back to end at r_end (wave-uniform row base, no per-lane
   // clamps) and its rows below rc0 — already counted — zeroed on the X side, as in
-  // reorth.hip's k_gram44.  With nrows < 16 the chunk starts at row 0 and over-reads into the
-  // next basis slot or the zeroed allocation pad (rbl_start): finite rows met by zero X.
+  // reorth.hip's k_gram44.  With nrows < kG32Rows the chunk starts at row 0 and over-reads into
+  // the next basis slot or the zeroed allocation pad (kRowPad32, rbl_start): finite rows met
+  // by zero X.
   const int xrow = tid >> 4, xcc = tid & 15;
   const float* xsl[CT];
 #pragma unroll
@@ -71,29 +83,69 @@ __global__ __launch_bounds__(256) void k_gram32(int64_t nrows, const float* __re
     const int64_t r = rc0 < r_end - kG32Rows ? rc0 : r_end - kG32Rows;
     return r > 0 ? r : 0;
   };
-  auto load_x = [&](int64_t rc0, float (&xr)[CT]) {
+  auto load_x = [&](int64_t rc0, float (&xr)[XR][CT]) {
     const int64_t o = shift(rc0) * W;
 #pragma unroll
-    for (int ct = 0; ct < CT; ++ct) xr[ct] = xsl[ct][o];
-  };
-  auto store_x = [&](int buf, int64_t rc0, const float (&xr)[CT]) {
-    const int64_t row = shift(rc0) + xrow;
-    const bool ok = row >= rc0 && row < r_end;
-    float* d = &xs[buf][xrow * 64 + 4 * xcc];
+    for (int h = 0; h < XR; ++h)
 #pragma unroll
-    for (int ct = 0; ct < CT; ++ct) d[ct] = ok ? xr[ct] : 0.f;
+      for (int ct = 0; ct < CT; ++ct) xr[h][ct] = xsl[ct][o + 16 * h * W];
   };
-  auto load_a = [&](int64_t rc0, float (&ar)[4][AT]) {
+  auto store_x = [&](int buf, int64_t rc0, const float (&xr)[XR][CT]) {
+#pragma unroll
+    for (int h = 0; h < XR; ++h) {
+      const int64_t row = shift(rc0) + xrow + 16 * h;
+      const bool ok = row >= rc0 && row < r_end;
+      float* d = &xs[buf][(xrow + 16 * h) * 64 + 4 * xcc];
+#pragma unroll
+      for (int ct = 0; ct < CT; ++ct) d[ct] = ok ? xr[h][ct] : 0.f;
+    }
+  };
+  auto load_a = [&](int64_t rc0, float (&ar)[KS][AT]) {
     const float* p = wl + shift(rc0) * W;
 #pragma unroll
-    for (int ks = 0; ks < 4; ++ks)
+    for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
       for (int a = 0; a < AT; ++a) ar[ks][a] = p[4 * ks * W + 16 * a];
   };
 
   const int64_t nchunks = r_end > r_begin ? (r_end - r_begin + kG32Rows - 1) / kG32Rows : 0;
-  float xr[CT];
-  float acur[4][AT], anext[4][AT];
+  float xr[XR][CT];
+  auto mma = [&](int64_t ch, const float (&acur)[KS][AT]) {
+    const float* xb = xs[ch & 1] + 4 * c16;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const f4v bv = *reinterpret_cast<const f4v*>(xb + (4 * ks + q) * 64);
+#pragma unroll
+      for (int a = 0; a < AT; ++a)
+#pragma unroll
+        for (int c = 0; c < CT; ++c) acc[a][c] = mfma16(acur[ks][a], bv[c], acc[a][c]);
+    }
+  };
+#if RBL_G32_PF >= 2
+  // basis operands two chunks ahead in three rotating register sets (as k_gram44)
+  float a0[KS][AT], a1[KS][AT], a2[KS][AT];
+  if (nchunks > 0) {
+    load_x(r_begin, xr);
+    store_x(0, r_begin, xr);
+    load_a(r_begin, a0);
+    load_a(r_begin + kG32Rows, a1);
+  }
+  __syncthreads();
+  auto step = [&](int64_t ch, const float (&acur)[KS][AT], float (&afut)[KS][AT]) {
+    const int64_t rc0 = r_begin + ch * kG32Rows;
+    load_x(rc0 + kG32Rows, xr);
+    load_a(rc0 + 2 * kG32Rows, afut);
+    if (active && ch < nchunks) mma(ch, acur);  // no loads inside
+    store_x((int)((ch + 1) & 1), rc0 + kG32Rows, xr);
+    __syncthreads();
+  };
+  for (int64_t ch = 0; ch < nchunks; ch += 3) {
+    step(ch, a0, a2);
+    step(ch + 1, a1, a0);
+    step(ch + 2, a2, a1);
+  }
+#else
+  float acur[KS][AT], anext[KS][AT];
   if (nchunks > 0) {
     load_x(r_begin, xr);
     store_x(0, r_begin, xr);
@@ -104,24 +156,15 @@ __global__ __launch_bounds__(256) void k_gram32(int64_t nrows, const float* __re
     const int64_t rc0 = r_begin + ch * kG32Rows;
     load_x(rc0 + kG32Rows, xr);  // unconditional (clamped): see reorth.hip
     load_a(rc0 + kG32Rows, anext);
-    if (active) {
-      const float* xb = xs[ch & 1] + 4 * c16;
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        const f4v bv = *reinterpret_cast<const f4v*>(xb + (4 * ks + q) * 64);
-#pragma unroll
-        for (int a = 0; a < AT; ++a)
-#pragma unroll
-          for (int c = 0; c < CT; ++c) acc[a][c] = mfma16(acur[ks][a], bv[c], acc[a][c]);
-      }
-    }
+    if (active) mma(ch, acur);
     store_x((int)((ch + 1) & 1), rc0 + kG32Rows, xr);
 #pragma unroll
-    for (int ks = 0; ks < 4; ++ks)
+    for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
       for (int a = 0; a < AT; ++a) acur[ks][a] = anext[ks][a];
     __syncthreads();
   }
+#endif
   if (!active) return;
   // D[a][c] tile (16 x 16): lane holds rows 4q + v, column c16 of the tile
   double* out = slab + (s * (int64_t)nW * W + (int64_t)j * W) * KC;
