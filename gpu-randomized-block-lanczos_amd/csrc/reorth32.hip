@@ -444,12 +444,18 @@ __global__ __launch_bounds__(256) void k_tsmm32(int64_t nrows, const float* __re
 // multiple of 32, nrows >= 32): 32 k per chunk (half the barriers), wave-uniform bases plus
 // lane constants (no per-load clamps), a wave past nrows computes the last 32 rows and stores
 // only its own, 16-B Y stores through the wave's LDS tile.
-constexpr int kT32KF = 32;
+// KF: k per chunk (one barrier per 2 KF MFMAs per wave), 32 or 64 (two basis panels; even nX).
+// 64 measured 1.5 % slower (occupancy 5 -> 4; profiles/r03_tsmm32_kf_ab.log), so 32
+#ifndef RBL_T32_KF
+#define RBL_T32_KF 32
+#endif
+template <int KF>
 __global__ __launch_bounds__(256) void k_tsmm32f(int64_t nrows, const float* __restrict__ Xb,
                                                  int64_t xstride, int nX, const double* __restrict__ C,
                                                  int ldc, float* Y0, float* Y1, float alpha,
                                                  float beta) {
   constexpr int W = 32, KYP = 64, CT = 4, CLD = 64;
+  constexpr int kT32KF = KF, HH = KF / 16;
   // two C buffers; after the k-loop the same LDS holds the 4 waves' 16 x (64 + 4) Y tiles
   __shared__ __attribute__((aligned(16))) float cs[2][kT32KF * CLD + 128];
   static_assert(2 * (kT32KF * CLD + 128) >= 4 * 16 * (KYP + 4), "epilogue tiles fit");
@@ -466,36 +472,38 @@ __global__ __launch_bounds__(256) void k_tsmm32f(int64_t nrows, const float* __r
 #pragma unroll
     for (int c = 0; c < CT; ++c) acc[rt][c] = f4v{0.f, 0.f, 0.f, 0.f};
 
-  // A: rows rw + 16 rt + c16; k = 32 ch + 16 hh + 4 q + s (one float4 per (rt, hh))
+  // A: rows rw + 16 rt + c16; k = KF ch + 16 hh + 4 q + s (one float4 per (rt, hh)); the
+  // chunk spans KF / 32 basis panels (hh / 2 selects the panel at KF = 64)
   const int aoff = c16 * W + 4 * q;
-  auto load_a = [&](int ch, f4v (&ar)[2][2]) {
+  auto load_a = [&](int ch, f4v (&ar)[2][HH]) {
     const int chc = ch < nch ? ch : nch - 1;
-    const float* xb = Xb + (int64_t)chc * xstride + rw * W;  // W = 32 = k per chunk: panel chc
 #pragma unroll
-    for (int rt = 0; rt < 2; ++rt)
+    for (int hh = 0; hh < HH; ++hh) {
+      const float* xb = Xb + (int64_t)(KF / W * chc + hh / 2) * xstride + rw * W;
 #pragma unroll
-      for (int hh = 0; hh < 2; ++hh)
-        ar[rt][hh] = *reinterpret_cast<const f4v*>(xb + aoff + 16 * rt * W + 16 * hh);
+      for (int rt = 0; rt < 2; ++rt)
+        ar[rt][hh] = *reinterpret_cast<const f4v*>(xb + aoff + 16 * rt * W + 16 * (hh & 1));
+    }
   };
-  // C chunk: 32 x 64; thread (k = tid / 16 + 16 hh, cc = tid % 16) moves C[k][cc + 16 ct]
+  // C chunk: KF x 64; thread (k = tid / 16 + 16 hh, cc = tid % 16) moves C[k][cc + 16 ct]
   const int ck = tid >> 4, ccc = tid & 15;
-  auto load_c = [&](int ch, float (&cr)[2][CT]) {
+  auto load_c = [&](int ch, float (&cr)[HH][CT]) {
     const int chc = ch < nch ? ch : nch - 1;
     const double* cb = C + (int64_t)(kT32KF * chc + ck) * ldc + ccc;
 #pragma unroll
-    for (int hh = 0; hh < 2; ++hh)
+    for (int hh = 0; hh < HH; ++hh)
 #pragma unroll
       for (int ct = 0; ct < CT; ++ct) cr[hh][ct] = alpha * (float)cb[(int64_t)(16 * hh) * ldc + 16 * ct];
   };
-  auto store_c = [&](int buf, const float (&cr)[2][CT]) {
+  auto store_c = [&](int buf, const float (&cr)[HH][CT]) {
 #pragma unroll
-    for (int hh = 0; hh < 2; ++hh)
+    for (int hh = 0; hh < HH; ++hh)
       *reinterpret_cast<f4v*>(&cs[buf][(ck + 16 * hh) * CLD + 4 * ccc]) =
           f4v{cr[hh][0], cr[hh][1], cr[hh][2], cr[hh][3]};
   };
 
-  f4v acur[2][2], anext[2][2];
-  float cr[2][CT];
+  f4v acur[2][HH], anext[2][HH];
+  float cr[HH][CT];
   load_c(0, cr);
   store_c(0, cr);
   load_a(0, acur);
@@ -505,7 +513,7 @@ __global__ __launch_bounds__(256) void k_tsmm32f(int64_t nrows, const float* __r
     load_a(ch + 1, anext);
     const float* cb = cs[ch & 1] + 4 * c16;
 #pragma unroll
-    for (int hh = 0; hh < 2; ++hh)
+    for (int hh = 0; hh < HH; ++hh)
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
         const f4v bv = *reinterpret_cast<const f4v*>(cb + (16 * hh + 4 * q + s) * CLD);
@@ -516,10 +524,9 @@ __global__ __launch_bounds__(256) void k_tsmm32f(int64_t nrows, const float* __r
       }
     store_c((ch + 1) & 1, cr);
 #pragma unroll
-    for (int rt = 0; rt < 2; ++rt) {
-      acur[rt][0] = anext[rt][0];
-      acur[rt][1] = anext[rt][1];
-    }
+    for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+      for (int hh = 0; hh < HH; ++hh) acur[rt][hh] = anext[rt][hh];
     __syncthreads();
   }
   // epilogue: D tile (lane: rows 4q + v, column c16 of tile c) -> LDS (free after the last
@@ -631,8 +638,12 @@ void tsmm32(int64_t nrows, const float* Xb, int64_t xstride, int nX, int w, cons
   }
   if (w == 32 && KY == 64 && nrows >= kT32Rows) {
     const int64_t wgs = (nrows + 4 * kT32Rows - 1) / (4 * kT32Rows);
-    hipLaunchKernelGGL(k_tsmm32f, dim3((unsigned)wgs), dim3(256), 0, st, nrows, Xb, xstride, nX, C,
-                       ldc, Y0, Y1, alpha, beta);
+    if (RBL_T32_KF == 64 && nX % 2 == 0)
+      hipLaunchKernelGGL(k_tsmm32f<64>, dim3((unsigned)wgs), dim3(256), 0, st, nrows, Xb, xstride, nX, C,
+                         ldc, Y0, Y1, alpha, beta);
+    else
+      hipLaunchKernelGGL(k_tsmm32f<32>, dim3((unsigned)wgs), dim3(256), 0, st, nrows, Xb, xstride, nX, C,
+                         ldc, Y0, Y1, alpha, beta);
     return;
   }
   if (w == 32) {
