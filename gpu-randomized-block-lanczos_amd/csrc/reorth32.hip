@@ -177,6 +177,112 @@ __global__ __launch_bounds__(256) void k_gram32(int64_t nrows, const float* __re
         out[(int64_t)(16 * a + 4 * q + v) * KC + 16 * c + c16] = (double)acc[a][c][v];
 }
 
+// The same Gram on v_mfma_f32_32x32x2f32 (b = 32, X = [Q_i, Q_{i-1}]): one 32 x 32 output tile
+// per X panel, 4096 flops per instruction (the shape measured 149 vs 136 TF/s for 16x16x4 in a
+// register loop, tools/mfma_probe.hip).  Step s of a chunk takes rows 2s and 2s + 1: lane l
+// holds A[i = l % 32][k = l / 32] = W[2s + l / 32][l % 32], i.e. one contiguous 256-B load of
+// the two rows per step, and B[k][j] = X[2s + k][j] (+32 for the second panel), adjacent in the
+// LDS image (row r, column c at r * 64 + 2 (c % 32) + c / 32) so one ds_read_b64 per step feeds
+// both tiles.  D[i][j]: lane l, register v holds i = 4 (l / 32) + (v % 4) + 8 (v / 4), j = l % 32.
+#ifndef RBL_G32_MFMA32
+#define RBL_G32_MFMA32 1
+#endif
+typedef float f16v __attribute__((ext_vector_type(16)));
+__global__ __launch_bounds__(256) void k_gram32x(int64_t nrows, const float* __restrict__ Wb,
+                                                 int64_t wstride, int nW, const float* __restrict__ X0,
+                                                 const float* __restrict__ X1, double* __restrict__ slab,
+                                                 int npg, int64_t rows_per) {
+  constexpr int W = 32, KC = 64, NS = kG32Rows / 2;  // k steps (2 rows each) per chunk
+  constexpr int XE = kG32Rows * KC / 256;            // X elements staged per thread per chunk
+  __shared__ __attribute__((aligned(16))) float xs[2][kG32Rows * KC];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, t = bid >> 3;  // XCD-aware: a split's panel groups share an L2
+  const int pg = t % npg;
+  const int64_t s = (int64_t)(t / npg) * 8 + xcd;
+  const int64_t r_begin = s * rows_per;
+  const int64_t r_end = r_begin + rows_per < nrows ? r_begin + rows_per : nrows;
+  const int j = pg * kG32Waves + wave;
+  const bool active = j < nW;
+  const float* wpan = Wb + (int64_t)(active ? j : 0) * wstride;  // wave-uniform
+
+  f16v acc[2];
+#pragma unroll
+  for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+    for (int v = 0; v < 16; ++v) acc[tt][v] = 0.f;
+
+  auto shift = [&](int64_t rc0) -> int64_t {
+    const int64_t r = rc0 < r_end - kG32Rows ? rc0 : r_end - kG32Rows;
+    return r > 0 ? r : 0;
+  };
+  // X staging: thread (row = e / 64, column c = e % 64) for e = 4 tid + 1024 h .. + 3 (float4 of
+  // one panel: 4 consecutive columns of the same panel)
+  auto load_x = [&](int64_t rc0, f4v (&xr)[XE / 4]) {
+    const int64_t rb = shift(rc0);
+#pragma unroll
+    for (int h = 0; h < XE / 4; ++h) {
+      const int e = 4 * tid + 1024 * h, row = e / KC, c = e % KC;
+      const float* src = (c < W ? X0 + c : X1 + (c - W)) + (rb + row) * W;
+      xr[h] = *reinterpret_cast<const f4v*>(src);
+    }
+  };
+  auto store_x = [&](int buf, int64_t rc0, const f4v (&xr)[XE / 4]) {
+    const int64_t rb = shift(rc0);
+#pragma unroll
+    for (int h = 0; h < XE / 4; ++h) {
+      const int e = 4 * tid + 1024 * h, row = e / KC, c = e % KC;
+      const bool ok = rb + row >= rc0 && rb + row < r_end;
+      float* d = &xs[buf][row * KC + 2 * (c % W) + c / W];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) d[2 * u] = ok ? xr[h][u] : 0.f;
+    }
+  };
+  auto load_a = [&](int64_t rc0, float (&ar)[NS]) {
+    const float* p = wpan + shift(rc0) * W;  // uniform
+#pragma unroll
+    for (int st = 0; st < NS; ++st) ar[st] = p[(unsigned)(2 * st * W + lane)];
+  };
+
+  const int64_t nchunks = r_end > r_begin ? (r_end - r_begin + kG32Rows - 1) / kG32Rows : 0;
+  f4v xr[XE / 4];
+  float acur[NS], anext[NS];
+  if (nchunks > 0) {
+    load_x(r_begin, xr);
+    store_x(0, r_begin, xr);
+    load_a(r_begin, acur);
+  }
+  __syncthreads();
+  for (int64_t ch = 0; ch < nchunks; ++ch) {
+    const int64_t rc0 = r_begin + ch * kG32Rows;
+    load_x(rc0 + kG32Rows, xr);  // unconditional (clamped): see reorth.hip
+    load_a(rc0 + kG32Rows, anext);
+    if (active) {
+      const float* xb = xs[ch & 1] + 2 * lane;
+#pragma unroll
+      for (int st = 0; st < NS; ++st) {
+        const float2 bv = *reinterpret_cast<const float2*>(xb + st * 2 * KC);
+        acc[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(acur[st], bv.x, acc[0], 0, 0, 0);
+        acc[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(acur[st], bv.y, acc[1], 0, 0, 0);
+      }
+    }
+    store_x((int)((ch + 1) & 1), rc0 + kG32Rows, xr);
+#pragma unroll
+    for (int st = 0; st < NS; ++st) acur[st] = anext[st];
+    __syncthreads();
+  }
+  if (!active) return;
+  double* out = slab + (s * (int64_t)nW * W + (int64_t)j * W) * KC;
+#pragma unroll
+  for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+      const int a = 4 * (lane / 32) + (v % 4) + 8 * (v / 4);
+      out[(int64_t)a * KC + W * tt + (lane % 32)] = (double)acc[tt][v];
+    }
+}
+
 // The local-reorth Gram C = Q_{i-1}^T Q_i (one 32-column panel, 32 X columns): k_gram32 gives
 // each wave its own panel, so with one panel three of its four waves only stage X.  Here the
 // four waves take consecutive 16-row slices of a 64-row chunk, load both operands straight
@@ -329,6 +435,14 @@ void gram32_partial(int64_t nrows, const float* Wb, int64_t wstride, int nW, int
     return;
   }
   if (w == 32) {
+    if (xcount == 2 && RBL_G32_MFMA32) {
+      const int npg = (nW + kG32Waves - 1) / kG32Waves;
+      int64_t rows_per = (nrows + splits - 1) / splits;
+      rows_per = (rows_per + kG32Rows - 1) / kG32Rows * kG32Rows;
+      hipLaunchKernelGGL(k_gram32x, dim3(npg * splits), dim3(256), 0, st, nrows, Wb, wstride, nW, X0, X1,
+                         slab, npg, rows_per);
+      return;
+    }
     if (xcount == 2) return launch_gram32<32, 2>(nrows, Wb, wstride, nW, X0, X1, slab, splits, st);
     return launch_gram32<32, 1>(nrows, Wb, wstride, nW, X0, X1, slab, splits, st);
   }
@@ -556,6 +670,113 @@ __global__ __launch_bounds__(256) void k_tsmm32f(int64_t nrows, const float* __r
   }
 }
 
+// The partial-reorth update on v_mfma_f32_32x32x2f32 (W = 32, 64 output columns): a wave owns
+// 32 rows (one 32 x 32 tile per output panel).  Step s of a 32-k chunk (one basis panel) takes
+// k = s for lanes 0-31 and k = 16 + s for lanes 32-63, so lane l loads its row's 16
+// consecutive k once per chunk (four float4: row rw + l % 32, k 16 (l / 32) ..) and B[k][j] =
+// alpha C[k][j] (+32 for the second panel) sits pairwise in LDS (row k, column c at
+// k * 64 + 2 (c % 32) + c / 32): one ds_read_b64 per step feeds both tiles.  Epilogue as
+// k_tsmm32f, by 16-row halves (registers v < 8 hold rows 0-15 of the tile).
+#ifndef RBL_T32_MFMA32
+#define RBL_T32_MFMA32 1
+#endif
+__global__ __launch_bounds__(256) void k_tsmm32x(int64_t nrows, const float* __restrict__ Xb,
+                                                 int64_t xstride, int nX, const double* __restrict__ C,
+                                                 int ldc, float* Y0, float* Y1, float alpha,
+                                                 float beta) {
+  constexpr int W = 32, KYP = 64, KF = 32, NS = 16, CLD = 64;
+  __shared__ __attribute__((aligned(16))) float cs[2][KF * CLD + 128];
+  static_assert(2 * (KF * CLD + 128) >= 4 * 16 * (KYP + 4), "epilogue tiles fit");
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int64_t r0 = ((int64_t)blockIdx.x * 4 + wave) * kT32Rows;
+  const int64_t rw = r0 + kT32Rows <= nrows ? r0 : nrows - kT32Rows;  // wave-uniform
+  const int nch = nX;  // one 32-column basis panel per chunk
+
+  f16v acc[2];
+#pragma unroll
+  for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+    for (int v = 0; v < 16; ++v) acc[tt][v] = 0.f;
+
+  const unsigned aoff = (unsigned)((lane % 32) * W + 16 * (lane / 32));
+  auto load_a = [&](int ch, f4v (&ar)[4]) {
+    const int chc = ch < nch ? ch : nch - 1;
+    const float* xb = Xb + (int64_t)chc * xstride + rw * W;  // uniform
+#pragma unroll
+    for (int u = 0; u < 4; ++u) ar[u] = *reinterpret_cast<const f4v*>(xb + (aoff + 4u * u));
+  };
+  // C chunk 32 x 64: thread (k = tid / 8, c0 = 4 (tid % 8)) moves C[k][c0 .. c0 + 3] and
+  // C[k][32 + c0 .. 32 + c0 + 3] into 8 consecutive floats (pairwise interleaved)
+  const int ck = tid >> 3, cc0 = 4 * (tid & 7);
+  auto load_c = [&](int ch, float (&cr)[8]) {
+    const int chc = ch < nch ? ch : nch - 1;
+    const double* cb = C + (int64_t)(KF * chc + ck) * ldc + cc0;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      cr[2 * u] = alpha * (float)cb[u];
+      cr[2 * u + 1] = alpha * (float)cb[W + u];
+    }
+  };
+  auto store_c = [&](int buf, const float (&cr)[8]) {
+    float* d = &cs[buf][ck * CLD + 2 * cc0];
+    *reinterpret_cast<f4v*>(d) = f4v{cr[0], cr[1], cr[2], cr[3]};
+    *reinterpret_cast<f4v*>(d + 4) = f4v{cr[4], cr[5], cr[6], cr[7]};
+  };
+
+  f4v acur[4], anext[4];
+  float cr[8];
+  load_c(0, cr);
+  store_c(0, cr);
+  load_a(0, acur);
+  __syncthreads();
+  for (int ch = 0; ch < nch; ++ch) {
+    load_c(ch + 1, cr);
+    load_a(ch + 1, anext);
+    const float* cb = cs[ch & 1] + 16 * (lane / 32) * CLD + 2 * (lane % 32);
+#pragma unroll
+    for (int st = 0; st < NS; ++st) {
+      const float2 bv = *reinterpret_cast<const float2*>(cb + st * CLD);
+      const float a = acur[st / 4][st % 4];
+      acc[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bv.x, acc[0], 0, 0, 0);
+      acc[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bv.y, acc[1], 0, 0, 0);
+    }
+    store_c((ch + 1) & 1, cr);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acur[u] = anext[u];
+    __syncthreads();
+  }
+  // epilogue: D (lane l, register v: row 4 (l / 32) + v % 4 + 8 (v / 4), column l % 32 of tile
+  // tt) -> LDS by 16-row halves -> row-major float4 stores of Y0 | Y1 (rows below r0: the
+  // previous wave's)
+  float* ot = &cs[0][0] + wave * 16 * (KYP + 4);
+#pragma unroll
+  for (int rt = 0; rt < 2; ++rt) {
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+      for (int v = 8 * rt; v < 8 * rt + 8; ++v) {
+        const int i = 4 * (lane / 32) + (v % 4) + 8 * (v / 4) - 16 * rt;
+        ot[i * (KYP + 4) + W * tt + (lane % 32)] = acc[tt][v];
+      }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const int e = 4 * lane + 256 * m, row = e / KYP, col = e % KYP;
+      const int64_t r = rw + 16 * rt + row;
+      f4v y = *reinterpret_cast<const f4v*>(ot + row * (KYP + 4) + col);
+      if (r >= r0 && r < nrows) {
+        float* yp = (col < W ? Y0 + col : Y1 + (col - W)) + r * W;
+        if (beta != 0.f) y += beta * *reinterpret_cast<const f4v*>(yp);
+        *reinterpret_cast<f4v*>(yp) = y;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
 template <int W, int KYP>
 static void launch_tsmm32(int64_t nrows, const float* Xb, int64_t xstride, int nX, const double* C,
                           int ldc, int KY, float* Y0, float* Y1, float alpha, float beta,
@@ -638,6 +859,11 @@ void tsmm32(int64_t nrows, const float* Xb, int64_t xstride, int nX, int w, cons
   }
   if (w == 32 && KY == 64 && nrows >= kT32Rows) {
     const int64_t wgs = (nrows + 4 * kT32Rows - 1) / (4 * kT32Rows);
+    if (RBL_T32_MFMA32) {
+      hipLaunchKernelGGL(k_tsmm32x, dim3((unsigned)wgs), dim3(256), 0, st, nrows, Xb, xstride, nX, C,
+                         ldc, Y0, Y1, alpha, beta);
+      return;
+    }
     if (RBL_T32_KF == 64 && nX % 2 == 0)
       hipLaunchKernelGGL(k_tsmm32f<64>, dim3((unsigned)wgs), dim3(256), 0, st, nrows, Xb, xstride, nX, C,
                          ldc, Y0, Y1, alpha, beta);
