@@ -62,6 +62,9 @@ constexpr int kG44Waves = 4;
 #ifndef RBL_G44_W16
 #define RBL_G44_W16 1
 #endif
+#ifndef RBL_G44_DUO_WPE
+#define RBL_G44_DUO_WPE 1
+#endif
 #ifndef RBL_G44_GLDS
 #define RBL_G44_GLDS 1
 #endif
@@ -89,12 +92,19 @@ struct G44Lines {
 
 // PAIR (B = 16): a wave's "panel" j is the pair of basis panels 2j, 2j+1 (32 columns, as one
 // B = 32 panel: the same registers and MFMAs per chunk), so b = 16 runs the b = 32 tile shape
-template <int B, int NX, int NPH, bool PAIR = false, bool GL = false>
+// DUO (B = 32, even panel count; RBL_G44_DUO=1, off by default): a wave's "panel" j is the pair
+// of basis panels 2j, 2j+1 (64 columns, four column groups in two 16-B loads per row quad):
+// twice the MFMAs per X operand read from LDS and half the panel groups.  Bit-identical, but
+// measured slower (profiles/r03_gram_duo_ab.log): 289 ms summed over the probe at one wave per
+// SIMD, 299 ms at two (19 VGPRs spilled), against 262 ms for one panel per wave at three waves
+// per SIMD; C4a 45.4 vs 47.2 block-iters/s.  The extra waves hide the per-chunk barrier.
+template <int B, int NX, int NPH, bool PAIR = false, bool GL = false, bool DUO = false>
 __device__ __forceinline__ void gram44_body(int64_t r_begin, int64_t r_end, int64_t s, int pg,
                                             int r, const PanelRun& W, const Panels& X,
                                             double* slab, double* xs_base) {
   constexpr int KC = NX * B;
-  constexpr int WB = PAIR ? 2 * B : B;  // basis columns per wave
+  static_assert(!DUO || (B == 32 && !PAIR), "DUO: b = 32 panel pairs");
+  constexpr int WB = PAIR || DUO ? 2 * B : B;  // basis columns per wave
   constexpr int AG = WB / 16;
   constexpr int CG = KC / 4;
   constexpr int CGP = CG / NPH;  // column groups of this wave (even: read in pairs)
@@ -131,10 +141,10 @@ __device__ __forceinline__ void gram44_body(int64_t r_begin, int64_t r_end, int6
   // column group ag of the wave's panel (PAIR: ag = the pair member).  W16 (b = 32): lane
   // column 2 (lane & 15) + ag, both ag in one 16-B load (W16 = 0: columns (lane & 15) + 16 ag,
   // two 8-B loads); the MFMAs see the same operands per output, only C's row order differs
-  constexpr bool W16 = RBL_G44_W16 && !PAIR && AG == 2;
+  constexpr bool W16 = (RBL_G44_W16 && !PAIR && AG == 2) || DUO;
   // the basis loads: a wave-uniform base (the panel, the chunk's rows) plus an unsigned 32-bit
   // lane offset, so they can issue in the saddr form without per-load 64-bit address VALU
-  const double* wpan = W.base + (int64_t)__builtin_amdgcn_readfirstlane(PAIR ? 2 * j : j) * W.stride;
+  const double* wpan = W.base + (int64_t)__builtin_amdgcn_readfirstlane(PAIR || DUO ? 2 * j : j) * W.stride;
   const unsigned wlo = (unsigned)((W16 ? 2 * (lane & 15) : (lane & 15)) + q * B);
   const int64_t wag = PAIR ? W.stride : 16;
   auto shift = [&](int64_t rc0) -> int64_t { return rc0 < r_end - kG44Rows ? rc0 : r_end - kG44Rows; };
@@ -168,7 +178,16 @@ __device__ __forceinline__ void gram44_body(int64_t r_begin, int64_t r_end, int6
   };
   auto load_a = [&](int64_t rc0, double (&ar)[KS][AG]) {
     const double* p = wpan + shift(rc0) * B;  // uniform
-    if constexpr (W16) {
+    if constexpr (DUO) {
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const d2v v = ldw(reinterpret_cast<const d2v*>(p + h * W.stride + (wlo + (unsigned)(4 * ks * B))));
+          ar[ks][2 * h] = v.x;
+          ar[ks][2 * h + 1] = v.y;
+        }
+    } else if constexpr (W16) {
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
         const d2v v = ldw(reinterpret_cast<const d2v*>(p + (wlo + (unsigned)(4 * ks * B))));
@@ -281,14 +300,16 @@ __device__ __forceinline__ void gram44_body(int64_t r_begin, int64_t r_end, int6
   for (int ag = 0; ag < AG; ++ag)
 #pragma unroll
     for (int cg = 0; cg < CGP; ++cg) {
-      const int a = W16 ? 2 * (4 * g + (lane >> 4)) + ag : 16 * ag + 4 * g + (lane >> 4);
+      const int a = DUO   ? 32 * (ag >> 1) + 2 * (4 * g + (lane >> 4)) + (ag & 1)
+                    : W16 ? 2 * (4 * g + (lane >> 4)) + ag
+                          : 16 * ag + 4 * g + (lane >> 4);
       const int cc = GL ? 8 * (cg >> 1) + 2 * (lane & 3) + (cg & 1) : 4 * cg + (lane & 3);
       out[(int64_t)a * KC + cc] = acc[ag][cg];
     }
 }
 
-template <int B, int NX, bool PAIR = false, bool GL = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RBL_G44_WPE))) void k_gram44(
+template <int B, int NX, bool PAIR = false, bool GL = false, bool DUO = false>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DUO ? RBL_G44_DUO_WPE : RBL_G44_WPE))) void k_gram44(
     int64_t nrows, PanelRun W, Panels X, double* slab, int npg, int64_t rows_per, const int* skip) {
   if (skip && *skip) return;
   constexpr int KC = NX * B;
@@ -305,11 +326,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RBL_G44_WPE
   const int64_t s = (int64_t)(t / npg) * 8 + xcd;
   const int64_t r_begin = s * rows_per;
   const int64_t r_end = r_begin + rows_per < nrows ? r_begin + rows_per : nrows;
-  const int rem = (PAIR ? W.count / 2 : W.count) - pg * kG44Waves;
+  const int rem = (PAIR || DUO ? W.count / 2 : W.count) - pg * kG44Waves;
   const int r = rem < kG44Waves ? rem : kG44Waves;  // panels in this group (workgroup-uniform)
-  if (r >= 3) gram44_body<B, NX, 1, PAIR, GL>(r_begin, r_end, s, pg, r, W, X, slab, xs);
-  else if (r == 2) gram44_body<B, NX, NPH2, PAIR, GL>(r_begin, r_end, s, pg, r, W, X, slab, xs);
-  else gram44_body<B, NX, NPH4, PAIR, GL>(r_begin, r_end, s, pg, r, W, X, slab, xs);
+  if (r >= 3) gram44_body<B, NX, 1, PAIR, GL, DUO>(r_begin, r_end, s, pg, r, W, X, slab, xs);
+  else if (r == 2) gram44_body<B, NX, NPH2, PAIR, GL, DUO>(r_begin, r_end, s, pg, r, W, X, slab, xs);
+  else gram44_body<B, NX, NPH4, PAIR, GL, DUO>(r_begin, r_end, s, pg, r, W, X, slab, xs);
 }
 
 bool gram44_ok(int64_t nrows, int nW, int w, int xcount, int xw) {
@@ -338,10 +359,10 @@ int gram44_splits(int64_t nrows, int nW, int w) {
   return (int)(s8 * 8);
 }
 
-template <int B, int NX, bool PAIR = false>
+template <int B, int NX, bool PAIR = false, bool DUO = false>
 static void launch_gram44(int64_t nrows, const PanelRun& W, const Panels& X, double* slab,
                           int splits, const int* skip, hipStream_t st) {
-  const int units = PAIR ? W.count / 2 : W.count;
+  const int units = PAIR || DUO ? W.count / 2 : W.count;
   const int npg = (units + kG44Waves - 1) / kG44Waves;
   int64_t rows_per = (nrows + splits - 1) / splits;
   rows_per = (rows_per + kG44Rows - 1) / kG44Rows * kG44Rows;
@@ -349,16 +370,23 @@ static void launch_gram44(int64_t nrows, const PanelRun& W, const Panels& X, dou
   bool gl = kGL;
   for (int t = 0; t < X.count; ++t) gl &= reinterpret_cast<uintptr_t>(X.ptr[t]) % 16 == 0;
   if (gl)
-    hipLaunchKernelGGL((k_gram44<B, NX, PAIR, kGL>), dim3(npg * splits), dim3(256), 0, st, nrows, W, X,
+    hipLaunchKernelGGL((k_gram44<B, NX, PAIR, kGL, DUO>), dim3(npg * splits), dim3(256), 0, st, nrows, W, X,
                        slab, npg, rows_per, skip);
   else
-    hipLaunchKernelGGL((k_gram44<B, NX, PAIR, false>), dim3(npg * splits), dim3(256), 0, st, nrows, W, X,
-                       slab, npg, rows_per, skip);
+    hipLaunchKernelGGL((k_gram44<B, NX, PAIR, false, DUO>), dim3(npg * splits), dim3(256), 0, st, nrows, W,
+                       X, slab, npg, rows_per, skip);
 }
 
 void gram44_partial(int64_t nrows, const PanelRun& W, const Panels& X, double* slab, int splits,
                     const int* skip, hipStream_t st) {
   if (W.w == 32) {
+    // RBL_G44_DUO=1: panel pairs per wave (A/B; see gram44_body)
+    static const bool duo_ok = [] {
+      const char* e = getenv("RBL_G44_DUO");
+      return e && atoi(e) != 0;
+    }();
+    if (duo_ok && X.count == 2 && W.count % 2 == 0)
+      return launch_gram44<32, 2, false, true>(nrows, W, X, slab, splits, skip, st);
     if (X.count == 2) return launch_gram44<32, 2>(nrows, W, X, slab, splits, skip, st);
     return launch_gram44<32, 1>(nrows, W, X, slab, splits, skip, st);
   }
