@@ -74,6 +74,9 @@ __global__ __launch_bounds__(256) void k_spmm_gather(int64_t nrows, const int64_
 // gathers back to back.  Segments write partial rows to `scratch`; k_seg_fixup sums each long
 // row's segments in order (deterministic) and applies the 3-term epilogue there.
 // ----------------------------------------------------------------------------------------
+#ifndef RBL_SEG_HOT
+#define RBL_SEG_HOT 0
+#endif
 template <int BP>
 __global__ __launch_bounds__(256) void k_spmm_seg(
     int64_t ntasks, const int64_t* __restrict__ trow, const int32_t* __restrict__ tinfo,
@@ -103,7 +106,16 @@ __global__ __launch_bounds__(256) void k_spmm_seg(
         for (int jj = 0; jj < 8; ++jj) {
           const int cj = __shfl(cl, j0 + jj, BP);
           v[jj] = __shfl(vl, j0 + jj, BP);
-          q[jj] = Q[(int64_t)(cj - col_off) * BP + c];
+          const double* qp = Q + ((int64_t)(cj - col_off) * BP + c);
+          if constexpr (RBL_SEG_HOT > 0) {
+            // columns past the hot set (R-MAT: high ids, low degree) load non-temporally so the
+            // hub rows' lines stay in L2 — measured no faster at hot sets of 16 K and 128 K
+            // rows (profiles/r03_rmat_hot_nt_ab.log), so off
+            if (cj < RBL_SEG_HOT) q[jj] = *qp;
+            else q[jj] = __builtin_nontemporal_load(qp);
+          } else {
+            q[jj] = *qp;
+          }
         }
 #pragma unroll
         for (int jj = 0; jj < 8; jj += 2) {

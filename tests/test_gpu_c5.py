@@ -97,3 +97,26 @@ def test_c5_mixed_rbl_gpu_spilled(c5):
     rq = np.einsum("ij,ij->j", V, AV) / np.einsum("ij,ij->j", V, V)
     assert np.all(np.abs(rq - D) <= RAYLEIGH_TOL * np.abs(D)), np.abs(rq - D) / np.abs(D)
     log("Ritz pairs checked")
+
+
+def test_c5_deep_spill_bit_identical(c5):
+    """The capacity regime at C5's n: 16 fixed steps with only DEVICE_BLOCKS slots in HBM (10 of
+    the 16 fp32 blocks, 64 GB, in pinned host memory, streamed back over PCIe for every partial
+    reorth) against the same 16 steps with the whole basis resident (109 GB of fp32 slots).  In
+    the reference's block-MGS order (RBL_OPT_REORTH_ORDER = 1, RBL_gpu.jl:62-68) both apply the
+    same kernels to the same blocks in the same order, so every A_i and B_{i+1} is the same bits."""
+    rbl, ctx = c5
+    steps = 16
+    traces = []
+    for device_blocks in (DEVICE_BLOCKS, 0):
+        ctx.set_option(rbl._lib.RBL_OPT_REORTH_ORDER, 1)
+        ctx.set_option(rbl._lib.RBL_OPT_DEVICE_BLOCKS, device_blocks)
+        _, _, info = rbl.lanczos(ctx, K, B, seed=SEED + 4, check=False, max_steps=steps, trace=True,
+                                 ritz=False, basis_bits=32)
+        assert info.iters == steps and len(info.trace_A) == steps
+        traces.append(info)
+        log(f"{steps} steps, device blocks {device_blocks or 'all'}")
+    ctx.set_option(rbl._lib.RBL_OPT_REORTH_ORDER, 0)
+    spilled, resident = traces
+    for a1, a2 in zip(spilled.trace_A + spilled.trace_B, resident.trace_A + resident.trace_B):
+        assert np.all(np.isfinite(a1)) and np.array_equal(a1, a2)
