@@ -62,6 +62,15 @@ constexpr int kG44Waves = 4;
 #ifndef RBL_G44_W16
 #define RBL_G44_W16 1
 #endif
+#ifndef RBL_G44_WPE16
+// b = 16 (panel pairs, HBM-bound at ~5 TB/s): 4 waves per SIMD (106 VGPRs) measured neutral on
+// the probe and 0.5-0.8 % slower on the C2 / C3 lines (profiles/r03_gram16_wpe4_ab.log); the
+// update spills at 4 (RBL_T44_WPE16), so both stay at 3
+#define RBL_G44_WPE16 RBL_G44_WPE
+#endif
+#ifndef RBL_T44_WPE16
+#define RBL_T44_WPE16 3
+#endif
 #ifndef RBL_G44_DUO_WPE
 #define RBL_G44_DUO_WPE 1
 #endif
@@ -309,7 +318,7 @@ __device__ __forceinline__ void gram44_body(int64_t r_begin, int64_t r_end, int6
 }
 
 template <int B, int NX, bool PAIR = false, bool GL = false, bool DUO = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DUO ? RBL_G44_DUO_WPE : RBL_G44_WPE))) void k_gram44(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DUO ? RBL_G44_DUO_WPE : B == 16 ? RBL_G44_WPE16 : RBL_G44_WPE))) void k_gram44(
     int64_t nrows, PanelRun W, Panels X, double* slab, int npg, int64_t rows_per, const int* skip) {
   if (skip && *skip) return;
   constexpr int KC = NX * B;
@@ -349,8 +358,8 @@ bool gram44_ok(int64_t nrows, int nW, int w, int xcount, int xw) {
 #endif
 int gram44_splits(int64_t nrows, int nW, int w) {
   (void)nW;
-  (void)w;
-  const int64_t slots8 = (int64_t)RBL_G44_WPE * window_grid() / 8;  // XCD mapping: multiples of 8
+  const int64_t wpe = w == 16 ? RBL_G44_WPE16 : RBL_G44_WPE;
+  const int64_t slots8 = wpe * window_grid() / 8;  // XCD mapping: multiples of 8
   int64_t s8 = nrows / (8 * (int64_t)RBL_G44_SPLIT_ROWS);
   s8 = std::min(std::max(s8, slots8), 2 * slots8);
   const int64_t max_s8 = (nrows + 8 * 128 - 1) / (8 * 128);  // each split >= 128 rows
@@ -417,7 +426,7 @@ constexpr int kT44fRows = 16 * kT44fNrt;   // rows per wave (k_tsmm44f)
 constexpr int kT44K = 32;      // k per chunk
 
 template <int B, int KYP, bool F32X = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void k_tsmm44(int64_t nrows, PanelRun X, const double* __restrict__ C,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(B == 16 ? RBL_T44_WPE16 : 3))) void k_tsmm44(int64_t nrows, PanelRun X, const double* __restrict__ C,
                                                 int ldc, int KY, Panels Y, double alpha, double beta,
                                                 const int* skip) {
   if (skip && *skip) return;

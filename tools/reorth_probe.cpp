@@ -25,7 +25,9 @@ static void fill(double* p, int64_t n, uint64_t seed) {
 
 int main(int argc, char** argv) {
   const int64_t n = argc > 1 ? atoll(argv[1]) : 10000000;
-  const int b = 32, nWmax = 36;
+  // argv: n, b (32 or 16), nWmax (default 36; C3 at b = 16: 1585478 16 72)
+  const int b = argc > 2 ? atoi(argv[2]) : 32, nWmax = argc > 3 ? atoi(argv[3]) : 36;
+  const int xw = 2 * b;  // X = [Q_i, Q_{i-1}] columns
   double *W, *X0, *X1, *slab, *C, *Cg;
   if (hipMalloc(&W, (size_t)n * b * nWmax * 8) != hipSuccess) return 1;
   (void)hipMalloc(&X0, (size_t)n * b * 8);
@@ -35,11 +37,11 @@ int main(int argc, char** argv) {
   fill(X1, n * b, 3);
   size_t slab_elems = 0;  // the split count may depend on nW: size for the largest product
   for (int nW = 2; nW <= nWmax; nW += 2)
-    slab_elems = std::max(slab_elems, (size_t)rbl::gram44_splits(n, nW) * nW * b * 64);
+    slab_elems = std::max(slab_elems, (size_t)rbl::gram44_splits(n, nW) * nW * b * xw);
   (void)hipMalloc(&slab, slab_elems * 8);
-  (void)hipMalloc(&C, (size_t)nWmax * b * 64 * 8);
-  fill(C, nWmax * b * 64, 4);
-  (void)hipMalloc(&Cg, (size_t)nWmax * b * 64 * 8);
+  (void)hipMalloc(&C, (size_t)nWmax * b * xw * 8);
+  fill(C, nWmax * b * xw, 4);
+  (void)hipMalloc(&Cg, (size_t)nWmax * b * xw * 8);
   // PROBE_XG=1: the update also forms Q_{i-1}^T Q_i (the fused local-reorth Gram)
   const bool xg = getenv("PROBE_XG") && atoi(getenv("PROBE_XG"));
   double* xslab = nullptr;
@@ -49,7 +51,7 @@ int main(int argc, char** argv) {
   (void)hipEventCreate(&e0);
   (void)hipEventCreate(&e1);
   (void)hipEventCreate(&e2);
-  double tg = 0, tt = 0, fl = 0;
+  double tg = 0, tt = 0, fl = 0, byg = 0, byt = 0;
   for (int nW = 2; nW <= nWmax; nW += 2) {
     rbl::PanelRun Wr;
     Wr.base = W;
@@ -68,9 +70,9 @@ int main(int argc, char** argv) {
     for (int rep = 0; rep < 3; ++rep) {
       (void)hipEventRecord(e0);
       rbl::gram44_partial(n, Wr, X, slab, splits, nullptr, 0);
-      rbl::reduce_slab(slab, splits, (int64_t)nW * b * 64, Cg, nullptr, 0);  // C stays fixed: X must not blow up
+      rbl::reduce_slab(slab, splits, (int64_t)nW * b * xw, Cg, nullptr, 0);  // C stays fixed: X must not blow up
       (void)hipEventRecord(e1);
-      rbl::tsmm44(n, Wr, C, 64, X, -1.0, 1.0, nullptr, 0, xg ? xslab : nullptr, &xgrid);
+      rbl::tsmm44(n, Wr, C, xw, X, -1.0, 1.0, nullptr, 0, xg ? xslab : nullptr, &xgrid);
       (void)hipEventRecord(e2);
       (void)hipEventSynchronize(e2);
       float g, t;
@@ -81,14 +83,16 @@ int main(int argc, char** argv) {
         bt = t < bt ? t : bt;
       }
     }
-    const double f = 2.0 * n * nW * b * 64;
+    const double f = 2.0 * n * nW * b * xw;
     printf("nW=%2d  splits %4d  gram %7.3f ms %5.1f TF   tsmm %7.3f ms %5.1f TF\n", nW, splits, bg, f / bg / 1e9, bt,
            f / bt / 1e9);
+    byg += 8.0 * n * (nW * b + xw);       // basis + X read once
+    byt += 8.0 * n * (nW * b + 2 * xw);   // basis read, X read and written
     tg += bg;
     tt += bt;
     fl += f;
   }
-  printf("sum over nW=2..36 step 2: gram %.1f ms (%.1f TF)  tsmm %.1f ms (%.1f TF)\n", tg,
-         fl / tg / 1e9, tt, fl / tt / 1e9);
+  printf("sum over nW=2..%d step 2: gram %.1f ms (%.1f TF, %.2f TB/s)  tsmm %.1f ms (%.1f TF, %.2f TB/s)\n", nWmax,
+         tg, fl / tg / 1e9, byg / tg / 1e9, tt, fl / tt / 1e9, byt / tt / 1e9);
   return 0;
 }
