@@ -30,7 +30,11 @@ def short(name):
 
 def main():
     d = sys.argv[1]
-    out_path = sys.argv[2] if len(sys.argv) > 2 else None
+    out_path = sys.argv[2] if len(sys.argv) > 2 and sys.argv[2] != "-" else None
+    # optional: the workload the passes ran (default C4a), e.g. "rmat 10000000 32 38" or
+    # "circuit 1585478 16 75" (matrix, n, b, block steps per run)
+    wl = sys.argv[3].split() if len(sys.argv) > 3 else ["hashwindow", "10000000", "32", "38"]
+    matrix, wn, wb, wm = wl[0], int(wl[1]), int(wl[2]), int(wl[3])
     cf = load(os.path.join(d, "calib_fetch", "c_counter_collection.csv"))
     cw = load(os.path.join(d, "calib_write", "c_counter_collection.csv"))
     cal = {}
@@ -59,7 +63,9 @@ def main():
     spmm = {k: v for k, v in kern.items() if k.startswith("k_spmm")}
     tot_l = sum(v["launches"] for v in spmm.values())
     spmm_bytes = sum(v["hbm_bytes_per_launch"] * v["launches"] for v in spmm.values()) / max(tot_l, 1)
-    reo = {k: v for k, v in kern.items() if k.startswith(("k_gram44", "k_tsmm44<32, 64>", "k_tsmm44f"))}
+    # the partial-reorth pair: the Gram and the 64- (b = 32) or 32-column (b = 16) update
+    upd = ("k_tsmm44<32, 64,", "k_tsmm44f") if wb == 32 else ("k_tsmm44<16, 32,",)
+    reo = {k: v for k, v in kern.items() if k.startswith((f"k_gram44<{wb}, 2",) + upd)}
     runs = 1  # bench.py --steps 1 --warmup 0: one 38-step run
     reorth_bytes = sum(v["hbm_bytes_per_launch"] * v["launches"] for v in reo.values()) / runs
     # the kernels measured: the bench line of the FETCH pass names the fusions and the format
@@ -68,15 +74,19 @@ def main():
         with open(os.path.join(d, "fetch.log")) as fh:
             j = json.loads([ln for ln in fh if ln.startswith('{"metric"')][0])
         extra = {"fuse": j["config"].get("fuse", 7),
-                 "matrix_format": j["roofline_secondary"].get("matrix_format")}
+                 "matrix_format": (j["roofline"].get("matrix_format")
+                                   or j["roofline_secondary"].get("matrix_format"))}
     except (OSError, IndexError, KeyError, ValueError):
         pass
+    name = {"hashwindow": "C4a (bench.py defaults)", "rmat": "C4b R-MAT (bench.py --matrix rmat)",
+            "circuit": "C3 shape (bench.py --matrix circuit --n 1585478 --b 16)"}[matrix]
     res = {
-        "config": {"n": 10_000_000, "b": 32, "workload": "C4a (bench.py defaults), 1 run = 38 steps",
-                   **extra},
+        "config": {"n": wn, "b": wb, **({"matrix": matrix} if matrix != "hashwindow" else {}),
+                   "workload": f"{name}, 1 run = {wm} steps", **extra},
         "calibration": cal,
         "correction_used": {"fetch": fetch_corr, "write": write_corr},
         "spmm_hbm_bytes_per_launch": spmm_bytes,
+        "reorth_launches": {k: v["launches"] for k, v in reo.items()},
         "part_reorth_hbm_bytes_per_run": reorth_bytes,
         "kernels": kern,
         "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes over "
