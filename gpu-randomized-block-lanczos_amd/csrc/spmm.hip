@@ -74,11 +74,27 @@ __global__ __launch_bounds__(256) void k_spmm_gather(int64_t nrows, const int64_
 // gathers back to back.  Segments write partial rows to `scratch`; k_seg_fixup sums each long
 // row's segments in order (deterministic) and applies the 3-term epilogue there.
 // ----------------------------------------------------------------------------------------
+#ifndef RBL_SEG_BLDS
+#define RBL_SEG_BLDS 1
+#endif
+#ifndef RBL_SEG_G
+#define RBL_SEG_G 8  // Q-row gathers issued back to back per lane group
+#endif
+// minimum waves per SIMD (0: the compiler's choice).  b = 32 with B_i in LDS: 79 VGPRs, 6 waves;
+// forcing 8 (62 VGPRs, no spill) measured the same (37.2 vs 37.05 ms, r03_seg_blds8_ab.log)
+#ifndef RBL_SEG_WPE
+#define RBL_SEG_WPE 0
+#endif
+// b = 16: 94 VGPRs, 5 waves; 6 or 8 spill (28 / 58 VGPRs), and B_i in LDS measured slower
+#ifndef RBL_SEG_WPE16
+#define RBL_SEG_WPE16 1
+#endif
+constexpr int kSegG = RBL_SEG_G;
 #ifndef RBL_SEG_HOT
 #define RBL_SEG_HOT 0
 #endif
 template <int BP>
-__global__ __launch_bounds__(256) void k_spmm_seg(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BP == 16 ? RBL_SEG_WPE16 : RBL_SEG_WPE ? RBL_SEG_WPE : 1))) void k_spmm_seg(
     int64_t ntasks, const int64_t* __restrict__ trow, const int32_t* __restrict__ tinfo,
     const int64_t* __restrict__ rowptr, const int32_t* __restrict__ col,
     const double* __restrict__ val, const double* __restrict__ Q, int64_t col_off,
@@ -87,6 +103,18 @@ __global__ __launch_bounds__(256) void k_spmm_seg(
   constexpr int R = kWave / BP;
   const int lane = threadIdx.x & 63;
   const int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  // BLDS (b = 32): B_i for the 3-term epilogue in LDS, bs[u * BP + c] = B_i[c][u] (a lane group
+  // reads 256 consecutive bytes: conflict-free) instead of 32 doubles per lane in registers:
+  // 126 -> 79 VGPRs, 4 -> 6 waves per SIMD, R-MAT SpMM 39.8 -> 37.5 ms, bit-identical
+  // (profiles/r03_seg_blds_ab.log).  At b = 16 the register copy is 16 doubles and the LDS
+  // reads cost more than the occupancy gains (C3 0.328 -> 0.335 ms), so it stays there.
+  constexpr bool kBlds = RBL_SEG_BLDS && BP == 32;
+  __shared__ double bs[kBlds ? BP * BP : 1];
+  if constexpr (kBlds) {
+    if (Qprev)
+      for (int e = threadIdx.x; e < BP * BP; e += 256) bs[(e % BP) * BP + e / BP] = Bi[e];
+    __syncthreads();
+  }
   if (t >= ntasks) return;
   const int h = lane / BP, c = lane % BP;
   const int64_t r0 = trow[t];
@@ -100,10 +128,10 @@ __global__ __launch_bounds__(256) void k_spmm_seg(
       const int cl = ok ? col[kk] : (int)col_off;  // padding: Q row 0 times 0
       const double vl = ok ? val[kk] : 0.0;
       const int cnt = e - k < BP ? (int)(e - k) : BP;
-      for (int j0 = 0; j0 < cnt; j0 += 8) {
-        double q[8], v[8];
+      for (int j0 = 0; j0 < cnt; j0 += kSegG) {
+        double q[kSegG], v[kSegG];
 #pragma unroll
-        for (int jj = 0; jj < 8; ++jj) {
+        for (int jj = 0; jj < kSegG; ++jj) {
           const int cj = __shfl(cl, j0 + jj, BP);
           v[jj] = __shfl(vl, j0 + jj, BP);
           const double* qp = Q + ((int64_t)(cj - col_off) * BP + c);
@@ -118,7 +146,7 @@ __global__ __launch_bounds__(256) void k_spmm_seg(
           }
         }
 #pragma unroll
-        for (int jj = 0; jj < 8; jj += 2) {
+        for (int jj = 0; jj < kSegG; jj += 2) {
           acc0 = fma(v[jj], q[jj], acc0);
           acc1 = fma(v[jj + 1], q[jj + 1], acc1);
         }
@@ -127,10 +155,10 @@ __global__ __launch_bounds__(256) void k_spmm_seg(
     return acc0 + acc1;
   };
   if (info > 0) {
-    double bt[BP];  // epilogue operand B_i[c][t]
-    if (Qprev) {
+    double bt[kBlds ? 1 : BP];  // epilogue operand B_i[c][t] (registers unless kBlds)
+    if (!kBlds && Qprev) {
 #pragma unroll
-      for (int u = 0; u < BP; ++u) bt[u] = Bi[c * BP + u];
+      for (int u = 0; u < (kBlds ? 1 : BP); ++u) bt[u] = Bi[c * BP + u];
     }
     for (int rr = h; rr < info; rr += R) {  // lane-group-uniform row loop
       const int64_t row = r0 + rr;
@@ -139,7 +167,9 @@ __global__ __launch_bounds__(256) void k_spmm_seg(
       if (Qprev) {
         const double qv = Qprev[row * BP + c];
 #pragma unroll
-        for (int u = 0; u < BP; ++u) acc = fma(-__shfl(qv, u, BP), bt[u], acc);
+        for (int u = 0; u < BP; ++u) {
+          acc = fma(-__shfl(qv, u, BP), kBlds ? bs[u * BP + c] : bt[kBlds ? 0 : u], acc);
+        }
       }
       U[row * BP + c] = acc;
     }
