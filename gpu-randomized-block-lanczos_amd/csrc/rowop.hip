@@ -39,6 +39,19 @@ namespace rbl {
 namespace {
 
 constexpr int kRowThreads = 256;  // 4 waves
+// minimum waves per SIMD asked of the compiler: the Gram / cross-Gram forms, the others.
+// Four waves for CholQR2's Gram-only pass (132 -> 126 VGPRs) and the plain row update (130 ->
+// 126) measured ~2 % slower on both (qr 71.5 -> 73.0 ms per C4a run, R-MAT loc reorth 51.5 ->
+// 52.5 ms; profiles/r03_rowop_wpe4_ab.log): these MFMA-heavy streams prefer fewer waves
+#ifndef RBL_RG_WPE_G
+#define RBL_RG_WPE_G 2
+#endif
+#ifndef RBL_RG_WPE
+#define RBL_RG_WPE 3
+#endif
+#ifndef RBL_RG_WPE_M1  // MODE 1 (CholQR2's Gram-only pass)
+#define RBL_RG_WPE_M1 RBL_RG_WPE_G
+#endif
 constexpr int kBlockRows = 16;    // rows per wave per iteration (one MFMA row tile)
 
 typedef double d4v __attribute__((ext_vector_type(4)));
@@ -82,7 +95,7 @@ __device__ __forceinline__ void mfma_row(const int k0, double a, const double* c
 // (RBL_gpu.jl:182 `Qg = FLOAT(Qg_d)`) without a separate narrowing pass.
 template <int B, bool GRAM, bool XF = false, bool YF = false, int MODE = 0, bool XG = false,
           bool TRI = false>
-__global__ __launch_bounds__(kRowThreads) __attribute__((amdgpu_waves_per_eu(GRAM || XG ? 2 : 3))) void k_rowgram(int64_t nrows, const double* X,  // X may alias Y (in-place apply)
+__global__ __launch_bounds__(kRowThreads) __attribute__((amdgpu_waves_per_eu(MODE == 1 ? RBL_RG_WPE_M1 : GRAM || XG ? RBL_RG_WPE_G : RBL_RG_WPE))) void k_rowgram(int64_t nrows, const double* X,  // X may alias Y (in-place apply)
                                                          const double* __restrict__ C, int ldc,
                                                          double* Y, double alpha, double beta,
                                                          double* __restrict__ slab, const int* skip,
