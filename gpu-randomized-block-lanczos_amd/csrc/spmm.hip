@@ -77,6 +77,9 @@ __global__ __launch_bounds__(256) void k_spmm_gather(int64_t nrows, const int64_
 #ifndef RBL_SEG_BLDS
 #define RBL_SEG_BLDS 1
 #endif
+#ifndef RBL_SEG_PF
+#define RBL_SEG_PF 0
+#endif
 #ifndef RBL_SEG_G
 #define RBL_SEG_G 8  // Q-row gathers issued back to back per lane group
 #endif
@@ -122,11 +125,34 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BP == 16 ? 
   // nonzeros [k, e) of one row, lane c: column c; chunks of BP entries, k stepping by `step`
   auto dot = [&](int64_t k, int64_t e, int64_t step) -> double {
     double acc0 = 0.0, acc1 = 0.0;
-    for (; k < e; k += step) {
+    // PF: the next chunk's col / val are loaded before this chunk's gathers issue, so their
+    // latency hides behind the gathers instead of stalling the chunk's first round.  Measured
+    // neutral at 5 and at 7 waves per SIMD (37.44 / 37.47 vs 37.43 ms, profiles/r03_seg_pf_ab.log):
+    // the other waves already cover it.  Off.
+    int cl_n = 0;
+    double vl_n = 0.0;
+    if constexpr (RBL_SEG_PF) {
       const int64_t kk = k + c;
       const bool ok = kk < e;
-      const int cl = ok ? col[kk] : (int)col_off;  // padding: Q row 0 times 0
-      const double vl = ok ? val[kk] : 0.0;
+      cl_n = ok ? col[kk] : (int)col_off;
+      vl_n = ok ? val[kk] : 0.0;
+    }
+    for (; k < e; k += step) {
+      int cl;
+      double vl;
+      if constexpr (RBL_SEG_PF) {
+        cl = cl_n;
+        vl = vl_n;
+        const int64_t kn = k + step + c;
+        const bool okn = kn < e;
+        cl_n = okn ? col[kn] : (int)col_off;
+        vl_n = okn ? val[kn] : 0.0;
+      } else {
+        const int64_t kk = k + c;
+        const bool ok = kk < e;
+        cl = ok ? col[kk] : (int)col_off;  // padding: Q row 0 times 0
+        vl = ok ? val[kk] : 0.0;
+      }
       const int cnt = e - k < BP ? (int)(e - k) : BP;
       for (int j0 = 0; j0 < cnt; j0 += kSegG) {
         double q[kSegG], v[kSegG];
