@@ -37,7 +37,7 @@ int main(int argc, char** argv) {
   fill(X1, n * b, 3);
   size_t slab_elems = 0;  // the split count may depend on nW: size for the largest product
   for (int nW = 2; nW <= nWmax; nW += 2)
-    slab_elems = std::max(slab_elems, (size_t)rbl::gram44_splits(n, nW) * nW * b * xw);
+    slab_elems = std::max(slab_elems, (size_t)rbl::gram44_splits(n, nW, b) * nW * b * xw);
   (void)hipMalloc(&slab, slab_elems * 8);
   (void)hipMalloc(&C, (size_t)nWmax * b * xw * 8);
   fill(C, nWmax * b * xw, 4);
@@ -65,7 +65,7 @@ int main(int argc, char** argv) {
     X.ptr[1] = X1;
     X.count = 2;
     X.w = b;
-    const int splits = rbl::gram44_splits(n, nW);
+    const int splits = rbl::gram44_splits(n, nW, b);
     float bg = 1e30f, bt = 1e30f;
     for (int rep = 0; rep < 3; ++rep) {
       (void)hipEventRecord(e0);
