@@ -128,7 +128,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BP == 16 ? 
     // PF: the next chunk's col / val are loaded before this chunk's gathers issue, so their
     // latency hides behind the gathers instead of stalling the chunk's first round.  Measured
     // neutral at 5 and at 7 waves per SIMD (37.44 / 37.47 vs 37.43 ms, profiles/r03_seg_pf_ab.log):
-    // the other waves already cover it.  Off.
+    // the other waves already cover it.  Off.  A row pipeline over the lane group's rows (bounds
+    // two rows ahead, first chunk one row ahead: the rowptr -> col -> Q chain of C3's ~5-nonzero
+    // rows) measured the same at b = 16 (0.328 / 0.329 ms) and slower at b = 32 (37.8 vs 37.4 ms;
+    // profiles/r03_seg_rowpipe_ab.log), so not kept.
     int cl_n = 0;
     double vl_n = 0.0;
     if constexpr (RBL_SEG_PF) {
