@@ -471,15 +471,27 @@ def main():
                     "stage_ms": {s_: round(v, 3) for s_, v in st_.items()}}
 
     # ---- BASELINE config 4 (C4b): the R-MAT pattern at the same n, b, k, same ranks ----
+    # A sub-record that raises on one rank leaves the headline line unprinted; on one rank
+    # (no collectives in flight) the error is recorded in the sub-record instead.  On several
+    # ranks it propagates, so torch.distributed.run ends the peers instead of leaving them
+    # waiting in a collective.
+    def guarded(fn, *a):
+        try:
+            return fn(*a)
+        except Exception as e:  # noqa: BLE001 — reported in the line
+            if world > 1:
+                raise
+            return {"error": f"{type(e).__name__}: {e}"}
+
     rmat_rec = None
     if args.matrix == "hashwindow" and args.rmat_steps > 0 and args.basis_bits == 64:
-        rmat_rec = rmat_subrecord(ctx, args, plant, world, barrier, allmax, allsum,
-                                  allgather_i64)
+        rmat_rec = guarded(rmat_subrecord, ctx, args, plant, world, barrier, allmax, allsum,
+                           allgather_i64)
 
     # ---- BASELINE config 3's shape: the circuit-like matrix at G3_circuit's n, b = 16 ----
     c3_rec = None
     if args.matrix == "hashwindow" and args.c3_steps > 0 and args.basis_bits == 64:
-        c3_rec = c3_subrecord(ctx, args, world, barrier, allmax, allsum, allgather_i64)
+        c3_rec = guarded(c3_subrecord, ctx, args, world, barrier, allmax, allsum, allgather_i64)
 
     # ---- CPU baseline: the oracle (port of RBL.jl) on a bounded sample, rank 0, N = 1 ----
     cpu = None
