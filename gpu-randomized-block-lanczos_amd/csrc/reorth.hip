@@ -53,6 +53,8 @@ constexpr int kG44Waves = 4;
 #ifndef RBL_G44_ROWS
 #define RBL_G44_ROWS 16
 #endif
+// 3 waves per SIMD (160 VGPRs); forcing 4 (128 VGPRs, 15 spilled) measured 9 % slower on the
+// probe (287 vs 264 ms, profiles/r03_gram_wpe4_ab.log)
 #ifndef RBL_G44_WPE
 #define RBL_G44_WPE 3
 #endif
