@@ -77,6 +77,11 @@ def parse():
                     help="timed runs of the C4b R-MAT sub-record that follows a hash-window "
                          "run (BASELINE config 4 in the same job; 0 skips it)")
     ap.add_argument("--rmat-warmup", type=int, default=1)
+    ap.add_argument("--rmat-relabel", default="auto", choices=("auto", "0", "1"),
+                    help="RBL_OPT_RELABEL for the R-MAT matrix: store P A P^T for a seeded vertex "
+                         "permutation, so the nnz-balanced row split spreads R-MAT's hubs (its low "
+                         "ids) and the halo each rank sends evenly over the ranks; auto = on for "
+                         "several ranks, off for one")
     ap.add_argument("--rmat-edges", type=int, default=0,
                     help="R-MAT draws (0: 0.66 n x 100: ~1e9 nonzeros at n = 1e7 after merging)")
     ap.add_argument("--device-blocks", type=int, default=0,
@@ -89,6 +94,11 @@ def parse():
                     help="RBL_OPT_FUSE: bit 0 the 3-pass CholQR2, bit 1 the local-reorth Gram formed "
                          "by the producing QR / partial-reorth update, bit 2 the local-reorth "
                          "update applied by the band-tile SpMM (A/B switch)")
+    ap.add_argument("--transport", default="rccl", choices=("rccl", "shm"),
+                    help="collectives between the rank processes: rccl (production, one GPU per "
+                         "rank) or shm (rbl_create_shm: host-staged through POSIX shared memory; "
+                         "ranks may share a GPU, so N ranks run on a one-GPU box — a rehearsal "
+                         "of the multi-process path, not a scaling measurement)")
     ap.add_argument("--basis-bits", type=int, default=64, choices=(64, 32),
                     help="32: the mixed mode (fp32 Krylov basis + reorth on fp32 MFMA, fp64 A*Q / "
                          "3-term / QR) of BASELINE config 5, on this workload")
@@ -159,7 +169,8 @@ def launch_ranks(args) -> None:
     import subprocess
     import socket
     have = gpu_count_sysfs()
-    if have is not None and have < args.gpus:
+    # the shm transport may put several ranks on one GPU (RCCL refuses that)
+    if have is not None and have < args.gpus and args.transport != "shm":
         sys.exit(f"bench.py: --gpus {args.gpus} needs {args.gpus} GPUs, this node has {have}")
     with socket.socket() as sk:
         sk.bind(("127.0.0.1", 0))
@@ -168,6 +179,11 @@ def launch_ranks(args) -> None:
            f"--nproc-per-node={args.gpus}", "--master-addr=127.0.0.1", f"--master-port={port}",
            os.path.abspath(__file__)] + sys.argv[1:]
     sys.exit(subprocess.run(cmd).returncode)
+
+
+def rmat_relabel(args, world: int) -> int:
+    """RBL_OPT_RELABEL for the R-MAT matrix (--rmat-relabel; auto: on for several ranks)."""
+    return int(world > 1) if args.rmat_relabel == "auto" else int(args.rmat_relabel)
 
 
 def workload_name(args) -> str:
@@ -383,7 +399,17 @@ def main():
     import rbl
     from rbl import _lib
     uid = None
-    if world > 1:
+    shm_path = None
+    device = local_rank
+    ngpu = gpu_count_sysfs() or 1
+    if world > 1 and args.transport == "shm":
+        # one segment per job, named by rank 0; ranks beyond the GPU count share GPUs
+        import uuid
+        obj = [f"/dev/shm/rbl_bench_{os.getpid()}_{uuid.uuid4().hex[:12]}" if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        shm_path = obj[0]
+        device = local_rank % ngpu
+    elif world > 1:
         buf = np.zeros(128, np.uint8)
         if rank == 0:
             st = _lib.lib.rbl_get_unique_id(_lib.u8ptr(buf))
@@ -391,7 +417,7 @@ def main():
         obj = [bytes(buf)]
         dist.broadcast_object_list(obj, src=0)
         uid = obj[0]
-    ctx = rbl.Context(local_rank, nranks=world, rank=rank, unique_id=uid)
+    ctx = rbl.Context(device, nranks=world, rank=rank, unique_id=uid, shm_path=shm_path)
 
     n, b, k = args.n, args.b, args.k
     ctx.set_option(_lib.RBL_OPT_KEEP_CSR, args.keep_csr)
@@ -400,6 +426,7 @@ def main():
     if args.matrix == "rmat":
         if not args.rmat_edges:
             args.rmat_edges = int(0.66 * 100 * n)
+        ctx.set_option(_lib.RBL_OPT_RELABEL, rmat_relabel(args, world))
         ctx.gen_rmat(n, args.rmat_scale, args.rmat_edges, args.seed, plant)
     elif args.matrix == "circuit":
         ctx.gen_circuit(n, args.seed, plant)
@@ -505,7 +532,7 @@ def main():
             "metric": metric_name(args, nnz),
             "value": round(value, 3),
             "unit": "block iterations/s",
-            "n_gpus": world,
+            "n_gpus": world if args.transport == "rccl" else min(world, ngpu),
             "steps": K,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / K * 1e3, 3),
@@ -519,10 +546,13 @@ def main():
                        **({"halfwidth": args.halfwidth, "density": args.density}
                           if args.matrix == "hashwindow" else
                           {"rmat_scale": args.rmat_scale, "rmat_edges": args.rmat_edges,
-                           "rmat_abcd": [0.57, 0.19, 0.19, 0.05]} if args.matrix == "rmat" else
+                           "rmat_abcd": [0.57, 0.19, 0.19, 0.05],
+                           "relabel": bool(rmat_relabel(args, world))} if args.matrix == "rmat" else
                           {"circuit_width": 1259, "circuit_p_edge": 0.95873}),
                        "block_steps_per_run": m_max, "parallelism": f"rows{world}",
                        "transport": comm["transport"], "transport_ranks": comm["nranks"],
+                       **({"ranks_share_gpus": True, "gpus_used": min(world, ngpu)}
+                          if args.transport == "shm" and world > ngpu else {}),
                        "nnz_per_rank": nnz_ranks,
                        **({"device_blocks": args.device_blocks} if args.device_blocks else {}),
                        **({"keep_csr": 0} if not args.keep_csr else {}),
@@ -556,9 +586,13 @@ def rmat_subrecord(ctx, args, plant, world, barrier, allmax, allsum, allgather_i
     import rbl
     ra = copy.copy(args)
     ra.matrix = "rmat"
+    from rbl import _lib
     edges = args.rmat_edges or int(0.66 * 100 * args.n)
+    relabel = rmat_relabel(args, world)
+    ctx.set_option(_lib.RBL_OPT_RELABEL, relabel)
     t0 = time.perf_counter()
     ctx.gen_rmat(args.n, args.rmat_scale, edges, args.seed, plant)
+    ctx.set_option(_lib.RBL_OPT_RELABEL, 0)
     gen_s = time.perf_counter() - t0
     _, r0, r1, nnz_loc = ctx.matrix_info()
     nloc = r1 - r0
@@ -583,6 +617,8 @@ def rmat_subrecord(ctx, args, plant, world, barrier, allmax, allsum, allgather_i
             "ms_per_step": round(meas["elapsed"] / K * 1e3, 3),
             "n": args.n, "nnz": nnz, "rmat_scale": args.rmat_scale, "rmat_edges": edges,
             "rmat_abcd": [0.57, 0.19, 0.19, 0.05], "nnz_per_rank": allgather_i64(nnz_loc),
+            "relabel": bool(relabel),
+            "send_bytes_per_step_by_rank": allgather_i64(int(meas["comm_per_step"]["send_bytes"])),
             "roofline": meas["roofline"], "roofline_secondary": meas["roofline_secondary"],
             "stage_ms_per_run": {s_: round(v / K, 3) for s_, v in meas["stage"].items()},
             "comm_per_step": meas["comm_per_step"],

@@ -11,6 +11,12 @@
 //                 partitioning, halos, distributed Grams — runs on a single-GPU box, where RCCL
 //                 refuses two ranks on one device.  Sums are formed on the host in rank order,
 //                 so every rank gets bit-identical results (RCCL's guarantee too).
+//   * ShmComm   — one PROCESS per rank, as in production, with the collectives staged through
+//                 a POSIX shared-memory segment (host memory registered with HIP) instead of
+//                 RCCL: the process-per-GPU orchestration (launcher, rendezvous, per-process
+//                 HIP contexts, the setup collectives, the side-stream exchange) runs on a
+//                 one-GPU box, where RCCL refuses two ranks on one device.  Same rank-order
+//                 sums as LocalComm.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -53,5 +59,9 @@ struct LocalGroup;
 LocalGroup* local_group_create(int nranks);
 void local_group_release(LocalGroup* g);  // drops one reference
 Comm* make_local_comm(LocalGroup* g, int rank, std::string* err);
+
+// `path`: a file name every rank passes (e.g. /dev/shm/rbl_<nonce>); rank 0 creates it, the
+// others wait for it (bounded), and rank 0 unlinks it once every rank has mapped it.
+Comm* make_shm_comm(int nranks, int rank, const char* path, std::string* err);
 
 }  // namespace rbl

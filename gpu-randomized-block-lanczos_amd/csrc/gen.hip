@@ -199,22 +199,25 @@ void remap_cols(int32_t* col, int64_t nnz, const int32_t* map, hipStream_t s) {
   hipLaunchKernelGGL(k_remap_cols, dim3(4096), dim3(256), 0, s, col, nnz, map);
 }
 
-__global__ void k_randn(double* Q, int64_t nrows, int b, int64_t r0, uint64_t seed) {
+__global__ void k_randn(double* Q, int64_t nrows, int b, int64_t r0, uint64_t seed, bool relabel,
+                        Scatter perm) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= nrows * b) return;
   const int64_t r = e / b;
   const int c = (int)(e - r * b);
-  const uint64_t h = mix64(seed ^ mix64((uint64_t)(r0 + r) * 1024u + (uint64_t)c));
+  const int64_t id = relabel ? scatter_inv(perm, r0 + r) : r0 + r;
+  const uint64_t h = mix64(seed ^ mix64((uint64_t)id * 1024u + (uint64_t)c));
   const double u1 = ((double)(h >> 11) + 0.5) * 0x1.0p-53;
   const double u2 = (double)(mix64(h) >> 11) * 0x1.0p-53;
   Q[e] = sqrt(-2.0 * log(u1)) * cospi(2.0 * u2);
 }
 
-void randn_block(double* Q, int64_t nrows, int b, int64_t r0, uint64_t seed, hipStream_t s) {
+void randn_block(double* Q, int64_t nrows, int b, int64_t r0, uint64_t seed, hipStream_t s,
+                 const Scatter* perm) {
   const int64_t m = nrows * b;
   if (m <= 0) return;
   hipLaunchKernelGGL(k_randn, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, Q, nrows, b, r0,
-                     seed);
+                     seed, perm != nullptr, perm ? *perm : Scatter());
 }
 
 __global__ void k_tile_cols(int64_t nrows, const int64_t* __restrict__ rowptr,

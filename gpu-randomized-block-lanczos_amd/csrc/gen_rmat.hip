@@ -36,14 +36,19 @@ __device__ inline void rmat_draw(const RmatParams& p, int64_t e, int64_t* r, int
   *c = cc;
 }
 
+// vertex id -> stored row / column id (RBL_OPT_RELABEL: P A P^T)
+__device__ inline int64_t rmat_id(const RmatParams& p, int64_t v) {
+  return p.relabel ? scatter(p.perm, v) : v;
+}
+
 __global__ void k_rmat_degree(RmatParams p, int32_t* __restrict__ deg) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < p.edges; e += stride) {
     int64_t r, c;
     rmat_draw(p, e, &r, &c);
     if (r < p.n && c < p.n && r != c) {
-      atomicAdd(deg + r, 1);
-      atomicAdd(deg + c, 1);
+      atomicAdd(deg + rmat_id(p, r), 1);
+      atomicAdd(deg + rmat_id(p, c), 1);
     }
   }
 }
@@ -56,6 +61,8 @@ __global__ void k_rmat_keys(RmatParams p, int64_t r0, int64_t r1, uint64_t* __re
     int64_t r, c;
     rmat_draw(p, e, &r, &c);
     if (r >= p.n || c >= p.n || r == c) continue;
+    r = rmat_id(p, r);
+    c = rmat_id(p, c);
     if (r >= r0 && r < r1) keys[atomicAdd(count, 1ull)] = ((uint64_t)(r - r0) << 32) | (uint64_t)c;
     if (c >= r0 && c < r1) keys[atomicAdd(count, 1ull)] = ((uint64_t)(c - r0) << 32) | (uint64_t)r;
   }
@@ -71,7 +78,7 @@ __global__ void k_rmat_diag(int64_t r0, int64_t r1, uint64_t* __restrict__ keys)
 __global__ void k_rmat_csr(const uint64_t* __restrict__ keys, int64_t nnz, int64_t r0, int64_t m,
                            uint64_t seed, int nplant, const double* __restrict__ plant, int64_t n,
                            int64_t* __restrict__ rowptr, int32_t* __restrict__ col,
-                           double* __restrict__ val) {
+                           double* __restrict__ val, bool relabel, Scatter perm) {
   const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= nnz) {
     if (k == nnz) rowptr[m] = nnz;
@@ -81,16 +88,18 @@ __global__ void k_rmat_csr(const uint64_t* __restrict__ keys, int64_t nnz, int64
   const int64_t i = (int64_t)(key >> 32);
   const int64_t c = (int64_t)(key & 0xffffffffull);
   if (k == 0 || (int64_t)(keys[k - 1] >> 32) != i) rowptr[i] = k;
-  const int64_t r = r0 + i;
+  col[k] = (int32_t)c;
+  // values (and the plant) of the original vertex ids
+  const int64_t r = relabel ? scatter_inv(perm, r0 + i) : r0 + i;
+  const int64_t co = relabel ? scatter_inv(perm, c) : c;
   double v;
-  if (c == r) {
+  if (co == r) {
     v = hw_value(seed, r, r);
     const int64_t st = nplant > 0 ? n / nplant : 0;
     if (st > 0 && r % st == 0 && r / st < nplant) v += plant[r / st];
   } else {
-    v = hw_value(seed, c < r ? c : r, c < r ? r : c);
+    v = hw_value(seed, co < r ? co : r, co < r ? r : co);
   }
-  col[k] = (int32_t)c;
   val[k] = v;
 }
 
@@ -181,7 +190,8 @@ int rmat_local_csr(const RmatParams& p, int64_t r0, int64_t r1, int64_t max_keys
       ok(hipMemsetAsync(*col_dev + nnz, 0, kCsrPad * sizeof(int32_t), s));
       ok(hipMemsetAsync(*val_dev + nnz, 0, kCsrPad * sizeof(double), s));
       hipLaunchKernelGGL(k_rmat_csr, dim3((unsigned)((nnz + 1 + 255) / 256)), dim3(256), 0, s, k0, nnz,
-                         r0, m, p.seed, nplant, plant_dev, p.n, rowptr_dev, *col_dev, *val_dev);
+                         r0, m, p.seed, nplant, plant_dev, p.n, rowptr_dev, *col_dev, *val_dev,
+                         p.relabel, p.perm);
       ok(hipGetLastError());
       ok(hipStreamSynchronize(s));
       *nnz_out = nnz;

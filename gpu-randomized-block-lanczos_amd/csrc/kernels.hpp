@@ -310,7 +310,13 @@ struct RmatParams {
   int64_t edges = 0;
   double a = 0.57, b = 0.19, c = 0.19;
   uint64_t seed = 0;
+  // RBL_OPT_RELABEL: the matrix is P A P^T, vertex v stored as row / column perm(v) (a seeded
+  // Feistel bijection, make_scatter(n, seed ^ kRelabelK)); values and the planted diagonal
+  // stay those of the original ids, so the spectrum is A's
+  bool relabel = false;
+  Scatter perm;
 };
+constexpr uint64_t kRelabelK = 0x52454C4142454C31ull;  // "RELABEL1"
 // deg[r] += 1 per kept draw endpoint (duplicates counted; zero-filled deg of n int32)
 void rmat_degree(const RmatParams& p, int32_t* deg, hipStream_t s);
 // local CSR of rows [r0, r1): rowptr_dev (m+1, caller-allocated), col/val allocated here (with
@@ -345,7 +351,11 @@ void hw_fill(int64_t n, int64_t W, double p, uint64_t seed, int64_t r0, int64_t 
              const int64_t* rowptr, int nplant, const double* plant_dev, int32_t* col,
              double* val, hipStream_t s);
 // N(0,1) block, row-major n_local x b, global row offset r0, counter-based from seed.
-void randn_block(double* Q, int64_t nrows, int b, int64_t r0, uint64_t seed, hipStream_t s);
+// N(0,1) start block of global rows r0.. (row r drawn from its id; with `perm` (the relabel of
+// the matrix, RBL_OPT_RELABEL) from its original id perm^-1(r), so a relabelled run starts
+// from the same block as the plain one, its rows permuted)
+void randn_block(double* Q, int64_t nrows, int b, int64_t r0, uint64_t seed, hipStream_t s,
+                 const Scatter* perm = nullptr);
 // Per-tile column range of the CSR (tile = `tile_rows` rows), for the LDS-window SpMM.
 void tile_col_range(const CsrDev& A, int tile_rows, int64_t* cmin, int64_t* cmax, hipStream_t s);
 // column-major (ld = nrows) <-> row-major (ld = w) transposes for the boundary

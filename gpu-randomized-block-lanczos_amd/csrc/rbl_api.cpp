@@ -81,6 +81,7 @@ struct rbl_ctx {
   int32_t* d_send_idx = nullptr;
   double* d_sendbuf = nullptr;        // n_send x b, per run
   const double* ghost_local = nullptr;  // the block the last exchange sent from
+  bool ghost_active = false;          // the last exchange was the indexed one (use_ghost)
   bool halo_overlap = true;           // RBL_OPT_HALO_OVERLAP
   hipStream_t hstream = nullptr;      // the overlapped halo exchange
   hipEvent_t ev_qready = nullptr, ev_halo = nullptr;
@@ -103,6 +104,9 @@ struct rbl_ctx {
   int64_t ext_lo = 0, ext_hi = 0;         // global rows held in d_qext
   bool split_halo = true;                 // RBL_OPT_SPLIT_HALO
   bool keep_csr = true;                   // RBL_OPT_KEEP_CSR
+  int relabel_opt = 0;                    // RBL_OPT_RELABEL (applies to the next generator call)
+  bool relabeled = false;                 // the matrix held is P A P^T (rmat generator)
+  Scatter relabel_perm;                   //   with this P: vertex v at row perm(v)
   bool csr_dropped = false;               // values / column ids released (band tiles only)
 
   // Krylov run
@@ -136,6 +140,7 @@ struct rbl_ctx {
   double* d_T = nullptr;      // scratch n_local x max(b,k)
   int64_t T_cols = 0;
   double* d_qext = nullptr;   // halo-extended Q_i (multi-rank)
+  size_t qext_cap = 0;        // its capacity in doubles (grown by ensure_qext)
   double* d_slab = nullptr;
   size_t slab_elems = 0;
   double* d_C = nullptr;      // Gram result (<= (max_blocks)*b x 2b)
@@ -503,11 +508,13 @@ int build_ghosts(rbl_ctx* ctx, int32_t** d_map) {
 // flight (step_impl); the sum order per row is the same with or without the overlap.
 int prepare_tiers(rbl_ctx* ctx, const std::vector<int64_t>& rp) {
   free_tiers(ctx);
-  if (ctx->seg_ntasks == 0 || ctx->nnz == 0) return RBL_OK;
   if (ctx->nranks > 1) {
-    // every rank must take the same branch (the setup below runs collectives)
+    // every rank must take the same branch (the setup below runs collectives), so the vote
+    // comes before any per-rank condition: a rank with no rows or no nonzeros still takes
+    // part in build_ghosts (with no requests), and a rank that released its CSR for band tiles
+    // (RBL_OPT_KEEP_CSR = 0) votes banded, which stops every rank here
     const int64_t banded = (ctx->bt_ng || ctx->band_ok16 || ctx->band_ok32 || ctx->window_ok16 ||
-                            ctx->window_ok32 || ctx->dense) ? 1 : 0;
+                            ctx->window_ok32 || ctx->dense || ctx->csr_dropped) ? 1 : 0;
     std::vector<int64_t> all(ctx->nranks);
     COMMC(ctx->comm->allgather_host(&banded, all.data(), 1, ctx->stream, &ctx->err));
     for (int64_t v : all)
@@ -529,6 +536,7 @@ int prepare_tiers(rbl_ctx* ctx, const std::vector<int64_t>& rp) {
     ctx->ghost = true;
     return RBL_OK;
   }
+  if (ctx->seg_ntasks == 0 || ctx->nnz == 0 || ctx->csr_dropped) return RBL_OK;
   const char* e = std::getenv("RBL_SEG_TIERS");
   if (!e || ctx->nloc != ctx->n) return RBL_OK;
   std::vector<int64_t> sz;
@@ -614,7 +622,7 @@ int prepare_window_formats(rbl_ctx* ctx, const std::vector<int64_t>& rp);
 // band-tile formats, then (unbanded only) the column tiers.
 int prepare_window(rbl_ctx* ctx, const std::vector<int64_t>& rp) {
   CHK(prepare_window_formats(ctx, rp));
-  if (!ctx->csr_dropped) CHK(prepare_tiers(ctx, rp));
+  CHK(prepare_tiers(ctx, rp));  // (collective on several ranks: every rank calls it)
   return RBL_OK;
 }
 
@@ -996,6 +1004,32 @@ int ensure_qm64(rbl_ctx* ctx) {
   return RBL_OK;
 }
 
+// The indexed halo serves only the segmented gather's own / halo column tiers (b in {16, 32});
+// any other SpMM (another b, a kernel pinned by RBL_OPT_SPMM_KERNEL) reads the range halo,
+// which is kept beside it.  The rule depends only on state every rank shares (the collective
+// `ghost` decision, b, the option), so all ranks pick the same exchange for a call.
+bool use_ghost(const rbl_ctx* ctx, int b) {
+  return ctx->ghost && ctx->nranks > 1 && (b == 16 || b == 32) &&
+         (ctx->spmm_variant == 0 || ctx->spmm_variant == 5);
+}
+// rows of the halo buffer for block size b: the ghost slots, or the range [ext_lo, ext_hi)
+int64_t qext_rows(const rbl_ctx* ctx, int b) {
+  return std::max<int64_t>(use_ghost(ctx, b) ? ctx->n_ghost : ctx->ext_hi - ctx->ext_lo, 1);
+}
+// grow the halo buffer (zeroed: rows between the received ranges stay finite) for block size b
+int ensure_qext(rbl_ctx* ctx, int b, hipStream_t st) {
+  const size_t need = (size_t)qext_rows(ctx, b) * b;
+  if (ctx->d_qext && ctx->qext_cap >= need) return RBL_OK;
+  HIPC(hipStreamSynchronize(ctx->stream));
+  hipFree(ctx->d_qext);
+  ctx->d_qext = nullptr;
+  ctx->qext_cap = 0;
+  HIPC(hipMalloc(&ctx->d_qext, need * sizeof(double)));
+  HIPC(hipMemsetAsync(ctx->d_qext, 0, need * sizeof(double), st));
+  ctx->qext_cap = need;
+  return RBL_OK;
+}
+
 // U = A Qin (+ U -= Qprev Bi^T when Qprev): the SpMM of RBL_gpu.jl:176-177, or for a dense
 // A (RBL_gpu.jl:205 with A::Matrix) the panel GEMM on fp64 MFMA (tsmm44 over the panels of
 // the local rows, Q gathered to all n rows by the halo exchange).  Returns the number of
@@ -1010,8 +1044,10 @@ int apply_A(rbl_ctx* ctx, const double* Qin, int64_t off, int b, double* U, cons
                                     "SpMM (b in {16, 32}) can run");
   if (!ctx->dense) {
     CsrDev A = csr(ctx);
-    // indexed halo: the own-column tier always reads the block the exchange sent from
-    if (!qloc && ctx->ghost && ctx->nranks > 1) qloc = ctx->ghost_local;
+    // indexed halo: the own-column tier always reads the block the exchange sent from (a rank
+    // without nonzeros runs the plain gather, which reads no Q row at all)
+    if (!qloc && ctx->ghost_active && ctx->nranks > 1 && rbl_spmm_kernel_for(ctx, b) == 6)
+      qloc = ctx->ghost_local;
     if (qloc) {  // own rows from the block itself (halo_exchange without the local copy)
       A.qloc = qloc;
       A.loc_lo = ctx->r0;
@@ -1391,8 +1427,10 @@ int halo_exchange(rbl_ctx* ctx, const double* Q, const double** Qin, int64_t* of
   if (!st) st = ctx->stream;
   StageScope t(ctx, RBL_STAGE_COMM, st);
   const int b = ctx->b;
+  CHK(ensure_qext(ctx, b, st));
   double* ext = ctx->d_qext;
-  if (ctx->ghost) {  // indexed halo: pack the asked-for rows, receive into the ghost slots
+  ctx->ghost_active = use_ghost(ctx, b);
+  if (ctx->ghost_active) {  // indexed halo: pack the asked-for rows, receive into the ghost slots
     gather_rows(Q, ctx->d_send_idx, ctx->n_send, b, ctx->d_sendbuf, st);
     HIPC(hipGetLastError());
     std::vector<Comm::Xfer> x(ctx->nranks);
@@ -1486,7 +1524,7 @@ void free_run(rbl_ctx* ctx) {
   ctx->basis_bits = 64;
   hipFree(ctx->d_U); ctx->d_U = nullptr;
   hipFree(ctx->d_T); ctx->d_T = nullptr;
-  hipFree(ctx->d_qext); ctx->d_qext = nullptr;
+  hipFree(ctx->d_qext); ctx->d_qext = nullptr; ctx->qext_cap = 0;
   hipFree(ctx->d_sendbuf); ctx->d_sendbuf = nullptr;
   hipFree(ctx->d_slab); ctx->d_slab = nullptr;
   hipFree(ctx->d_C); ctx->d_C = nullptr;
@@ -1537,6 +1575,7 @@ void free_matrix(rbl_ctx* ctx) {
   ctx->window_ok16 = ctx->window_ok32 = false;
   ctx->band_ok16 = ctx->band_ok32 = false;
   ctx->csr_dropped = false;
+  ctx->relabeled = false;
 }
 
 // Exchange halo needs among ranks and size the extended buffer.
@@ -1764,6 +1803,20 @@ int rbl_create_local(rbl_ctx** out, int device, rbl_group* group, int rank) {
   return RBL_OK;
 }
 
+int rbl_create_shm(rbl_ctx** out, int device, int nranks, int rank, const char* path) {
+  if (!out || nranks < 1 || rank < 0 || rank >= nranks || !path) return RBL_ERR_INVALID;
+  int s = rbl_create(out, device);
+  if (s != RBL_OK) return s;
+  rbl_ctx* ctx = *out;
+  ctx->nranks = nranks;
+  ctx->rank = rank;
+  if (nranks > 1) {
+    ctx->comm = make_shm_comm(nranks, rank, path, &ctx->err);
+    if (!ctx->comm) return RBL_ERR_RCCL;
+  }
+  return RBL_OK;
+}
+
 int rbl_free(rbl_ctx* ctx) {
   if (!ctx) return RBL_OK;
   hipSetDevice(ctx->device);
@@ -1829,6 +1882,10 @@ int rbl_set_option(rbl_ctx* ctx, int option, int64_t value) {
     case RBL_OPT_SPLIT_HALO: ctx->split_halo = value != 0; return RBL_OK;
     case RBL_OPT_HALO_OVERLAP: ctx->halo_overlap = value != 0; return RBL_OK;
     case RBL_OPT_KEEP_CSR: ctx->keep_csr = value != 0; return RBL_OK;
+    case RBL_OPT_RELABEL:
+      if (value < 0 || value > 1) return fail(ctx, RBL_ERR_INVALID, "RBL_OPT_RELABEL must be 0|1");
+      ctx->relabel_opt = (int)value;
+      return RBL_OK;
     case RBL_OPT_FUSE:
       if (value < 0 || value > 7) return fail(ctx, RBL_ERR_INVALID, "RBL_OPT_FUSE is a 3-bit mask");
       ctx->fuse = (int)value;
@@ -2062,6 +2119,8 @@ int rbl_gen_matrix_rmat(rbl_ctx* ctx, int64_t n, int scale, int64_t edges, doubl
   p.b = b;
   p.c = c;
   p.seed = seed;
+  p.relabel = ctx->relabel_opt != 0;
+  if (p.relabel) p.perm = make_scatter(n, seed ^ kRelabelK);
   // degrees of every row (all ranks draw every edge): they size the key buffer and balance
   // the row split by nonzeros (R-MAT's low ids are its hubs)
   int32_t* d_deg = nullptr;
@@ -2100,6 +2159,8 @@ int rbl_gen_matrix_rmat(rbl_ctx* ctx, int64_t n, int scale, int64_t edges, doubl
   const int st = rmat_local_csr(p, r0, r1, own, nplant, d_plant, ctx->d_rowptr, &ctx->d_col,
                                 &ctx->d_val, &nnz, ctx->stream);
   hipFree(d_plant);
+  ctx->relabeled = p.relabel;
+  ctx->relabel_perm = p.perm;
   if (st == -1) return fail(ctx, RBL_ERR_INVALID, "rbl_gen_matrix_rmat: > 2^31 keys on one rank");
   if (st < 0) return fail(ctx, st == -3 ? RBL_ERR_OOM : RBL_ERR_HIP, "rbl_gen_matrix_rmat: device generation failed");
   ctx->nnz = nnz;
@@ -2117,6 +2178,14 @@ int rbl_matrix_info(rbl_ctx* ctx, int64_t* n, int64_t* row_begin, int64_t* row_e
   if (row_begin) *row_begin = ctx->r0;
   if (row_end) *row_end = ctx->r1;
   if (nnz_local) *nnz_local = ctx->nnz;
+  return RBL_OK;
+}
+
+int rbl_row_ids(rbl_ctx* ctx, int64_t* ids) {
+  if (!ctx || !ids) return RBL_ERR_INVALID;
+  if (!has_matrix(ctx)) return fail(ctx, RBL_ERR_STATE, "rbl_row_ids: no matrix");
+  for (int64_t i = 0; i < ctx->nloc; ++i)
+    ids[i] = ctx->relabeled ? scatter_inv(ctx->relabel_perm, ctx->r0 + i) : ctx->r0 + i;
   return RBL_OK;
 }
 
@@ -2175,19 +2244,23 @@ int rbl_apply(rbl_ctx* ctx, int b, const double* X, double* Y) {
   int64_t off = 0;
   DevBuf sendbuf;
   if (ctx->nranks > 1) {  // halo exchange through a private extended buffer
-    const int64_t ext_rows = std::max<int64_t>(ctx->ghost ? ctx->n_ghost : ctx->ext_hi - ctx->ext_lo, 1);
+    const int64_t ext_rows = qext_rows(ctx, b);
     HIPC(hipMalloc(&ext.p, ext_rows * b * sizeof(double)));
     // rows between the received ranges stay finite (band-tile kernel multiplies them by 0)
     HIPC(hipMemsetAsync(ext.p, 0, ext_rows * b * sizeof(double), ctx->stream));
-    if (ctx->ghost) HIPC(hipMalloc(&sendbuf.p, std::max<int64_t>(ctx->n_send, 1) * b * sizeof(double)));
+    if (use_ghost(ctx, b))
+      HIPC(hipMalloc(&sendbuf.p, std::max<int64_t>(ctx->n_send, 1) * b * sizeof(double)));
     double* keep_ext = ctx->d_qext;
+    const size_t keep_cap = ctx->qext_cap;
     double* keep_send = ctx->d_sendbuf;
     const int keep_b = ctx->b;
     ctx->d_qext = ext.d();
+    ctx->qext_cap = (size_t)ext_rows * b;
     ctx->d_sendbuf = sendbuf.d();
     ctx->b = b;
     const int st = halo_exchange(ctx, xr.d(), &Qin, &off);
     ctx->d_qext = keep_ext;
+    ctx->qext_cap = keep_cap;
     ctx->d_sendbuf = keep_send;
     ctx->b = keep_b;
     if (st < 0) return st;
@@ -2308,9 +2381,7 @@ int rbl_start(rbl_ctx* ctx, int b, int max_blocks, int basis_bits, const double*
   ctx->T_cols = b;
   HIPC(hipMalloc(&ctx->d_T, nl * b * sizeof(double)));
   if (ctx->nranks > 1) {
-    const int64_t ext_rows = std::max<int64_t>(ctx->ghost ? ctx->n_ghost : ctx->ext_hi - ctx->ext_lo, 1);
-    HIPC(hipMalloc(&ctx->d_qext, ext_rows * b * sizeof(double)));
-    HIPC(hipMemsetAsync(ctx->d_qext, 0, ext_rows * b * sizeof(double), ctx->stream));
+    CHK(ensure_qext(ctx, b, ctx->stream));
     if (ctx->ghost)
       HIPC(hipMalloc(&ctx->d_sendbuf, std::max<int64_t>(ctx->n_send, 1) * b * sizeof(double)));
   }
@@ -2334,7 +2405,8 @@ int rbl_start(rbl_ctx* ctx, int b, int max_blocks, int basis_bits, const double*
                         ctx->stream));
     colmajor_to_rowmajor(d_tmp, ctx->nloc, b, ctx->d_T, ctx->stream);
   } else {
-    randn_block(ctx->d_T, ctx->nloc, b, ctx->r0, seed, ctx->stream);
+    randn_block(ctx->d_T, ctx->nloc, b, ctx->r0, seed, ctx->stream,
+                ctx->relabeled ? &ctx->relabel_perm : nullptr);
   }
   // Q_1 = qr(A * Omega).Q   (RBL_gpu.jl:213-214)
   const double* Qin = nullptr;

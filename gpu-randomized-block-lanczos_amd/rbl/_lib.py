@@ -32,6 +32,7 @@ RBL_OPT_SPLIT_HALO = 4
 RBL_OPT_KEEP_CSR = 5
 RBL_OPT_FUSE = 6
 RBL_OPT_HALO_OVERLAP = 7
+RBL_OPT_RELABEL = 8
 
 _p = C.c_void_p
 _i64 = C.c_int64
@@ -50,6 +51,7 @@ SIGNATURES = {
     "rbl_local_group_create": (C.c_int, [C.POINTER(_p), C.c_int]),
     "rbl_local_group_free": (C.c_int, [_p]),
     "rbl_create_local": (C.c_int, [C.POINTER(_p), C.c_int, _p, C.c_int]),
+    "rbl_create_shm": (C.c_int, [C.POINTER(_p), C.c_int, C.c_int, C.c_int, C.c_char_p]),
     "rbl_free": (C.c_int, [_p]),
     "rbl_last_error": (C.c_char_p, [_p]),
     "rbl_comm_info": (C.c_int, [_p, C.POINTER(C.c_int), C.POINTER(C.c_int), C.c_char_p, C.c_int]),
@@ -63,6 +65,7 @@ SIGNATURES = {
                                       _u64, C.c_int, _pd]),
     "rbl_matrix_info": (C.c_int, [_p, _pi64, _pi64, _pi64, _pi64]),
     "rbl_get_matrix_csr": (C.c_int, [_p, _pi64, _pi32, _pd]),
+    "rbl_row_ids": (C.c_int, [_p, _pi64]),
     "rbl_apply": (C.c_int, [_p, C.c_int, _pd, _pd]),
     "rbl_spmm_kernel_for": (C.c_int, [_p, C.c_int]),
     "rbl_matrix_format": (C.c_int, [_p]),

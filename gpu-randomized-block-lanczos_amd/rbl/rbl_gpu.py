@@ -61,15 +61,20 @@ class Context:
     """One librbl_hip context: one GPU, or one rank of a row-partitioned job."""
 
     def __init__(self, device: int = 0, nranks: int = 1, rank: int = 0,
-                 unique_id: bytes | None = None, group: "LocalGroup | None" = None):
+                 unique_id: bytes | None = None, group: "LocalGroup | None" = None,
+                 shm_path: str | None = None):
         """nranks == 1: a single-GPU context.  nranks > 1 with `unique_id`: one rank of an RCCL
         job (one process per GPU).  `group`: one rank of an in-process LocalGroup (each rank
-        driven by its own thread; ranks may share a GPU)."""
+        driven by its own thread; ranks may share a GPU).  `shm_path`: one rank of a
+        process-per-rank job over the shared-memory transport (rbl_create_shm; ranks may share
+        a GPU; every rank passes the same path, unique per job)."""
         import ctypes as C
         self._h = C.c_void_p()
         if group is not None:
             nranks = group.nranks
             st = lib.rbl_create_local(C.byref(self._h), device, group._h, rank)
+        elif shm_path is not None:
+            st = lib.rbl_create_shm(C.byref(self._h), device, nranks, rank, shm_path.encode())
         elif nranks == 1:
             st = lib.rbl_create(C.byref(self._h), device)
         else:
@@ -174,6 +179,14 @@ class Context:
         self._check(lib.rbl_matrix_info(self._h, *[i64ptr(x) for x in v]), "rbl_matrix_info")
         n, r0, r1, nnz = (int(x[0]) for x in v)
         return n, r0, r1, nnz
+
+    def row_ids(self) -> np.ndarray:
+        """Original (generator) id of each local row (rbl_row_ids): r0..r1-1, or the inverse
+        relabel of a matrix generated with RBL_OPT_RELABEL — the order of omega's and V's rows."""
+        n, r0, r1, _ = self.matrix_info()
+        ids = np.zeros(max(r1 - r0, 1), np.int64)
+        self._check(lib.rbl_row_ids(self._h, i64ptr(ids)), "rbl_row_ids")
+        return ids[: r1 - r0]
 
     def get_matrix_csr(self):
         n, r0, r1, nnz = self.matrix_info()

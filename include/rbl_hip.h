@@ -26,7 +26,10 @@
 extern "C" {
 #endif
 
-#define RBL_ABI_VERSION 1
+/* 2: RBL_OPT_SPMM_KERNEL takes the kernel ids of rbl_spmm_kernel_for (5 band tiles, 6 segmented
+ *    gather; version 1 took 4 / 5 for them) and rbl_create_shm was added.  A caller built
+ *    against version 1 should check rbl_abi_version() before passing kernel ids. */
+#define RBL_ABI_VERSION 2
 /* Largest Krylov block size b (RBL_gpu(A, k, b) takes any b, RBL_gpu.jl:205; the reference's
  * scripts use b <= 8, the north star b = 32).  The MFMA fast paths cover b in {16, 32}. */
 #define RBL_MAX_BLOCK 512
@@ -105,6 +108,16 @@ extern "C" {
                                    * each row, the halo-column part after it lands; 0 the same
                                    * two parts after the exchange (same results, bit for bit) */
 
+#define RBL_OPT_RELABEL       8   /* 1: the next rbl_gen_matrix_rmat stores P A P^T for a seeded
+                                   * permutation P (a Feistel bijection of the vertex ids): R-MAT's
+                                   * hubs (its low ids) spread over the row range, so an
+                                   * nnz-balanced row split gives every rank a like share of hub
+                                   * and tail rows and of the halo it sends.  Eigenvalues are A's;
+                                   * the device start block (omega NULL) draws row perm(v) from
+                                   * v's id, so the run is the plain run permuted; rbl_row_ids gives
+                                   * each local row's original id (a caller's omega and V rows are
+                                   * in that order).  0 (default): A as drawn.                  */
+
 typedef struct rbl_ctx rbl_ctx;
 
 int rbl_abi_version(void);
@@ -130,6 +143,15 @@ typedef struct rbl_group rbl_group;
 int rbl_local_group_create(rbl_group** group, int nranks);
 int rbl_local_group_free(rbl_group* group);
 int rbl_create_local(rbl_ctx** ctx, int device, rbl_group* group, int rank);
+/* One rank of a process-per-rank job whose collectives go through a POSIX shared-memory
+ * segment (host-staged, pinned) instead of RCCL: the production orchestration — one process
+ * and one HIP context per rank, rendezvous, setup collectives, the side-stream halo exchange —
+ * with ranks that may share one GPU (RCCL refuses that).  Every rank passes the same `path`
+ * (e.g. "/dev/shm/rbl_<nonce>", unique per job); rank 0 creates it, the others wait for it,
+ * and it is unlinked once all ranks have mapped it.  A rank that exits or stalls past
+ * RBL_SHM_TIMEOUT_S seconds (default 120) makes its peers' calls fail with RBL_ERR_RCCL.
+ * Transport name "shm" (rbl_comm_info). */
+int rbl_create_shm(rbl_ctx** ctx, int device, int nranks, int rank, const char* path);
 int rbl_free(rbl_ctx* ctx);
 const char* rbl_last_error(const rbl_ctx* ctx);
 /* Ranks as the transport itself counts them (RCCL: ncclCommCount; in-process group: its size;
@@ -181,6 +203,9 @@ int rbl_gen_matrix_circuit(rbl_ctx* ctx, int64_t n, int64_t width, double p_edge
                            int nplant, const double* plant);
 int rbl_matrix_info(rbl_ctx* ctx, int64_t* n, int64_t* row_begin, int64_t* row_end,
                     int64_t* nnz_local);
+/* Original (generator) id of each local row: r0 + i, or perm^-1(r0 + i) for a matrix generated
+ * with RBL_OPT_RELABEL.  ids: n_local int64. */
+int rbl_row_ids(rbl_ctx* ctx, int64_t* ids);
 /* Download the local CSR (0-based) — test/inspection only. */
 int rbl_get_matrix_csr(rbl_ctx* ctx, int64_t* rowptr, int32_t* colind, double* val);
 /* Y = A X for a host n_local x b column-major block (the operator of RBL_gpu.jl:176,

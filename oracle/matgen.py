@@ -86,19 +86,37 @@ def rmat_draws(n: int, scale: int, edges: int, seed: int, a=0.57, b=0.19, c=0.19
     return r[keep], cc[keep]
 
 
+_RELABEL_K = 0x52454C4142454C31  # kernels.hpp kRelabelK ("RELABEL1")
+
+
+def rmat_relabel(n: int, seed: int, idx, inverse=False):
+    """RBL_OPT_RELABEL's permutation of the R-MAT vertex ids (gen_rmat.hip rmat_id): the Feistel
+    bijection of scatter_perm under the key seed ^ kRelabelK."""
+    return scatter_perm(n, int(np.uint64(seed) ^ np.uint64(_RELABEL_K)), idx, inverse)
+
+
 def rmat_csr(n: int, scale: int, edges: int, seed: int, plant=None, row_begin=0, row_end=None,
-             a=0.57, b=0.19, c=0.19):
+             a=0.57, b=0.19, c=0.19, relabel=False):
     """Rows [row_begin, row_end) of the symmetric R-MAT matrix as SciPy CSR,
     restating gen_rmat.hip: both orientations of every kept draw (duplicates merged), the
     hash-window pair values off the diagonal, every diagonal entry with its hash value plus
-    the planted spectrum."""
+    the planted spectrum.  relabel: P A P^T with vertex v at row / column rmat_relabel(v) (the
+    values those of the original ids), as gen_rmat.hip with RBL_OPT_RELABEL = 1."""
     row_end = n if row_end is None else row_end
     r, cc = rmat_draws(n, scale, edges, seed, a, b, c)
     R = np.concatenate([r, cc, np.arange(n, dtype=np.int64)])
     C = np.concatenate([cc, r, np.arange(n, dtype=np.int64)])
-    sel = (R >= row_begin) & (R < row_end)
-    key = np.unique(R[sel] * np.int64(n) + C[sel])
-    R, C = key // n, key % n
+    if relabel:
+        Rn = rmat_relabel(n, seed, R)
+        sel = (Rn >= row_begin) & (Rn < row_end)
+        key = np.unique(Rn[sel] * np.int64(n) + rmat_relabel(n, seed, C[sel]))
+        Rn, Cn = key // n, key % n
+        R, C = rmat_relabel(n, seed, Rn, inverse=True), rmat_relabel(n, seed, Cn, inverse=True)
+    else:
+        sel = (R >= row_begin) & (R < row_end)
+        key = np.unique(R[sel] * np.int64(n) + C[sel])
+        R, C = key // n, key % n
+        Rn, Cn = R, C
     lo, hi = np.minimum(R, C), np.maximum(R, C)
     u = u53(mix64(pair_hash(seed, lo, hi) ^ _K))
     val = (u + u) - 1.0
@@ -109,7 +127,7 @@ def rmat_csr(n: int, scale: int, edges: int, seed: int, plant=None, row_begin=0,
         sel2 = d & (R % stride == 0) & (R // stride < len(plant))
         val[sel2] += plant[R[sel2] // stride]
     m = row_end - row_begin
-    A = sp.csr_matrix((val, (R - row_begin, C)), shape=(m, n))
+    A = sp.csr_matrix((val, (Rn - row_begin, Cn)), shape=(m, n))
     A.sort_indices()
     return A
 

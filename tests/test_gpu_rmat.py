@@ -220,3 +220,175 @@ def test_rmat_indexed_halo_small_and_ragged(rbl):
     Y = np.vstack([y for _, y in parts])
     bound = (abs(A) @ np.abs(X)) * 1e-13 + 1e-300
     assert np.all(np.abs(Y - A @ X) <= bound)
+
+
+def test_rmat_relabel_generator_bit_exact(rbl):
+    """RBL_OPT_RELABEL = 1: the device generator stores P A P^T (vertex v at row / column
+    perm(v)), bit for bit the restatement matgen.rmat_csr(relabel=True), on one rank and on the
+    nnz-balanced slices of 3 ranks; rbl_row_ids returns perm^-1 of the local rows."""
+    from rbl import _lib
+    plant = matgen.planted_spectrum(5)
+    ref = matgen.rmat_csr(CASE["n"], CASE["scale"], CASE["edges"], CASE["seed"], plant,
+                          relabel=True)
+    perm_inv = matgen.rmat_relabel(CASE["n"], CASE["seed"], np.arange(CASE["n"]), inverse=True)
+
+    def fn(ctx, r):
+        ctx.set_option(_lib.RBL_OPT_RELABEL, 1)
+        ctx.gen_rmat(CASE["n"], CASE["scale"], CASE["edges"], CASE["seed"], plant)
+        _, r0, r1, _ = ctx.matrix_info()
+        return r0, r1, ctx.get_matrix_csr(), ctx.row_ids()
+
+    with rbl.Context(0) as ctx:
+        r0, r1, csr, ids = fn(ctx, 0)
+    assert (r0, r1) == (0, CASE["n"])
+    _csr_equal(ref, *csr)
+    assert np.array_equal(ids, perm_inv)
+    for r0, r1, csr, ids in run_ranks(rbl, 3, fn):
+        _csr_equal(ref[r0:r1], *csr)
+        assert np.array_equal(ids, perm_inv[r0:r1])
+
+
+def test_rmat_relabel_is_the_plain_run_permuted(rbl):
+    """The relabelled matrix with the device start block (drawn per original id) runs the plain
+    run's Krylov sequence with its rows permuted: per-step A_i / B_{i+1} to 1e-9 (the SpMM sums
+    a row's nonzeros in another column order), eigenvalues < 1e-10, and the Ritz vectors, put
+    back in original row order by rbl_row_ids, equal up to sign (1 - |v.v'| < 1e-8)."""
+    from rbl import _lib
+    k, b = 10, 32
+    plant = matgen.planted_spectrum(k)
+    n, scale, edges, seed = 60000, 16, 60000 * 66, 7
+    out = {}
+    for rl in (0, 1):
+        with rbl.Context(0) as ctx:
+            ctx.set_option(_lib.RBL_OPT_RELABEL, rl)
+            ctx.gen_rmat(n, scale, edges, seed, plant)
+            ids = ctx.row_ids()
+            D, V, info = rbl.lanczos(ctx, k, b, seed=4, check=True, trace=True)
+            Vo = np.zeros_like(V)
+            Vo[ids] = V
+            out[rl] = (D, Vo, info)
+    (D0, V0, i0), (D1, V1, i1) = out[0], out[1]
+    assert i0.converged and i1.converged and i0.iters == i1.iters
+    assert np.max(np.abs(D1 - D0) / np.abs(D0)) < 1e-10
+    for a, a0 in zip(i1.trace_A + i1.trace_B, i0.trace_A + i0.trace_B):
+        assert np.abs(a - a0).max() <= 1e-9 * np.abs(a0).max()
+    assert np.all(1 - np.abs(np.sum(V0 * V1, axis=0)) < 1e-8)
+
+
+def test_rmat_relabel_balances_the_halo(rbl):
+    """The reason for the relabel (BASELINE config 4 on 8 GPUs): with R-MAT's hubs at the low ids
+    the nnz-balanced split gives one rank most of the rows its peers reference, so it sends far
+    more than the others.  Relabelled, the busiest sender is within 1.2x the mean on 4 and 8
+    in-process ranks (n = 2e5, the bench's draw density), and the traces match the single-rank
+    relabelled run."""
+    from rbl import _lib
+    n, scale, edges, seed = 200_000, 18, int(0.66 * 100 * 200_000), 20261015
+    plant = matgen.planted_spectrum(5)
+    for P in (4, 8):
+        sends = {}
+        for rl in (0, 1):
+            def fn(ctx, r):
+                ctx.set_option(_lib.RBL_OPT_RELABEL, rl)
+                ctx.gen_rmat(n, scale, edges, seed, plant)
+                ctx.comm_stats(reset=True)
+                _, _, info = rbl.lanczos(ctx, 5, 32, seed=9, check=False, max_steps=4, trace=True,
+                                         ritz=False)
+                return ctx.comm_stats()["send_bytes"], info
+            res = run_ranks(rbl, P, fn, timeout=400)
+            sends[rl] = np.array([s for s, _ in res], dtype=float)
+        ratio0 = sends[0].max() / sends[0].mean()
+        ratio1 = sends[1].max() / sends[1].mean()
+        print(f"P={P}: busiest sender / mean: plain {ratio0:.2f}, relabelled {ratio1:.2f}")
+        assert ratio1 <= 1.2 < ratio0
+
+
+@pytest.mark.parametrize("b,kernel", [(8, 0), (32, 1), (16, 1), (40, 0)])
+def test_rmat_multirank_range_halo_beside_ghosts(rbl, b, kernel):
+    """A ghost-built (indexed-halo) context still runs every block size and kernel: for b outside
+    {16, 32}, or the gather pinned by RBL_OPT_SPMM_KERNEL = 1, the ranks use the range halo kept
+    beside the ghost tables (all ranks pick the same exchange); traces equal the single-rank
+    run's, and rbl_apply matches SciPy."""
+    from rbl import _lib
+    plant = matgen.planted_spectrum(3)
+    A = matgen.rmat_csr(CASE["n"], CASE["scale"], CASE["edges"], CASE["seed"], plant)
+    X = np.random.default_rng(b).standard_normal((CASE["n"], b))
+
+    def run(ctx):
+        ctx.set_option(_lib.RBL_OPT_SPMM_KERNEL, kernel)
+        ctx.gen_rmat(CASE["n"], CASE["scale"], CASE["edges"], CASE["seed"], plant)
+        assert ctx.spmm_kernel_for(b) == 1
+        _, _, info = rbl.lanczos(ctx, 3, b, seed=2, check=False, max_steps=6, trace=True,
+                                 ritz=False)
+        return info
+
+    with rbl.Context(0) as ctx:
+        ref = run(ctx)
+
+    def fn(ctx, r):
+        info = run(ctx)
+        _, r0, r1, _ = ctx.matrix_info()
+        return info, r0, ctx.apply(X[r0:r1])
+
+    out = run_ranks(rbl, 3, fn)
+    for info, _, _ in out:
+        for a, a1 in zip(info.trace_A, ref.trace_A):
+            assert np.abs(a - a1).max() <= 1e-9 * np.abs(a1).max()
+    Y = np.vstack([y for _, _, y in sorted(out, key=lambda t: t[1])])
+    bound = (abs(A) @ np.abs(X)) * 1e-13 + 1e-300
+    assert np.all(np.abs(Y - A @ X) <= bound)
+
+
+def test_unbanded_ranks_without_rows_or_nonzeros(rbl):
+    """The setup collectives when some ranks hold nothing: an unbanded (scattered) user CSR on 4
+    ranks whose caller-given row split leaves two ranks with rows but no nonzeros, and a matrix
+    with n < P that leaves a rank without rows.  Every rank takes part in the banded vote and
+    the ghost exchange; the traces equal the single-rank run's."""
+    import scipy.sparse as sp
+    rng = np.random.default_rng(5)
+    n, live = 400, 300
+    R = sp.random(live, live, density=0.05, random_state=6, format="csr")
+    R = R + R.T + sp.diags(rng.uniform(1, 2, live))
+    M = sp.block_diag([R, sp.csr_matrix((n - live, n - live))]).tocsr()
+    M.sort_indices()
+    omega = rng.standard_normal((n, 16))
+    with rbl.Context(0) as ctx:
+        ctx.set_matrix(M)
+        _, _, ref = rbl.lanczos(ctx, 3, 16, omega=omega, check=False, max_steps=5, trace=True,
+                                ritz=False)
+    bounds = [0, 150, 300, 350, 400]
+
+    def fn(ctx, r):
+        r0, r1 = bounds[r], bounds[r + 1]
+        S = M[r0:r1]
+        ctx.set_matrix_rows(n, r0, r1, S.indptr, S.indices, S.data)
+        _, _, _, nnz = ctx.matrix_info()
+        _, _, info = rbl.lanczos(ctx, 3, 16, omega=omega[r0:r1], check=False, max_steps=5,
+                                 trace=True, ritz=False)
+        return info, nnz, ctx.spmm_kernel_for(16)
+
+    out = run_ranks(rbl, 4, fn)
+    assert [nnz == 0 for _, nnz, _ in out] == [False, False, True, True]
+    assert out[0][2] == 6       # the segmented gather with the indexed halo on the live ranks
+    for info, _, _ in out:
+        for a, a1 in zip(info.trace_A, ref.trace_A):
+            assert np.abs(a - a1).max() <= 1e-9 * np.abs(a1).max()
+
+    # n < P: a rank with no rows at all
+    T = sp.csr_matrix(np.array([[2.0, 1, 0], [1, 3, 0], [0, 0, 4]]))
+    om = rng.standard_normal((3, 2))
+    with rbl.Context(0) as ctx:
+        ctx.set_matrix(T)
+        _, _, ref = rbl.lanczos(ctx, 1, 2, omega=om, check=False, max_steps=1, trace=True,
+                                ritz=False)
+
+    def fn2(ctx, r):
+        ctx.set_matrix(T)
+        _, r0, r1, _ = ctx.matrix_info()
+        _, _, info = rbl.lanczos(ctx, 1, 2, omega=om[r0:r1], check=False, max_steps=1,
+                                 trace=True, ritz=False)
+        return info, r1 - r0
+
+    out = run_ranks(rbl, 4, fn2)
+    assert any(m == 0 for _, m in out)
+    for info, _ in out:
+        assert np.abs(info.trace_A[0] - ref.trace_A[0]).max() <= 1e-12 * np.abs(ref.trace_A[0]).max()

@@ -32,7 +32,7 @@ def test_library_exports_every_header_symbol():
 
 def test_abi_version_and_stage_names():
     from rbl import _lib
-    assert _lib.lib.rbl_abi_version() == 1
+    assert _lib.lib.rbl_abi_version() == 2
     assert _lib.stage_names() == ["AQ", "3-term", "qr", "part reorth", "loc reorth",
                                   "Ritz vectors", "comm", "spill wait"]
 
