@@ -69,11 +69,11 @@ def parse():
                     help="rmat: BASELINE config 4's power-law pattern (SURVEY §8(d) C4b); "
                          "circuit: BASELINE config 3's shape (G3_circuit-like SPD Laplacian, "
                          "scattered; use --n 1585478 --b 16)")
-    ap.add_argument("--c3-steps", type=int, default=3,
+    ap.add_argument("--c3-steps", type=int, default=6,
                     help="timed runs of the C3 circuit sub-record that follows a hash-window run "
                          "(n = 1,585,478, b = 16, k = 20: BASELINE config 3's shape; 0 skips it)")
     ap.add_argument("--rmat-scale", type=int, default=24)
-    ap.add_argument("--rmat-steps", type=int, default=2,
+    ap.add_argument("--rmat-steps", type=int, default=3,
                     help="timed runs of the C4b R-MAT sub-record that follows a hash-window "
                          "run (BASELINE config 4 in the same job; 0 skips it)")
     ap.add_argument("--rmat-warmup", type=int, default=1)
@@ -681,6 +681,19 @@ def cpu_model() -> str:
     return "unknown"
 
 
+def cpu_cross_check() -> dict:
+    """The larger CPU sample beside the n = 1e5 extrapolation: the same port at n = 1e6 (129 s on
+    the box, too long for the default run), read from its committed bench line."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "r02_bench_cpu1e6.json")) as f:
+            c = json.load(f)["cpu_baseline"]
+        return {"value_from_n1e6_sample": c["value"], "n1e6_sample_seconds": c["sample_seconds"],
+                "n1e6_sample_source": "profiles/r02_bench_cpu1e6.json (same port, same box type, "
+                                      "16 threads; scaled x10 to n = 1e7)"}
+    except (OSError, ValueError, KeyError):
+        return {}
+
+
 def cpu_baseline(args, m_max, plant):
     """Time the oracle (NumPy/SciPy restatement of RBL.jl) on n_s rows of the same generator
     for the same m_max fixed block steps (measured end to end, matrix generation excluded), and
@@ -717,15 +730,14 @@ def cpu_baseline(args, m_max, plant):
     scale = args.n / ns
     out = {"value": round(m_max / (t * scale), 5), "unit": "block iterations/s",
            "cores": threads, "kind": "port",
+           "threads_note": f"{threads} BLAS threads of the box's {os.cpu_count()} CPUs: the harness's "
+                           "OMP_NUM_THREADS for one GPU's share of the host",
            "sample": f"oracle RBL (RBL.jl restated, NumPy/SciPy OpenBLAS on {threads} threads; SpMM "
                      f"single-threaded as SparseArrays) on the same generator at n={ns} "
                      f"(nnz={A.nnz}) for the same {m_max} block steps: {t:.2f} s measured, i.e. "
                      f"{m_max / t:.4f} iters/s at n={ns}; value = that per-iteration time scaled "
                      f"x{scale:.0f} to n={args.n}",
-           "cross_check": "the same port at n = 1e6 (129 s on the box, profiles/r02_bench_cpu1e6.json) "
-                          "gave 0.0294 iters/s scaled to n = 1e7, ~10 % below this n = 1e5 "
-                          "extrapolation: the baseline is stated from the smaller sample to keep "
-                          "the default run within minutes",
+           **cpu_cross_check(),
            "sample_n": ns, "sample_seconds": round(t, 3),
            "sample_iters_per_s": round(m_max / t, 5),
            "host_cpus": os.cpu_count(), "cpu_model": cpu_model()}

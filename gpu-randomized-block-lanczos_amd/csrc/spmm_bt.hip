@@ -35,6 +35,7 @@
 // Accumulator acc[p][s] column j = lane&3 is U column 8p + 2j + s, so one ds_read_b128 of
 // ring row rho at 16-B slot 4p + j feeds acc[p][0] and acc[p][1].
 #include <cstdlib>
+#include <type_traits>
 
 #include <hipcub/hipcub.hpp>
 
@@ -617,6 +618,377 @@ void k_spmm_bt(BtArgs a) {
   }
 }
 
+// ---- two waves per SIMD (b = 32, fp64, dense or half tiles) ---------------------------------
+// k_spmm_bt holds one wave per SIMD (256 VGPRs + AGPRs), so the SIMD idles whenever that wave
+// waits on memory: with whole tiles it streams at the HBM rate anyway, but with half tiles (5.1
+// GB less per launch at C4a) it becomes issue-bound at the same time.  Here eight
+// waves share one ring: waves p and p + 4 (the same SIMD) split tile T0 + 4r + p by its band
+// groups — role 0 the left groups [0, NG0), role 1 the rest — so each holds half the A operands
+// and single-buffered B operands (<= 256 registers: two waves per SIMD).  Per round:
+//   phase 1  both roles multiply their groups; role 1 leaves its partial U tile in LDS;
+//   barrier
+//   phase 2  role 0 adds it (U = left part + right part), runs the 3-term epilogue, stores U and
+//            forms the A_i partials; role 1 stages the next round's ring rows (with the fused
+//            local reorth's 64 MFMAs per 16-row block);
+//   barrier.
+// The MFMAs per SIMD split ~evenly (role 0: 4 groups + epilogue + A_i, role 1: 5 groups +
+// staging at NG = 9).  U differs from k_spmm_bt's only in the association of the group sum.
+template <int NG, bool EPI, bool AIG, int VAR>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2)))
+void k_spmm_bt2(BtArgs a) {
+  constexpr int B = 32;
+  using L = bt::Geo<32>;
+  constexpr int NP = 4, NS = 16, NE = 8;
+  constexpr int H = 8 * (NG - 1);
+  constexpr int kRoundRows = 64;
+  constexpr int kRingSpan = kRoundRows + 2 * H;
+  static_assert(kRingSpan + kRoundRows <= bt::kRing, "ring");
+  constexpr bool LF = (VAR & 1024) != 0, HALF = (VAR & 2048) != 0;
+  static_assert(!(VAR & (64 | 128)), "fp64 dense or half tiles");
+  constexpr int NGL = (NG - 1) / 2, NGH = NG - NGL;
+  constexpr int NG0 = NGL, NG1 = NG - NG0;  // role 0: groups [0, NG0) (the left groups)
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int p4 = wv & 3, role = wv >> 2;
+  const int64_t T0 = (int64_t)blockIdx.x * a.tiles_per_wg;
+  const int64_t T1 = T0 + a.tiles_per_wg < a.ntiles ? T0 + a.tiles_per_wg : a.ntiles;
+  if (T0 >= T1) return;
+  const int q = lane >> 4, j = lane & 3, G = (lane >> 2) & 3, i16 = lane & 15;
+  const int64_t gq = a.row0 - H;
+
+  auto qload = [&](int64_t rho, int s) -> d2v {
+    const int64_t c = rho + gq;
+    const bool in = c >= a.q_lo && c < a.q_hi;
+    const bool own = c >= a.loc_lo && c < a.loc_hi;
+    const double* p = own ? static_cast<const double*>(a.Qloc) + (c - a.loc_lo) * B
+                          : in ? a.Q + (c - a.col_off) * B : a.zrow;
+    return reinterpret_cast<const d2v*>(p)[s];
+  };
+  auto ring_ptr = [&](int64_t rho, int s) -> d2v* {
+    return reinterpret_cast<d2v*>(smem + (unsigned)(rho & (bt::kRing - 1)) * L::kRowBytes + 16u * s);
+  };
+  if constexpr (EPI) {
+    double* btab = reinterpret_cast<double*>(smem + L::kBtOff);
+    for (int idx = tid; idx < B * B; idx += 512) {
+      const int sp = idx & 1, jj = (idx >> 1) & 3, qq = (idx >> 3) & 3, p = (idx >> 5) % NP,
+                e = (idx >> 5) / NP;
+      const int x = 8 * (e >> 1) + 2 * qq + (e & 1), y = 8 * p + 2 * jj + sp;
+      btab[idx] = -a.Bi[y * B + x];
+    }
+  }
+  double* const ct = reinterpret_cast<double*>(smem + L::kCtOff);
+  const int64_t own_lo = 16 * T0 + H > a.lf_lo ? 16 * T0 + H : a.lf_lo;
+  int64_t own_hi = 16 * T1 - H < a.nrows ? 16 * T1 - H : a.nrows;
+  own_hi = own_hi < a.lf_hi ? own_hi : a.lf_hi;
+  auto lf_issue = [&](int64_t rho0, d2v (&raw)[4], d2v (&qa)[4]) {
+    const int64_t cr = rho0 + gq + 4 * G + q, ca = rho0 + gq + i16;
+    const bool inr = cr >= a.q_lo && cr < a.q_hi;
+    const bool ownr = cr >= a.loc_lo && cr < a.loc_hi;
+    const int64_t la = ca - a.row0;
+    const double* rp = ownr ? static_cast<const double*>(a.Qloc) + (cr - a.loc_lo) * B
+                            : inr ? a.Q + (cr - a.col_off) * B : a.zrow;
+    lf_loads(rp, la >= a.lf_lo && la < a.lf_hi ? a.Qprev + la * B : a.zrow, lane, raw, qa);
+  };
+  auto lf_finish = [&](int64_t rho0, const d2v (&raw)[4], const d2v (&qa)[4]) {
+    double f[4][2];
+    lf_block(raw, qa, ct, lane, f);
+    const int64_t rr = rho0 + 4 * G + q;
+    const int64_t lr = rr + gq - a.row0;
+    const bool wb = lr >= own_lo && lr < own_hi;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const d2v v = d2v{f[p][0], f[p][1]};
+      *ring_ptr(rr, 4 * p + j) = v;
+      if (wb) reinterpret_cast<d2v*>(a.Qw + lr * B + 2 * j)[4 * p] = v;
+    }
+  };
+  if constexpr (LF) {
+    lf_table(a.Cl, ct, tid, 512);
+    __syncthreads();
+    for (int bb = wv; bb < kRingSpan / 16; bb += 8) {
+      d2v raw[4], qa[4];
+      lf_issue(16 * T0 + 16 * bb, raw, qa);
+      lf_finish(16 * T0 + 16 * bb, raw, qa);
+    }
+  } else {
+    for (int idx = tid; idx < kRingSpan * NS; idx += 512) {
+      const int64_t rho = 16 * T0 + idx / NS;
+      *ring_ptr(rho, idx % NS) = qload(rho, idx % NS);
+    }
+  }
+
+  const int64_t tslot0 = 4 * (int64_t)blockIdx.x;
+  const int64_t tslot_r = 4 * (int64_t)gridDim.x;
+  auto slot_of = [&](int64_t t) -> int64_t {
+    const int64_t w = t / a.tiles_per_wg, lt = t - w * a.tiles_per_wg;
+    return ((lt >> 2) * gridDim.x + w) * 4 + (lt & 3);
+  };
+  auto lslot = [&](int64_t t) -> int64_t {  // slot of a tile of this workgroup's range
+    const int64_t lt = t - T0;
+    return (lt >> 2) * tslot_r + tslot0 + (lt & 3);
+  };
+  // A operands of group g of tile t (whole tiles; half tiles: own groups from the tile's slot,
+  // left groups from the strip of tile t - NGL + g, edge tiles whole from Ae)
+  auto tile_a = [&](int64_t t, int g, int h) -> d2v {
+    if constexpr (HALF) {
+      const double* ptr;
+      if (t < NGL) {
+        ptr = a.Ae + ((((t * NG + g) * 2 + h) * 64) + lane) * 2;
+      } else if (g >= NGL) {
+        ptr = a.Ah + ((((lslot(t) * NGH + (g - NGL)) * 2 + h) * 64) + lane) * 2;
+      } else {
+        const int64_t st = t - NGL + g;
+        const int64_t ts = st >= T0 ? lslot(st) : slot_of(st);
+        ptr = a.Ah + ((((ts * NGH + (NGL - g)) * 2 + h) * 64) + lane) * 2;
+      }
+      const d2v* p = reinterpret_cast<const d2v*>(ptr);
+      if (g == NGL) return __builtin_nontemporal_load(p);  // the diagonal group: read once
+      return *p;  // strip groups are read again (transposed) by the next NGL tiles: keep in L2
+    } else {
+      const d2v* p = reinterpret_cast<const d2v*>(a.A + ((((lslot(t) * NG + g) * 2 + h) * 64) + lane) * 2);
+      return __builtin_nontemporal_load(p);
+    }
+  };
+  // half tiles: role 0's NG0 = NGL groups are the left groups, transposed through a wave-private
+  // LDS square each (as k_spmm_bt's bt_transpose)
+  auto transpose_left = [&](auto& v) {
+    double* tb0 = reinterpret_cast<double*>(smem + L::kTrOff + p4 * NGL * kTrBytes);
+#pragma unroll
+    for (int g = 0; g < NGL; ++g) {
+      double* tb = tb0 + g * (kTrBytes / 8);
+      tb[i16 * kTrLd + q] = v[g][0].x;
+      tb[i16 * kTrLd + 4 + q] = v[g][0].y;
+      tb[i16 * kTrLd + 8 + q] = v[g][1].x;
+      tb[i16 * kTrLd + 12 + q] = v[g][1].y;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int g = 0; g < NGL; ++g) {
+      const double* tb = tb0 + g * (kTrBytes / 8);
+      v[g][0].x = tb[q * kTrLd + i16];
+      v[g][0].y = tb[(4 + q) * kTrLd + i16];
+      v[g][1].x = tb[(8 + q) * kTrLd + i16];
+      v[g][1].y = tb[(12 + q) * kTrLd + i16];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  };
+  auto clamp_t = [&](int64_t t) -> int64_t { return t < T1 ? t : T1 - 1; };
+
+  auto qprev_load = [&](int64_t t, d2v (&qv)[NE / 2]) {
+    int64_t r = 16 * t + i16;
+    r = r < a.nrows ? r : a.nrows - 1;
+#pragma unroll
+    for (int m = 0; m < NE / 2; ++m) qv[m] = reinterpret_cast<const d2v*>(a.Qprev + r * B + 2 * q)[4 * m];
+  };
+  const unsigned lb = (unsigned)(q * L::kRowBytes + 16 * j);
+  const unsigned lbt = (unsigned)(L::kBtOff + 16 * (4 * q + j));
+  const unsigned lus = (unsigned)(L::kUOff + p4 * L::kUWave);  // U stage (also the exchange)
+  const unsigned lai = (unsigned)(16 * bt::pi_slot(i16));
+  constexpr int NXG = 2, NYQ = 8, NA = NXG * NYQ;
+
+  // The two roles run separate copies of the round loop (wave-uniform branch), so each copy's
+  // registers hold only its own state: role 0 its 4 left groups, the epilogue operand and the
+  // A_i accumulators; role 1 its 5 groups and the staging rows.  Both pass the same barriers.
+  auto run = [&](auto role_c) {
+    constexpr int R1 = decltype(role_c)::value;
+    constexpr int GB = R1 ? NG0 : 0, NGR = R1 ? NG1 : NG0;
+    d2v av[NGR][2];
+    {
+      const int64_t t0 = clamp_t(T0 + p4);
+#pragma unroll
+      for (int gi = 0; gi < NGR; ++gi) {
+        av[gi][0] = tile_a(t0, GB + gi, 0);
+        av[gi][1] = tile_a(t0, GB + gi, 1);
+      }
+      if constexpr (HALF && !R1) {
+        if (t0 >= NGL) transpose_left(av);
+      }
+    }
+    d2v qp[NE / 2];
+    if constexpr (EPI && !R1) qprev_load(clamp_t(T0 + p4), qp);
+    double ai[R1 ? 1 : NXG][R1 ? 1 : NYQ];
+    if constexpr (!R1) {
+#pragma unroll
+      for (int x = 0; x < NXG; ++x)
+#pragma unroll
+        for (int y = 0; y < NYQ; ++y) ai[x][y] = 0.0;
+    }
+    __syncthreads();  // the prologue's ring rows and tables
+
+    for (int64_t R = 16 * T0; R < 16 * T1; R += kRoundRows) {
+      const int64_t tw = R / 16 + p4;
+      const int64_t rn = R + kRingSpan + 16 * p4;  // role 1 stages these 16 rows
+      d2v st[R1 && !LF ? 4 : 1], lraw[R1 && LF ? 4 : 1], lqa[R1 && LF ? 4 : 1];
+      if constexpr (R1) {
+        if constexpr (LF) {
+          lf_issue(rn, lraw, lqa);
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) st[i] = qload(rn + 4 * i + q, i16);
+        }
+      }
+      const bool live = tw < T1;  // wave-uniform (the same for both roles of a pair)
+      const int64_t tn = clamp_t(tw + 4);
+      double acc[NP][2];
+#pragma unroll
+      for (int p = 0; p < NP; ++p) acc[p][0] = acc[p][1] = 0.0;
+      // ---- phase 1: this wave's groups ----
+      if (live) {
+#pragma unroll
+        for (int gi = 0; gi < NGR; ++gi) {
+          const int g = GB + gi;
+          d2v bp[4][NP];
+          const unsigned gb = (unsigned)((16 * (tw + g)) & (bt::kRing - 1)) * L::kRowBytes + lb;
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int p = 0; p < NP; ++p)
+              bp[u][p] = *reinterpret_cast<const d2v*>(smem + gb + u * 4 * L::kRowBytes + 64 * p);
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const double av_u = (u & 1) ? av[gi][u >> 1].y : av[gi][u >> 1].x;
+#pragma unroll
+            for (int p = 0; p < NP; ++p) {
+              acc[p][0] = mfma44(av_u, bp[u][p].x, acc[p][0]);
+              acc[p][1] = mfma44(av_u, bp[u][p].y, acc[p][1]);
+            }
+          }
+          av[gi][0] = tile_a(tn, g, 0);
+          av[gi][1] = tile_a(tn, g, 1);
+        }
+      }
+      double* xch = reinterpret_cast<double*>(smem + lus);
+      if constexpr (R1) {
+        if (live) {
+#pragma unroll
+          for (int p = 0; p < NP; ++p) {
+            xch[(2 * p) * 64 + lane] = acc[p][0];
+            xch[(2 * p + 1) * 64 + lane] = acc[p][1];
+          }
+        }
+      }
+      __syncthreads();
+      // ---- phase 2 ----
+      if constexpr (!R1) {
+        if (live) {
+#pragma unroll
+          for (int p = 0; p < NP; ++p) {
+            acc[p][0] = acc[p][0] + xch[(2 * p) * 64 + lane];
+            acc[p][1] = acc[p][1] + xch[(2 * p + 1) * 64 + lane];
+          }
+          if constexpr (EPI) {
+#pragma unroll
+            for (int e = 0; e < NE; ++e) {
+              const double qv = (e & 1) ? qp[e >> 1].y : qp[e >> 1].x;
+              d2v bv[NP];
+#pragma unroll
+              for (int p = 0; p < NP; ++p) bv[p] = *reinterpret_cast<const d2v*>(smem + lbt + 256 * (NP * e + p));
+#pragma unroll
+              for (int p = 0; p < NP; ++p) {
+                acc[p][0] = mfma44(qv, bv[p].x, acc[p][0]);
+                acc[p][1] = mfma44(qv, bv[p].y, acc[p][1]);
+              }
+            }
+            qprev_load(tn, qp);
+          }
+          const int64_t ru = 16 * tw + 4 * G + q;
+          d2v* urow = reinterpret_cast<d2v*>(a.U + ru * B + 2 * j);
+#pragma unroll
+          for (int p = 0; p < NP; ++p) __builtin_nontemporal_store(d2v{acc[p][0], acc[p][1]}, urow + 4 * p);
+          if constexpr (AIG) {
+            const bool lv = ru < a.nrows;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();  // the exchange reads above come before the stage
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+            for (int p = 0; p < NP; ++p)
+              *reinterpret_cast<d2v*>(smem + lus + (4 * G + q) * L::kUStride + 16 * (4 * p + j)) =
+                  lv ? d2v{acc[p][0], acc[p][1]} : d2v{0.0, 0.0};
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+            for (int ks = 0; ks < 4; ++ks) {
+              const int64_t rho = 16 * tw + H + 4 * ks + q;
+              const unsigned rb = (unsigned)(rho & (bt::kRing - 1)) * L::kRowBytes + lai;
+              const d2v v = *reinterpret_cast<const d2v*>(smem + rb);
+              const double aq[NXG] = {v.x, v.y};
+#pragma unroll
+              for (int m = 0; m < NYQ / 2; ++m) {
+                const d2v bu = *reinterpret_cast<const d2v*>(smem + lus + (4 * ks + q) * L::kUStride + 16 * (4 * m + j));
+#pragma unroll
+                for (int x = 0; x < NXG; ++x) {
+                  ai[x][2 * m] = mfma44(aq[x], bu.x, ai[x][2 * m]);
+                  ai[x][2 * m + 1] = mfma44(aq[x], bu.y, ai[x][2 * m + 1]);
+                }
+              }
+            }
+          }
+          if constexpr (HALF) {
+            if (tn >= NGL) transpose_left(av);
+          }
+        }
+      } else {
+        if constexpr (LF) {
+          lf_finish(rn, lraw, lqa);
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) *ring_ptr(rn + 4 * i + q, i16) = st[i];
+        }
+      }
+      __syncthreads();
+    }
+    // A_i: the four role-0 waves' partials summed through the (now free) ring area
+    double* red = reinterpret_cast<double*>(smem);
+    if constexpr (AIG && !R1) {
+      if (p4 > 0) {
+#pragma unroll
+        for (int x = 0; x < NXG; ++x)
+#pragma unroll
+          for (int y = 0; y < NYQ; ++y) red[((p4 - 1) * NA + x * NYQ + y) * 64 + lane] = ai[x][y];
+      }
+    }
+    __syncthreads();
+    if constexpr (AIG && !R1) {
+      if (p4 == 0) {
+        double* out = a.ai_slab + (int64_t)blockIdx.x * B * B;
+        const int xb = 2 * bt::pi_slot(4 * G + q);
+#pragma unroll
+        for (int x = 0; x < NXG; ++x)
+#pragma unroll
+          for (int y = 0; y < NYQ; ++y) {
+            double v = ai[x][y];
+#pragma unroll
+            for (int w = 0; w < 3; ++w) v += red[(w * NA + x * NYQ + y) * 64 + lane];
+            out[(xb + x) * B + 8 * (y >> 1) + 2 * j + (y & 1)] = v;
+          }
+      }
+    }
+  };
+  if (role) run(std::integral_constant<int, 1>());
+  else run(std::integral_constant<int, 0>());
+}
+
+template <int NG, bool EPI, bool AIG, int VAR>
+static void launch_bt2_v(const BtArgs& a, int grid, hipStream_t s) {
+  constexpr int lds = bt::Geo<32>::kLds + ((VAR & 2048) ? 9216 + 4 * ((NG - 1) / 2) * kTrBytes
+                                                       : (VAR & 1024) ? kCtBytes : 0);
+  ensure_lds_attr(reinterpret_cast<const void*>(&k_spmm_bt2<NG, EPI, AIG, VAR>), lds);
+  hipLaunchKernelGGL((k_spmm_bt2<NG, EPI, AIG, VAR>), dim3(grid), dim3(512), lds, s, a);
+}
+// RBL_BT2: 1 the two-waves-per-SIMD kernel for b = 32 fp64 steps (EPI + A_i, dense or half
+// tiles, with or without the fused local reorth); 0 k_spmm_bt everywhere
+static bool bt2_on() {
+  const char* e = getenv("RBL_BT2");  // read per launch (tests switch it)
+  return e ? atoi(e) != 0 : false;
+}
+
 template <int B, int NG, bool EPI, bool AIG, int VAR>
 static void launch_bt_v(const BtArgs& a, int grid, hipStream_t s) {
   constexpr int lds = bt::Geo<B>::kLds + ((VAR & 2048) ? 9216 + 4 * ((NG - 1) / 2) * kTrBytes
@@ -698,12 +1070,34 @@ bool spmm_bt(const CsrDev& A, const double* Qin, int64_t col_off, int b, double*
     if (b != 32 || f32 || a.hdr || !epi || !aig) return false;
     a.lf_lo = A.lfix_lo;
     a.lf_hi = A.lfix_hi;
+    if (bt2_on()) {
+      if (a.Ah) {
+        if (A.bt_ng == 9) launch_bt2_v<9, true, true, 1024 | 2048>(a, grid, s);
+        else launch_bt2_v<5, true, true, 1024 | 2048>(a, grid, s);
+      } else {
+        if (A.bt_ng == 9) launch_bt2_v<9, true, true, 1024>(a, grid, s);
+        else launch_bt2_v<5, true, true, 1024>(a, grid, s);
+      }
+      return true;
+    }
     if (a.Ah) {
       if (A.bt_ng == 9) launch_bt_v<32, 9, true, true, 3 | 1024 | 2048>(a, grid, s);
       else launch_bt_v<32, 5, true, true, 3 | 1024 | 2048>(a, grid, s);
     } else {
       if (A.bt_ng == 9) launch_bt_v<32, 9, true, true, 3 | 1024>(a, grid, s);
       else launch_bt_v<32, 5, true, true, 3 | 1024>(a, grid, s);
+    }
+    return true;
+  }
+  if (bt2_on() && b == 32 && epi && aig && !f32 && !a.hdr) {
+    a.lf_lo = 0;
+    a.lf_hi = 0;
+    if (a.Ah) {
+      if (A.bt_ng == 9) launch_bt2_v<9, true, true, 2048>(a, grid, s);
+      else launch_bt2_v<5, true, true, 2048>(a, grid, s);
+    } else {
+      if (A.bt_ng == 9) launch_bt2_v<9, true, true, 0>(a, grid, s);
+      else launch_bt2_v<5, true, true, 0>(a, grid, s);
     }
     return true;
   }

@@ -71,6 +71,7 @@ end
 # reference's labels (RBL_gpu.jl:152-187, 219), one call per label per run.  TimerOutputs has
 # no public call to add an externally measured time, so this writes the section's
 # accumulated data; if that internal layout ever changes, the times are printed instead.
+# UNVERIFIED: Julia is absent from the build image, so neither path has run (INTEGRATION.md).
 function fold_device_timers!(to, ctx::Ptr{Cvoid})
     ns = ccall((:rbl_num_stages, librbl_hip), Cint, ())
     ms = zeros(Float64, ns)

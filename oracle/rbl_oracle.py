@@ -25,7 +25,7 @@ with the GPU driver's loop bound (``Julia/RBL_gpu.jl:211``: 1200) available thro
 * P8 — partial reorth at even ``i`` touches ``Q_i`` and ``Q_{i-1}`` against
   ``Q_1..Q_{i-2}`` in ascending ``j`` (block MGS, ``RBL.jl:30-48``), before local reorth.
 
-Pinning: ``tests/test_oracle_known_answer.py`` runs the reference's own known-answer
+Pinning: ``tests/test_oracle.py`` runs the reference's own known-answer
 suites (``Julia/Unit Testing/test.jl:16-50`` via ``mod_dec.jl``/``slow_dec.jl``/
 ``step_dec.jl``: relative eigenvalue-error norm < 1e-13).  Julia is absent from the
 image, so no reference output can be generated; those suites are the pin.

@@ -8,7 +8,8 @@ Protocol (one JSON object per line): the request {"cmds": [argv, ...], "timeout"
 "env": {...}} starts one process per argv (its own session, output to a temporary file); the
 reply {"rc": [...], "out": [...]} carries each exit status and the tail of its output.  A rank
 that fails makes its peers fail within seconds (the shm transport notices the exited pid); past
-the timeout, or 20 s after the first failure, the remaining ranks' process groups are killed.
+the timeout, or `grace` (default 20) seconds after the first failure, the remaining ranks' process
+groups are killed.
 EOF on stdin ends the helper.
 """
 import json
@@ -30,6 +31,7 @@ def run(req):
                                       start_new_session=True))
         logs.append(f)
     deadline = time.time() + float(req.get("timeout", 240))
+    grace = float(req.get("grace", 20))
     first_fail = None
     rcs = [None] * len(procs)
     while any(rc is None for rc in rcs):
@@ -37,7 +39,7 @@ def run(req):
         now = time.time()
         if first_fail is None and any(rc not in (None, 0) for rc in rcs):
             first_fail = now
-        if now > deadline or (first_fail is not None and now - first_fail > 20):
+        if now > deadline or (first_fail is not None and now - first_fail > grace):
             for p, rc in zip(procs, rcs):
                 if rc is None:
                     try:

@@ -139,6 +139,7 @@ def test_spmm_band_tiles_packed_bit_identical(rbl, monkeypatch, n, W, p, b):
     A = matgen.hashwindow_csr(n, W, p, n + 11)
     X = np.random.default_rng(n + 1).standard_normal((n, b))
     out = []
+    monkeypatch.setenv("RBL_BT2", "0")  # packed tiles run k_spmm_bt only: compare like with like
     for pack in ("0", "1"):
         monkeypatch.setenv("RBL_BT_PACK", pack)
         with rbl.Context(0) as ctx:
@@ -238,3 +239,28 @@ def test_spmm_segmented_and_gather_agree_in_lanczos(rbl):
             out.append(info)
     for a1, a2 in zip(out[0].trace_A, out[1].trace_A):
         assert np.abs(a1 - a2).max() <= 1e-12 * np.abs(a1).max()
+
+
+@pytest.mark.parametrize("n,W,half,fuse", [(50003, 64, "0", 7), (50003, 64, "1", 7), (20001, 32, "0", 7),
+                                           (20001, 32, "1", 3), (300, 64, "0", 7), (4099, 64, "1", 3)])
+def test_spmm_band_tiles_two_waves_per_simd(rbl, monkeypatch, n, W, half, fuse):
+    """k_spmm_bt2 (RBL_BT2=1: eight waves share the Q ring, waves p and p + 4 of a SIMD split a
+    tile's band groups) against k_spmm_bt: the same products, the group sum associated as (left
+    groups) + (the rest), so per-step A_i / B_{i+1} agree to 1e-12 relative over a 10-step
+    Lanczos run (fused 3-term epilogue, A_i partials, with and without the fused local
+    reorth); whole and half tiles; H = 32 and 64; a matrix smaller than one round."""
+    plant = matgen.planted_spectrum(5)
+    A = matgen.hashwindow_csr(n, W, 0.7734, n + 9, plant)
+    monkeypatch.setenv("RBL_BT_HALF", half)
+    runs = []
+    for v in ("0", "1"):
+        monkeypatch.setenv("RBL_BT2", v)
+        with rbl.Context(0) as ctx:
+            ctx.set_option(rbl._lib.RBL_OPT_FUSE, fuse)
+            ctx.set_matrix(A)
+            assert ctx.spmm_kernel_for(32) == 5
+            _, _, info = rbl.lanczos(ctx, 5, 32, seed=4, check=False, max_steps=min(10, n // 32),
+                                     trace=True, ritz=False)
+        runs.append(info)
+    for a0, a1 in zip(runs[0].trace_A + runs[0].trace_B, runs[1].trace_A + runs[1].trace_B):
+        assert np.abs(a0 - a1).max() <= 1e-12 * np.abs(a0).max()

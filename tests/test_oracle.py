@@ -115,3 +115,25 @@ def test_rmat_restatement_properties():
     assert top > 0.1 * A.nnz
     part = matgen.rmat_csr(n, 12, 60_000, 11, plant, row_begin=1000, row_end=2500)
     assert (part != A[1000:2500]).nnz == 0
+
+
+def test_rmat_relabel_is_a_symmetric_permutation():
+    """RBL_OPT_RELABEL's restatement: matgen.rmat_csr(relabel=True) is P A P^T for the seeded
+    Feistel permutation rmat_relabel (so the spectrum is A's), row slices tile it, and the
+    permutation and its inverse are bijections of [0, n)."""
+    import scipy.sparse as sp
+    from oracle import matgen as m
+    n, seed = 3000, 5
+    A = m.rmat_csr(n, 12, n * 30, seed, m.planted_spectrum(5))
+    B = m.rmat_csr(n, 12, n * 30, seed, m.planted_spectrum(5), relabel=True)
+    perm = m.rmat_relabel(n, seed, np.arange(n))
+    assert np.array_equal(np.sort(perm), np.arange(n))
+    assert np.array_equal(m.rmat_relabel(n, seed, perm, inverse=True), np.arange(n))
+    P = sp.csr_matrix((np.ones(n), (perm, np.arange(n))), shape=(n, n))
+    assert abs(P @ A @ P.T - B).max() == 0.0 and abs(B - B.T).max() == 0.0
+    part = m.rmat_csr(n, 12, n * 30, seed, m.planted_spectrum(5), relabel=True, row_begin=700,
+                      row_end=1900)
+    assert abs(part - B[700:1900]).max() == 0.0
+    # the hubs (R-MAT's low ids) no longer sit in the first rows
+    deg = np.diff(B.indptr)
+    assert deg[: n // 8].sum() < 0.3 * deg.sum() < np.diff(A.indptr)[: n // 8].sum()
