@@ -116,13 +116,23 @@ constexpr int kCtLd = 36;
 constexpr int kCtBytes = 32 * kCtLd * 8;
 constexpr int kTrLd = 18;                  // half tiles: transpose square, doubles per row
 constexpr int kTrBytes = 16 * kTrLd * 8;   // per wave (4 x 2,304 B <= 9,216)
+// RBL_BT_QNT (diagnostics, default 0): the Q_i / Q_{i-1} rows the SpMM stages load
+// non-temporally, so they do not push the half tiles' strips (re-read from L2 by the next
+// tiles) out of L2
+#ifndef RBL_BT_QNT
+#define RBL_BT_QNT 0
+#endif
+__device__ __forceinline__ d2v qld(const d2v* p) {
+  if constexpr (RBL_BT_QNT) return __builtin_nontemporal_load(p);
+  return *p;
+}
 __device__ __forceinline__ void lf_loads(const double* rraw, const double* rprev, int lane,
                                          d2v (&raw)[4], d2v (&qa)[4]) {
   const int q = lane >> 4, j = lane & 3;
 #pragma unroll
-  for (int p = 0; p < 4; ++p) raw[p] = reinterpret_cast<const d2v*>(rraw + 2 * j)[4 * p];
+  for (int p = 0; p < 4; ++p) raw[p] = qld(reinterpret_cast<const d2v*>(rraw + 2 * j) + 4 * p);
 #pragma unroll
-  for (int m = 0; m < 4; ++m) qa[m] = reinterpret_cast<const d2v*>(rprev + 2 * q)[4 * m];
+  for (int m = 0; m < 4; ++m) qa[m] = qld(reinterpret_cast<const d2v*>(rprev + 2 * q) + 4 * m);
 }
 __device__ __forceinline__ void lf_table(const double* C, double* ct, int tid, int nthreads) {
   for (int idx = tid; idx < 32 * 32; idx += nthreads) ct[(idx >> 5) * kCtLd + (idx & 31)] = -C[idx];
@@ -196,7 +206,7 @@ void k_spmm_bt(BtArgs a) {
     } else {
       const double* p = own ? static_cast<const double*>(a.Qloc) + (c - a.loc_lo) * B
                             : in ? a.Q + (c - a.col_off) * B : a.zrow;
-      return reinterpret_cast<const d2v*>(p)[s];
+      return qld(reinterpret_cast<const d2v*>(p) + s);
     }
   };
   auto ring_ptr = [&](int64_t rho, int s) -> d2v* {
@@ -664,7 +674,7 @@ void k_spmm_bt2(BtArgs a) {
     const bool own = c >= a.loc_lo && c < a.loc_hi;
     const double* p = own ? static_cast<const double*>(a.Qloc) + (c - a.loc_lo) * B
                           : in ? a.Q + (c - a.col_off) * B : a.zrow;
-    return reinterpret_cast<const d2v*>(p)[s];
+    return qld(reinterpret_cast<const d2v*>(p) + s);
   };
   auto ring_ptr = [&](int64_t rho, int s) -> d2v* {
     return reinterpret_cast<d2v*>(smem + (unsigned)(rho & (bt::kRing - 1)) * L::kRowBytes + 16u * s);

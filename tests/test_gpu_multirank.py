@@ -202,7 +202,9 @@ def test_multirank_fused_local_reorth_runs(rbl, P):
         return run_ranks(rbl, P, fn)
 
     t7, t3 = run(7), run(3)
-    assert sum(t7) < 0.5 * sum(t3), (t7, t3)
+    # the ranks share one GPU here, so a rank's stage events can include the other rank's kernels
+    # (a 157 KB-LDS SpMM workgroup holds a whole CU): compare the least-disturbed rank
+    assert min(t7) < 0.5 * min(t3), (t7, t3)
 
 
 def test_multirank_half_band_tiles_bit_identical(rbl, monkeypatch):

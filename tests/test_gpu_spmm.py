@@ -248,7 +248,8 @@ def test_spmm_band_tiles_two_waves_per_simd(rbl, monkeypatch, n, W, half, fuse):
     tile's band groups) against k_spmm_bt: the same products, the group sum associated as (left
     groups) + (the rest), so per-step A_i / B_{i+1} agree to 1e-12 relative over a 10-step
     Lanczos run (fused 3-term epilogue, A_i partials, with and without the fused local
-    reorth); whole and half tiles; H = 32 and 64; a matrix smaller than one round."""
+    reorth); whole and half tiles; H = 32 and 64; a matrix smaller than one round (its run kept
+    well short of Krylov exhaustion, where the trace amplifies rounding)."""
     plant = matgen.planted_spectrum(5)
     A = matgen.hashwindow_csr(n, W, 0.7734, n + 9, plant)
     monkeypatch.setenv("RBL_BT_HALF", half)
@@ -259,7 +260,7 @@ def test_spmm_band_tiles_two_waves_per_simd(rbl, monkeypatch, n, W, half, fuse):
             ctx.set_option(rbl._lib.RBL_OPT_FUSE, fuse)
             ctx.set_matrix(A)
             assert ctx.spmm_kernel_for(32) == 5
-            _, _, info = rbl.lanczos(ctx, 5, 32, seed=4, check=False, max_steps=min(10, n // 32),
+            _, _, info = rbl.lanczos(ctx, 5, 32, seed=4, check=False, max_steps=min(10, n // 64),
                                      trace=True, ritz=False)
         runs.append(info)
     for a0, a1 in zip(runs[0].trace_A + runs[0].trace_B, runs[1].trace_A + runs[1].trace_B):

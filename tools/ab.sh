@@ -2,9 +2,9 @@
 # per-session A/B wrappers of rounds 2-3).
 #
 # usage: REPS=2 bash tools/ab.sh <tag> "<bench args>" <variant> [<variant> ...]
-#   variant "tree" = the in-tree librbl_hip.so; any other name = tools/variants/<name>/librbl_hip.so
-#   (built beforehand with tools/build_variant.sh <name> "<-D defines>"), or NAME=VAL:... to run
-#   the tree library with environment knobs (e.g. RBL_BT_VAR=35).
+#   variant = <lib>[:NAME=VAL[:NAME=VAL...]]: <lib> "tree" = the in-tree librbl_hip.so, any other
+#   name = tools/variants/<name>/librbl_hip.so (built beforehand with tools/build_variant.sh
+#   <name> "<-D defines>"); the NAME=VAL knobs are set for that run (e.g. tree:RBL_BT_HALF=1).
 # Each run's bench line goes to gpurun_out/<tag>_<variant>_<rep>.json; one summary line per run
 # (value, ms per step, the stage split, the SpMM and partial-reorth rooflines) is printed.
 set -u
@@ -14,17 +14,14 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 for rep in $(seq 1 "$REPS"); do
   for v in "$@"; do
-    envs=()
+    IFS=':' read -ra parts <<< "$v"
+    lib=${parts[0]}
+    envs=("${parts[@]:1}")
     unset RBL_LIB
-    if [ "$v" != tree ]; then
-      case "$v" in
-        *=*) IFS=':' read -ra envs <<< "$v" ;;
-        *) export RBL_LIB=$PWD/tools/variants/$v/librbl_hip.so ;;
-      esac
-    fi
+    if [ "$lib" != tree ]; then export RBL_LIB=$PWD/tools/variants/$lib/librbl_hip.so; fi
     safe=$(echo "$v" | tr '=:/' '__-')
     out=gpurun_out/${tag}_${safe}_${rep}.json
-    env "${envs[@]}" timeout -k 10 600 python bench.py $args > "$out" 2> "${out%.json}.err" || exit 1
+    env ${envs[@]+"${envs[@]}"} timeout -k 10 600 python bench.py $args > "$out" 2> "${out%.json}.err" || exit 1
     python - "$v" "$out" <<'PY'
 import json, sys
 d = json.loads(open(sys.argv[2]).read().strip().splitlines()[-1])

@@ -10,6 +10,10 @@ groups=(
  "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_VALU SQ_INST_LEVEL_LDS"
  "SQ_LDS_UNALIGNED_STALL SQ_LDS_ADDR_CONFLICT SQ_INSTS_LDS_LOAD SQ_INSTS_LDS_STORE SQ_INSTS_MFMA SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES"
 )
+# PMC_TCC=1: two more passes for the memory side (FETCH_SIZE alone takes 3 of the 4 TCC slots)
+if [ "${PMC_TCC:-0}" = 1 ]; then
+  groups+=("FETCH_SIZE" "WRITE_SIZE TCC_HIT_sum TCC_MISS_sum")
+fi
 i=0
 for g in "${groups[@]}"; do
   i=$((i+1))

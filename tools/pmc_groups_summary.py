@@ -34,3 +34,8 @@ for k, a in agg.items():
         a["SQ_INSTS_SALU"], a["SQ_WAVES"], a["SQ_LDS_DATA_FIFO_FULL"], a["SQ_LDS_CMD_FIFO_FULL"],
         a["SQ_LDS_UNALIGNED_STALL"], a["SQ_LDS_ADDR_CONFLICT"]))
     print("  raw GRBM_GUI_ACTIVE %.4g  LDS_IDX_ACTIVE %.4g  MFMA_BUSY %.4g" % (gui, a["SQ_LDS_IDX_ACTIVE"], a["SQ_VALU_MFMA_BUSY_CYCLES"]))
+    if a["FETCH_SIZE"] or a["WRITE_SIZE"]:
+        # FETCH_SIZE in KB, x2 for 16-B-per-lane streaming reads on gfx950 (MI355X_MICROARCH.md HBM)
+        hit = a["TCC_HIT_sum"] / max(1.0, a["TCC_HIT_sum"] + a["TCC_MISS_sum"])
+        print("  memory side: FETCH %.4g GB (x2 calibrated)  WRITE %.4g GB  L2 hit %.3f" % (
+            a["FETCH_SIZE"] * 2 * 1024 / 1e9, a["WRITE_SIZE"] * 1024 / 1e9, hit))
