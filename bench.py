@@ -72,11 +72,23 @@ def parse():
     ap.add_argument("--c3-steps", type=int, default=6,
                     help="timed runs of the C3 circuit sub-record that follows a hash-window run "
                          "(n = 1,585,478, b = 16, k = 20: BASELINE config 3's shape; 0 skips it)")
+    ap.add_argument("--c5-steps", type=int, default=2,
+                    help="timed runs of the C5 sub-record (BASELINE config 5: n = 5e7, ~100 nnz/row, "
+                         "fp32 Krylov basis, b = 32) that follows a hash-window run on two or more "
+                         "ranks, where the basis fits in HBM without spilling; 0 skips it")
+    ap.add_argument("--c5-n", type=int, default=50_000_000)
+    ap.add_argument("--c5-min-ranks", type=int, default=2,
+                    help="fewest ranks the C5 sub-record runs on (one GPU would spill the 243 GB "
+                         "fp32 basis to host memory: DESIGN §2)")
     ap.add_argument("--rmat-scale", type=int, default=24)
     ap.add_argument("--rmat-steps", type=int, default=3,
                     help="timed runs of the C4b R-MAT sub-record that follows a hash-window "
                          "run (BASELINE config 4 in the same job; 0 skips it)")
     ap.add_argument("--rmat-warmup", type=int, default=1)
+    ap.add_argument("--halo-push", type=int, default=2, choices=(0, 1, 2),
+                    help="RBL_OPT_HALO_PUSH for the unbanded sub-records on several ranks: the "
+                         "push/pull split of the indexed halo (2: when its setup predicts fewer "
+                         "moved rows)")
     ap.add_argument("--rmat-relabel", default="1", choices=("auto", "0", "1"),
                     help="RBL_OPT_RELABEL for the R-MAT matrix: store P A P^T for a seeded vertex "
                          "permutation (Graph500's generator scrambles its vertex ids the same way), "
@@ -529,6 +541,12 @@ def main():
     if args.matrix == "hashwindow" and args.c3_steps > 0 and args.basis_bits == 64:
         c3_rec = guarded(c3_subrecord, ctx, args, world, barrier, allmax, allsum, allgather_i64)
 
+    # ---- BASELINE config 5: n = 5e7, fp32 basis, on >= 2 ranks (no spill) ----
+    c5_rec = None
+    if (args.matrix == "hashwindow" and args.c5_steps > 0 and args.basis_bits == 64
+            and world >= args.c5_min_ranks):
+        c5_rec = guarded(c5_subrecord, ctx, args, world, barrier, allmax, allsum, allgather_i64)
+
     # ---- CPU baseline: the oracle (port of RBL.jl) on a bounded sample, rank 0, N = 1 ----
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -577,6 +595,7 @@ def main():
             "comm_per_step": meas["comm_per_step"],
             "c4b_rmat": rmat_rec,
             "c3_circuit": c3_rec,
+            "c5_mixed": c5_rec,
         }
         print(json.dumps(line), flush=True)
     ctx.close()
@@ -599,10 +618,12 @@ def rmat_subrecord(ctx, args, plant, world, barrier, allmax, allsum, allgather_i
     edges = args.rmat_edges or int(0.66 * 100 * args.n)
     relabel = rmat_relabel(args, world)
     ctx.set_option(_lib.RBL_OPT_RELABEL, relabel)
+    ctx.set_option(_lib.RBL_OPT_HALO_PUSH, args.halo_push)
     t0 = time.perf_counter()
     ctx.gen_rmat(args.n, args.rmat_scale, edges, args.seed, plant)
     ctx.set_option(_lib.RBL_OPT_RELABEL, 0)
     gen_s = time.perf_counter() - t0
+    plan = ctx.comm_stats()
     _, r0, r1, nnz_loc = ctx.matrix_info()
     nloc = r1 - r0
     nnz = allsum(nnz_loc)
@@ -627,6 +648,9 @@ def rmat_subrecord(ctx, args, plant, world, barrier, allmax, allsum, allgather_i
             "n": args.n, "nnz": nnz, "rmat_scale": args.rmat_scale, "rmat_edges": edges,
             "rmat_abcd": [0.57, 0.19, 0.19, 0.05], "nnz_per_rank": allgather_i64(nnz_loc),
             "relabel": bool(relabel),
+            "halo_plan": {"push_pull_split": bool(plan["halo_push"]),
+                          "rows_per_spmm_split": plan["push_rows_pred"],
+                          "rows_per_spmm_pull_all": plan["pull_rows_pred"]},
             "send_bytes_per_step_by_rank": allgather_i64(int(meas["comm_per_step"]["send_bytes"])),
             "roofline": meas["roofline"], "roofline_secondary": meas["roofline_secondary"],
             "stage_ms_per_run": {s_: round(v / K, 3) for s_, v in meas["stage"].items()},
@@ -669,6 +693,61 @@ def c3_subrecord(ctx, args, world, barrier, allmax, allsum, allgather_i64):
             "value": round(meas["value"], 3), "unit": "block iterations/s",
             "steps": K, "warmup": 1, "ms_per_step": round(meas["elapsed"] / K * 1e3, 3),
             "n": ra.n, "nnz": nnz, "b": ra.b, "k": ra.k, "block_steps_per_run": meas["m_max"],
+            "nnz_per_rank": allgather_i64(nnz_loc),
+            "roofline": meas["roofline"], "roofline_secondary": meas["roofline_secondary"],
+            "stage_ms_per_run": {s_: round(v / K, 3) for s_, v in meas["stage"].items()},
+            "comm_per_step": meas["comm_per_step"],
+            "time_to_k": {"seconds": round(ttk_s, 4), "iters": info.iters,
+                          "converged": info.converged, "k": ra.k,
+                          "top_eigenvalues": [round(float(x), 6) for x in D[:3]]},
+            "matrix_gen_s": round(gen_s, 3)}
+
+
+def c5_subrecord(ctx, args, world, barrier, allmax, allsum, allgather_i64):
+    """BASELINE config 5 in the same driver run: the hash-window matrix at
+    n = 5e7 (~5e9 nonzeros, int64 row pointers), b = 32, k = 20, with the fp32 Krylov basis (the
+    reference run with FLOAT = Float32: blocks and their reorth fp32, A*Q / 3-term / QR fp64),
+    the CSR released once the band tiles exist (RBL_OPT_KEEP_CSR = 0), on >= 2 ranks so the
+    basis (243 GB in fp32) stays in HBM; 1 untimed + `args.c5_steps` timed fixed-length runs and
+    a time-to-k.  It replaces the headline matrix (the last sub-record)."""
+    import copy
+    import rbl
+    from rbl import _lib
+    ra = copy.copy(args)
+    ra.n, ra.basis_bits, ra.keep_csr = args.c5_n, 32, 0
+    plant = np.array([100.0 * (2 * ra.k + 1 - l) for l in range(1, 2 * ra.k + 1)])
+    # every rank checks its HBM first and all skip together (a rank failing inside a collective
+    # would leave its peers waiting): per local row ~2.4 KB while the matrix is built (CSR + band
+    # tiles) and ~6.9 KB during the run (39 fp32 basis slots, band tiles, fp64 working blocks)
+    nloc_est = -(-ra.n // world)
+    need = 1.15 * nloc_est * max(2.4e3, 39 * 32 * 4 + 1152 + 3 * 256 + 64)
+    free, total = ctx.device_memory()  # (the C3 matrix and its ~16 GB of buffers still held)
+    if allsum(int(free < need)) > 0:
+        return {"skipped": f"needs ~{need / 1e9:.0f} GB of HBM per rank; a rank has "
+                           f"{free / 1e9:.0f} GB free"}
+    ctx.set_option(_lib.RBL_OPT_KEEP_CSR, 0)
+    t0 = time.perf_counter()
+    ctx.gen_hashwindow(ra.n, ra.halfwidth, ra.density, ra.seed, plant)
+    gen_s = time.perf_counter() - t0
+    _, r0, r1, nnz_loc = ctx.matrix_info()
+    nloc = r1 - r0
+    nnz = allsum(nnz_loc)
+    K = args.c5_steps
+    meas = measure(ctx, ra, "hashwindow", K, 1, nloc, nnz_loc, world, barrier, allmax)
+    barrier()
+    ctx.synchronize()
+    ctx.reset_timers()
+    t0 = time.perf_counter()
+    D, V, info = rbl.lanczos(ctx, ra.k, ra.b, kryl_sz=ra.kryl, seed=ra.seed + 2, check=True,
+                             ritz=True, basis_bits=32)
+    ctx.synchronize()
+    barrier()
+    ttk_s = allmax(time.perf_counter() - t0)
+    return {"workload": "C5 hash-window SpMM-Lanczos, mixed precision (fp32 basis)",
+            "metric": f"RBL iters/sec, n={ra.n:.0e} nnz/row={nnz / ra.n:.0f} b={ra.b} fp32 basis",
+            "value": round(meas["value"], 3), "unit": "block iterations/s",
+            "steps": K, "warmup": 1, "ms_per_step": round(meas["elapsed"] / K * 1e3, 3),
+            "n": ra.n, "nnz": nnz, "b": ra.b, "k": ra.k, "keep_csr": 0,
             "nnz_per_rank": allgather_i64(nnz_loc),
             "roofline": meas["roofline"], "roofline_secondary": meas["roofline_secondary"],
             "stage_ms_per_run": {s_: round(v / K, 3) for s_, v in meas["stage"].items()},

@@ -186,6 +186,28 @@ void seg_tier_count(int64_t m, const int64_t* rowptr, const int32_t* col, const 
 void seg_tier_fill(int64_t m, const int64_t* rowptr, const int32_t* col, const double* val,
                    const uint8_t* tier_of, int ntiers, int64_t* const* trp, int32_t* const* tcol,
                    double* const* tval, hipStream_t s);
+// The same by a per-nonzero rule instead of tier_of[col] (TierRule: several ranks, the halo split
+// into pulled and pushed products — rbl_api.cpp prepare_tiers): local row r (global row0 + r),
+// column c: tier 0 if c is an own row; else tier 1 if c ranks above r — (deg[c], c) >
+// (deg[r], r), deg indexed by global id — (the rank pulls Q_c); else tier 2 (the owner of c
+// computes the product and pushes it).
+struct TierRule {
+  const int32_t* deg = nullptr;  // n entries (device); null: use tier_of
+  int64_t row0 = 0, r0 = 0, r1 = 0;
+};
+void seg_tier_count_rule(int64_t m, const int64_t* rowptr, const int32_t* col, TierRule rule,
+                         int32_t* cnt, hipStream_t s);
+void seg_tier_fill_rule(int64_t m, const int64_t* rowptr, const int32_t* col, const double* val,
+                        TierRule rule, int64_t* const* trp, int32_t* const* tcol,
+                        double* const* tval, hipStream_t s);
+// One tier as a plain CSR product: out[row] = sum_k val[k] Q[col[k] - col_off] (no epilogue),
+// b in {16, 32} — the pushed partial rows of the halo split.
+void spmm_seg_tier(const CsrDev::Tier& T, const double* Q, int64_t col_off, int b, double* out,
+                   hipStream_t s);
+// U[rows[i]] += sum_{k in [ptr[i], ptr[i+1])} recv[slot[k]] (slots in order: deterministic), b
+// columns — the received pushed partials added to their rows.
+void push_add(const int64_t* rows, const int64_t* ptr, const int64_t* slot, int64_t nrows,
+              const double* recv, int b, double* U, hipStream_t s);
 // spmm_window.hip: persistent LDS-window kernel (b in {16,32}); false if not applicable.
 bool spmm_window(const CsrDev& A, const double* Qin, int64_t col_off, int b, double* U,
                  const double* Qprev, const double* Bi, hipStream_t s);

@@ -83,6 +83,25 @@ struct rbl_ctx {
   const double* ghost_local = nullptr;  // the block the last exchange sent from
   bool ghost_active = false;          // the last exchange was the indexed one (use_ghost)
   bool halo_overlap = true;           // RBL_OPT_HALO_OVERLAP
+  // push/pull split of the indexed halo (RBL_OPT_HALO_PUSH): of every off-rank product
+  // A[r,c] Q[c] the rank holding the higher-ranked endpoint ((degree, id) order) does the work —
+  // it pulls Q[c] when c ranks higher (tier 1: the ghost slots), and when r ranks higher the
+  // owner of c computes A[c,r] Q[c] from its own rows and pushes the partial row r (the push
+  // tier, rows = ghost slots of that owner, columns = its own rows); received partials are
+  // added to U in peer order (d_ps_*)
+  int halo_push_opt = 2;              // 0 off, 1 on, 2 on when it moves fewer rows (default)
+  bool push = false;
+  SegTierBuf push_tier;
+  int64_t push_rows = 0;              // = n_ghost (rows of the push tier)
+  double* d_pushbuf = nullptr;        // n_ghost x b: pushed partial rows (per run)
+  double* d_precv = nullptr;          // n_send x b: partial rows received for own rows (per run)
+  int64_t* d_ps_rows = nullptr;       // own rows that receive partials, ascending
+  int64_t* d_ps_ptr = nullptr;        //   their slots in d_precv (peer order)
+  int64_t* d_ps_slot = nullptr;
+  int64_t n_ps_rows = 0;
+  size_t push_cap = 0;                // capacity (doubles) of d_pushbuf / d_precv
+  int64_t push_pred_rows = 0, pull_pred_rows = 0;  // rows per SpMM, summed over ranks (setup)
+  hipEvent_t ev_push_ready = nullptr, ev_push_done = nullptr;
   hipStream_t hstream = nullptr;      // the overlapped halo exchange
   hipEvent_t ev_qready = nullptr, ev_halo = nullptr;
   // dense A (RBL_gpu(A::Matrix{Float64})): local rows in 32-column row-major panels
@@ -399,6 +418,13 @@ void free_tiers(rbl_ctx* ctx) {
   hipFree(ctx->d_send_idx); ctx->d_send_idx = nullptr;
   ctx->ghost = false;
   ctx->n_ghost = ctx->n_send = 0;
+  free_seg(ctx->push_tier, true);
+  ctx->push = false;
+  ctx->push_rows = 0;
+  hipFree(ctx->d_ps_rows); ctx->d_ps_rows = nullptr;
+  hipFree(ctx->d_ps_ptr); ctx->d_ps_ptr = nullptr;
+  hipFree(ctx->d_ps_slot); ctx->d_ps_slot = nullptr;
+  ctx->n_ps_rows = 0;
 }
 
 int prepare_segments(rbl_ctx* ctx, const std::vector<int64_t>& rp) {
@@ -416,7 +442,8 @@ int prepare_segments(rbl_ctx* ctx, const std::vector<int64_t>& rp) {
   return st;
 }
 
-int build_tiers(rbl_ctx* ctx, const std::vector<uint8_t>& tier_of, int nt);
+int build_tiers(rbl_ctx* ctx, const std::vector<uint8_t>& tier_of, int nt,
+                const TierRule* rule = nullptr);
 
 // nonzeros of tier t (its row pointer's last entry)
 int64_t tier_nnz(rbl_ctx* ctx, int t) {
@@ -429,13 +456,13 @@ int64_t tier_nnz(rbl_ctx* ctx, int t) {
 // Indexed halo: the columns this rank references outside its rows become ghost slots (sorted by
 // global id, so grouped by owner); the ranks exchange how many rows, then which rows, each asks
 // of each; *d_map (device, n int32) maps a ghost column to its slot (caller frees).
-int build_ghosts(rbl_ctx* ctx, int32_t** d_map) {
+int build_ghosts(rbl_ctx* ctx, int32_t** d_map, const int32_t* cols, int64_t ncols) {
   const int P = ctx->nranks, me = ctx->rank;
   const int64_t n = ctx->n;
   uint8_t* d_mark = nullptr;
   HIPC(hipMalloc(&d_mark, std::max<int64_t>(n, 1)));
   HIPC(hipMemsetAsync(d_mark, 0, n, ctx->stream));
-  mark_cols(ctx->d_col, ctx->nnz, ctx->r0, ctx->r1, d_mark, ctx->stream);
+  mark_cols(cols, ncols, ctx->r0, ctx->r1, d_mark, ctx->stream);
   HIPC(hipGetLastError());
   std::vector<uint8_t> mark(n);
   HIPC(hipMemcpyAsync(mark.data(), d_mark, n, hipMemcpyDeviceToHost, ctx->stream));
@@ -499,6 +526,156 @@ int build_ghosts(rbl_ctx* ctx, int32_t** d_map) {
   return RBL_OK;
 }
 
+// Push/pull split of the indexed halo (several ranks, unbanded A).  Every off-rank product
+// A[r,c] Q[c] is done by the rank of the endpoint that ranks higher by (row degree, smaller id):
+// when c ranks higher the rank of r pulls Q[c] (tier 1, as in the pull-all halo), otherwise the
+// rank of c — which holds A[c,r] = A[r,c] in its own rows — forms it from its own Q rows and
+// pushes the partial row r (tier 2 is dropped: its products arrive pushed).  Hub rows (the
+// high-degree rows of a power-law graph, referenced from every rank) then stay home and only
+// their partials move, one row per (hub, rank) pair in each direction.  The push tier is tier
+// 1 transposed (rows: the ghost slots, columns: own rows), so ghosts pulled = partials pushed.
+// Returns 1 when set up, 0 when the pull-all halo is to be used — off (RBL_OPT_HALO_PUSH 0),
+// predicted to move more rows (automatic: used when 2 x ghosts(tier 1) < 0.85 x ghosts(all),
+// summed over ranks), or A not structurally symmetric by the per-pair entry counts — the
+// same answer on every rank; < 0 on error.  Collective.
+int prepare_push(rbl_ctx* ctx, const std::vector<int64_t>& rp) {
+  const int P = ctx->nranks;
+  const int64_t n = ctx->n, m = ctx->nloc;
+  // global row degrees: every rank's slice (padded to the longest) all-gathered
+  int64_t w = 1;
+  for (int q = 0; q < P; ++q) w = std::max(w, ctx->bounds[q + 1] - ctx->bounds[q]);
+  std::vector<int64_t> mine(w, 0), all((size_t)P * w);
+  for (int64_t r = 0; r < m && r + 1 < (int64_t)rp.size(); ++r) mine[r] = rp[r + 1] - rp[r];
+  COMMC(ctx->comm->allgather_host(mine.data(), all.data(), w, ctx->stream, &ctx->err));
+  std::vector<int32_t> deg(std::max<int64_t>(n, 1), 0);
+  for (int q = 0; q < P; ++q)
+    for (int64_t i = 0; i < ctx->bounds[q + 1] - ctx->bounds[q]; ++i)
+      deg[ctx->bounds[q] + i] = (int32_t)std::min<int64_t>(all[(size_t)q * w + i], INT32_MAX);
+  std::vector<int64_t>().swap(all);
+  DevBuf d_deg;
+  HIPC(hipMalloc(&d_deg.p, deg.size() * sizeof(int32_t)));
+  HIPC(hipMemcpy(d_deg.p, deg.data(), deg.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+  TierRule R;
+  R.deg = static_cast<const int32_t*>(d_deg.p);
+  R.row0 = ctx->r0;
+  R.r0 = ctx->r0;
+  R.r1 = ctx->r1;
+  CHK(build_tiers(ctx, {}, 3, &R));
+  // per peer: my tier-1 / tier-2 entries by the owner of their column, and the distinct
+  // columns of tier 1 (the ghosts with the split) and of tiers 1 + 2 (without)
+  const int64_t nz1 = m > 0 ? tier_nnz(ctx, 1) : 0, nz2 = m > 0 ? tier_nnz(ctx, 2) : 0;
+  std::vector<int32_t> c1(std::max<int64_t>(nz1, 1)), c2(std::max<int64_t>(nz2, 1));
+  if (nz1) HIPC(hipMemcpy(c1.data(), ctx->seg_tier[1].col, nz1 * sizeof(int32_t), hipMemcpyDeviceToHost));
+  if (nz2) HIPC(hipMemcpy(c2.data(), ctx->seg_tier[2].col, nz2 * sizeof(int32_t), hipMemcpyDeviceToHost));
+  std::vector<int64_t> vote(2 * P + 2, 0);  // [tier-1 by owner | tier-2 by owner | d1 | d12]
+  std::vector<uint8_t> mark(std::max<int64_t>(n, 1), 0);
+  auto owner = [&](int64_t c) {
+    return (int)(std::upper_bound(ctx->bounds.begin(), ctx->bounds.end(), c) - ctx->bounds.begin()) - 1;
+  };
+  for (int64_t k = 0; k < nz1; ++k) {
+    ++vote[owner(c1[k])];
+    if (!mark[c1[k]]) { mark[c1[k]] = 1; ++vote[2 * P]; }
+  }
+  for (int64_t k = 0; k < nz2; ++k) {
+    ++vote[P + owner(c2[k])];
+    if (!mark[c2[k]]) { mark[c2[k]] = 2; ++vote[2 * P + 1]; }
+  }
+  vote[2 * P + 1] += vote[2 * P];
+  std::vector<int32_t>().swap(c2);
+  std::vector<uint8_t>().swap(mark);
+  std::vector<int64_t> votes((size_t)P * (2 * P + 2));
+  COMMC(ctx->comm->allgather_host(vote.data(), votes.data(), 2 * P + 2, ctx->stream, &ctx->err));
+  bool sym = true;
+  int64_t d1 = 0, d12 = 0;
+  for (int p = 0; p < P; ++p) {
+    const int64_t* vp = votes.data() + (size_t)p * (2 * P + 2);
+    d1 += vp[2 * P];
+    d12 += vp[2 * P + 1];
+    for (int q = 0; q < P; ++q)  // p's tier-2 entries towards q are q's tier-1 entries towards p
+      if (vp[P + q] != votes[(size_t)q * (2 * P + 2) + p]) sym = false;
+  }
+  ctx->push_pred_rows = 2 * d1;
+  ctx->pull_pred_rows = d12;
+  if (!sym) {
+    if (ctx->halo_push_opt == 1)
+      return fail(ctx, RBL_ERR_INVALID, "RBL_OPT_HALO_PUSH: A is not structurally symmetric");
+    return 0;
+  }
+  if (ctx->halo_push_opt == 2 && !(2.0 * (double)d1 < 0.85 * (double)d12)) return 0;
+  // split: tier 2 dropped, the ghosts are tier 1's columns
+  free_seg(ctx->seg_tier[2], true);
+  ctx->seg_ntiers = 2;
+  int32_t* d_map = nullptr;
+  CHK(build_ghosts(ctx, &d_map, ctx->seg_tier[1].col, nz1));
+  if (nz1) remap_cols(ctx->seg_tier[1].col, nz1, d_map, ctx->stream);
+  HIPC(hipGetLastError());
+  HIPC(hipStreamSynchronize(ctx->stream));
+  hipFree(d_map);
+  ctx->seg_split = true;
+  ctx->ghost = true;
+  // the push tier: tier 1 transposed, rows = ghost slots (in row order within a slot)
+  const int64_t G = ctx->n_ghost;
+  std::vector<int64_t> rp1(m + 1, 0);
+  std::vector<double> v1(std::max<int64_t>(nz1, 1));
+  if (m > 0) HIPC(hipMemcpy(rp1.data(), ctx->seg_tier[1].rowptr, (m + 1) * sizeof(int64_t), hipMemcpyDeviceToHost));
+  if (nz1) {
+    HIPC(hipMemcpy(c1.data(), ctx->seg_tier[1].col, nz1 * sizeof(int32_t), hipMemcpyDeviceToHost));
+    HIPC(hipMemcpy(v1.data(), ctx->seg_tier[1].val, nz1 * sizeof(double), hipMemcpyDeviceToHost));
+  }
+  std::vector<int64_t> prp(G + 1, 0);
+  for (int64_t k = 0; k < nz1; ++k) ++prp[c1[k] + 1];
+  for (int64_t g = 0; g < G; ++g) prp[g + 1] += prp[g];
+  std::vector<int64_t> pos(prp.begin(), prp.end() - 1);
+  std::vector<int32_t> pc(std::max<int64_t>(nz1, 1));
+  std::vector<double> pv(std::max<int64_t>(nz1, 1));
+  for (int64_t r = 0; r < m; ++r)
+    for (int64_t k = rp1[r]; k < rp1[r + 1]; ++k) {
+      const int64_t at = pos[c1[k]]++;
+      pc[at] = (int32_t)(ctx->r0 + r);
+      pv[at] = v1[k];
+    }
+  auto& T = ctx->push_tier;
+  HIPC(hipMalloc(&T.rowptr, (G + 1) * sizeof(int64_t)));
+  HIPC(hipMalloc(&T.col, (nz1 + kCsrPad) * sizeof(int32_t)));
+  HIPC(hipMalloc(&T.val, (nz1 + kCsrPad) * sizeof(double)));
+  HIPC(hipMemset(T.col, 0, (nz1 + kCsrPad) * sizeof(int32_t)));
+  HIPC(hipMemset(T.val, 0, (nz1 + kCsrPad) * sizeof(double)));
+  HIPC(hipMemcpy(T.rowptr, prp.data(), (G + 1) * sizeof(int64_t), hipMemcpyHostToDevice));
+  if (nz1) {
+    HIPC(hipMemcpy(T.col, pc.data(), nz1 * sizeof(int32_t), hipMemcpyHostToDevice));
+    HIPC(hipMemcpy(T.val, pv.data(), nz1 * sizeof(double), hipMemcpyHostToDevice));
+  }
+  CHK(build_seg(ctx, prp, T));
+  ctx->push_rows = G;
+  // where the received partials go: the own rows asked for, each with its slots in peer order
+  const int64_t ns = ctx->n_send;
+  std::vector<int32_t> sidx(std::max<int64_t>(ns, 1));
+  if (ns) HIPC(hipMemcpy(sidx.data(), ctx->d_send_idx, ns * sizeof(int32_t), hipMemcpyDeviceToHost));
+  std::vector<int64_t> cnt(std::max<int64_t>(m, 1) + 1, 0);
+  for (int64_t k = 0; k < ns; ++k) ++cnt[sidx[k] + 1];
+  for (int64_t r = 0; r < m; ++r) cnt[r + 1] += cnt[r];
+  std::vector<int64_t> slot(std::max<int64_t>(ns, 1)), rows, ptr(1, 0);
+  {
+    std::vector<int64_t> at(cnt.begin(), cnt.end() - 1);
+    for (int64_t k = 0; k < ns; ++k) slot[at[sidx[k]]++] = k;
+  }
+  for (int64_t r = 0; r < m; ++r)
+    if (cnt[r + 1] > cnt[r]) {
+      rows.push_back(r);
+      ptr.push_back(cnt[r + 1]);
+    }
+  ctx->n_ps_rows = (int64_t)rows.size();
+  HIPC(hipMalloc(&ctx->d_ps_rows, std::max<size_t>(rows.size(), 1) * sizeof(int64_t)));
+  HIPC(hipMalloc(&ctx->d_ps_ptr, ptr.size() * sizeof(int64_t)));
+  HIPC(hipMalloc(&ctx->d_ps_slot, slot.size() * sizeof(int64_t)));
+  if (!rows.empty())
+    HIPC(hipMemcpy(ctx->d_ps_rows, rows.data(), rows.size() * sizeof(int64_t), hipMemcpyHostToDevice));
+  HIPC(hipMemcpy(ctx->d_ps_ptr, ptr.data(), ptr.size() * sizeof(int64_t), hipMemcpyHostToDevice));
+  HIPC(hipMemcpy(ctx->d_ps_slot, slot.data(), slot.size() * sizeof(int64_t), hipMemcpyHostToDevice));
+  ctx->push = true;
+  return 1;
+}
+
 // Column tiers of the segmented gather (RBL_SEG_TIERS="h[,w]": the h highest-degree columns,
 // then the next w, then the rest; one rank, A symmetric so a column's degree is its row's).
 // The SpMM sweeps the tiers in order; each sweep's gathers hit a Q-row set sized for one cache
@@ -508,6 +685,7 @@ int build_ghosts(rbl_ctx* ctx, int32_t** d_map) {
 // flight (step_impl); the sum order per row is the same with or without the overlap.
 int prepare_tiers(rbl_ctx* ctx, const std::vector<int64_t>& rp) {
   free_tiers(ctx);
+  ctx->push_pred_rows = ctx->pull_pred_rows = 0;
   if (ctx->nranks > 1) {
     // every rank must take the same branch (the setup below runs collectives), so the vote
     // comes before any per-rank condition: a rank with no rows or no nonzeros still takes
@@ -521,8 +699,14 @@ int prepare_tiers(rbl_ctx* ctx, const std::vector<int64_t>& rp) {
       if (v) return RBL_OK;  // a banded kernel runs: its halo is a few rows
     std::vector<uint8_t> tier_of(ctx->n, 1);
     for (int64_t c = ctx->r0; c < ctx->r1; ++c) tier_of[c] = 0;
+    if (ctx->halo_push_opt != 0) {  // the push/pull split, if it moves fewer rows (collective)
+      const int ps = prepare_push(ctx, rp);
+      if (ps < 0) return ps;
+      if (ps == 1) return RBL_OK;
+      free_tiers(ctx);
+    }
     int32_t* d_map = nullptr;
-    CHK(build_ghosts(ctx, &d_map));
+    CHK(build_ghosts(ctx, &d_map, ctx->d_col, ctx->nnz));
     const int st = build_tiers(ctx, tier_of, 2);
     if (st == RBL_OK) {
       remap_cols(ctx->seg_tier[1].col, ctx->seg_tier[1].ntasks > 0 ? tier_nnz(ctx, 1) : 0, d_map,
@@ -564,15 +748,20 @@ int prepare_tiers(rbl_ctx* ctx, const std::vector<int64_t>& rp) {
   return build_tiers(ctx, tier_of, nt);
 }
 
-// The tier CSRs and task tables for a column -> tier map (tier_of: n entries, < nt).
-int build_tiers(rbl_ctx* ctx, const std::vector<uint8_t>& tier_of, int nt) {
+// The tier CSRs and task tables for a column -> tier map (tier_of: n entries, < nt), or for
+// the per-nonzero rule of the push/pull halo split (rule, nt = 3).
+int build_tiers(rbl_ctx* ctx, const std::vector<uint8_t>& tier_of, int nt, const TierRule* rule) {
   const int64_t n = ctx->n, m = ctx->nloc;
   uint8_t* d_tier = nullptr;
   int32_t* d_cnt = nullptr;
-  HIPC(hipMalloc(&d_tier, n));
-  HIPC(hipMalloc(&d_cnt, (size_t)nt * m * sizeof(int32_t)));
-  HIPC(hipMemcpy(d_tier, tier_of.data(), n, hipMemcpyHostToDevice));
-  seg_tier_count(m, ctx->d_rowptr, ctx->d_col, d_tier, nt, d_cnt, ctx->stream);
+  HIPC(hipMalloc(&d_tier, rule ? 1 : n));
+  HIPC(hipMalloc(&d_cnt, std::max<size_t>((size_t)nt * m, 1) * sizeof(int32_t)));
+  if (rule)
+    seg_tier_count_rule(m, ctx->d_rowptr, ctx->d_col, *rule, d_cnt, ctx->stream);
+  else {
+    HIPC(hipMemcpy(d_tier, tier_of.data(), n, hipMemcpyHostToDevice));
+    seg_tier_count(m, ctx->d_rowptr, ctx->d_col, d_tier, nt, d_cnt, ctx->stream);
+  }
   HIPC(hipGetLastError());
   std::vector<int32_t> cnt((size_t)nt * m);
   HIPC(hipMemcpyAsync(cnt.data(), d_cnt, cnt.size() * sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
@@ -596,7 +785,10 @@ int build_tiers(rbl_ctx* ctx, const std::vector<uint8_t>& tier_of, int nt) {
     valp[t] = T.val;
   }
   ctx->seg_ntiers = nt;  // (free_tiers releases partial state on a later failure)
-  seg_tier_fill(m, ctx->d_rowptr, ctx->d_col, ctx->d_val, d_tier, nt, rpp, colp, valp, ctx->stream);
+  if (rule)
+    seg_tier_fill_rule(m, ctx->d_rowptr, ctx->d_col, ctx->d_val, *rule, rpp, colp, valp, ctx->stream);
+  else
+    seg_tier_fill(m, ctx->d_rowptr, ctx->d_col, ctx->d_val, d_tier, nt, rpp, colp, valp, ctx->stream);
   HIPC(hipGetLastError());
   HIPC(hipStreamSynchronize(ctx->stream));
   hipFree(d_tier);
@@ -1508,6 +1700,77 @@ int halo_exchange32(rbl_ctx* ctx, const float* Q, const float** Qin, int64_t* of
   return RBL_OK;
 }
 
+// ---- the pushed half of the split halo (prepare_push) ----
+bool push_on(const rbl_ctx* ctx) { return ctx->push && ctx->ghost_active && ctx->nranks > 1; }
+
+int ensure_push(rbl_ctx* ctx, int b) {
+  const size_t need = (size_t)std::max<int64_t>(std::max(ctx->push_rows, ctx->n_send), 1) * b;
+  if (ctx->d_pushbuf && ctx->push_cap >= need) return RBL_OK;
+  HIPC(hipStreamSynchronize(ctx->stream));
+  if (ctx->hstream) HIPC(hipStreamSynchronize(ctx->hstream));
+  hipFree(ctx->d_pushbuf); ctx->d_pushbuf = nullptr;
+  hipFree(ctx->d_precv); ctx->d_precv = nullptr;
+  ctx->push_cap = 0;
+  HIPC(hipMalloc(&ctx->d_pushbuf, need * sizeof(double)));
+  HIPC(hipMalloc(&ctx->d_precv, need * sizeof(double)));
+  ctx->push_cap = need;
+  return RBL_OK;
+}
+
+// partial rows for the peers' ghost slots from the own rows of Q (n_local x b)
+int push_products(rbl_ctx* ctx, const double* Q, int b, hipStream_t st) {
+  StageScope t(ctx, RBL_STAGE_AQ, st);
+  CHK(ensure_push(ctx, b));
+  const auto& P = ctx->push_tier;
+  CsrDev::Tier T;
+  T.rowptr = P.rowptr;
+  T.col = P.col;
+  T.val = P.val;
+  T.ntasks = P.ntasks;
+  T.nlong = P.nlong;
+  T.trow = P.trow;
+  T.tinfo = P.tinfo;
+  T.slot_k0 = P.slot_k0;
+  T.lrow = P.lrow;
+  T.lslot = P.lslot;
+  T.scratch = P.scratch;
+  spmm_seg_tier(T, Q, ctx->r0, b, ctx->d_pushbuf, st);
+  HIPC(hipGetLastError());
+  return RBL_OK;
+}
+
+// partials out to the owners of the ghost slots, in from the peers for the rows they asked for
+// (the reverse of halo_exchange's directions and counts)
+int push_exchange(rbl_ctx* ctx, int b, hipStream_t st) {
+  StageScope t(ctx, RBL_STAGE_COMM, st);
+  std::vector<Comm::Xfer> x(ctx->nranks);
+  for (int q = 0; q < ctx->nranks; ++q) {
+    if (q == ctx->rank) continue;
+    x[q].send = ctx->d_pushbuf + ctx->ghost_off[q] * b;
+    x[q].nsend = (size_t)ctx->ghost_cnt[q] * b;
+    x[q].recv = ctx->d_precv + ctx->send_off[q] * b;
+    x[q].nrecv = (size_t)ctx->send_cnt[q] * b;
+  }
+  COMMC(ctx->comm->exchange(x, st, &ctx->err));
+  count_exchange(ctx, x);
+  return RBL_OK;
+}
+
+int push_finish(rbl_ctx* ctx, double* U, int b, hipStream_t st) {
+  StageScope t(ctx, RBL_STAGE_AQ, st);
+  push_add(ctx->d_ps_rows, ctx->d_ps_ptr, ctx->d_ps_slot, ctx->n_ps_rows, ctx->d_precv, b, U, st);
+  HIPC(hipGetLastError());
+  return RBL_OK;
+}
+
+// the whole pushed half on one stream, after apply_A: products, exchange, add
+int push_halo(rbl_ctx* ctx, const double* Q, int b, double* U) {
+  if (!push_on(ctx)) return RBL_OK;
+  CHK(push_products(ctx, Q, b, ctx->stream));
+  CHK(push_exchange(ctx, b, ctx->stream));
+  return push_finish(ctx, U, b, ctx->stream);
+}
+
 void free_run(rbl_ctx* ctx) {
   if (ctx->cstream) hipStreamSynchronize(ctx->cstream);
   hipFree(ctx->d_basis); ctx->d_basis = nullptr;
@@ -1526,6 +1789,10 @@ void free_run(rbl_ctx* ctx) {
   hipFree(ctx->d_T); ctx->d_T = nullptr;
   hipFree(ctx->d_qext); ctx->d_qext = nullptr; ctx->qext_cap = 0;
   hipFree(ctx->d_sendbuf); ctx->d_sendbuf = nullptr;
+  if (ctx->hstream) hipStreamSynchronize(ctx->hstream);
+  hipFree(ctx->d_pushbuf); ctx->d_pushbuf = nullptr;
+  hipFree(ctx->d_precv); ctx->d_precv = nullptr;
+  ctx->push_cap = 0;
   hipFree(ctx->d_slab); ctx->d_slab = nullptr;
   hipFree(ctx->d_C); ctx->d_C = nullptr;
   hipFree(ctx->d_small); ctx->d_small = nullptr;
@@ -1831,6 +2098,8 @@ int rbl_free(rbl_ctx* ctx) {
   if (ctx->stream) hipStreamDestroy(ctx->stream);
   if (ctx->cstream) hipStreamDestroy(ctx->cstream);
   if (ctx->hstream) hipStreamDestroy(ctx->hstream);
+  if (ctx->ev_push_ready) hipEventDestroy(ctx->ev_push_ready);
+  if (ctx->ev_push_done) hipEventDestroy(ctx->ev_push_done);
   for (hipEvent_t e : {ctx->ev_fin, ctx->ev_d2h[0], ctx->ev_d2h[1], ctx->ev_d2h_slot[0],
                        ctx->ev_d2h_slot[1], ctx->ev_qready, ctx->ev_halo})
     if (e) hipEventDestroy(e);
@@ -1841,6 +2110,16 @@ int rbl_free(rbl_ctx* ctx) {
 }
 
 const char* rbl_last_error(const rbl_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int rbl_device_memory(rbl_ctx* ctx, int64_t* free_bytes, int64_t* total_bytes) {
+  if (!ctx || !free_bytes || !total_bytes) return RBL_ERR_INVALID;
+  HIPC(hipSetDevice(ctx->device));
+  size_t fr = 0, tot = 0;
+  HIPC(hipMemGetInfo(&fr, &tot));
+  *free_bytes = (int64_t)fr;
+  *total_bytes = (int64_t)tot;
+  return RBL_OK;
+}
 
 int rbl_comm_info(rbl_ctx* ctx, int* nranks, int* rank, char* transport, int transport_len) {
   if (!ctx || !nranks || !rank) return RBL_ERR_INVALID;
@@ -1881,6 +2160,10 @@ int rbl_set_option(rbl_ctx* ctx, int option, int64_t value) {
       return RBL_OK;
     case RBL_OPT_SPLIT_HALO: ctx->split_halo = value != 0; return RBL_OK;
     case RBL_OPT_HALO_OVERLAP: ctx->halo_overlap = value != 0; return RBL_OK;
+    case RBL_OPT_HALO_PUSH:
+      if (value < 0 || value > 2) return fail(ctx, RBL_ERR_INVALID, "RBL_OPT_HALO_PUSH must be 0|1|2");
+      ctx->halo_push_opt = (int)value;
+      return RBL_OK;
     case RBL_OPT_KEEP_CSR: ctx->keep_csr = value != 0; return RBL_OK;
     case RBL_OPT_RELABEL:
       if (value < 0 || value > 1) return fail(ctx, RBL_ERR_INVALID, "RBL_OPT_RELABEL must be 0|1");
@@ -2270,6 +2553,7 @@ int rbl_apply(rbl_ctx* ctx, int b, const double* X, double* Y) {
     if (st < 0) return st;
   }
   HIPC(hipGetLastError());
+  CHK(push_halo(ctx, xr.d(), b, y.d()));
   rowmajor_to_colmajor(y.d(), ctx->nloc, b, x.d(), ctx->stream);
   HIPC(hipMemcpyAsync(Y, x.p, ctx->nloc * b * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
   HIPC(hipStreamSynchronize(ctx->stream));
@@ -2417,6 +2701,7 @@ int rbl_start(rbl_ctx* ctx, int b, int max_blocks, int basis_bits, const double*
     CHK(apply_A(ctx, Qin, off, b, ctx->d_U, nullptr, nullptr, nullptr));
     HIPC(hipGetLastError());
   }
+  CHK(push_halo(ctx, ctx->d_T, b, ctx->d_U));
   if (basis_bits == 64) {
     CHK(tsqr(ctx, ctx->d_U, slotp(ctx, 0)));
   } else {  // step 1 multiplies the unrounded fp64 Q_1 (RBL_gpu.jl:142, 152); the basis holds fp32
@@ -2600,6 +2885,7 @@ int step_impl(rbl_ctx* ctx, int i, int part_reorth, double* A_out, double* B_out
   ctx->cloc_final = false;
   // U = A Q_i - Q_{i-1} B_i^T   (RBL_gpu.jl:176-177)
   int ai_parts = 0;
+  bool pushed = false;  // the push/pull split's partials sent on the side stream
   {
     const double* Qin = nullptr;
     const float* Qin32 = nullptr;
@@ -2626,6 +2912,18 @@ int step_impl(rbl_ctx* ctx, int i, int part_reorth, double* A_out, double* B_out
       CHK(halo_exchange(ctx, Qi, &Qin, &off, false, ctx->hstream));
       HIPC(hipEventRecord(ctx->ev_halo, ctx->hstream));
       halo_ev = ctx->ev_halo;
+      if (push_on(ctx)) {  // the partials go out behind the pulled rows, before the SpMM
+        if (!ctx->ev_push_ready) {
+          HIPC(hipEventCreateWithFlags(&ctx->ev_push_ready, hipEventDisableTiming));
+          HIPC(hipEventCreateWithFlags(&ctx->ev_push_done, hipEventDisableTiming));
+        }
+        CHK(push_products(ctx, Qi, b, ctx->stream));
+        HIPC(hipEventRecord(ctx->ev_push_ready, ctx->stream));
+        HIPC(hipStreamWaitEvent(ctx->hstream, ctx->ev_push_ready, 0));
+        CHK(push_exchange(ctx, b, ctx->hstream));
+        HIPC(hipEventRecord(ctx->ev_push_done, ctx->hstream));
+        pushed = true;
+      }
     } else if (direct32) {
       CHK(halo_exchange32(ctx, Qi32, &Qin32, &off, !split));
     } else {
@@ -2649,6 +2947,13 @@ int step_impl(rbl_ctx* ctx, int i, int part_reorth, double* A_out, double* B_out
     }
     if (ai_parts < 0) return ai_parts;
     HIPC(hipGetLastError());
+  }
+  // the push/pull split: the received partials into U (A_i is formed after this, from all of U)
+  if (pushed) {
+    HIPC(hipStreamWaitEvent(ctx->stream, ctx->ev_push_done, 0));
+    CHK(push_finish(ctx, ctx->d_U, b, ctx->stream));
+  } else if (!direct32 && ai_parts == 0) {
+    CHK(push_halo(ctx, Qi, b, ctx->d_U));
   }
   // A_i = Q_i^T U ; U -= Q_i A_i   (RBL_gpu.jl:178-179); fused: the update pass also forms
   // U^T U, CholQR's first Gram
@@ -2922,7 +3227,11 @@ int rbl_timers(rbl_ctx* ctx, double* ms, int nstages) {
 int rbl_comm_stats(rbl_ctx* ctx, int64_t* out, int nstats, int reset) {
   if (!ctx || nstats < 0 || (nstats > 0 && !out)) return RBL_ERR_INVALID;
   for (int i = 0; i < nstats && i < RBL_COMM_NSTATS; ++i) out[i] = ctx->comm_stats[i];
-  for (int i = RBL_COMM_NSTATS; i < nstats; ++i) out[i] = 0;
+  // the halo plan of the matrix held (not counters: reset leaves them)
+  if (nstats > RBL_COMM_HALO_PUSH) out[RBL_COMM_HALO_PUSH] = ctx->push ? 1 : 0;
+  if (nstats > RBL_COMM_PUSH_ROWS) out[RBL_COMM_PUSH_ROWS] = ctx->push_pred_rows;
+  if (nstats > RBL_COMM_PULL_ROWS) out[RBL_COMM_PULL_ROWS] = ctx->pull_pred_rows;
+  for (int i = RBL_COMM_PULL_ROWS + 1; i < nstats; ++i) out[i] = 0;
   if (reset)
     for (int64_t& v : ctx->comm_stats) v = 0;
   return RBL_OK;

@@ -340,6 +340,80 @@ void seg_tier_fill(int64_t m, const int64_t* rowptr, const int32_t* col, const d
                      rowptr, col, val, tier_of, tp);
 }
 
+__device__ inline int tier_rule(const TierRule& R, int64_t r, int64_t c) {
+  if (c >= R.r0 && c < R.r1) return 0;
+  const int dc = R.deg[c], dr = R.deg[r];
+  return (dc > dr || (dc == dr && c < r)) ? 1 : 2;
+}
+__global__ void k_seg_tier_count_rule(int64_t m, const int64_t* __restrict__ rowptr,
+                                      const int32_t* __restrict__ col, TierRule R,
+                                      int32_t* __restrict__ cnt) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= m) return;
+  int c3[kMaxSegTiers] = {0, 0, 0};
+  for (int64_t k = rowptr[r]; k < rowptr[r + 1]; ++k) ++c3[tier_rule(R, R.row0 + r, col[k])];
+  for (int t = 0; t < kMaxSegTiers; ++t) cnt[t * m + r] = c3[t];
+}
+__global__ void k_seg_tier_fill_rule(int64_t m, const int64_t* __restrict__ rowptr,
+                                     const int32_t* __restrict__ col, const double* __restrict__ val,
+                                     TierRule R, TierPtrs tp) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= m) return;
+  int64_t pos[kMaxSegTiers];
+  for (int t = 0; t < kMaxSegTiers; ++t) pos[t] = tp.rp[t] ? tp.rp[t][r] : 0;
+  for (int64_t k = rowptr[r]; k < rowptr[r + 1]; ++k) {
+    const int c = col[k];
+    const int t = tier_rule(R, R.row0 + r, c);
+    tp.col[t][pos[t]] = c;
+    tp.val[t][pos[t]] = val[k];
+    ++pos[t];
+  }
+}
+void seg_tier_count_rule(int64_t m, const int64_t* rowptr, const int32_t* col, TierRule rule,
+                         int32_t* cnt, hipStream_t s) {
+  if (m <= 0) return;
+  hipLaunchKernelGGL(k_seg_tier_count_rule, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, m,
+                     rowptr, col, rule, cnt);
+}
+void seg_tier_fill_rule(int64_t m, const int64_t* rowptr, const int32_t* col, const double* val,
+                        TierRule rule, int64_t* const* trp, int32_t* const* tcol,
+                        double* const* tval, hipStream_t s) {
+  if (m <= 0) return;
+  TierPtrs tp;
+  for (int t = 0; t < kMaxSegTiers; ++t) {
+    tp.rp[t] = trp[t];
+    tp.col[t] = tcol[t];
+    tp.val[t] = tval[t];
+  }
+  hipLaunchKernelGGL(k_seg_tier_fill_rule, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, s, m,
+                     rowptr, col, val, rule, tp);
+}
+
+void spmm_seg_tier(const CsrDev::Tier& T, const double* Q, int64_t col_off, int b, double* out,
+                   hipStream_t s) {
+  if (b == 32) launch_seg<32>(T, Q, col_off, out, nullptr, nullptr, false, s);
+  else launch_seg<16>(T, Q, col_off, out, nullptr, nullptr, false, s);
+}
+
+// one lane group (b lanes) per row with received partials; lane c sums column c in slot order
+__global__ void k_push_add(const int64_t* __restrict__ rows, const int64_t* __restrict__ ptr,
+                           const int64_t* __restrict__ slot, int64_t nrows,
+                           const double* __restrict__ recv, int b, double* __restrict__ U) {
+  const int64_t g = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / b;
+  const int c = (int)(threadIdx.x % b);
+  if (g >= nrows) return;
+  double acc = 0.0;
+  for (int64_t k = ptr[g]; k < ptr[g + 1]; ++k) acc += recv[slot[k] * b + c];
+  U[rows[g] * b + c] += acc;
+}
+void push_add(const int64_t* rows, const int64_t* ptr, const int64_t* slot, int64_t nrows,
+              const double* recv, int b, double* U, hipStream_t s) {
+  if (nrows <= 0) return;
+  const int64_t th = nrows * b;
+  hipLaunchKernelGGL(k_push_add, dim3((unsigned)((th + 255) / 256)), dim3(256), 0, s, rows, ptr,
+                     slot, nrows, recv, b, U);
+}
+
 bool spmm_seg_ok(const CsrDev& A, int b) { return A.seg_ntasks > 0 && (b == 16 || b == 32); }
 
 template <int BP>

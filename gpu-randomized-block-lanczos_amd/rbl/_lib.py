@@ -33,6 +33,7 @@ RBL_OPT_KEEP_CSR = 5
 RBL_OPT_FUSE = 6
 RBL_OPT_HALO_OVERLAP = 7
 RBL_OPT_RELABEL = 8
+RBL_OPT_HALO_PUSH = 9
 
 _p = C.c_void_p
 _i64 = C.c_int64
@@ -56,6 +57,7 @@ SIGNATURES = {
     "rbl_last_error": (C.c_char_p, [_p]),
     "rbl_comm_info": (C.c_int, [_p, C.POINTER(C.c_int), C.POINTER(C.c_int), C.c_char_p, C.c_int]),
     "rbl_set_option": (C.c_int, [_p, C.c_int, _i64]),
+    "rbl_device_memory": (C.c_int, [_p, _pi64, _pi64]),
     "rbl_set_matrix_csc": (C.c_int, [_p, _i64, _i64, _pi64, _pi64, _pd, C.c_int]),
     "rbl_set_matrix_csr_rows": (C.c_int, [_p, _i64, _i64, _i64, _pi64, _pi64, _pd, C.c_int]),
     "rbl_set_matrix_dense": (C.c_int, [_p, _i64, _i64, _i64, _pd, _i64]),

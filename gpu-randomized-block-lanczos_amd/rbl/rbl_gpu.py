@@ -294,6 +294,12 @@ class Context:
     def reset_timers(self) -> None:
         self._check(lib.rbl_reset_timers(self._h), "rbl_reset_timers")
 
+    def device_memory(self) -> tuple:
+        """(free, total) bytes of the context's GPU (rbl_device_memory)."""
+        f, t = np.zeros(1, np.int64), np.zeros(1, np.int64)
+        self._check(lib.rbl_device_memory(self._h, i64ptr(f), i64ptr(t)), "rbl_device_memory")
+        return int(f[0]), int(t[0])
+
     def comm_info(self) -> dict:
         """Ranks as the transport counts them (RCCL: ncclCommCount), this rank, transport name."""
         import ctypes as C
@@ -304,11 +310,14 @@ class Context:
 
     def comm_stats(self, reset: bool = False) -> dict:
         """Collectives this rank issued since the last reset (rbl_comm_stats): all-reduce
-        calls / bytes, halo exchanges, bytes sent / received."""
-        out = np.zeros(5, np.int64)
-        self._check(lib.rbl_comm_stats(self._h, i64ptr(out), 5, int(reset)), "rbl_comm_stats")
+        calls / bytes, halo exchanges, bytes sent / received; and the halo plan of the matrix
+        held (not reset): halo_push (the push/pull split runs, RBL_OPT_HALO_PUSH) and the Q rows
+        per SpMM summed over ranks its setup predicted with the split / with the pull-all halo."""
+        out = np.zeros(8, np.int64)
+        self._check(lib.rbl_comm_stats(self._h, i64ptr(out), 8, int(reset)), "rbl_comm_stats")
         return dict(zip(("allreduce_calls", "allreduce_bytes", "exchange_calls", "send_bytes",
-                         "recv_bytes"), (int(x) for x in out)))
+                         "recv_bytes", "halo_push", "push_rows_pred", "pull_rows_pred"),
+                        (int(x) for x in out)))
 
     def synchronize(self) -> None:
         self._check(lib.rbl_synchronize(self._h), "rbl_synchronize")

@@ -118,6 +118,18 @@ extern "C" {
                                    * each local row's original id (a caller's omega and V rows are
                                    * in that order).  0 (default): A as drawn.                  */
 
+#define RBL_OPT_HALO_PUSH     9   /* several ranks, unbanded A (the indexed halo of the segmented
+                                   * gather), read when the matrix is set: each off-rank product
+                                   * A[r,c] Q[c] is formed on the rank of the endpoint with the
+                                   * larger (row degree, smaller id) — pulled Q[c] when that is c,
+                                   * else computed by c's owner and its partial row pushed — so
+                                   * the high-degree rows every rank references stay home and
+                                   * only their partial rows move.  Needs A structurally
+                                   * symmetric (checked from per-pair entry counts).  2 (default)
+                                   * when its setup predicts fewer moved rows than pulling every
+                                   * referenced row (< 0.85x); 1 always; 0 never.  Results differ
+                                   * from the pull-all halo only in the order of each row's sum. */
+
 typedef struct rbl_ctx rbl_ctx;
 
 int rbl_abi_version(void);
@@ -158,6 +170,9 @@ const char* rbl_last_error(const rbl_ctx* ctx);
  * one rank: 1, transport "none"), this context's rank, and the transport's name. */
 int rbl_comm_info(rbl_ctx* ctx, int* nranks, int* rank, char* transport, int transport_len);
 int rbl_set_option(rbl_ctx* ctx, int option, int64_t value);
+/* Free and total HBM of the context's device (hipMemGetInfo): what a caller checks before it
+ * sizes a run (the reference sizes its buffer from CUDA.available_memory, RBL_gpu.jl:95-104). */
+int rbl_device_memory(rbl_ctx* ctx, int64_t* free_bytes, int64_t* total_bytes);
 
 /* ---- matrix --------------------------------------------------------------------------
  * Replaces `Ag = adapt(CuArray, A)` (RBL_gpu.jl:209).  A is symmetric, so the CSC arrays
@@ -300,6 +315,13 @@ int rbl_synchronize(rbl_ctx* ctx);
 #define RBL_COMM_SEND_BYTES      3
 #define RBL_COMM_RECV_BYTES      4
 #define RBL_COMM_NSTATS          5
+/* the halo plan of the matrix held (set by rbl_set_matrix_* / the generators; reset keeps them):
+ * RBL_COMM_HALO_PUSH 1 when the push/pull split runs (RBL_OPT_HALO_PUSH), and the Q rows per
+ * SpMM summed over ranks that its setup predicted with the split (pulled + pushed) and with
+ * the pull-all halo (0 on one rank or a banded A) */
+#define RBL_COMM_HALO_PUSH       5
+#define RBL_COMM_PUSH_ROWS       6
+#define RBL_COMM_PULL_ROWS       7
 int rbl_comm_stats(rbl_ctx* ctx, int64_t* out, int nstats, int reset);
 
 /* ---- host-only planning (callable without a GPU) -------------------------------------- */

@@ -34,6 +34,8 @@ def run_case(rbl, ctx, c):
     from rbl import _lib
     k, b = c.get("k", 10), c["b"]
     omega = None
+    # read when the matrix is set: the push/pull split of the indexed halo (2: automatic)
+    ctx.set_option(_lib.RBL_OPT_HALO_PUSH, c.get("push", 2))
     if c.get("golden"):
         cfg = golden_cfg(c["golden"])
         k, b = cfg["k"], cfg["b"]
@@ -66,7 +68,8 @@ def run_case(rbl, ctx, c):
            "iters": info.iters, "converged": info.converged, "r0": r0, "r1": r1, "nnz": nnz,
            "kid": kid, "comm": np.array([comm[x] for x in ("allreduce_calls", "allreduce_bytes",
                                                             "exchange_calls", "send_bytes",
-                                                            "recv_bytes")])}
+                                                            "recv_bytes", "halo_push",
+                                                            "push_rows_pred", "pull_rows_pred")])}
     if V is not None:
         out["V"] = V
     return out

@@ -15,6 +15,9 @@ Checks, per world size 2 and 4:
     partition, kernels and rank-order sums — so the process boundary changes nothing);
   * the single-rank run within 1e-10 relative per step (fp64; 1e-5 for the fp32 basis) —
     the partitioned sums only reorder additions;
+  * the push/pull split of the indexed halo (RBL_OPT_HALO_PUSH 1, with and without the side
+    stream) and the pull-all halo (0): the moved-row counts its setup predicted are the rows
+    the exchanges moved;
   * BASELINE config 4 (R-MAT, n = 1e6) and config 3's shape against the oracle fixtures
     golden_c4b / golden_c3: same step count, eigenvalues < 1e-10.
 """
@@ -41,6 +44,9 @@ CASES = [
      "steps": 10, "bits": 32},
     {"name": "rmat", **RM, "b": 32, "steps": 10},                    # indexed halo + overlap
     {"name": "rmat_seq", **RM, "b": 32, "steps": 10, "overlap": 0},  # exchange before the SpMM
+    {"name": "rmat_pull", **RM, "b": 32, "steps": 10, "push": 0},     # pull-all indexed halo
+    {"name": "rmat_push", **RM, "b": 32, "steps": 10, "push": 1},     # push/pull split
+    {"name": "rmat_push_seq", **RM, "b": 16, "steps": 10, "push": 1, "overlap": 0},
     {"name": "rmat32", **RM, "b": 32, "steps": 10, "bits": 32},
     {"name": "rmat_b8", **RM, "b": 8, "steps": 8},                    # range halo, ghost-built
     {"name": "rmat_gather", **RM, "b": 32, "steps": 6, "spmm_kernel": 1},
@@ -142,6 +148,12 @@ def test_ranks_agree_and_match_inprocess_and_single(procs, single, inproc, case)
         assert kid == 6  # segmented gather with the indexed halo
     if case in ("rmat_b8", "rmat_gather"):
         assert kid == 1  # plain gather over the range halo of a ghost-built context
+    if c.get("push") is not None:  # the halo plan asked for, with its moved-row count exact
+        for cm in comm:
+            assert cm[5] == c["push"]
+        rows = sum(int(cm[4]) for cm in comm) // ((c["steps"] + 1) * c["b"] * 8)
+        assert rows == int(comm[0][6 if c["push"] else 7])
+        assert all(cm[2] == (c["steps"] + 1) * (2 if c["push"] else 1) for cm in comm)
 
 
 @pytest.mark.parametrize("case", ["c4b", "c3"])

@@ -156,6 +156,7 @@ def test_rmat_multirank_halo_overlap_bit_identical(rbl, P):
     def run(overlap):
         def fn(ctx, r):
             ctx.set_option(_lib.RBL_OPT_HALO_OVERLAP, overlap)
+            ctx.set_option(_lib.RBL_OPT_HALO_PUSH, 0)   # the pull-all halo (counted below)
             ctx.gen_rmat(CASE["n"], CASE["scale"], CASE["edges"], CASE["seed"], plant)
             _, r0, r1, _ = ctx.matrix_info()
             _, col, _ = ctx.get_matrix_csr()
@@ -289,6 +290,7 @@ def test_rmat_relabel_balances_the_halo(rbl):
         for rl in (0, 1):
             def fn(ctx, r):
                 ctx.set_option(_lib.RBL_OPT_RELABEL, rl)
+                ctx.set_option(_lib.RBL_OPT_HALO_PUSH, 0)   # the pull-all halo's balance
                 ctx.gen_rmat(n, scale, edges, seed, plant)
                 ctx.comm_stats(reset=True)
                 _, _, info = rbl.lanczos(ctx, 5, 32, seed=9, check=False, max_steps=4, trace=True,
@@ -338,38 +340,53 @@ def test_rmat_multirank_range_halo_beside_ghosts(rbl, b, kernel):
     assert np.all(np.abs(Y - A @ X) <= bound)
 
 
+def _scattered(n, live, seed=6):
+    """A symmetric scattered pattern on the first `live` rows (~30 nonzeros per row, no band,
+    no window fit: every SpMM format votes unbanded) and empty rows after them."""
+    import scipy.sparse as sp
+    rng = np.random.default_rng(seed)
+    R = sp.random(live, live, density=15 / live, random_state=seed, format="csr")
+    R = R + R.T + sp.diags(rng.uniform(1, 2, live))
+    M = sp.block_diag([R, sp.csr_matrix((n - live, n - live))]).tocsr()
+    M.sort_indices()
+    return M
+
+
 def test_unbanded_ranks_without_rows_or_nonzeros(rbl):
     """The setup collectives when some ranks hold nothing: an unbanded (scattered) user CSR on 4
     ranks whose caller-given row split leaves two ranks with rows but no nonzeros, and a matrix
     with n < P that leaves a rank without rows.  Every rank takes part in the banded vote and
-    the ghost exchange; the traces equal the single-rank run's."""
+    the ghost exchange (the pull-all indexed halo here); the traces equal the single-rank run's."""
     import scipy.sparse as sp
+    from rbl import _lib
     rng = np.random.default_rng(5)
-    n, live = 400, 300
-    R = sp.random(live, live, density=0.05, random_state=6, format="csr")
-    R = R + R.T + sp.diags(rng.uniform(1, 2, live))
-    M = sp.block_diag([R, sp.csr_matrix((n - live, n - live))]).tocsr()
-    M.sort_indices()
+    n, live = 4000, 3000
+    M = _scattered(n, live)
     omega = rng.standard_normal((n, 16))
     with rbl.Context(0) as ctx:
         ctx.set_matrix(M)
         _, _, ref = rbl.lanczos(ctx, 3, 16, omega=omega, check=False, max_steps=5, trace=True,
                                 ritz=False)
-    bounds = [0, 150, 300, 350, 400]
+    bounds = [0, 1500, 3000, 3500, 4000]
 
     def fn(ctx, r):
         r0, r1 = bounds[r], bounds[r + 1]
         S = M[r0:r1]
+        ctx.set_option(_lib.RBL_OPT_HALO_PUSH, 0)
         ctx.set_matrix_rows(n, r0, r1, S.indptr, S.indices, S.data)
         _, _, _, nnz = ctx.matrix_info()
+        ctx.comm_stats(reset=True)
         _, _, info = rbl.lanczos(ctx, 3, 16, omega=omega[r0:r1], check=False, max_steps=5,
                                  trace=True, ritz=False)
-        return info, nnz, ctx.spmm_kernel_for(16)
+        return info, nnz, ctx.spmm_kernel_for(16), ctx.comm_stats()
 
     out = run_ranks(rbl, 4, fn)
-    assert [nnz == 0 for _, nnz, _ in out] == [False, False, True, True]
+    assert [nnz == 0 for _, nnz, _, _ in out] == [False, False, True, True]
     assert out[0][2] == 6       # the segmented gather with the indexed halo on the live ranks
-    for info, _, _ in out:
+    # the unbanded vote held on every rank: the indexed halo moves the referenced rows only
+    assert out[0][3]["pull_rows_pred"] > 0
+    assert sum(st["recv_bytes"] for *_, st in out) == 6 * out[0][3]["pull_rows_pred"] * 16 * 8
+    for info, _, _, _ in out:
         for a, a1 in zip(info.trace_A, ref.trace_A):
             assert np.abs(a - a1).max() <= 1e-9 * np.abs(a1).max()
 
@@ -392,3 +409,160 @@ def test_unbanded_ranks_without_rows_or_nonzeros(rbl):
     assert any(m == 0 for _, m in out)
     for info, _ in out:
         assert np.abs(info.trace_A[0] - ref.trace_A[0]).max() <= 1e-12 * np.abs(ref.trace_A[0]).max()
+
+
+def _push_plan(A, bounds):
+    """The push/pull split's moved rows per SpMM (summed over ranks) restated from the full CSR:
+    rank p pulls the off-rank columns c of its rows r with (deg c, -c) > (deg r, -r) and pushes
+    as many partial rows; the pull-all halo moves every distinct off-rank column."""
+    deg = np.diff(A.indptr)
+    push = pull = 0
+    for r0, r1 in zip(bounds[:-1], bounds[1:]):
+        S = A[r0:r1].tocoo()
+        rows, cols = S.row + r0, S.col
+        off = (cols < r0) | (cols >= r1)
+        rows, cols = rows[off], cols[off]
+        up = (deg[cols] > deg[rows]) | ((deg[cols] == deg[rows]) & (cols < rows))
+        push += 2 * np.unique(cols[up]).size
+        pull += np.unique(cols).size
+    return push, pull
+
+
+@pytest.mark.parametrize("P", [2, 3, 4])
+def test_rmat_halo_push_split(rbl, P):
+    """RBL_OPT_HALO_PUSH: the hub-aware push/pull split of the indexed halo.  Each off-rank
+    product is formed on the rank of its higher-(degree, id) endpoint — pulled Q rows for the
+    columns above the row, pushed partial rows (the push tier: the pulled entries transposed)
+    for the rest.  Checked: the moved rows per SpMM equal the restated plan and the exchanges'
+    byte counts (send = recv on every rank: the push mirrors the pull), two exchanges per SpMM,
+    A_i / B_{i+1} bit-identical with the side stream on and off, equal to the pull-all halo and
+    the single-rank run to 1e-9 (only the order of each row's sum differs), and rbl_apply
+    through the split within 1e-13 |A||X| of SciPy."""
+    from rbl import _lib
+    plant = matgen.planted_spectrum(5)
+    A = matgen.rmat_csr(CASE["n"], CASE["scale"], CASE["edges"], CASE["seed"], plant)
+    X = np.random.default_rng(3).standard_normal((CASE["n"], 32))
+    steps, b = 8, 32
+
+    def run(push, overlap):
+        def fn(ctx, r):
+            ctx.set_option(_lib.RBL_OPT_HALO_OVERLAP, overlap)
+            ctx.set_option(_lib.RBL_OPT_HALO_PUSH, push)
+            ctx.gen_rmat(CASE["n"], CASE["scale"], CASE["edges"], CASE["seed"], plant)
+            _, r0, r1, _ = ctx.matrix_info()
+            Y = ctx.apply(X[r0:r1])
+            ctx.comm_stats(reset=True)
+            _, _, info = rbl.lanczos(ctx, 5, b, seed=9, check=False, max_steps=steps,
+                                     trace=True, ritz=False)
+            return info, ctx.comm_stats(), r0, r1, Y
+        return run_ranks(rbl, P, fn)
+
+    on, seq, pull = run(1, 1), run(1, 0), run(0, 1)
+    with rbl.Context(0) as ctx:
+        ctx.gen_rmat(CASE["n"], CASE["scale"], CASE["edges"], CASE["seed"], plant)
+        _, _, single = rbl.lanczos(ctx, 5, b, seed=9, check=False, max_steps=steps, trace=True,
+                                   ritz=False)
+    bounds = [r0 for _, _, r0, _, _ in on] + [CASE["n"]]
+    want_push, want_pull = _push_plan(A, bounds)
+    print(f"P={P}: rows moved per SpMM: push/pull split {want_push}, pull-all {want_pull}")
+    for (i_on, st, _, _, _), (i_seq, st_seq, _, _, _), (i_pl, st_pl, _, _, _) in zip(on, seq, pull):
+        for a, a0 in zip(i_on.trace_A + i_on.trace_B, i_seq.trace_A + i_seq.trace_B):
+            assert np.array_equal(a, a0)
+        for a, a1, a2 in zip(i_on.trace_A, single.trace_A, i_pl.trace_A):
+            assert np.abs(a - a1).max() <= 1e-9 * np.abs(a1).max()
+            assert np.abs(a - a2).max() <= 1e-9 * np.abs(a2).max()
+        assert st["halo_push"] == 1 and st_pl["halo_push"] == 0
+        assert (st["push_rows_pred"], st["pull_rows_pred"]) == (want_push, want_pull)
+        assert st["exchange_calls"] == 2 * (steps + 1) and st_pl["exchange_calls"] == steps + 1
+        assert st["send_bytes"] == st["recv_bytes"] and st == st_seq
+    moved = sum(st["recv_bytes"] for _, st, _, _, _ in on) // ((steps + 1) * b * 8)
+    moved_pl = sum(st["recv_bytes"] for _, st, _, _, _ in pull) // ((steps + 1) * b * 8)
+    assert (moved, moved_pl) == (want_push, want_pull)
+    bound = (abs(A) @ np.abs(X)) * 1e-13 + 1e-300
+    for res in (on, seq):
+        Y = np.vstack([y for _, _, _, _, y in res])
+        assert np.all(np.abs(Y - A @ X) <= bound)
+
+
+def test_rmat_halo_push_small_and_ragged(rbl):
+    """The split at the edges: n = 700 on 4 ranks with b = 16 and 32 (peers that push nothing to
+    some ranks), and a user CSR whose caller-given split leaves ranks with rows but no nonzeros
+    and one with no rows at all (n = 3, P = 4); the traces equal the single-rank ones."""
+    import scipy.sparse as sp
+    from rbl import _lib
+    plant = matgen.planted_spectrum(3)
+    n, scale, edges, seed = 700, 10, 30_000, 13
+    for b in (16, 32):
+        def run(ctx):
+            ctx.set_option(_lib.RBL_OPT_HALO_PUSH, 1)
+            ctx.gen_rmat(n, scale, edges, seed, plant)
+            _, _, info = rbl.lanczos(ctx, 3, b, seed=2, check=False, max_steps=6, trace=True,
+                                     ritz=False)
+            return info, ctx.comm_stats()["halo_push"]
+
+        with rbl.Context(0) as ctx:
+            ref, _ = run(ctx)
+        for info, hp in run_ranks(rbl, 4, lambda ctx, r: run(ctx)):
+            assert hp == 1
+            for a, a1 in zip(info.trace_A, ref.trace_A):
+                assert np.abs(a - a1).max() <= 1e-9 * np.abs(a1).max()
+    rng = np.random.default_rng(5)
+    n, live = 4000, 3000
+    M = _scattered(n, live)
+    omega = rng.standard_normal((n, 16))
+    with rbl.Context(0) as ctx:
+        ctx.set_matrix(M)
+        _, _, ref = rbl.lanczos(ctx, 3, 16, omega=omega, check=False, max_steps=5, trace=True,
+                                ritz=False)
+    for bounds in ([0, 1500, 3000, 3500, 4000], [0, 1000, 2000, 3000, 4000]):
+        def fn(ctx, r):
+            r0, r1 = bounds[r], bounds[r + 1]
+            S = M[r0:r1]
+            ctx.set_option(_lib.RBL_OPT_HALO_PUSH, 1)
+            ctx.set_matrix_rows(n, r0, r1, S.indptr, S.indices, S.data)
+            _, _, info = rbl.lanczos(ctx, 3, 16, omega=omega[r0:r1], check=False, max_steps=5,
+                                     trace=True, ritz=False)
+            return info, ctx.comm_stats()["halo_push"]
+        for info, hp in run_ranks(rbl, 4, fn):
+            assert hp == 1
+            for a, a1 in zip(info.trace_A, ref.trace_A):
+                assert np.abs(a - a1).max() <= 1e-9 * np.abs(a1).max()
+
+
+def test_rmat_halo_push_needs_symmetric_pattern(rbl):
+    """The split relies on A[c, r] = A[r, c] (the owner of c forms the product from its own row).
+    A pattern that is not symmetric across ranks is caught by the per-pair entry counts at setup:
+    RBL_OPT_HALO_PUSH 1 fails with a message, the automatic mode keeps the pull-all halo (and
+    the product stays exact)."""
+    import scipy.sparse as sp
+    from rbl import _lib
+    rng = np.random.default_rng(2)
+    n = 3000
+    M = _scattered(n, n, seed=4)
+    j = next(j for j in range(1500, n) if M[5, j] == 0 and M[j, 5] == 0)
+    M = M.tolil()
+    M[5, j] = 0.7            # one entry without its mirror, across the ranks' boundary
+    M = M.tocsr()
+    M.sort_indices()
+    X = rng.standard_normal((n, 16))
+    bounds = [0, 1500, 3000]
+
+    def fn(mode):
+        def f(ctx, r):
+            r0, r1 = bounds[r], bounds[r + 1]
+            Sr = M[r0:r1]
+            ctx.set_option(_lib.RBL_OPT_HALO_PUSH, mode)
+            try:
+                ctx.set_matrix_rows(n, r0, r1, Sr.indptr, Sr.indices, Sr.data)
+            except Exception as e:  # noqa: BLE001 - the failure is the result
+                return str(e)
+            return ctx.comm_stats()["halo_push"], ctx.apply(X[r0:r1])
+        return run_ranks(rbl, 2, f)
+
+    forced = fn(1)
+    assert all(isinstance(x, str) and "symmetric" in x for x in forced), forced
+    auto = fn(2)
+    assert all(hp == 0 for hp, _ in auto)
+    Y = np.vstack([y for _, y in auto])
+    bound = (abs(M) @ np.abs(X)) * 1e-13 + 1e-300
+    assert np.all(np.abs(Y - M @ X) <= bound)
