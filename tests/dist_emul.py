@@ -6,6 +6,7 @@ rbl_plan_row_partition / rbl_plan_halo / rbl_hashwindow_rows_host, which need no
 mirrors the library's data movement step for step (csrc/rbl_api.cpp):
   * setup_halo      — all-gather of every rank's need table -> the rows each rank gives;
   * halo_exchange   — grouped point-to-point Q rows (ncclSend/ncclRecv in the library);
+  * PushPullRows    — the indexed halo with the push/pull split (RBL_OPT_HALO_PUSH);
   * gram            — local W^T X partial + all-reduce sum (ncclAllReduce);
   * tsqr            — CholQR2 on the all-reduced Gram (positive-diagonal R);
   * rbl_step order  — partial reorth (block CGS) at even i, local reorth, U = A Q_i -
@@ -92,6 +93,90 @@ class DistRows:
 
     def spmm(self, Q: np.ndarray) -> np.ndarray:
         return self.A_ext @ self.halo(Q)
+
+
+class PushPullRows(DistRows):
+    """The indexed halo with the push/pull split (RBL_OPT_HALO_PUSH; rbl_api.cpp prepare_push,
+    push_products / push_exchange / push_finish): each off-rank product A[r,c] Q[c] is formed on
+    the rank of the endpoint with the larger (row degree, smaller id) — Q[c] pulled into a ghost
+    slot when that is c (tier 1), else A[c,r] Q[c] formed by c's owner from its own rows and the
+    partial row r pushed (tier 2 dropped here).  Ghost slots = the tier-1 columns sorted by id;
+    the push tier is tier 1 transposed; received partials are added in peer order."""
+
+    def __init__(self, n, csr_global):
+        super().__init__(n, csr_global=csr_global)
+        P, me, r0, r1 = self.P, self.me, self.r0, self.r1
+        A = self.A.tocsr()
+        rp = A.indptr
+        # global row degrees: every rank's slice padded to the longest, all-gathered
+        w = int(max(self.bounds[q + 1] - self.bounds[q] for q in range(P)))
+        mine = np.zeros(max(w, 1), np.int64)
+        mine[:r1 - r0] = np.diff(rp)
+        allg = allgather_i64(mine)
+        deg = np.concatenate([allg[q][:self.bounds[q + 1] - self.bounds[q]] for q in range(P)])
+        coo = A.tocoo()
+        rows, cols, vals = coo.row.astype(np.int64), coo.col.astype(np.int64), coo.data
+        grow = rows + r0
+        own = (cols >= r0) & (cols < r1)
+        up = (deg[cols] > deg[grow]) | ((deg[cols] == deg[grow]) & (cols < grow))
+        t1, t2 = ~own & up, ~own & ~up
+        owner = np.searchsorted(self.bounds, cols, side="right") - 1
+        # symmetry check: my tier-2 entries towards q are q's tier-1 entries towards me
+        cnt = np.concatenate([np.bincount(owner[t1], minlength=P), np.bincount(owner[t2], minlength=P)])
+        table = allgather_i64(cnt)
+        self.symmetric = all(table[p][P + q] == table[q][p] for p in range(P) for q in range(P))
+        self.ghost = np.unique(cols[t1])                      # sorted: grouped by owner
+        gown = np.searchsorted(self.bounds, self.ghost, side="right") - 1
+        self.ghost_cnt = np.bincount(gown, minlength=P).astype(np.int64)
+        self.ghost_off = np.concatenate([[0], np.cumsum(self.ghost_cnt)[:-1]])
+        counts = allgather_i64(self.ghost_cnt)               # [p][q]: rows p asks of q
+        self.send_cnt = counts[:, me].copy()
+        self.send_cnt[me] = 0
+        self.send_off = np.concatenate([[0], np.cumsum(self.send_cnt)[:-1]])
+        got = self._exchange_rows(self.ghost.reshape(-1, 1).astype(np.float64),
+                                  self.ghost_off, self.ghost_cnt, self.send_off, self.send_cnt, 1)
+        self.send_idx = got[:, 0].astype(np.int64) - r0
+        assert np.all((self.send_idx >= 0) & (self.send_idx < r1 - r0))
+        slot = np.searchsorted(self.ghost, cols[t1])
+        m = r1 - r0
+        self.A_own = sp.csr_matrix((vals[own], (rows[own], cols[own] - r0)), shape=(m, m))
+        self.A_pull = sp.csr_matrix((vals[t1], (rows[t1], slot)), shape=(m, self.ghost.size))
+        self.A_push = self.A_pull.T.tocsr()                   # ghost slot x own row
+        self.rows_moved = 2 * self.ghost.size                 # pulled + pushed, this rank
+
+    def _exchange_rows(self, send_src, src_off, src_cnt, dst_off, dst_cnt, b):
+        """Grouped point-to-point: rows src_off[q]:+src_cnt[q] of send_src go to q; dst_cnt[q]
+        rows from q land at dst_off[q] (the library's Comm::exchange)."""
+        out = np.zeros((int(dst_cnt.sum()), b))
+        reqs, bufs = [], []
+        for q in range(self.P):
+            if q == self.me:
+                continue
+            if src_cnt[q]:
+                reqs.append(dist.isend(torch.from_numpy(np.ascontiguousarray(
+                    send_src[src_off[q]:src_off[q] + src_cnt[q]])), q))
+            if dst_cnt[q]:
+                r = torch.zeros((int(dst_cnt[q]), b), dtype=torch.float64)
+                reqs.append(dist.irecv(r, q))
+                bufs.append((q, r))
+        for r in reqs:
+            r.wait()
+        for q, r in bufs:
+            out[dst_off[q]:dst_off[q] + dst_cnt[q]] = r.numpy()
+        return out
+
+    def spmm(self, Q: np.ndarray) -> np.ndarray:
+        b = Q.shape[1]
+        # pull: the rows my peers asked for, received into my ghost slots
+        ghosts = self._exchange_rows(Q[self.send_idx], self.send_off, self.send_cnt,
+                                     self.ghost_off, self.ghost_cnt, b)
+        U = self.A_own @ Q + self.A_pull @ ghosts
+        # push: partial rows for my ghost slots to their owners; mine added in peer order
+        partial = self.A_push @ Q
+        got = self._exchange_rows(partial, self.ghost_off, self.ghost_cnt, self.send_off,
+                                  self.send_cnt, b)
+        np.add.at(U, self.send_idx, got)
+        return U
 
 
 def gram(X: np.ndarray, Y: np.ndarray) -> np.ndarray:

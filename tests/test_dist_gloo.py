@@ -6,7 +6,9 @@ the library's distributed step order (tests/dist_emul.py) with gloo standing in 
   * the per-step A_i / B_i of the partitioned run match the single-process oracle
     (block-CGS partial reorth, positive-diagonal QR) within 1e-10 relative, on an
     nnz-balanced split of a random sparse matrix and on the row-sliced hash-window generator;
-  * every rank ends with the same T_j entries (the host eigensolve sees identical input).
+  * every rank ends with the same T_j entries (the host eigensolve sees identical input);
+  * on an R-MAT pattern, the push/pull split of the indexed halo (dist_emul.PushPullRows):
+    the same SpMM and traces, with fewer rows moved than pulling every referenced row.
 The device-side transport of the same code path is exercised on the GPU box by
 tests/test_gpu_multirank.py.
 """
@@ -54,6 +56,16 @@ def _run_case(case):
     if case == "csc":
         A = _rand_sym(1500, 0.004, 5)
         M = de.DistRows(A.shape[0], csr_global=A)
+    elif case == "rmat_push":   # power-law pattern, the push/pull split of the indexed halo
+        A = matgen.rmat_csr(3000, 12, 60_000, 7, matgen.planted_spectrum(6))
+        M = de.PushPullRows(A.shape[0], csr_global=A)
+        assert M.symmetric
+        moved = int(de.allreduce(np.array([float(M.rows_moved)]))[0])
+        r0, r1 = M.r0, M.r1
+        offr = A[r0:r1].tocoo()
+        pull_all = np.unique(offr.col[(offr.col < r0) | (offr.col >= r1)]).size
+        pull_all = int(de.allreduce(np.array([float(pull_all)]))[0])
+        assert 0 < moved < pull_all, (moved, pull_all)   # the hubs' rows stay home
     else:
         n, W, p, seed = 2400, 30, 0.6, 17
         plant = matgen.planted_spectrum(6)
@@ -83,6 +95,7 @@ def _run_case(case):
     assert np.all(allA == allA[0])
 
 
-@pytest.mark.parametrize("world,case", [(2, "csc"), (2, "hashwindow"), (3, "csc")])
+@pytest.mark.parametrize("world,case", [(2, "csc"), (2, "hashwindow"), (3, "csc"),
+                                        (2, "rmat_push"), (3, "rmat_push")])
 def test_gloo_partitioned_lanczos(world, case):
     mp.spawn(_worker, args=(world, _free_port(), case), nprocs=world, join=True)
