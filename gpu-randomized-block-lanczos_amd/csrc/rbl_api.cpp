@@ -718,6 +718,11 @@ int prepare_tiers(rbl_ctx* ctx, const std::vector<int64_t>& rp) {
     CHK(st);
     ctx->seg_split = true;
     ctx->ghost = true;
+    // the rows this halo moves per SpMM, summed over ranks (rbl_comm_stats' halo plan)
+    std::vector<int64_t> ng(ctx->nranks);
+    COMMC(ctx->comm->allgather_host(&ctx->n_ghost, ng.data(), 1, ctx->stream, &ctx->err));
+    ctx->pull_pred_rows = 0;
+    for (int64_t v : ng) ctx->pull_pred_rows += v;
     return RBL_OK;
   }
   if (ctx->seg_ntasks == 0 || ctx->nnz == 0 || ctx->csr_dropped) return RBL_OK;

@@ -318,7 +318,8 @@ int rbl_synchronize(rbl_ctx* ctx);
 /* the halo plan of the matrix held (set by rbl_set_matrix_* / the generators; reset keeps them):
  * RBL_COMM_HALO_PUSH 1 when the push/pull split runs (RBL_OPT_HALO_PUSH), and the Q rows per
  * SpMM summed over ranks that its setup predicted with the split (pulled + pushed) and with
- * the pull-all halo (0 on one rank or a banded A) */
+ * the pull-all halo (0 on one rank or a banded A; the split's count also 0 when
+ * RBL_OPT_HALO_PUSH is 0, which skips its evaluation) */
 #define RBL_COMM_HALO_PUSH       5
 #define RBL_COMM_PUSH_ROWS       6
 #define RBL_COMM_PULL_ROWS       7
