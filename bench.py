@@ -368,7 +368,11 @@ def measure(ctx, args, matrix, K, W, nloc, nnz_loc, world, barrier, allmax):
         roofline, roofline2 = roof_spmm, roof_reorth
     # collectives per block step on this rank (all-reduces, grouped send/recv), from the library
     steps_timed = K * (m_max + 1)
-    comm_per_step = {key: round(v / steps_timed, 3) for key, v in comm.items()}
+    # (the halo-plan entries of rbl_comm_stats are per matrix, not counters: the R-MAT
+    # sub-record reports them as halo_plan)
+    plan_keys = ("halo_push", "push_rows_pred", "pull_rows_pred")
+    comm_per_step = {key: round(v / steps_timed, 3) for key, v in comm.items()
+                     if key not in plan_keys}
     # the host side of a run (rbl.lanczos): rbl_start (blocks until A Omega + QR are done),
     # enqueueing the steps, and waiting in rbl_fetch for the last one
     host_ms = {key: round(v / K, 1) for key, v in host.items()}
