@@ -526,12 +526,15 @@ def main():
     # A sub-record that raises on one rank leaves the headline line unprinted; on one rank
     # (no collectives in flight) the error is recorded in the sub-record instead.  On several
     # ranks it propagates, so torch.distributed.run ends the peers instead of leaving them
-    # waiting in a collective.
+    # waiting in a collective — except a run that could not allocate its buffers: rbl_start
+    # votes on that before its collectives, so every rank raises it together and all record it.
     def guarded(fn, *a):
         try:
             return fn(*a)
         except Exception as e:  # noqa: BLE001 — reported in the line
-            if world > 1:
+            collective = (isinstance(e, rbl.RBLError) and e.code == _lib.RBL_ERR_OOM
+                          and "rbl_start" in str(e))
+            if world > 1 and not collective:
                 raise
             return {"error": f"{type(e).__name__}: {e}"}
 
@@ -725,6 +728,9 @@ def c5_subrecord(ctx, args, world, barrier, allmax, allsum, allgather_i64):
     # tiles) and ~6.9 KB during the run (39 fp32 basis slots, band tiles, fp64 working blocks)
     nloc_est = -(-ra.n // world)
     need = 1.15 * nloc_est * max(2.4e3, 39 * 32 * 4 + 1152 + 3 * 256 + 64)
+    # ranks sharing one GPU (the shm transport on a one-GPU box) all draw on its free memory
+    devs = allgather_i64(ctx.device)
+    need *= sum(1 for d in devs if d == ctx.device)
     free, total = ctx.device_memory()  # (the C3 matrix and its ~16 GB of buffers still held)
     if allsum(int(free < need)) > 0:
         return {"skipped": f"needs ~{need / 1e9:.0f} GB of HBM per rank; a rank has "

@@ -2616,6 +2616,10 @@ int rbl_start(rbl_ctx* ctx, int b, int max_blocks, int basis_bits, const double*
   ctx->nlock = 0;  // a new problem: no locked vectors
   ctx->cloc_step = 0;
   ctx->step_flags.clear();
+  // the allocations below fail alone on one rank (its HBM): every rank then learns of it before
+  // the collectives of the start, and all return the error, instead of the peers waiting in the
+  // halo exchange for a rank that has left
+  const int alloc_st = [&]() -> int {
   if (reuse) {
     ctx->nblocks = 0;
     if (ctx->cstream) HIPC(hipStreamSynchronize(ctx->cstream));
@@ -2685,6 +2689,26 @@ int rbl_start(rbl_ctx* ctx, int b, int max_blocks, int basis_bits, const double*
   HIPC(hipHostMalloc(&ctx->h_pin, 2 * b * b * sizeof(double), hipHostMallocDefault));
   HIPC(hipHostMalloc(&ctx->h_hist, (size_t)(max_blocks + 2) * 2 * b * b * sizeof(double), hipHostMallocDefault));
   HIPC(hipHostMalloc(&ctx->h_hflags, (size_t)(max_blocks + 2) * 4 * sizeof(int), hipHostMallocDefault));
+  }
+  return RBL_OK;
+  }();
+  if (ctx->nranks > 1) {
+    const int64_t mine = alloc_st;
+    std::vector<int64_t> all(ctx->nranks);
+    COMMC(ctx->comm->allgather_host(&mine, all.data(), 1, ctx->stream, &ctx->err));
+    int bad = -1;
+    for (int q = 0; q < ctx->nranks && bad < 0; ++q)
+      if (all[q] != RBL_OK) bad = q;
+    if (bad >= 0) {
+      (void)hipGetLastError();  // the failed hipMalloc's error must not surface in a later check
+      free_run(ctx);  // (a later start re-plans from scratch)
+      if (alloc_st != RBL_OK) return alloc_st;
+      return fail(ctx, (int)all[bad], "rbl_start: rank " + std::to_string(bad) +
+                                          " could not allocate its run buffers");
+    }
+  } else if (alloc_st != RBL_OK) {
+    (void)hipGetLastError();
+    return alloc_st;
   }
 
   // Omega (row-major) in d_T

@@ -291,3 +291,32 @@ def test_multirank_matrix_sequence_like_bench(rbl):
                 assert np.abs(a - a1).max() <= 1e-9 * np.abs(a1).max()
             for bb, bb1 in zip(info.trace_B, ref.trace_B):
                 assert np.abs(bb - bb1).max() <= 1e-9 * np.abs(bb1).max()
+
+
+def test_start_allocation_failure_is_collective(rbl):
+    """A run whose buffers do not fit on one rank: rbl_start votes on its allocations before the
+    collectives of the start, so every rank returns RBL_ERR_OOM (the peers naming the rank that
+    failed) instead of waiting in the halo exchange for it; the contexts then run a normal start.
+    (Rank 0 keeps every block in HBM, RBL_OPT_DEVICE_BLOCKS = 0, for 321 blocks of 1 GB; rank 1
+    keeps 3 and would spill the rest, which fits.)"""
+    from rbl import _lib
+    plant = np.array([100.0 * (7 - l) for l in range(1, 7)])
+
+    def fn(ctx, r):
+        ctx.gen_hashwindow(8_000_000, 16, 0.5, 3, plant)
+        ctx.set_option(_lib.RBL_OPT_DEVICE_BLOCKS, 0 if r == 0 else 3)
+        err = None
+        try:
+            ctx.start(32, 320)
+        except rbl.RBLError as e:
+            err = (e.code, str(e))
+        ctx.set_option(_lib.RBL_OPT_DEVICE_BLOCKS, 0)
+        _, _, info = rbl.lanczos(ctx, 3, 32, seed=1, check=False, max_steps=3, trace=True,
+                                 ritz=False)
+        return err, info
+
+    out = run_ranks(rbl, 2, fn)
+    assert out[0][0] is not None and out[0][0][0] == _lib.RBL_ERR_OOM
+    assert out[1][0] is not None and out[1][0][0] == _lib.RBL_ERR_OOM and "rank 0" in out[1][0][1]
+    for a, a1 in zip(out[0][1].trace_A, out[1][1].trace_A):
+        assert np.array_equal(a, a1)
