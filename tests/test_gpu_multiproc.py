@@ -158,11 +158,14 @@ def test_ranks_agree_and_match_inprocess_and_single(procs, single, inproc, case)
 
 @pytest.mark.parametrize("case", ["c4b", "c3"])
 def test_golden_fixtures_on_processes(procs, case):
-    """BASELINE config 4 (R-MAT, n = 1e6, b = 32) and config 3's shape (n = 1,585,478, b = 16)
-    on P processes: the oracle fixture's step count and eigenvalues (< 1e-10), Ritz rows
+    """BASELINE config 4 (R-MAT, n = 1e6, b = 32; the push/pull halo split on) and config 3's
+    shape (n = 1,585,478, b = 16) on P processes: the oracle fixture's step count and eigenvalues
+    (< 1e-10), Ritz rows
     gathered from the ranks matching the fixture's largest entries (1e-6, up to sign)."""
     P, res = procs
     g = np.load(os.path.join(HERE, "golden", f"golden_{case}.npz"))
+    if case == "c4b":  # R-MAT's hubs: the automatic halo plan takes the push/pull split
+        assert all(int(r["c4b__comm"][5]) == 1 for r in res)
     for r in res:
         assert bool(r[f"{case}__converged"]) and int(r[f"{case}__iters"]) == int(g["iters"])
         rel = np.abs(r[f"{case}__D"] - g["D"]) / np.abs(g["D"])
