@@ -88,3 +88,18 @@ def test_plan_halo_window():
     assert (lo[1], hi[1]) == (250, 500)
     assert (lo[2], hi[2]) == (500, 510)
     assert hi[3] == lo[3] == 0
+
+
+def test_python_constants_match_the_header():
+    """Every option / status / collective-counter constant the Python binding names has the
+    value include/rbl_hip.h gives it, and every RBL_OPT_* of the header is named there."""
+    from rbl import _lib
+    txt = open(HEADER).read()
+    defs = {m.group(1): int(m.group(2))
+            for m in re.finditer(r"^#define\s+(RBL_\w+)\s+(-?\d+)\b", txt, re.M)}
+    assert len(defs) >= 20
+    mism = {k: (v, getattr(_lib, k)) for k, v in defs.items()
+            if hasattr(_lib, k) and getattr(_lib, k) != v}
+    assert not mism, mism
+    missing = [k for k in defs if k.startswith("RBL_OPT_") and not hasattr(_lib, k)]
+    assert not missing, missing
