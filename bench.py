@@ -265,11 +265,17 @@ def measure(ctx, args, matrix, K, W, nloc, nnz_loc, world, barrier, allmax):
     ctx.comm_stats(reset=True)
     barrier()
     t0 = time.perf_counter()
+    marks = [t0]
     for _ in range(K):
-        one_run()
+        one_run()  # (returns once the run's last block step has been fetched)
+        marks.append(time.perf_counter())
     ctx.synchronize()
     barrier()
     elapsed = allmax(time.perf_counter() - t0)
+    # the spread of the timed runs on this rank (rank 0's is reported): run-to-run variation
+    runs_ms = sorted((b_ - a_) * 1e3 for a_, b_ in zip(marks, marks[1:]))
+    run_spread = {"min": round(runs_ms[0], 2), "median": round(runs_ms[len(runs_ms) // 2], 2),
+                  "max": round(runs_ms[-1], 2)} if runs_ms else None
     stage = ctx.timers()
     comm = ctx.comm_stats()
     iters = K * m_max
@@ -379,7 +385,7 @@ def measure(ctx, args, matrix, K, W, nloc, nnz_loc, world, barrier, allmax):
     return {"elapsed": elapsed, "stage": stage, "value": value, "roofline": roofline,
             "host_ms_per_run": host_ms,
             "roofline_secondary": roofline2, "spmm_kernel": spmm_kernel,
-            "comm_per_step": comm_per_step, "m_max": m_max}
+            "comm_per_step": comm_per_step, "m_max": m_max, "run_ms": run_spread}
 
 
 def main():
@@ -599,7 +605,7 @@ def main():
             "time_to_k_slow_spectrum": ttk_slow,
             "matrix_gen_s": round(gen_s, 3),
             "cpu_baseline": cpu,
-            "comm_per_step": meas["comm_per_step"],
+            "comm_per_step": meas["comm_per_step"], "run_ms_rank0": meas["run_ms"],
             "c4b_rmat": rmat_rec,
             "c3_circuit": c3_rec,
             "c5_mixed": c5_rec,
@@ -661,7 +667,7 @@ def rmat_subrecord(ctx, args, plant, world, barrier, allmax, allsum, allgather_i
             "send_bytes_per_step_by_rank": allgather_i64(int(meas["comm_per_step"]["send_bytes"])),
             "roofline": meas["roofline"], "roofline_secondary": meas["roofline_secondary"],
             "stage_ms_per_run": {s_: round(v / K, 3) for s_, v in meas["stage"].items()},
-            "comm_per_step": meas["comm_per_step"],
+            "comm_per_step": meas["comm_per_step"], "run_ms_rank0": meas["run_ms"],
             "time_to_k": {"seconds": round(ttk_s, 4), "iters": info.iters,
                           "converged": info.converged, "k": args.k,
                           "top_eigenvalues": [round(float(x), 6) for x in D[:3]]},
@@ -703,7 +709,7 @@ def c3_subrecord(ctx, args, world, barrier, allmax, allsum, allgather_i64):
             "nnz_per_rank": allgather_i64(nnz_loc),
             "roofline": meas["roofline"], "roofline_secondary": meas["roofline_secondary"],
             "stage_ms_per_run": {s_: round(v / K, 3) for s_, v in meas["stage"].items()},
-            "comm_per_step": meas["comm_per_step"],
+            "comm_per_step": meas["comm_per_step"], "run_ms_rank0": meas["run_ms"],
             "time_to_k": {"seconds": round(ttk_s, 4), "iters": info.iters,
                           "converged": info.converged, "k": ra.k,
                           "top_eigenvalues": [round(float(x), 6) for x in D[:3]]},
@@ -761,7 +767,7 @@ def c5_subrecord(ctx, args, world, barrier, allmax, allsum, allgather_i64):
             "nnz_per_rank": allgather_i64(nnz_loc),
             "roofline": meas["roofline"], "roofline_secondary": meas["roofline_secondary"],
             "stage_ms_per_run": {s_: round(v / K, 3) for s_, v in meas["stage"].items()},
-            "comm_per_step": meas["comm_per_step"],
+            "comm_per_step": meas["comm_per_step"], "run_ms_rank0": meas["run_ms"],
             "time_to_k": {"seconds": round(ttk_s, 4), "iters": info.iters,
                           "converged": info.converged, "k": ra.k,
                           "top_eigenvalues": [round(float(x), 6) for x in D[:3]]},
