@@ -680,6 +680,9 @@ __global__ __launch_bounds__(256) void k_tsmm32f(int64_t nrows, const float* __r
 #ifndef RBL_T32_MFMA32
 #define RBL_T32_MFMA32 1
 #endif
+#ifndef RBL_T32X_PINGPONG
+#define RBL_T32X_PINGPONG 0
+#endif
 __global__ __launch_bounds__(256) void k_tsmm32x(int64_t nrows, const float* __restrict__ Xb,
                                                  int64_t xstride, int nX, const double* __restrict__ C,
                                                  int ldc, float* Y0, float* Y1, float alpha,
@@ -730,22 +733,37 @@ __global__ __launch_bounds__(256) void k_tsmm32x(int64_t nrows, const float* __r
   store_c(0, cr);
   load_a(0, acur);
   __syncthreads();
-  for (int ch = 0; ch < nch; ++ch) {
+  // one chunk: MFMAs on `use` while chunk ch + 1's operands land in `pf`
+  auto chunk = [&](int ch, const f4v (&use)[4], f4v (&pf)[4]) {
     load_c(ch + 1, cr);
-    load_a(ch + 1, anext);
+    load_a(ch + 1, pf);
     const float* cb = cs[ch & 1] + 16 * (lane / 32) * CLD + 2 * (lane % 32);
 #pragma unroll
     for (int st = 0; st < NS; ++st) {
       const float2 bv = *reinterpret_cast<const float2*>(cb + st * CLD);
-      const float a = acur[st / 4][st % 4];
+      const float a = use[st / 4][st % 4];
       acc[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bv.x, acc[0], 0, 0, 0);
       acc[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bv.y, acc[1], 0, 0, 0);
     }
     store_c((ch + 1) & 1, cr);
+    __syncthreads();
+  };
+#if RBL_T32X_PINGPONG
+  // chunks in pairs with the two operand sets swapping roles: no register rotation per chunk
+  // (16 v_mov per 32 MFMAs in the rotating form; VALU per MFMA 1.2 -> 0.67 in the loop), but
+  // measured 5 % slower (partial reorth 288 vs 274 ms per fp32 C4a run, 3 alternating
+  // reps, profiles/r04_t32pp_ab.log: the 64-MFMA loop body), so off
+  for (int ch = 0; ch < nch; ch += 2) {
+    chunk(ch, acur, anext);
+    if (ch + 1 < nch) chunk(ch + 1, anext, acur);  // (wave-uniform)
+  }
+#else
+  for (int ch = 0; ch < nch; ++ch) {
+    chunk(ch, acur, anext);
 #pragma unroll
     for (int u = 0; u < 4; ++u) acur[u] = anext[u];
-    __syncthreads();
   }
+#endif
   // epilogue: D (lane l, register v: row 4 (l / 32) + v % 4 + 8 (v / 4), column l % 32 of tile
   // tt) -> LDS by 16-row halves -> row-major float4 stores of Y0 | Y1 (rows below r0: the
   // previous wave's)
