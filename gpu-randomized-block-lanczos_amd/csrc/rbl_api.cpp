@@ -2976,6 +2976,9 @@ int step_impl(rbl_ctx* ctx, int i, int part_reorth, double* A_out, double* B_out
     }
     if (ai_parts < 0) return ai_parts;
     HIPC(hipGetLastError());
+    // the main stream's next collective must follow the side stream's exchange on every rank,
+    // also where the SpMM never waited for it (a rank without rows returns from apply_A early)
+    if (halo_ev) HIPC(hipStreamWaitEvent(ctx->stream, halo_ev, 0));
   }
   // the push/pull split: the received partials into U (A_i is formed after this, from all of U)
   if (pushed) {
