@@ -9,6 +9,10 @@ vote, build_ghosts' request exchange), the indexed halo with the side-stream ove
 halo a ghost-built context falls back to for b outside {16, 32} or a pinned gather kernel, fp64
 and fp32 bases, and matrices replaced in place on one context (bench.py's sub-records).
 
+The same cases also run over RCCL itself with 2 and 4 processes on the one GPU
+(tests/rccl_rank.py: each rank declares its own host id, so RCCL connects the ranks through its
+network transport on the loopback interface instead of refusing two ranks on one device).
+
 Checks, per world size 2 and 4:
   * every rank returns the same A_i / B_{i+1} bit for bit (the sums are formed identically);
   * bit for bit the in-process LocalComm run at the same P (threads in one process: the same
@@ -111,6 +115,73 @@ def inproc(rbl):
             cache[P] = run_ranks(rbl, P, fn, timeout=280)
         return cache[P]
     return get
+
+
+def _launch_rccl(rank_launcher, P, tmp):
+    """P processes of tests/rccl_rank.py, all on GPU 0, over RCCL itself (one host id per rank:
+    RCCL's network transport on the loopback interface instead of xGMI)."""
+    import json
+    uid = os.path.join(tmp, "rccl_uid")
+    outs = [os.path.join(tmp, f"rccl{r}.npz") for r in range(P)]
+    cmds = [[sys.executable, "-u", os.path.join(HERE, "rccl_rank.py"), "--uid-file", uid,
+             "--nranks", str(P), "--rank", str(r), "--cases", json.dumps(CASES), "--out", outs[r]]
+            for r in range(P)]
+    t0 = time.time()
+    rcs, logs = rank_launcher.run(cmds, timeout=400, env={"NCCL_SOCKET_IFNAME": "lo",
+                                                          "NCCL_DEBUG": "WARN"})
+    assert rcs == [0] * P, "\n".join(f"--- rank {r} rc={rc}\n{log}" for r, (rc, log) in
+                                      enumerate(zip(rcs, logs)))
+    print(f"RCCL P={P}: {time.time() - t0:.1f} s for {len(CASES)} cases")
+    res = []
+    for o in outs:
+        with np.load(o) as z:
+            res.append({k: z[k] for k in z.files})
+    return res
+
+
+@pytest.fixture(scope="module", params=[2, 4])
+def rccl_procs(request, rank_launcher, tmp_path_factory):
+    P = request.param
+    return P, _launch_rccl(rank_launcher, P, str(tmp_path_factory.mktemp(f"rccl{P}")))
+
+
+@pytest.mark.parametrize("case", [c["name"] for c in TRACE_CASES])
+def test_rccl_ranks_on_one_gpu(rccl_procs, single, inproc, case):
+    """The production transport, RCCL (rbl_create_dist: ncclAllReduce, grouped ncclSend /
+    ncclRecv, ncclAllGather in the setup), with real processes: every rank returns the same
+    A_i / B_{i+1}; at 2 ranks bit for bit the in-process run (a two-term sum is the same in any
+    order), at 4 within 1e-10 of the single-rank run like the other transports."""
+    P, res = rccl_procs
+    c = next(x for x in CASES if x["name"] == case)
+    for r in res:
+        assert str(r["transport"]) == "rccl" and int(r["transport_ranks"]) == P
+    A0, B0 = res[0][f"{case}__A"], res[0][f"{case}__B"]
+    assert len(A0) == c["steps"]
+    for r in res[1:]:
+        assert np.array_equal(r[f"{case}__A"], A0) and np.array_equal(r[f"{case}__B"], B0)
+    if P == 2:
+        ip = inproc(P)
+        assert np.array_equal(ip[0][case]["A"], A0) and np.array_equal(ip[0][case]["B"], B0)
+    tol = 1e-10 if c.get("bits", 64) == 64 else 1e-5
+    s = single[case]
+    for a, a1 in zip(list(A0) + list(B0), list(s["A"]) + list(s["B"])):
+        assert np.abs(a - a1).max() <= tol * np.abs(a1).max()
+    comm = [r[f"{case}__comm"] for r in res]
+    assert all(cm[2] > 0 for cm in comm), "no halo exchange"
+    if c.get("push") is not None:
+        assert all(cm[2] == (c["steps"] + 1) * (2 if c["push"] else 1) for cm in comm)
+
+
+@pytest.mark.parametrize("case", ["c4b", "c3"])
+def test_rccl_golden_fixtures(rccl_procs, case):
+    """BASELINE config 4 (R-MAT, n = 1e6, the push/pull split) and config 3's shape over RCCL
+    on 2 and 4 processes: the oracle fixture's step count and eigenvalues (< 1e-10)."""
+    P, res = rccl_procs
+    g = np.load(os.path.join(HERE, "golden", f"golden_{case}.npz"))
+    for r in res:
+        assert bool(r[f"{case}__converged"]) and int(r[f"{case}__iters"]) == int(g["iters"])
+        rel = np.abs(r[f"{case}__D"] - g["D"]) / np.abs(g["D"])
+        assert rel.max() < 1e-10, rel
 
 
 def test_transport_is_shm_processes(procs):
