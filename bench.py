@@ -187,8 +187,10 @@ def launch_ranks(args) -> None:
     import subprocess
     import socket
     have = gpu_count_sysfs()
-    # the shm transport may put several ranks on one GPU (RCCL refuses that)
-    if have is not None and have < args.gpus and args.transport != "shm":
+    # the shm transport may put several ranks on one GPU (RCCL refuses that, unless each rank
+    # declares its own host: the one-GPU rehearsal of the RCCL path, RBL_RCCL_HOST_PER_RANK=1)
+    if (have is not None and have < args.gpus and args.transport != "shm"
+            and not rccl_host_per_rank()):
         sys.exit(f"bench.py: --gpus {args.gpus} needs {args.gpus} GPUs, this node has {have}")
     with socket.socket() as sk:
         sk.bind(("127.0.0.1", 0))
@@ -200,6 +202,14 @@ def launch_ranks(args) -> None:
            os.path.abspath(__file__), "--argv-env"]
     env = dict(os.environ, RBL_BENCH_ARGV=json.dumps(sys.argv[1:]))
     sys.exit(subprocess.run(cmd, env=env).returncode)
+
+
+def rccl_host_per_rank() -> bool:
+    """RBL_RCCL_HOST_PER_RANK=1 (a rehearsal on a box with fewer GPUs than ranks, not a
+    measurement): every rank declares its own RCCL host id, so RCCL connects ranks that share a
+    GPU through its network transport on the loopback interface instead of refusing them; the
+    ranks go round-robin over the GPUs there are."""
+    return os.environ.get("RBL_RCCL_HOST_PER_RANK", "0") == "1"
 
 
 def rmat_relabel(args, world: int) -> int:
@@ -441,6 +451,10 @@ def main():
         shm_path = obj[0]
         device = local_rank % ngpu
     elif world > 1:
+        if rccl_host_per_rank():  # one-GPU rehearsal of the RCCL path (see rccl_host_per_rank)
+            os.environ["NCCL_HOSTID"] = f"rbl-bench-host-{rank}"
+            os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+            device = local_rank % ngpu
         buf = np.zeros(128, np.uint8)
         if rank == 0:
             st = _lib.lib.rbl_get_unique_id(_lib.u8ptr(buf))
@@ -572,7 +586,7 @@ def main():
             "metric": metric_name(args, nnz),
             "value": round(value, 3),
             "unit": "block iterations/s",
-            "n_gpus": world if args.transport == "rccl" else min(world, ngpu),
+            "n_gpus": world if args.transport == "rccl" and not rccl_host_per_rank() else min(world, ngpu),
             "steps": K,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / K * 1e3, 3),
@@ -592,7 +606,10 @@ def main():
                        "block_steps_per_run": m_max, "parallelism": f"rows{world}",
                        "transport": comm["transport"], "transport_ranks": comm["nranks"],
                        **({"ranks_share_gpus": True, "gpus_used": min(world, ngpu)}
-                          if args.transport == "shm" and world > ngpu else {}),
+                          if (args.transport == "shm" or rccl_host_per_rank()) and world > ngpu
+                          else {}),
+                       **({"rccl_host_per_rank": True} if rccl_host_per_rank() and world > 1
+                          else {}),
                        "nnz_per_rank": nnz_ranks,
                        **({"device_blocks": args.device_blocks} if args.device_blocks else {}),
                        **({"keep_csr": 0} if not args.keep_csr else {}),
