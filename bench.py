@@ -404,6 +404,11 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # stdout carries the one JSON line and nothing else: what libraries print there (gloo's
+    # connection notes, RCCL's banner and warnings) goes to stderr from here on
+    sys.stdout.flush()
+    line_fd = os.dup(1)
+    os.dup2(2, 1)
     dist = None
     if world > 1:
         import torch.distributed as dist
@@ -627,7 +632,9 @@ def main():
             "c3_circuit": c3_rec,
             "c5_mixed": c5_rec,
         }
-        print(json.dumps(line), flush=True)
+        out = (json.dumps(line) + "\n").encode()
+        while out:
+            out = out[os.write(line_fd, out):]
     ctx.close()
     if dist is not None:
         dist.destroy_process_group()
