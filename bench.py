@@ -58,6 +58,10 @@ def parse():
                     help="skip the CPU baseline's second timing at 1 BLAS thread (benchmark.jl:49 "
                          "sets BLAS.set_num_threads(1); on by default)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-check-n", type=int, default=1_000_000,
+                    help="n of the CPU baseline's fixed-step cross-check (0 skips it): the first "
+                         "--cpu-check-steps block steps timed at the sample's n and at this n")
+    ap.add_argument("--cpu-check-steps", type=int, default=8)
     ap.add_argument("--no-ttk", action="store_true")
     ap.add_argument("--no-ttk-slow", action="store_true",
                     help="skip the second time-to-k on a slowly decaying planted spectrum "
@@ -97,6 +101,10 @@ def parse():
                          "the mean instead of 2.1x), and on one GPU the gather SpMM runs 34.3 "
                          "instead of 37.5 ms per launch (profiles/r04_bench_rmat_relabel*.json); "
                          "auto = on for several ranks only")
+    ap.add_argument("--rmat-as-drawn-steps", type=int, default=1,
+                    help="timed runs of the R-MAT matrix as drawn (no relabel) after the relabelled "
+                         "sub-record, so the line stays comparable with rounds before the relabel "
+                         "(0 skips it)")
     ap.add_argument("--rmat-edges", type=int, default=0,
                     help="R-MAT draws (0: 0.66 n x 100: ~1e9 nonzeros at n = 1e7 after merging)")
     ap.add_argument("--device-blocks", type=int, default=0,
@@ -573,12 +581,6 @@ def main():
     if args.matrix == "hashwindow" and args.c3_steps > 0 and args.basis_bits == 64:
         c3_rec = guarded(c3_subrecord, ctx, args, world, barrier, allmax, allsum, allgather_i64)
 
-    # ---- BASELINE config 5: n = 5e7, fp32 basis, on >= 2 ranks (no spill) ----
-    c5_rec = None
-    if (args.matrix == "hashwindow" and args.c5_steps > 0 and args.basis_bits == 64
-            and world >= args.c5_min_ranks):
-        c5_rec = guarded(c5_subrecord, ctx, args, world, barrier, allmax, allsum, allgather_i64)
-
     # ---- CPU baseline: the oracle (port of RBL.jl) on a bounded sample, rank 0, N = 1 ----
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -586,55 +588,73 @@ def main():
 
     comm = ctx.comm_info()
     nnz_ranks = allgather_i64(nnz_loc)
-    if rank == 0:
-        line = {
-            "metric": metric_name(args, nnz),
-            "value": round(value, 3),
-            "unit": "block iterations/s",
-            "n_gpus": world if args.transport == "rccl" and not rccl_host_per_rank() else min(world, ngpu),
-            "steps": K,
-            "warmup": args.warmup,
-            "ms_per_step": round(elapsed / K * 1e3, 3),
-            "higher_is_better": True,
-            "scaling": "strong",
-            "vs_baseline": None,
-            "dtype": "f64" if args.basis_bits == 64 else "f64 (A*Q, 3-term, QR) + f32 (basis, reorth)",
-            "data": f"synthetic (seeded {args.matrix} symmetric matrix generated on device)",
-            "config": {"workload": workload_name(args),
-                       "n": n, "nnz": nnz, "b": b, "k": k, "matrix": args.matrix,
-                       **({"halfwidth": args.halfwidth, "density": args.density}
-                          if args.matrix == "hashwindow" else
-                          {"rmat_scale": args.rmat_scale, "rmat_edges": args.rmat_edges,
-                           "rmat_abcd": [0.57, 0.19, 0.19, 0.05],
-                           "relabel": bool(rmat_relabel(args, world))} if args.matrix == "rmat" else
-                          {"circuit_width": 1259, "circuit_p_edge": 0.95873}),
-                       "block_steps_per_run": m_max, "parallelism": f"rows{world}",
-                       "transport": comm["transport"], "transport_ranks": comm["nranks"],
-                       **({"ranks_share_gpus": True, "gpus_used": min(world, ngpu)}
-                          if (args.transport == "shm" or rccl_host_per_rank()) and world > ngpu
-                          else {}),
-                       **({"rccl_host_per_rank": True} if rccl_host_per_rank() and world > 1
-                          else {}),
-                       "nnz_per_rank": nnz_ranks,
-                       **({"device_blocks": args.device_blocks} if args.device_blocks else {}),
-                       **({"keep_csr": 0} if not args.keep_csr else {}),
-                       **({"fuse": args.fuse} if args.fuse != 7 else {})},
-            "roofline": roofline,
-            "roofline_secondary": roofline2,
-            "stage_ms_per_run": {s: round(v, 3) for s, v in stage_per_run.items()},
-            "host_ms_per_run": meas["host_ms_per_run"],
-            "time_to_k": ttk,
-            "time_to_k_slow_spectrum": ttk_slow,
-            "matrix_gen_s": round(gen_s, 3),
-            "cpu_baseline": cpu,
-            "comm_per_step": meas["comm_per_step"], "run_ms_rank0": meas["run_ms"],
-            "c4b_rmat": rmat_rec,
-            "c3_circuit": c3_rec,
-            "c5_mixed": c5_rec,
-        }
-        out = (json.dumps(line) + "\n").encode()
-        while out:
-            out = out[os.write(line_fd, out):]
+    # the line is complete but for C5 before C5 runs: a C5 failure on this rank still prints it
+    # (with the error in c5_mixed) before the job ends non-zero
+    line = {
+        "metric": metric_name(args, nnz),
+        "value": round(value, 3),
+        "unit": "block iterations/s",
+        "n_gpus": world if args.transport == "rccl" and not rccl_host_per_rank() else min(world, ngpu),
+        "steps": K,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / K * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f64" if args.basis_bits == 64 else "f64 (A*Q, 3-term, QR) + f32 (basis, reorth)",
+        "data": f"synthetic (seeded {args.matrix} symmetric matrix generated on device)",
+        "config": {"workload": workload_name(args),
+                   "n": n, "nnz": nnz, "b": b, "k": k, "matrix": args.matrix,
+                   **({"halfwidth": args.halfwidth, "density": args.density}
+                      if args.matrix == "hashwindow" else
+                      {"rmat_scale": args.rmat_scale, "rmat_edges": args.rmat_edges,
+                       "rmat_abcd": [0.57, 0.19, 0.19, 0.05],
+                       "relabel": bool(rmat_relabel(args, world))} if args.matrix == "rmat" else
+                      {"circuit_width": 1259, "circuit_p_edge": 0.95873}),
+                   "block_steps_per_run": m_max, "parallelism": f"rows{world}",
+                   "transport": comm["transport"], "transport_ranks": comm["nranks"],
+                   **({"rccl_version": comm["rccl_version"], "rccl_path": comm["rccl_path"]}
+                      if comm["transport"] == "rccl" else {}),
+                   **({"ranks_share_gpus": True, "gpus_used": min(world, ngpu)}
+                      if (args.transport == "shm" or rccl_host_per_rank()) and world > ngpu
+                      else {}),
+                   **({"rccl_host_per_rank": True} if rccl_host_per_rank() and world > 1
+                      else {}),
+                   "nnz_per_rank": nnz_ranks,
+                   **({"device_blocks": args.device_blocks} if args.device_blocks else {}),
+                   **({"keep_csr": 0} if not args.keep_csr else {}),
+                   **({"fuse": args.fuse} if args.fuse != 7 else {})},
+        "roofline": roofline,
+        "roofline_secondary": roofline2,
+        "stage_ms_per_run": {s: round(v, 3) for s, v in stage_per_run.items()},
+        "host_ms_per_run": meas["host_ms_per_run"],
+        "time_to_k": ttk,
+        "time_to_k_slow_spectrum": ttk_slow,
+        "matrix_gen_s": round(gen_s, 3),
+        "cpu_baseline": cpu,
+        "comm_per_step": meas["comm_per_step"], "run_ms_rank0": meas["run_ms"],
+        "c4b_rmat": rmat_rec,
+        "c3_circuit": c3_rec,
+        "c5_mixed": None,
+    }
+
+    def emit():
+        if rank == 0:
+            out = (json.dumps(line) + "\n").encode()
+            while out:
+                out = out[os.write(line_fd, out):]
+
+    # ---- BASELINE config 5: n = 5e7, fp32 basis, on >= 2 ranks (no spill) ----
+    if (args.matrix == "hashwindow" and args.c5_steps > 0 and args.basis_bits == 64
+            and world >= args.c5_min_ranks):
+        try:
+            line["c5_mixed"] = guarded(c5_subrecord, ctx, args, world, barrier, allmax, allsum,
+                                       allgather_i64)
+        except Exception as e:  # noqa: BLE001 — a rank-local failure: report, then end non-zero
+            line["c5_mixed"] = {"error": f"{type(e).__name__}: {e}", "rank": rank}
+            emit()
+            raise
+    emit()
     ctx.close()
     if dist is not None:
         dist.destroy_process_group()
@@ -676,6 +696,21 @@ def rmat_subrecord(ctx, args, plant, world, barrier, allmax, allsum, allgather_i
     ctx.synchronize()
     barrier()
     ttk_s = allmax(time.perf_counter() - t0)
+    # the relabelled matrix is P A P^T of the one drawn: the as-drawn matrix measured beside it
+    # keeps the line comparable with the rounds before the relabel (round 3: 16.95)
+    as_drawn = None
+    if relabel and args.rmat_as_drawn_steps > 0:
+        ctx.gen_rmat(args.n, args.rmat_scale, edges, args.seed, plant)
+        _, r0d, r1d, nnz_d = ctx.matrix_info()
+        md = measure(ctx, ra, "rmat", args.rmat_as_drawn_steps, 1, r1d - r0d, nnz_d, world,
+                     barrier, allmax)
+        as_drawn = {"value": round(md["value"], 3), "unit": "block iterations/s",
+                    "steps": args.rmat_as_drawn_steps, "warmup": 1,
+                    "ms_per_step": round(md["elapsed"] / args.rmat_as_drawn_steps * 1e3, 3),
+                    "spmm_ms_per_launch": next(r_["ms_per_launch"] for r_ in
+                                               (md["roofline"], md["roofline_secondary"])
+                                               if r_["kernel"].startswith("spmm")),
+                    "nnz_per_rank": allgather_i64(nnz_d)}
     return {"workload": "C4b R-MAT SpMM-Lanczos" if (args.n, args.b) == (10_000_000, 32)
             else "R-MAT SpMM-Lanczos",
             "metric": f"RBL iters/sec, n={args.n:.0e} nnz/row={nnz / args.n:.0f} b={args.b} (rmat)",
@@ -695,7 +730,8 @@ def rmat_subrecord(ctx, args, plant, world, barrier, allmax, allsum, allgather_i
             "time_to_k": {"seconds": round(ttk_s, 4), "iters": info.iters,
                           "converged": info.converged, "k": args.k,
                           "top_eigenvalues": [round(float(x), 6) for x in D[:3]]},
-            "matrix_gen_s": round(gen_s, 3)}
+            "matrix_gen_s": round(gen_s, 3),
+            **({"as_drawn": as_drawn} if as_drawn else {})}
 
 
 def c3_subrecord(ctx, args, world, barrier, allmax, allsum, allgather_i64):
@@ -809,19 +845,6 @@ def cpu_model() -> str:
     return "unknown"
 
 
-def cpu_cross_check() -> dict:
-    """The larger CPU sample beside the n = 1e5 extrapolation: the same port at n = 1e6 (129 s on
-    the box, too long for the default run), read from its committed bench line."""
-    try:
-        with open(os.path.join(ROOT, "profiles", "r02_bench_cpu1e6.json")) as f:
-            c = json.load(f)["cpu_baseline"]
-        return {"value_from_n1e6_sample": c["value"], "n1e6_sample_seconds": c["sample_seconds"],
-                "n1e6_sample_source": "profiles/r02_bench_cpu1e6.json (same port, same box type, "
-                                      "16 threads; scaled x10 to n = 1e7)"}
-    except (OSError, ValueError, KeyError):
-        return {}
-
-
 def cpu_baseline(args, m_max, plant):
     """Time the oracle (NumPy/SciPy restatement of RBL.jl) on n_s rows of the same generator
     for the same m_max fixed block steps (measured end to end, matrix generation excluded), and
@@ -865,7 +888,6 @@ def cpu_baseline(args, m_max, plant):
                      f"(nnz={A.nnz}) for the same {m_max} block steps: {t:.2f} s measured, i.e. "
                      f"{m_max / t:.4f} iters/s at n={ns}; value = that per-iteration time scaled "
                      f"x{scale:.0f} to n={args.n}",
-           **cpu_cross_check(),
            "sample_n": ns, "sample_seconds": round(t, 3),
            "sample_iters_per_s": round(m_max / t, 5),
            "host_cpus": os.cpu_count(), "cpu_model": cpu_model()}
@@ -874,7 +896,36 @@ def cpu_baseline(args, m_max, plant):
             t1 = timed()
         out.update({"value_1thread": round(m_max / (t1 * scale), 5),
                     "sample_seconds_1thread": round(t1, 3)})
+    if args.cpu_check_n and args.matrix == "hashwindow" and args.basis_bits == 64:
+        out["linear_scaling_check"] = cpu_scaling_check(args, plant, A, omega)
     return out
+
+
+def cpu_scaling_check(args, plant, A_small, omega_small):
+    """Measured in this run: the first `--cpu-check-steps` block steps (a fixed-step run, SURVEY
+    §8(d)) at the sample's n and at `--cpu-check-n` (10x by default), so the line itself shows
+    how the per-step time grows with n — the basis of the sample's linear scaling to n = 1e7."""
+    from oracle import matgen
+    from oracle import rbl_oracle as o
+    steps, n_big = args.cpu_check_steps, min(args.cpu_check_n, args.n)
+    A_big = matgen.hashwindow_csr(n_big, args.halfwidth, args.density, args.seed, plant)
+    omega_big = np.random.default_rng(0).standard_normal((n_big, args.b))
+
+    def fixed(A, om):
+        t0 = time.perf_counter()
+        o.RBL_gpu_semantics(A, args.k, args.b, omega=om, kryl_sz=args.kryl, check=False,
+                            max_steps=steps)
+        return time.perf_counter() - t0
+
+    t_small, t_big = fixed(A_small, omega_small), fixed(A_big, omega_big)
+    n_small = A_small.shape[0]
+    return {"block_steps": steps, "n_small": n_small, "seconds_small": round(t_small, 3),
+            "n_big": n_big, "nnz_big": int(A_big.nnz), "seconds_big": round(t_big, 3),
+            "time_ratio": round(t_big / t_small, 3), "n_ratio": round(n_big / n_small, 3),
+            "ms_per_block_step_big": round(t_big / steps * 1e3, 1),
+            "note": "rbl_start + the first block steps, convergence checks off, both timed in "
+                    "this run on the same threads; time_ratio ~ n_ratio supports the linear "
+                    "scaling of `value`"}
 
 
 if __name__ == "__main__":

@@ -1,11 +1,13 @@
 // comm.cpp — RCCL and in-process transports behind rbl::Comm (see comm.hpp).
 #include "comm.hpp"
 
+#include <dlfcn.h>
 #include <rccl/rccl.h>
 
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 
@@ -13,12 +15,79 @@ namespace rbl {
 
 namespace {
 
+// ---------------------------------------------------------------------------------------
+// The RCCL this library calls is ROCm's own (/opt/rocm/lib/librccl.so.1, or $RBL_RCCL_LIB),
+// opened here with RTLD_LOCAL | RTLD_DEEPBIND and called through the pointers below.  The
+// library is not linked against RCCL: with a DT_NEEDED entry, a process that imported torch
+// first had torch's bundled RCCL (same soname) serve every call, and one that did not had
+// ROCm's — the copy depended on import order.  Opened by path, ROCm's copy is the one used in
+// every process (a second copy beside torch's when torch is loaded; torch keeps its own).
+struct RcclApi {
+  bool ok = false;
+  std::string path, error;
+  int version = 0;
+  decltype(&::ncclGetErrorString) GetErrorString = nullptr;
+  decltype(&::ncclGetVersion) GetVersion = nullptr;
+  decltype(&::ncclGetUniqueId) GetUniqueId = nullptr;
+  decltype(&::ncclCommInitRank) CommInitRank = nullptr;
+  decltype(&::ncclCommDestroy) CommDestroy = nullptr;
+  decltype(&::ncclCommCount) CommCount = nullptr;
+  decltype(&::ncclAllReduce) AllReduce = nullptr;
+  decltype(&::ncclAllGather) AllGather = nullptr;
+  decltype(&::ncclSend) Send = nullptr;
+  decltype(&::ncclRecv) Recv = nullptr;
+  decltype(&::ncclGroupStart) GroupStart = nullptr;
+  decltype(&::ncclGroupEnd) GroupEnd = nullptr;
+};
+
+const RcclApi& rccl() {
+  static RcclApi api;
+  static std::once_flag once;
+  std::call_once(once, [] {
+    const char* env = std::getenv("RBL_RCCL_LIB");
+    const char* cands[] = {env && *env ? env : "/opt/rocm/lib/librccl.so.1", "librccl.so.1"};
+    void* h = nullptr;
+    for (const char* c : cands) {
+      h = dlopen(c, RTLD_NOW | RTLD_LOCAL | RTLD_DEEPBIND);
+      if (h) break;
+      api.error += std::string(api.error.empty() ? "" : "; ") + dlerror();
+    }
+    if (!h) return;
+    bool all = true;
+    auto sym = [&](auto& fp, const char* name) {
+      fp = reinterpret_cast<std::remove_reference_t<decltype(fp)>>(dlsym(h, name));
+      if (!fp) {
+        all = false;
+        api.error += std::string("; missing ") + name;
+      }
+    };
+    sym(api.GetErrorString, "ncclGetErrorString");
+    sym(api.GetVersion, "ncclGetVersion");
+    sym(api.GetUniqueId, "ncclGetUniqueId");
+    sym(api.CommInitRank, "ncclCommInitRank");
+    sym(api.CommDestroy, "ncclCommDestroy");
+    sym(api.CommCount, "ncclCommCount");
+    sym(api.AllReduce, "ncclAllReduce");
+    sym(api.AllGather, "ncclAllGather");
+    sym(api.Send, "ncclSend");
+    sym(api.Recv, "ncclRecv");
+    sym(api.GroupStart, "ncclGroupStart");
+    sym(api.GroupEnd, "ncclGroupEnd");
+    if (!all) return;
+    Dl_info di;
+    if (dladdr(reinterpret_cast<void*>(api.AllReduce), &di) && di.dli_fname) api.path = di.dli_fname;
+    if (api.GetVersion(&api.version) != ncclSuccess) api.version = 0;
+    api.ok = true;
+  });
+  return api;
+}
+
 int hip_fail(hipError_t e, const char* what, std::string* err) {
   if (err) *err = std::string(what) + ": " + hipGetErrorString(e);
   return -2;  // RBL_ERR_HIP
 }
 int nccl_fail(ncclResult_t r, const char* what, std::string* err) {
-  if (err) *err = std::string(what) + ": " + ncclGetErrorString(r);
+  if (err) *err = std::string(what) + ": " + rccl().GetErrorString(r);
   return -4;  // RBL_ERR_RCCL
 }
 
@@ -37,15 +106,15 @@ int nccl_fail(ncclResult_t r, const char* what, std::string* err) {
 struct RcclComm final : Comm {
   ncclComm_t comm = nullptr;
   ~RcclComm() override {
-    if (comm) ncclCommDestroy(comm);
+    if (comm) rccl().CommDestroy(comm);
   }
   const char* name() const override { return "rccl"; }
   int count(int* n, std::string* err) override {
-    NCCLX(ncclCommCount(comm, n));
+    NCCLX(rccl().CommCount(comm, n));
     return 0;
   }
   int allreduce_sum(double* dbuf, size_t count, hipStream_t st, std::string* err) override {
-    NCCLX(ncclAllReduce(dbuf, dbuf, count, ncclDouble, ncclSum, comm, st));
+    NCCLX(rccl().AllReduce(dbuf, dbuf, count, ncclDouble, ncclSum, comm, st));
     return 0;
   }
   int allgather_host(const int64_t* mine, int64_t* all, size_t n, hipStream_t st,
@@ -54,7 +123,7 @@ struct RcclComm final : Comm {
     HIPX(hipMalloc(&d_in, n * sizeof(int64_t)));
     HIPX(hipMalloc(&d_out, n * nranks * sizeof(int64_t)));
     HIPX(hipMemcpyAsync(d_in, mine, n * sizeof(int64_t), hipMemcpyHostToDevice, st));
-    NCCLX(ncclAllGather(d_in, d_out, n, ncclInt64, comm, st));
+    NCCLX(rccl().AllGather(d_in, d_out, n, ncclInt64, comm, st));
     HIPX(hipMemcpyAsync(all, d_out, n * nranks * sizeof(int64_t), hipMemcpyDeviceToHost, st));
     HIPX(hipStreamSynchronize(st));
     hipFree(d_in);
@@ -62,34 +131,47 @@ struct RcclComm final : Comm {
     return 0;
   }
   int exchange(const std::vector<Xfer>& x, hipStream_t st, std::string* err) override {
-    NCCLX(ncclGroupStart());
+    const RcclApi& api = rccl();
+    NCCLX(api.GroupStart());
     for (int q = 0; q < nranks; ++q) {
       if (q == rank) continue;
-      if (x[q].nsend) NCCLX(ncclSend(x[q].send, x[q].nsend, ncclDouble, q, comm, st));
-      if (x[q].nrecv) NCCLX(ncclRecv(x[q].recv, x[q].nrecv, ncclDouble, q, comm, st));
+      if (x[q].nsend) NCCLX(api.Send(x[q].send, x[q].nsend, ncclDouble, q, comm, st));
+      if (x[q].nrecv) NCCLX(api.Recv(x[q].recv, x[q].nrecv, ncclDouble, q, comm, st));
     }
-    NCCLX(ncclGroupEnd());
+    NCCLX(api.GroupEnd());
     return 0;
   }
 };
 
 }  // namespace
 
+int rccl_library(int* version, std::string* path, std::string* err) {
+  const RcclApi& api = rccl();
+  if (!api.ok) {
+    if (err) *err = "RCCL not loaded: " + api.error;
+    return -4;
+  }
+  if (version) *version = api.version;
+  if (path) *path = api.path;
+  return 0;
+}
+
 int rccl_unique_id(uint8_t unique_id[128]) {
   ncclUniqueId id;
   static_assert(sizeof(id) == 128, "ncclUniqueId size");
-  if (ncclGetUniqueId(&id) != ncclSuccess) return -4;
+  if (!rccl().ok || rccl().GetUniqueId(&id) != ncclSuccess) return -4;
   memcpy(unique_id, &id, 128);
   return 0;
 }
 
 Comm* make_rccl_comm(int nranks, int rank, const uint8_t unique_id[128], std::string* err) {
+  if (rccl_library(nullptr, nullptr, err)) return nullptr;
   auto* c = new RcclComm();
   c->nranks = nranks;
   c->rank = rank;
   ncclUniqueId id;
   memcpy(&id, unique_id, 128);
-  const ncclResult_t r = ncclCommInitRank(&c->comm, nranks, id, rank);
+  const ncclResult_t r = rccl().CommInitRank(&c->comm, nranks, id, rank);
   if (r != ncclSuccess) {
     nccl_fail(r, "ncclCommInitRank", err);
     c->comm = nullptr;

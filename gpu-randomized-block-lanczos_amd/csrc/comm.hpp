@@ -54,6 +54,9 @@ struct Comm {
 
 Comm* make_rccl_comm(int nranks, int rank, const uint8_t unique_id[128], std::string* err);
 int rccl_unique_id(uint8_t unique_id[128]);
+// the RCCL every RcclComm calls (ROCm's, opened by path: comm.cpp): ncclGetVersion's code
+// (e.g. 22707 for 2.27.7) and the file it was loaded from
+int rccl_library(int* version, std::string* path, std::string* err);
 
 struct LocalGroup;
 LocalGroup* local_group_create(int nranks);

@@ -78,6 +78,7 @@ struct CsrDev {
   // (spmm_bt_locfix_ok: applicable; spmm_bt_locfix_edges: the rank-edge rows beforehand)
   const double* lfix_c = nullptr;
   double* lfix_q = nullptr;
+  int* two_wave = nullptr;          // set to 1 when the two-waves-per-SIMD kernel (k_spmm_bt2) ran
   int64_t lfix_lo = 0, lfix_hi = 0;  // local rows still raw (several ranks: the rank's first and
                                      // last H rows were corrected before the halo exchange)
   // packed band tiles (bt_pack): per tile slot a header of bt_pack_words(NG) 8-B words (per

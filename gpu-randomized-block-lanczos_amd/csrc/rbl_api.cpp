@@ -192,6 +192,9 @@ struct rbl_ctx {
   // collectives issued by this rank since the last reset (rbl_comm_stats): all-reduce calls and
   // bytes, grouped halo exchanges and the bytes sent / received in them
   int64_t comm_stats[RBL_COMM_NSTATS] = {0};
+  // which code path each step took (rbl_path_stats): counted on the host as the work is issued,
+  // so a test can assert the path itself instead of timing it
+  int64_t path_stats[RBL_PATH_NSTATS] = {0};
   struct Mark { int stage; hipEvent_t a, b; };
   std::vector<Mark> marks;
   std::vector<hipEvent_t> ev_pool;
@@ -1251,6 +1254,8 @@ int apply_A(rbl_ctx* ctx, const double* Qin, int64_t off, int b, double* U, cons
       A.loc_hi = ctx->r0 + ctx->nloc;
     }
     A.seg_wait = seg_wait;  // own/halo column tiers: the halo tier waits for the exchange
+    int two_wave = 0;
+    A.two_wave = &two_wave;
     if (lfix_c) {  // local reorth fused into the SpMM's staging (RBL_OPT_FUSE bit 2)
       A.lfix_c = lfix_c;
       A.lfix_q = lfix_q;
@@ -1259,7 +1264,11 @@ int apply_A(rbl_ctx* ctx, const double* Qin, int64_t off, int b, double* U, cons
     }
     const int parts = spmm(A, Qin, off, b, U, Qprev, Bi, ctx->spmm_variant, ctx->stream, slab);
     if (parts < 0) return fail(ctx, RBL_ERR_INVALID, "internal: split-source SpMM needs the band-tile kernel");
+    ctx->path_stats[RBL_PATH_SPMM] += 1;
+    ctx->path_stats[RBL_PATH_SPMM_TWO_WAVE] += two_wave;
     if (lfix_c) {
+      ctx->path_stats[RBL_PATH_SPMM_LOC_FUSED] += 1;
+      ctx->path_stats[RBL_PATH_LOCFIX_REST] += 1;
       StageScope t(ctx, RBL_STAGE_LOC_REORTH);
       spmm_bt_locfix_rest(A, lfix_q, Qprev, lfix_c, ctx->stream);
     }
@@ -2142,6 +2151,14 @@ int rbl_comm_info(rbl_ctx* ctx, int* nranks, int* rank, char* transport, int tra
   return RBL_OK;
 }
 
+int rbl_rccl_version(int* version, char* path, int path_len) {
+  if (!version) return RBL_ERR_INVALID;
+  std::string p, err;
+  const int s = rbl::rccl_library(version, &p, &err);
+  if (path && path_len > 0) snprintf(path, (size_t)path_len, "%s", s ? err.c_str() : p.c_str());
+  return s ? RBL_ERR_RCCL : RBL_OK;
+}
+
 int rbl_set_option(rbl_ctx* ctx, int option, int64_t value) {
   if (!ctx) return RBL_ERR_INVALID;
   switch (option) {
@@ -2690,6 +2707,15 @@ int rbl_start(rbl_ctx* ctx, int b, int max_blocks, int basis_bits, const double*
   HIPC(hipHostMalloc(&ctx->h_hist, (size_t)(max_blocks + 2) * 2 * b * b * sizeof(double), hipHostMallocDefault));
   HIPC(hipHostMalloc(&ctx->h_hflags, (size_t)(max_blocks + 2) * 4 * sizeof(int), hipHostMallocDefault));
   }
+  // the push/pull split's partial-row buffers (sized by the matrix held, so also on a reused
+  // plan): allocated here, inside the vote, not lazily in the first push exchange — a rank
+  // failing there would leave its peers waiting in that exchange
+  if (ctx->push && ctx->nranks > 1 && use_ghost(ctx, b)) {  // push_on() once this b exchanges
+    const char* inj = std::getenv("RBL_FAULT_PUSH_ALLOC");  // fault injection for the vote's test
+    if (inj && *inj && std::atoi(inj) == ctx->rank)
+      return fail(ctx, RBL_ERR_OOM, "rbl_start: push buffers (injected by RBL_FAULT_PUSH_ALLOC)");
+    CHK(ensure_push(ctx, b));
+  }
   return RBL_OK;
   }();
   if (ctx->nranks > 1) {
@@ -2895,7 +2921,10 @@ int step_impl(rbl_ctx* ctx, int i, int part_reorth, double* A_out, double* B_out
     StageScope t(ctx, RBL_STAGE_LOC_REORTH);
     const bool have = ctx->cloc_step == i && (ctx->cloc_final || !modifies(i, part_reorth));
     const double* C = have ? smallp(ctx, S_CLOC) : ctx->d_C;
-    if (!have) CHK(gram(ctx, run1(Qm, b), pan1(Qi, b), ctx->d_C, nullptr));
+    if (!have) {
+      CHK(gram(ctx, run1(Qm, b), pan1(Qi, b), ctx->d_C, nullptr));
+      ctx->path_stats[RBL_PATH_LOC_GRAM] += 1;
+    }
     if (lfuse) {
       Cloc = C;
       if (ctx->nranks > 1) {  // the rows the neighbours receive: corrected before the exchange
@@ -2904,11 +2933,15 @@ int step_impl(rbl_ctx* ctx, int i, int part_reorth, double* A_out, double* B_out
         lf_hi = std::max<int64_t>(lf_lo, ctx->nloc - H);
         spmm_bt_locfix_edges(csr(ctx), Qi, Qm, C, 0, lf_lo, lf_hi, ctx->nloc, ctx->stream);
         HIPC(hipGetLastError());
+        ctx->path_stats[RBL_PATH_LOCFIX_EDGES] += 1;
       }
-    } else if (fused)
+    } else if (fused) {
       CHK(rowop(ctx, Qm, C, Qi, -1.0, 1.0, nullptr, nullptr));
-    else
+      ctx->path_stats[RBL_PATH_LOC_SEPARATE] += 1;
+    } else {
       CHK(tsmm_checked(ctx, run1(Qm, b), C, b, pan1(Qi, b), -1.0, 1.0, nullptr));
+      ctx->path_stats[RBL_PATH_LOC_SEPARATE] += 1;
+    }
   }
   ctx->cloc_step = 0;
   ctx->cloc_final = false;
@@ -3266,6 +3299,14 @@ int rbl_comm_stats(rbl_ctx* ctx, int64_t* out, int nstats, int reset) {
   for (int i = RBL_COMM_PULL_ROWS + 1; i < nstats; ++i) out[i] = 0;
   if (reset)
     for (int64_t& v : ctx->comm_stats) v = 0;
+  return RBL_OK;
+}
+
+int rbl_path_stats(rbl_ctx* ctx, int64_t* out, int nstats, int reset) {
+  if (!ctx || nstats < 0 || (nstats > 0 && !out)) return RBL_ERR_INVALID;
+  for (int i = 0; i < nstats; ++i) out[i] = i < RBL_PATH_NSTATS ? ctx->path_stats[i] : 0;
+  if (reset)
+    for (int64_t& v : ctx->path_stats) v = 0;
   return RBL_OK;
 }
 

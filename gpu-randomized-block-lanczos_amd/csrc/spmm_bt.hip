@@ -1081,6 +1081,7 @@ bool spmm_bt(const CsrDev& A, const double* Qin, int64_t col_off, int b, double*
     a.lf_lo = A.lfix_lo;
     a.lf_hi = A.lfix_hi;
     if (bt2_on()) {
+      if (A.two_wave) *A.two_wave = 1;
       if (a.Ah) {
         if (A.bt_ng == 9) launch_bt2_v<9, true, true, 1024 | 2048>(a, grid, s);
         else launch_bt2_v<5, true, true, 1024 | 2048>(a, grid, s);
@@ -1100,6 +1101,7 @@ bool spmm_bt(const CsrDev& A, const double* Qin, int64_t col_off, int b, double*
     return true;
   }
   if (bt2_on() && b == 32 && epi && aig && !f32 && !a.hdr) {
+    if (A.two_wave) *A.two_wave = 1;
     a.lf_lo = 0;
     a.lf_hi = 0;
     if (a.Ah) {

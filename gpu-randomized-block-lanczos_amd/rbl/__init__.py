@@ -8,4 +8,5 @@ from ._lib import RBLError, lib, stage_names  # noqa: F401  (raises ImportError 
 from .host import TBand, check_convergence, dsbev, sort_eig_abs  # noqa: F401
 from . import io  # noqa: F401
 from .restarted import RBL_gpu_restarted, RBL_restarted  # noqa: F401
-from .rbl_gpu import KRYL_SZ_GPU, RESIDUAL_TOL, Context, RBL_gpu, RBLInfo, LocalGroup, lanczos  # noqa: F401
+from .rbl_gpu import (KRYL_SZ_GPU, RESIDUAL_TOL, Context, RBL_gpu, RBLInfo, LocalGroup,  # noqa: F401
+                      lanczos, rccl_version)

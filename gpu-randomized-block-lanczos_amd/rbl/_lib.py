@@ -34,6 +34,15 @@ RBL_OPT_FUSE = 6
 RBL_OPT_HALO_OVERLAP = 7
 RBL_OPT_RELABEL = 8
 RBL_OPT_HALO_PUSH = 9
+# rbl_path_stats entries
+RBL_PATH_SPMM = 0
+RBL_PATH_SPMM_LOC_FUSED = 1
+RBL_PATH_LOC_SEPARATE = 2
+RBL_PATH_LOC_GRAM = 3
+RBL_PATH_LOCFIX_EDGES = 4
+RBL_PATH_LOCFIX_REST = 5
+RBL_PATH_SPMM_TWO_WAVE = 6
+RBL_PATH_NSTATS = 7
 
 _p = C.c_void_p
 _i64 = C.c_int64
@@ -56,6 +65,7 @@ SIGNATURES = {
     "rbl_free": (C.c_int, [_p]),
     "rbl_last_error": (C.c_char_p, [_p]),
     "rbl_comm_info": (C.c_int, [_p, C.POINTER(C.c_int), C.POINTER(C.c_int), C.c_char_p, C.c_int]),
+    "rbl_rccl_version": (C.c_int, [C.POINTER(C.c_int), C.c_char_p, C.c_int]),
     "rbl_set_option": (C.c_int, [_p, C.c_int, _i64]),
     "rbl_device_memory": (C.c_int, [_p, _pi64, _pi64]),
     "rbl_set_matrix_csc": (C.c_int, [_p, _i64, _i64, _pi64, _pi64, _pd, C.c_int]),
@@ -89,6 +99,7 @@ SIGNATURES = {
     "rbl_timers": (C.c_int, [_p, _pd, C.c_int]),
     "rbl_reset_timers": (C.c_int, [_p]),
     "rbl_comm_stats": (C.c_int, [_p, _pi64, C.c_int, C.c_int]),
+    "rbl_path_stats": (C.c_int, [_p, _pi64, C.c_int, C.c_int]),
     "rbl_synchronize": (C.c_int, [_p]),
     "rbl_plan_row_partition": (C.c_int, [_i64, _pi64, C.c_int, _pi64]),
     "rbl_plan_halo": (C.c_int, [_i64, _pi64, _pi64, C.c_int, C.c_int, _pi64, _pi64, _pi64]),

@@ -306,7 +306,10 @@ class Context:
         n, r = C.c_int(0), C.c_int(0)
         buf = C.create_string_buffer(32)
         self._check(lib.rbl_comm_info(self._h, C.byref(n), C.byref(r), buf, 32), "rbl_comm_info")
-        return {"nranks": n.value, "rank": r.value, "transport": buf.value.decode()}
+        out = {"nranks": n.value, "rank": r.value, "transport": buf.value.decode()}
+        if out["transport"] == "rccl":
+            out.update(rccl_version())
+        return out
 
     def comm_stats(self, reset: bool = False) -> dict:
         """Collectives this rank issued since the last reset (rbl_comm_stats): all-reduce
@@ -318,6 +321,17 @@ class Context:
         return dict(zip(("allreduce_calls", "allreduce_bytes", "exchange_calls", "send_bytes",
                          "recv_bytes", "halo_push", "push_rows_pred", "pull_rows_pred"),
                         (int(x) for x in out)))
+
+    def path_stats(self, reset: bool = False) -> dict:
+        """Which code path the steps took since the last reset (rbl_path_stats), counted as the
+        work is issued: SpMM launches, those that applied the local-reorth update, separate
+        local-reorth passes and Grams, the fused path's edge fix-ups, two-wave SpMM launches."""
+        from . import _lib as L
+        out = np.zeros(L.RBL_PATH_NSTATS, np.int64)
+        self._check(lib.rbl_path_stats(self._h, i64ptr(out), L.RBL_PATH_NSTATS, int(reset)),
+                    "rbl_path_stats")
+        return dict(zip(("spmm", "spmm_loc_fused", "loc_separate", "loc_gram", "locfix_edges",
+                         "locfix_rest", "spmm_two_wave"), (int(x) for x in out)))
 
     def synchronize(self) -> None:
         self._check(lib.rbl_synchronize(self._h), "rbl_synchronize")
@@ -337,6 +351,22 @@ class RBLInfo:
     enqueue_ms: float = 0.0      # host time inside rbl_step_async (enqueueing the steps)
     trace_A: list = field(default_factory=list)
     trace_B: list = field(default_factory=list)
+
+
+def rccl_version() -> dict:
+    """The RCCL the library's RCCL transport calls (rbl_rccl_version: ROCm's own, opened by path
+    whatever copy the process loaded first): {"rccl_version": "2.27.7", "rccl_version_code":
+    22707, "rccl_path": file}.  No GPU call."""
+    import ctypes as C
+    v = C.c_int(0)
+    buf = C.create_string_buffer(512)
+    st = lib.rbl_rccl_version(C.byref(v), buf, 512)
+    if st != 0:
+        raise RBLError(st, f"rbl_rccl_version: {buf.value.decode()}")
+    code = v.value
+    # NCCL_VERSION(X,Y,Z): X*10000 + Y*100 + Z from 2.9 on
+    return {"rccl_version": f"{code // 10000}.{code // 100 % 100}.{code % 100}",
+            "rccl_version_code": code, "rccl_path": buf.value.decode()}
 
 
 def max_steps_for(kryl_sz: int, b: int) -> int:

@@ -169,6 +169,12 @@ const char* rbl_last_error(const rbl_ctx* ctx);
 /* Ranks as the transport itself counts them (RCCL: ncclCommCount; in-process group: its size;
  * one rank: 1, transport "none"), this context's rank, and the transport's name. */
 int rbl_comm_info(rbl_ctx* ctx, int* nranks, int* rank, char* transport, int transport_len);
+/* The RCCL library every RCCL-transport context calls: ROCm's own, opened by path
+ * (/opt/rocm/lib/librccl.so.1, or $RBL_RCCL_LIB) with a private symbol scope, whatever else
+ * the process loaded first (torch bundles another RCCL with the same soname).  version gets
+ * ncclGetVersion's code (22707 = 2.27.7); path (optional) the file it was loaded from, or the
+ * loader's error.  No GPU call: safe before any context exists. */
+int rbl_rccl_version(int* version, char* path, int path_len);
 int rbl_set_option(rbl_ctx* ctx, int option, int64_t value);
 /* Free and total HBM of the context's device (hipMemGetInfo): what a caller checks before it
  * sizes a run (the reference sizes its buffer from CUDA.available_memory, RBL_gpu.jl:95-104). */
@@ -324,6 +330,19 @@ int rbl_synchronize(rbl_ctx* ctx);
 #define RBL_COMM_PUSH_ROWS       6
 #define RBL_COMM_PULL_ROWS       7
 int rbl_comm_stats(rbl_ctx* ctx, int64_t* out, int nstats, int reset);
+
+/* Which code path the block steps took, counted as the work is issued (since the last reset;
+ * nstats entries, missing ones 0).  Stage timers cannot show this when ranks share a GPU (a
+ * stage's events also span the other ranks' kernels); these counts are exact. */
+#define RBL_PATH_SPMM            0  /* SpMM launches on a sparse A                              */
+#define RBL_PATH_SPMM_LOC_FUSED  1  /* ... of which applied the local-reorth update to Q_i      */
+#define RBL_PATH_LOC_SEPARATE    2  /* local-reorth updates run as their own pass              */
+#define RBL_PATH_LOC_GRAM        3  /* local-reorth Grams not formed by the producing pass     */
+#define RBL_PATH_LOCFIX_EDGES    4  /* rank-edge rows corrected before the halo exchange       */
+#define RBL_PATH_LOCFIX_REST     5  /* range-edge rows corrected after a fused SpMM            */
+#define RBL_PATH_SPMM_TWO_WAVE   6  /* SpMM launches served by the two-waves-per-SIMD kernel   */
+#define RBL_PATH_NSTATS          7
+int rbl_path_stats(rbl_ctx* ctx, int64_t* out, int nstats, int reset);
 
 /* ---- host-only planning (callable without a GPU) -------------------------------------- */
 /* nnz-balanced contiguous row partition: bounds_out[0..nranks] (bounds_out[0]=0). */

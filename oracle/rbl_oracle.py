@@ -105,7 +105,10 @@ def part_reorth(Q: list, mode: str = "mgs") -> None:
     """RBL.jl:30-48: reorthogonalise Q[i] and Q[i-1] against Q[1..i-2] (1-based).
 
     ``mode="mgs"`` is the reference's ascending-j block MGS; ``"cgs"`` is one block-CGS
-    projection against all j at once (the HIP path's batched form).
+    projection against all j at once (the HIP path's batched form).  ``"cgs_blocked"`` is the
+    same CGS projection (every coefficient from the unmodified X) evaluated block by block, so
+    that no (n x (i-2)b) copy of the basis is made: it differs from ``"cgs"`` only in the
+    association of the sums, and lets the oracle run at n = 1e7 in a 62 GB container.
     """
     i = len(Q)
     if i < 3:
@@ -115,6 +118,11 @@ def part_reorth(Q: list, mode: str = "mgs") -> None:
             Qj = Q[j]
             Q[i - 1] -= Qj @ (Qj.T @ Q[i - 1])
             Q[i - 2] -= Qj @ (Qj.T @ Q[i - 2])
+    elif mode == "cgs_blocked":
+        C = [(Q[j].T @ Q[i - 1], Q[j].T @ Q[i - 2]) for j in range(i - 2)]
+        for j in range(i - 2):
+            Q[i - 1] -= Q[j] @ C[j][0]
+            Q[i - 2] -= Q[j] @ C[j][1]
     else:
         W = np.hstack(Q[: i - 2])
         X = np.hstack([Q[i - 1], Q[i - 2]])

@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Full-size eigenvalue fixtures for BASELINE configs 2 and 3 (committed; regenerate from the
-repo root with ``python tests/golden/make_fullsize.py [c2|c3|c4b]``; ~2-10 min each on 8 cores).
+repo root with ``python tests/golden/make_fullsize.py [c2|c3|c4b|c4a]``; ~2-10 min each on 8
+cores, c4a ~30 min and ~45 GB of host memory).
 
 The expected outputs come from the oracle (oracle/rbl_oracle.py: the CPU restatement of
 RBL.jl:74-142 with the GPU driver's bounds, RBL_gpu.jl:134-219, and the HIP path's choices —
@@ -19,6 +20,12 @@ Fixtures are data only: the generator parameters, Omega's seed, and the outputs.
                  C4b draw density: ~100 nnz/row after symmetrising and merging; hub rows of
                  ~1e5 nonzeros, so the segmented gather splits them), planted top spectrum;
                  b = 32, k = 20.  The device generator (gen_rmat.hip) builds the same bits.
+
+  golden_c4a.npz BASELINE's headline config at FULL size (the bench's C4a workload): n = 1e7
+                 hash-window (half-width 64, density 0.7734: ~100 nnz/row, 0.9999 G nonzeros),
+                 planted top spectrum, b = 32, k = 20.  Built in row chunks; the partial
+                 reorth is the same block CGS evaluated block by block (reorth_mode
+                 "cgs_blocked") so the oracle fits the 62 GB container.
 
 Each holds D (k, descending |lambda|), the iteration count, and per Ritz vector its 16
 largest-magnitude entries (row ids + values) — enough to compare vectors up to sign without
@@ -40,6 +47,8 @@ from oracle import rbl_oracle as o  # noqa: E402
 C2 = dict(n=1_000_000, halfwidth=32, density=0.7734, seed=20261015, b=16, k=20, omega_seed=2)
 C3 = dict(n=matgen.G3_CIRCUIT_N, seed=20261015, b=16, k=20, omega_seed=3)
 C4B = dict(n=1_000_000, scale=20, edges=66_000_000, seed=20261015, b=32, k=20, omega_seed=4)
+# BASELINE's headline config (the bench's C4a workload): n = 1e7, half-width 64, ~100 nnz/row
+C4A = dict(n=10_000_000, halfwidth=64, density=0.7734, seed=20261015, b=32, k=20, omega_seed=5)
 TOP = 16
 
 
@@ -57,14 +66,35 @@ def c4b_matrix():
                            matgen.planted_spectrum(C4B["k"]))
 
 
+def c4a_matrix(chunk=200_000):
+    """C4a's CSR built in row chunks (the one-shot generator would need ~10 GB per candidate
+    array at n = 1e7); the chunks are matgen.hashwindow_csr's own rows, so the result is the
+    same matrix bit for bit.  int32 indices: nnz < 2^31."""
+    import scipy.sparse as sp
+    n, W, p, seed = C4A["n"], C4A["halfwidth"], C4A["density"], C4A["seed"]
+    plant = matgen.planted_spectrum(C4A["k"])
+    vals, cols, counts = [], [], []
+    for r0 in range(0, n, chunk):
+        A = matgen.hashwindow_csr(n, W, p, seed, plant, r0, min(n, r0 + chunk))
+        vals.append(A.data)
+        cols.append(A.indices.astype(np.int32))
+        counts.append(np.diff(A.indptr))
+    rowptr = np.zeros(n + 1, dtype=np.int64)
+    np.cumsum(np.concatenate(counts), out=rowptr[1:])
+    val = np.concatenate(vals); del vals
+    col = np.concatenate(cols); del cols
+    assert rowptr[-1] < 2 ** 31
+    return sp.csr_matrix((val, col, rowptr.astype(np.int32)), shape=(n, n))
+
+
 def omega_for(cfg):
     return np.random.default_rng(cfg["omega_seed"]).standard_normal((cfg["n"], cfg["b"]))
 
 
-def run(name, cfg, A):
+def run(name, cfg, A, reorth_mode="cgs"):
     t0 = time.perf_counter()
     res = o.RBL_gpu_semantics(A, cfg["k"], cfg["b"], omega=omega_for(cfg), qr_mode="posdiag",
-                              reorth_mode="cgs")
+                              reorth_mode=reorth_mode)
     dt = time.perf_counter() - t0
     assert res.converged, name
     V = res.V
@@ -72,11 +102,15 @@ def run(name, cfg, A):
     vals = np.take_along_axis(V, idx, axis=0)
     r = np.linalg.norm(A @ V - V * res.D, axis=0) / np.abs(res.D)
     out = os.path.join(HERE, f"golden_{name}.npz")
+    import resource
+    peak_rss_gb = resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 2 ** 20
     np.savez_compressed(out, D=res.D, iters=res.iters, top_idx=idx.astype(np.int64), top_val=vals,
-                        residual=r, nnz=A.nnz, oracle_seconds=dt,
+                        residual=r, nnz=A.nnz, oracle_seconds=dt, peak_rss_gb=peak_rss_gb,
+                        reorth_mode=reorth_mode,
                         **{f"cfg_{key}": v for key, v in cfg.items()})
     print(f"{name}: n={A.shape[0]} nnz={A.nnz} iters={res.iters} D[:3]={res.D[:3]} "
-          f"max residual={r.max():.2e} ({dt:.1f} s) -> {out}", flush=True)
+          f"max residual={r.max():.2e} ({dt:.1f} s, peak RSS {peak_rss_gb:.1f} GB) -> {out}",
+          flush=True)
 
 
 def main(which):
@@ -86,6 +120,12 @@ def main(which):
         run("c3", C3, c3_matrix())
     if "c4b" in which:
         run("c4b", C4B, c4b_matrix())
+    if "c4a" in which:
+        t0 = time.perf_counter()
+        A = c4a_matrix()
+        print(f"c4a: matrix {A.nnz} nonzeros in {time.perf_counter() - t0:.1f} s", flush=True)
+        # block CGS evaluated block by block: no n x (i-2)b copy of the basis (62 GB container)
+        run("c4a", C4A, A, reorth_mode="cgs_blocked")
 
 
 if __name__ == "__main__":

@@ -59,6 +59,8 @@ def main():
         info = ctx.comm_info()
         res["transport"] = np.array(info["transport"])
         res["transport_ranks"] = info["nranks"]
+        res["rccl_version"] = np.array(info["rccl_version"])
+        res["rccl_path"] = np.array(info["rccl_path"])
         for c in cases:
             for key, v in mp_rank.run_case(rbl, ctx, c).items():
                 res[f"{c['name']}__{key}"] = v

@@ -9,7 +9,8 @@ vote, build_ghosts' request exchange), the indexed halo with the side-stream ove
 halo a ghost-built context falls back to for b outside {16, 32} or a pinned gather kernel, fp64
 and fp32 bases, and matrices replaced in place on one context (bench.py's sub-records).
 
-The same cases also run over RCCL itself with 2 and 4 processes on the one GPU
+The same cases also run over RCCL itself with 2, 3, 4 and 8 processes on the one GPU (8: the
+largest point of the driver's 1 -> 8 curve; 3: a ragged, non-power-of-two split)
 (tests/rccl_rank.py: each rank declares its own host id, so RCCL connects the ranks through its
 network transport on the loopback interface instead of refusing two ranks on one device).
 
@@ -139,7 +140,7 @@ def _launch_rccl(rank_launcher, P, tmp):
     return res
 
 
-@pytest.fixture(scope="module", params=[2, 4])
+@pytest.fixture(scope="module", params=[2, 3, 4, 8])
 def rccl_procs(request, rank_launcher, tmp_path_factory):
     P = request.param
     return P, _launch_rccl(rank_launcher, P, str(tmp_path_factory.mktemp(f"rccl{P}")))
@@ -170,6 +171,19 @@ def test_rccl_ranks_on_one_gpu(rccl_procs, single, inproc, case):
     assert all(cm[2] > 0 for cm in comm), "no halo exchange"
     if c.get("push") is not None:
         assert all(cm[2] == (c["steps"] + 1) * (2 if c["push"] else 1) for cm in comm)
+
+
+def test_rccl_library_is_rocms(rccl_procs, rbl):
+    """Every rank's RCCL transport calls ROCm's own RCCL (rbl_rccl_version: opened by path with
+    a private symbol scope), the same copy as this process and as bench.py — whatever else a
+    process loaded first (torch bundles another RCCL under the same soname)."""
+    P, res = rccl_procs
+    mine = rbl.rccl_version()
+    print(f"RCCL P={P}: {mine}")
+    assert mine["rccl_path"].startswith("/opt/rocm")
+    for r in res:
+        assert str(r["rccl_version"]) == mine["rccl_version"]
+        assert str(r["rccl_path"]) == mine["rccl_path"]
 
 
 @pytest.mark.parametrize("case", ["c4b", "c3"])

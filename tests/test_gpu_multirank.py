@@ -182,29 +182,52 @@ def test_multirank_local_reorth_fused_into_spmm(rbl, P, n, W):
             assert d < 1e-12, d
 
 
+@pytest.mark.parametrize("bt2", ["0", "1"])
 @pytest.mark.parametrize("P", [1, 2])
-def test_multirank_fused_local_reorth_runs(rbl, P):
-    """The fused path really replaces the separate pass on 1 and 2 ranks: its loc-reorth stage
-    (the rank-edge and range-edge fix-ups only) takes a fraction of the separate pass's time."""
-    n, W, k, b = 2_000_000, 64, 10, 32
+def test_multirank_fused_local_reorth_runs(rbl, monkeypatch, P, bt2):
+    """The fused path really replaces the separate pass on 1 and 2 ranks, with the one-wave
+    band-tile SpMM (RBL_BT2=0, default) and the two-waves-per-SIMD one (RBL_BT2=1).  Asserted on
+    the library's path counters (rbl_path_stats), not on stage times: with both ranks on one GPU
+    a stage's events also span the other rank's kernels (round 4's RBL_BT2=1 run measured rank
+    0's loc-reorth stage at 2.65 ms fused against 1.46 ms separate — about one of rank 1's SpMM
+    launches per step, ~0.37 ms at 1e6 rows, waiting in front of rank 0's small fix-up kernels
+    while the persistent SpMM held every CU's LDS).  Fused (RBL_OPT_FUSE 7): every step from
+    i = 2 on applies the update inside the SpMM, fixes the range edges after it (and on several
+    ranks the rank edges before the exchange), and runs no separate pass; unfused (3): a
+    separate pass per step and no fused SpMM.  Both give the same A_i / B_{i+1} to 1e-12."""
+    monkeypatch.setenv("RBL_BT2", bt2)
+    n, W, k, b, steps = 2_000_000, 64, 10, 32, 8
     plant = matgen.planted_spectrum(k)
 
     def run(fuse):
         def fn(ctx, r):
-            ctx.set_option(rbl._lib.RBL_OPT_TIMERS, 1)
             ctx.set_option(rbl._lib.RBL_OPT_FUSE, fuse)
             ctx.gen_hashwindow(n, W, 0.7734, 17, plant)
-            rbl.lanczos(ctx, k, b, seed=9, check=False, max_steps=8, ritz=False)
-            return ctx.timers()["loc reorth"]
+            assert ctx.spmm_kernel_for(b) == 5
+            ctx.path_stats(reset=True)
+            _, _, info = rbl.lanczos(ctx, k, b, seed=9, check=False, max_steps=steps,
+                                     ritz=False, trace=True)
+            return ctx.path_stats(), info
         if P == 1:
             with rbl.Context(0) as ctx:
                 return [fn(ctx, 0)]
         return run_ranks(rbl, P, fn)
 
     t7, t3 = run(7), run(3)
-    # the ranks share one GPU here, so a rank's stage events can include the other rank's kernels
-    # (a 157 KB-LDS SpMM workgroup holds a whole CU): compare the least-disturbed rank
-    assert min(t7) < 0.5 * min(t3), (t7, t3)
+    for (p7, i7), (p3, i3) in zip(t7, t3):
+        loc_steps = len(i7.trace_A) - 1                    # block steps i >= 2
+        assert loc_steps >= 6 and p7["spmm"] == p3["spmm"] == len(i7.trace_A) + 1
+        assert p7["spmm_loc_fused"] == loc_steps and p7["loc_separate"] == 0
+        assert p7["locfix_rest"] == loc_steps
+        assert p7["locfix_edges"] == (loc_steps if P > 1 else 0)
+        assert p3["spmm_loc_fused"] == 0 and p3["loc_separate"] == loc_steps
+        assert p3["locfix_rest"] == p3["locfix_edges"] == 0
+        if bt2 == "1":   # every step launch (EPI + A_i partials) on the two-wave kernel
+            assert p7["spmm_two_wave"] >= loc_steps and p3["spmm_two_wave"] >= loc_steps
+        else:
+            assert p7["spmm_two_wave"] == p3["spmm_two_wave"] == 0
+        for a, a1 in zip(i7.trace_A + i7.trace_B, i3.trace_A + i3.trace_B):
+            assert np.abs(a - a1).max() <= 1e-12 * np.abs(a1).max()
 
 
 def test_multirank_half_band_tiles_bit_identical(rbl, monkeypatch):

@@ -6,6 +6,8 @@ The device generator must match the NumPy restatement (oracle/matgen.py rmat_csr
 in-process ranks.  SpMM: every element within 1e-13 (|A| |X|) of SciPy.  Eigenvalues: 1e-10
 relative against the oracle (parity unpinned beyond the restatement: the reference has no
 R-MAT fixture)."""
+import os
+
 import numpy as np
 import pytest
 
@@ -566,3 +568,39 @@ def test_rmat_halo_push_needs_symmetric_pattern(rbl):
     Y = np.vstack([y for _, y in auto])
     bound = (abs(M) @ np.abs(X)) * 1e-13 + 1e-300
     assert np.all(np.abs(Y - M @ X) <= bound)
+
+
+def test_push_buffer_allocation_failure_is_collective(rbl, monkeypatch):
+    """The push/pull split's partial-row buffers are allocated inside rbl_start's allocation
+    vote (not lazily in the first push exchange): when rank 1 cannot allocate them
+    (RBL_FAULT_PUSH_ALLOC=1 injects the failure at exactly that allocation) every rank returns
+    RBL_ERR_OOM from rbl_start — rank 0 naming rank 1 — instead of rank 0 waiting in the push
+    exchange for a rank that has left; a normal run then follows on the same contexts."""
+    from rbl import _lib
+    plant = matgen.planted_spectrum(5)
+
+    def fn(ctx, r):
+        ctx.set_option(_lib.RBL_OPT_HALO_PUSH, 1)
+        ctx.gen_rmat(CASE["n"], CASE["scale"], CASE["edges"], CASE["seed"], plant)
+        err = None
+        try:
+            ctx.start(32, 8, seed=9)
+        except rbl.RBLError as e:
+            err = (e.code, str(e))
+        barrier.wait(timeout=60)           # both ranks are past the failed start
+        if r == 0:
+            os.environ.pop("RBL_FAULT_PUSH_ALLOC", None)
+        barrier.wait(timeout=60)
+        _, _, info = rbl.lanczos(ctx, 5, 32, seed=9, check=False, max_steps=4, trace=True,
+                                 ritz=False)
+        return err, info, ctx.comm_stats()
+
+    import threading
+    barrier = threading.Barrier(2)
+    monkeypatch.setenv("RBL_FAULT_PUSH_ALLOC", "1")
+    out = run_ranks(rbl, 2, fn)
+    assert out[1][0] is not None and out[1][0][0] == _lib.RBL_ERR_OOM and "injected" in out[1][0][1]
+    assert out[0][0] is not None and out[0][0][0] == _lib.RBL_ERR_OOM and "rank 1" in out[0][0][1]
+    for a, a1 in zip(out[0][1].trace_A, out[1][1].trace_A):
+        assert np.array_equal(a, a1)
+    assert all(st["halo_push"] == 1 for _, _, st in out)

@@ -103,3 +103,25 @@ def test_python_constants_match_the_header():
     assert not mism, mism
     missing = [k for k in defs if k.startswith("RBL_OPT_") and not hasattr(_lib, k)]
     assert not missing, missing
+
+
+def test_rccl_is_rocms_whatever_was_loaded_first():
+    """rbl_rccl_version (no GPU call): the library's RCCL transport calls ROCm's own RCCL,
+    opened by path with a private symbol scope, also in a process that imported torch — which
+    bundles another RCCL under the same soname — before the library (bench.py's order).  Both
+    import orders run in fresh interpreters."""
+    import json
+    import subprocess
+    import sys
+    prog = ("import sys, json; sys.path[:0] = {paths!r}; {first}; import rbl; "
+            "print(json.dumps(rbl.rccl_version()))")
+    paths = [ROOT, os.path.join(ROOT, "gpu-randomized-block-lanczos_amd")]
+    out = []
+    for first in ("import torch", "pass"):
+        r = subprocess.run([sys.executable, "-c", prog.format(paths=paths, first=first)],
+                           capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr
+        out.append(json.loads(r.stdout.strip().splitlines()[-1]))
+    assert out[0] == out[1]
+    v = out[0]
+    assert v["rccl_path"].startswith("/opt/rocm") and v["rccl_version_code"] >= 22700
