@@ -251,6 +251,17 @@ def metric_name(args, nnz: int) -> str:
             + f" ({args.matrix})")
 
 
+T_START = time.perf_counter()
+
+
+def progress(msg: str) -> None:
+    """One line on stderr from rank 0 per phase and per fixed-length run: the JSON line is the
+    only stdout, and a long multi-rank job must not look silent (gpurun ends a run that writes
+    nothing for 3 minutes)."""
+    if os.environ.get("RANK", "0") == "0":
+        print(f"[bench {time.perf_counter() - T_START:7.1f} s] {msg}", file=sys.stderr, flush=True)
+
+
 def measure(ctx, args, matrix, K, W, nloc, nnz_loc, world, barrier, allmax):
     """W untimed + K timed fixed-length runs (rbl_start + m_max block steps, convergence checks
     off) on the matrix the context holds; the max over ranks of the timed region, the stage
@@ -273,8 +284,9 @@ def measure(ctx, args, matrix, K, W, nloc, nnz_loc, world, barrier, allmax):
         host["enqueue"] += info.enqueue_ms
         host["fetch_wait"] += info.fetch_ms
 
-    for _ in range(W):
+    for w_ in range(W):
         one_run()
+        progress(f"{matrix} n={n} b={b}: warmup run {w_ + 1}/{W}")
     for key in host:
         host[key] = 0.0
     barrier()
@@ -284,9 +296,10 @@ def measure(ctx, args, matrix, K, W, nloc, nnz_loc, world, barrier, allmax):
     barrier()
     t0 = time.perf_counter()
     marks = [t0]
-    for _ in range(K):
+    for k_ in range(K):
         one_run()  # (returns once the run's last block step has been fetched)
         marks.append(time.perf_counter())
+        progress(f"{matrix} n={n} b={b}: timed run {k_ + 1}/{K} {(marks[-1] - marks[-2]) * 1e3:.1f} ms")
     ctx.synchronize()
     barrier()
     elapsed = allmax(time.perf_counter() - t0)
@@ -491,6 +504,7 @@ def main():
     else:
         ctx.gen_hashwindow(n, args.halfwidth, args.density, args.seed, plant)
     gen_s = time.perf_counter() - t0
+    progress(f"{args.matrix} matrix generated ({gen_s:.1f} s)")
     _, r0, r1, nnz_loc = ctx.matrix_info()
     nloc = r1 - r0
     nnz = allsum(nnz_loc)
@@ -507,6 +521,7 @@ def main():
     roofline, roofline2 = meas["roofline"], meas["roofline_secondary"]
 
     # ---- time-to-k (convergence on, start -> converged Ritz vectors) ----
+    progress("time-to-k")
     ttk = None
     if not args.no_ttk:
         barrier()
@@ -573,17 +588,20 @@ def main():
 
     rmat_rec = None
     if args.matrix == "hashwindow" and args.rmat_steps > 0 and args.basis_bits == 64:
+        progress("C4b sub-record")
         rmat_rec = guarded(rmat_subrecord, ctx, args, plant, world, barrier, allmax, allsum,
                            allgather_i64)
 
     # ---- BASELINE config 3's shape: the circuit-like matrix at G3_circuit's n, b = 16 ----
     c3_rec = None
     if args.matrix == "hashwindow" and args.c3_steps > 0 and args.basis_bits == 64:
+        progress("C3 sub-record")
         c3_rec = guarded(c3_subrecord, ctx, args, world, barrier, allmax, allsum, allgather_i64)
 
     # ---- CPU baseline: the oracle (port of RBL.jl) on a bounded sample, rank 0, N = 1 ----
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        progress("CPU baseline")
         cpu = cpu_baseline(args, m_max, plant)
 
     comm = ctx.comm_info()
@@ -647,6 +665,7 @@ def main():
     # ---- BASELINE config 5: n = 5e7, fp32 basis, on >= 2 ranks (no spill) ----
     if (args.matrix == "hashwindow" and args.c5_steps > 0 and args.basis_bits == 64
             and world >= args.c5_min_ranks):
+        progress("C5 sub-record")
         try:
             line["c5_mixed"] = guarded(c5_subrecord, ctx, args, world, barrier, allmax, allsum,
                                        allgather_i64)

@@ -570,7 +570,8 @@ int prepare_push(rbl_ctx* ctx, const std::vector<int64_t>& rp) {
   std::vector<int32_t> c1(std::max<int64_t>(nz1, 1)), c2(std::max<int64_t>(nz2, 1));
   if (nz1) HIPC(hipMemcpy(c1.data(), ctx->seg_tier[1].col, nz1 * sizeof(int32_t), hipMemcpyDeviceToHost));
   if (nz2) HIPC(hipMemcpy(c2.data(), ctx->seg_tier[2].col, nz2 * sizeof(int32_t), hipMemcpyDeviceToHost));
-  std::vector<int64_t> vote(2 * P + 2, 0);  // [tier-1 by owner | tier-2 by owner | d1 | d12]
+  // [tier-1 entries by owner | tier-2 by owner | d1 | d12 | tier-1 hash by owner | tier-2 hash]
+  std::vector<int64_t> vote(4 * P + 2, 0);
   std::vector<uint8_t> mark(std::max<int64_t>(n, 1), 0);
   auto owner = [&](int64_t c) {
     return (int)(std::upper_bound(ctx->bounds.begin(), ctx->bounds.end(), c) - ctx->bounds.begin()) - 1;
@@ -584,24 +585,51 @@ int prepare_push(rbl_ctx* ctx, const std::vector<int64_t>& rp) {
     if (!mark[c2[k]]) { mark[c2[k]] = 2; ++vote[2 * P + 1]; }
   }
   vote[2 * P + 1] += vote[2 * P];
-  std::vector<int32_t>().swap(c2);
   std::vector<uint8_t>().swap(mark);
-  std::vector<int64_t> votes((size_t)P * (2 * P + 2));
-  COMMC(ctx->comm->allgather_host(vote.data(), votes.data(), 2 * P + 2, ctx->stream, &ctx->err));
+  // the entries themselves, not only their counts: the split forms A[r,c] Q[c] on c's rank from
+  // A[c,r], so p's tier-2 entries towards q must be q's tier-1 entries towards p transposed,
+  // values included.  Per peer an order-free hash (wrapping sum of mixed (row, col, value
+  // bits), tier 2 keyed transposed) is compared: a pattern or a value that is not symmetric
+  // keeps the pull-all halo (or fails under RBL_OPT_HALO_PUSH 1) instead of a wrong SpMM.
+  auto tier_hash = [&](int t, int64_t nz, const std::vector<int32_t>& cols, int64_t* out) -> int {
+    if (nz == 0) return RBL_OK;
+    std::vector<int64_t> trp(m + 1);
+    std::vector<double> tv(nz);
+    HIPC(hipMemcpy(trp.data(), ctx->seg_tier[t].rowptr, (m + 1) * sizeof(int64_t), hipMemcpyDeviceToHost));
+    HIPC(hipMemcpy(tv.data(), ctx->seg_tier[t].val, nz * sizeof(double), hipMemcpyDeviceToHost));
+    for (int64_t r = 0; r < m; ++r)
+      for (int64_t k = trp[r]; k < trp[r + 1]; ++k) {
+        const uint64_t row = (uint64_t)(ctx->r0 + r), col = (uint64_t)cols[k];
+        uint64_t vb;
+        memcpy(&vb, &tv[k], sizeof(vb));
+        const uint64_t a = t == 1 ? row : col, b2 = t == 1 ? col : row;  // tier 2: transposed
+        const uint64_t h = mix64(mix64(a * 0x9E3779B97F4A7C15ull ^ b2) ^ vb);
+        out[owner(cols[k])] = (int64_t)((uint64_t)out[owner(cols[k])] + h);
+      }
+    return RBL_OK;
+  };
+  CHK(tier_hash(1, nz1, c1, vote.data() + 2 * P + 2));
+  CHK(tier_hash(2, nz2, c2, vote.data() + 3 * P + 2));
+  std::vector<int32_t>().swap(c2);
+  const int V = 4 * P + 2;
+  std::vector<int64_t> votes((size_t)P * V);
+  COMMC(ctx->comm->allgather_host(vote.data(), votes.data(), V, ctx->stream, &ctx->err));
   bool sym = true;
   int64_t d1 = 0, d12 = 0;
   for (int p = 0; p < P; ++p) {
-    const int64_t* vp = votes.data() + (size_t)p * (2 * P + 2);
+    const int64_t* vp = votes.data() + (size_t)p * V;
     d1 += vp[2 * P];
     d12 += vp[2 * P + 1];
-    for (int q = 0; q < P; ++q)  // p's tier-2 entries towards q are q's tier-1 entries towards p
-      if (vp[P + q] != votes[(size_t)q * (2 * P + 2) + p]) sym = false;
+    for (int q = 0; q < P; ++q) {  // p's tier-2 entries towards q are q's tier-1 entries towards p
+      const int64_t* vq = votes.data() + (size_t)q * V;
+      if (vp[P + q] != vq[p] || vp[3 * P + 2 + q] != vq[2 * P + 2 + p]) sym = false;
+    }
   }
   ctx->push_pred_rows = 2 * d1;
   ctx->pull_pred_rows = d12;
   if (!sym) {
     if (ctx->halo_push_opt == 1)
-      return fail(ctx, RBL_ERR_INVALID, "RBL_OPT_HALO_PUSH: A is not structurally symmetric");
+      return fail(ctx, RBL_ERR_INVALID, "RBL_OPT_HALO_PUSH: A is not symmetric (pattern or values)");
     return 0;
   }
   if (ctx->halo_push_opt == 2 && !(2.0 * (double)d1 < 0.85 * (double)d12)) return 0;

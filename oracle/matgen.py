@@ -70,9 +70,13 @@ def hashwindow_csr(n: int, W: int, p: float, seed: int, plant=None, row_begin=0,
 _RMAT_K = np.uint64(0xD1B54A32D192ED03)
 
 
-def rmat_draws(n: int, scale: int, edges: int, seed: int, a=0.57, b=0.19, c=0.19):
-    """Kept R-MAT draws (r, c) in draw order (gen_rmat.hip: rmat_draw)."""
-    e = np.arange(edges, dtype=np.int64)
+def rmat_draws(n: int, scale: int, edges: int, seed: int, a=0.57, b=0.19, c=0.19,
+               edge_begin: int = 0, edge_end: int | None = None):
+    """Kept R-MAT draws (r, c) in draw order (gen_rmat.hip: rmat_draw); draws
+    [edge_begin, edge_end) of the `edges` (all by default), so large draws can be made in chunks."""
+    edge_end = edges if edge_end is None else min(edge_end, edges)
+    e = np.arange(edge_begin, edge_end, dtype=np.int64)
+    edges = e.size
     s2 = np.uint64(seed) ^ _RMAT_K
     ab, abc = a + b, a + b + c
     r = np.zeros(edges, np.int64)

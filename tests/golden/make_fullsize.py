@@ -87,6 +87,65 @@ def c4a_matrix(chunk=200_000):
     return sp.csr_matrix((val, col, rowptr.astype(np.int32)), shape=(n, n))
 
 
+# C4b at BASELINE's full size (the bench's sub-record, as drawn: RBL_OPT_RELABEL 0)
+C4B_FULL = dict(n=10_000_000, scale=24, edges=660_000_000, seed=20261015, b=32, k=20, omega_seed=6)
+
+
+def c4b_full_matrix(edge_chunk=20_000_000, row_chunk=1_000_000):
+    """matgen.rmat_csr (relabel off) built in chunks: the kept draws made [edge_chunk] at a time
+    and kept as int32 (n < 2^31), then each row range's keys (both orientations of every draw
+    plus the diagonal) merged with np.unique, values and plant exactly as rmat_csr — the same
+    matrix bit for bit (checked against rmat_csr at small n by test_oracle), in ~1/5 of the
+    memory.  int32 indices: nnz < 2^31."""
+    import scipy.sparse as sp
+    cfg = C4B_FULL
+    n, scale, edges, seed = cfg["n"], cfg["scale"], cfg["edges"], cfg["seed"]
+    return rmat_csr_chunked(n, scale, edges, seed, matgen.planted_spectrum(cfg["k"]),
+                            edge_chunk, row_chunk)
+
+
+def rmat_csr_chunked(n, scale, edges, seed, plant, edge_chunk, row_chunk):
+    import scipy.sparse as sp
+    rs, cs = [], []
+    for e0 in range(0, edges, edge_chunk):
+        r, c = matgen.rmat_draws(n, scale, edges, seed, edge_begin=e0, edge_end=e0 + edge_chunk)
+        rs.append(r.astype(np.int32))
+        cs.append(c.astype(np.int32))
+    r = np.concatenate(rs); del rs
+    c = np.concatenate(cs); del cs
+    plant = np.asarray(plant, dtype=np.float64)
+    stride = n // len(plant)
+    vals, cols, counts = [], [], []
+    for a in range(0, n, row_chunk):
+        b = min(n, a + row_chunk)
+        s1 = (r >= a) & (r < b)
+        s2 = (c >= a) & (c < b)
+        R = np.concatenate([r[s1], c[s2]]).astype(np.int64)
+        C = np.concatenate([c[s1], r[s2]]).astype(np.int64)
+        del s1, s2
+        d = np.arange(a, b, dtype=np.int64)
+        key = np.unique(np.concatenate([R * np.int64(n) + C, d * np.int64(n) + d]))
+        del R, C
+        R, C = key // n, key % n
+        del key
+        lo, hi = np.minimum(R, C), np.maximum(R, C)
+        u = matgen.u53(matgen.mix64(matgen.pair_hash(seed, lo, hi) ^ matgen._K))
+        val = (u + u) - 1.0
+        dg = R == C
+        sel2 = dg & (R % stride == 0) & (R // stride < len(plant))
+        val[sel2] += plant[R[sel2] // stride]
+        vals.append(val)
+        cols.append(C.astype(np.int32))
+        counts.append(np.bincount(R - a, minlength=b - a))
+    del r, c
+    rowptr = np.zeros(n + 1, dtype=np.int64)
+    np.cumsum(np.concatenate(counts), out=rowptr[1:])
+    val = np.concatenate(vals); del vals
+    col = np.concatenate(cols); del cols
+    assert rowptr[-1] < 2 ** 31
+    return sp.csr_matrix((val, col, rowptr.astype(np.int32)), shape=(n, n))
+
+
 def omega_for(cfg):
     return np.random.default_rng(cfg["omega_seed"]).standard_normal((cfg["n"], cfg["b"]))
 
@@ -120,6 +179,15 @@ def main(which):
         run("c3", C3, c3_matrix())
     if "c4b" in which:
         run("c4b", C4B, c4b_matrix())
+    if "c4b_full" in which:
+        import resource
+        # a MemoryError instead of the OOM killer if the estimate (~55 GB) is wrong
+        lim = int(float(os.environ.get("RBL_FIXTURE_MEM_GB", "58")) * 2 ** 30)
+        resource.setrlimit(resource.RLIMIT_DATA, (lim, lim))
+        t0 = time.perf_counter()
+        A = c4b_full_matrix()
+        print(f"c4b_full: matrix {A.nnz} nonzeros in {time.perf_counter() - t0:.1f} s", flush=True)
+        run("c4b_full", C4B_FULL, A, reorth_mode="cgs_blocked")
     if "c4a" in which:
         t0 = time.perf_counter()
         A = c4a_matrix()

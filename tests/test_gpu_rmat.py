@@ -531,9 +531,13 @@ def test_rmat_halo_push_small_and_ragged(rbl):
                 assert np.abs(a - a1).max() <= 1e-9 * np.abs(a1).max()
 
 
-def test_rmat_halo_push_needs_symmetric_pattern(rbl):
+@pytest.mark.parametrize("kind", ["pattern", "value", "swap"])
+def test_rmat_halo_push_needs_symmetric_pattern(rbl, kind):
     """The split relies on A[c, r] = A[r, c] (the owner of c forms the product from its own row).
-    A pattern that is not symmetric across ranks is caught by the per-pair entry counts at setup:
+    A matrix that is not symmetric across ranks is caught at setup — by the per-pair entry
+    counts, and by per-pair hashes of the entries themselves (row, column, value bits): one
+    entry without its mirror ("pattern"), a mirrored pair with different values ("value"), two
+    unmirrored entries in opposite directions ("swap": the per-pair counts may still agree).
     RBL_OPT_HALO_PUSH 1 fails with a message, the automatic mode keeps the pull-all halo (and
     the product stays exact)."""
     import scipy.sparse as sp
@@ -541,9 +545,15 @@ def test_rmat_halo_push_needs_symmetric_pattern(rbl):
     rng = np.random.default_rng(2)
     n = 3000
     M = _scattered(n, n, seed=4)
-    j = next(j for j in range(1500, n) if M[5, j] == 0 and M[j, 5] == 0)
+    free = [j for j in range(1500, n) if M[5, j] == 0 and M[j, 5] == 0]
+    j, j2 = free[0], free[1]
     M = M.tolil()
-    M[5, j] = 0.7            # one entry without its mirror, across the ranks' boundary
+    if kind == "pattern":
+        M[5, j] = 0.7            # one entry without its mirror, across the ranks' boundary
+    elif kind == "value":
+        M[5, j], M[j, 5] = 0.7, 0.7000000000000001   # mirrored, one ulp apart
+    else:
+        M[5, j], M[j2, 5] = 0.7, 0.7
     M = M.tocsr()
     M.sort_indices()
     X = rng.standard_normal((n, 16))
