@@ -64,6 +64,11 @@ constexpr int kG44Waves = 4;
 #ifndef RBL_G44_W16
 #define RBL_G44_W16 1
 #endif
+// b = 16 (panel pairs): basis operands this many chunks ahead (2 or 3).  A 16-row chunk is half
+// the MFMAs of a b = 32 chunk, so the same distance covers half the time
+#ifndef RBL_G44_PF16
+#define RBL_G44_PF16 RBL_G44_PF
+#endif
 #ifndef RBL_G44_WPE16
 // b = 16 (panel pairs, HBM-bound at ~5 TB/s): 4 waves per SIMD (106 VGPRs) measured neutral on
 // the probe and 0.5-0.8 % slower on the C2 / C3 lines (profiles/r03_gram16_wpe4_ab.log); the
@@ -234,7 +239,53 @@ __device__ __forceinline__ void gram44_body(int64_t r_begin, int64_t r_end, int6
   // rc0 zeroed) goes through the register path after it
   const int64_t nchunks = r_end > r_begin ? (r_end - r_begin + (GL ? 0 : kG44Rows - 1)) / kG44Rows : 0;
   double xr[EPT];
-#if RBL_G44_PF >= 2
+  constexpr int PFD = B == 16 ? RBL_G44_PF16 : RBL_G44_PF;
+  static_assert(PFD >= 1 && PFD <= 3, "prefetch distance");
+  if constexpr (PFD == 3) {
+    // four rotating register sets, the loop unrolled by 4
+    double a0[KS][AG], a1[KS][AG], a2[KS][AG], a3[KS][AG];
+    if (nchunks > 0) {
+      if constexpr (GL) {
+        dma_x(0, r_begin);
+      } else {
+        load_x(r_begin, xr);
+        store_x(0, r_begin, xr);
+      }
+      load_a(r_begin, a0);
+      load_a(r_begin + kG44Rows, a1);
+      load_a(r_begin + 2 * kG44Rows, a2);
+    }
+    __syncthreads();
+    auto step = [&](int64_t c, const double (&acur)[KS][AG], double (&afut)[KS][AG]) {
+      const int64_t rc0 = r_begin + c * kG44Rows;
+      if constexpr (GL) dma_x((int)((c + 1) & 1), rc0 + kG44Rows);
+      else load_x(rc0 + kG44Rows, xr);
+      load_a(rc0 + 3 * kG44Rows, afut);
+      if (active && c < nchunks) mma(xs[c & 1], acur);
+      if constexpr (!GL) store_x((int)((c + 1) & 1), rc0 + kG44Rows, xr);
+      __syncthreads();
+    };
+    for (int64_t c = 0; c < nchunks; c += 4) {
+      step(c, a0, a3);
+      step(c + 1, a1, a0);
+      step(c + 2, a2, a1);
+      step(c + 3, a3, a2);
+    }
+    if constexpr (GL) {
+      const int64_t rc0 = r_begin + nchunks * kG44Rows;
+      if (rc0 < r_end) {
+        load_x(rc0, xr);
+        load_a(rc0, a0);
+#pragma unroll
+        for (int v = 0; v < EPT; ++v) {
+          const int64_t row = shift(rc0) + xrow;
+          xs[0][GLn::off(xrow) + xcol + v] = row >= rc0 ? xr[v] : 0.0;
+        }
+        __syncthreads();
+        if (active) mma(xs[0], a0);
+      }
+    }
+  } else if constexpr (PFD == 2) {
   // basis operands two chunks ahead in three rotating register sets (no copies: a copy of a
   // landing prefetch would make the wave wait for it one chunk early)
   double a0[KS][AG], a1[KS][AG], a2[KS][AG];
@@ -277,7 +328,7 @@ __device__ __forceinline__ void gram44_body(int64_t r_begin, int64_t r_end, int6
       if (active) mma(xs[0], a0);
     }
   }
-#else
+  } else {
   static_assert(!GL, "GL: PF = 2 only");
   double acur[KS][AG], anext[KS][AG];
   if (nchunks > 0) {
@@ -302,7 +353,7 @@ __device__ __forceinline__ void gram44_body(int64_t r_begin, int64_t r_end, int6
       for (int ag = 0; ag < AG; ++ag) acur[ks][ag] = anext[ks][ag];
     if (!(RBL_REORTH_ABL & 2)) __syncthreads();
   }
-#endif
+  }
   if (!active) return;
   const int KW = W.count * B;
   double* out = slab + (s * KW + (int64_t)j * WB) * KC + 4 * (2 * cp0);
@@ -377,7 +428,7 @@ static void launch_gram44(int64_t nrows, const PanelRun& W, const Panels& X, dou
   const int npg = (units + kG44Waves - 1) / kG44Waves;
   int64_t rows_per = (nrows + splits - 1) / splits;
   rows_per = (rows_per + kG44Rows - 1) / kG44Rows * kG44Rows;
-  constexpr bool kGL = RBL_G44_GLDS && RBL_G44_PF >= 2 && kG44Rows == 16 && (NX * B == 32 || NX * B == 64);
+  constexpr bool kGL = RBL_G44_GLDS && (B == 16 ? RBL_G44_PF16 : RBL_G44_PF) >= 2 && kG44Rows == 16 && (NX * B == 32 || NX * B == 64);
   bool gl = kGL;
   for (int t = 0; t < X.count; ++t) gl &= reinterpret_cast<uintptr_t>(X.ptr[t]) % 16 == 0;
   if (gl)

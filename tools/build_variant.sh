@@ -16,7 +16,7 @@ for s in $srcs; do
   pids="$pids $!"
 done
 for p in $pids; do wait $p; done
-/opt/rocm/bin/hipcc -fPIC --offload-arch=gfx950 $out/obj/*.o -shared -L/opt/rocm/lib -lrccl \
+/opt/rocm/bin/hipcc -fPIC --offload-arch=gfx950 $out/obj/*.o -shared -L/opt/rocm/lib \
   -lrocprofiler-sdk-roctx -Wl,-rpath,/opt/rocm/lib -o $out/librbl_hip.so
 rm -rf $out/obj
 echo "built $out/librbl_hip.so"
