@@ -84,6 +84,13 @@ constexpr int kG44Waves = 4;
 #ifndef RBL_G44_GLDS
 #define RBL_G44_GLDS 1
 #endif
+// b = 16: the X chunk by LDS-DMA as well?  While a global_load_lds is in flight hipcc (ROCm 7.2)
+// closes every __syncthreads() with vmcnt(0), which also drains the basis prefetch issued for two
+// chunks ahead (cdna_hip_programming.md, 'Pipelining across barriers'): the prefetch then covers
+// one chunk.  Register staging keeps it (the barrier waits vmcnt(8): the X loads only)
+#ifndef RBL_G44_GLDS16
+#define RBL_G44_GLDS16 RBL_G44_GLDS
+#endif
 constexpr int kG44Rows = RBL_G44_ROWS;
 typedef __attribute__((address_space(3))) void* lds_vptr;
 typedef __attribute__((address_space(1))) void* glb_vptr;
@@ -428,7 +435,7 @@ static void launch_gram44(int64_t nrows, const PanelRun& W, const Panels& X, dou
   const int npg = (units + kG44Waves - 1) / kG44Waves;
   int64_t rows_per = (nrows + splits - 1) / splits;
   rows_per = (rows_per + kG44Rows - 1) / kG44Rows * kG44Rows;
-  constexpr bool kGL = RBL_G44_GLDS && (B == 16 ? RBL_G44_PF16 : RBL_G44_PF) >= 2 && kG44Rows == 16 && (NX * B == 32 || NX * B == 64);
+  constexpr bool kGL = (B == 16 ? RBL_G44_GLDS16 : RBL_G44_GLDS) && (B == 16 ? RBL_G44_PF16 : RBL_G44_PF) >= 2 && kG44Rows == 16 && (NX * B == 32 || NX * B == 64);
   bool gl = kGL;
   for (int t = 0; t < X.count; ++t) gl &= reinterpret_cast<uintptr_t>(X.ptr[t]) % 16 == 0;
   if (gl)
