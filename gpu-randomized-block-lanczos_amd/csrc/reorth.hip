@@ -69,6 +69,13 @@ constexpr int kG44Waves = 4;
 #ifndef RBL_G44_PF16
 #define RBL_G44_PF16 RBL_G44_PF
 #endif
+// interleaved row splits (see k_gram44): b = 32 / b = 16
+#ifndef RBL_G44_INTER
+#define RBL_G44_INTER 0
+#endif
+#ifndef RBL_G44_INTER16
+#define RBL_G44_INTER16 RBL_G44_INTER
+#endif
 #ifndef RBL_G44_WPE16
 // b = 16 (panel pairs, HBM-bound at ~5 TB/s): 4 waves per SIMD (106 VGPRs) measured neutral on
 // the probe and 0.5-0.8 % slower on the C2 / C3 lines (profiles/r03_gram16_wpe4_ab.log); the
@@ -122,7 +129,7 @@ struct G44Lines {
 // SIMD, 299 ms at two (19 VGPRs spilled), against 262 ms for one panel per wave at three waves
 // per SIMD; C4a 45.4 vs 47.2 block-iters/s.  The extra waves hide the per-chunk barrier.
 template <int B, int NX, int NPH, bool PAIR = false, bool GL = false, bool DUO = false>
-__device__ __forceinline__ void gram44_body(int64_t r_begin, int64_t r_end, int64_t s, int pg,
+__device__ __forceinline__ void gram44_body(int64_t r_begin, int64_t r_end, int64_t cs, int64_t s, int pg,
                                             int r, const PanelRun& W, const Panels& X,
                                             double* slab, double* xs_base) {
   constexpr int KC = NX * B;
@@ -244,7 +251,13 @@ __device__ __forceinline__ void gram44_body(int64_t r_begin, int64_t r_end, int6
 
   // GL: the loop covers whole chunks only; a last partial chunk (shifted back, rows below
   // rc0 zeroed) goes through the register path after it
-  const int64_t nchunks = r_end > r_begin ? (r_end - r_begin + (GL ? 0 : kG44Rows - 1)) / kG44Rows : 0;
+  // cs: rows from one chunk of this split to its next (16: a contiguous split; 16 x splits:
+  // interleaved, every split's k-th chunk adjacent to the others' so the chip sweeps the basis
+  // front to back).  GL counts whole chunks only (a partial last chunk goes through the tail).
+  const int64_t nchunks =
+      r_end > r_begin ? (GL ? (r_end - r_begin >= kG44Rows ? (r_end - r_begin - kG44Rows) / cs + 1 : 0)
+                            : (r_end - r_begin + cs - 1) / cs)
+                      : 0;
   double xr[EPT];
   constexpr int PFD = B == 16 ? RBL_G44_PF16 : RBL_G44_PF;
   static_assert(PFD >= 1 && PFD <= 3, "prefetch distance");
@@ -259,17 +272,17 @@ __device__ __forceinline__ void gram44_body(int64_t r_begin, int64_t r_end, int6
         store_x(0, r_begin, xr);
       }
       load_a(r_begin, a0);
-      load_a(r_begin + kG44Rows, a1);
-      load_a(r_begin + 2 * kG44Rows, a2);
+      load_a(r_begin + cs, a1);
+      load_a(r_begin + 2 * cs, a2);
     }
     __syncthreads();
     auto step = [&](int64_t c, const double (&acur)[KS][AG], double (&afut)[KS][AG]) {
-      const int64_t rc0 = r_begin + c * kG44Rows;
-      if constexpr (GL) dma_x((int)((c + 1) & 1), rc0 + kG44Rows);
-      else load_x(rc0 + kG44Rows, xr);
-      load_a(rc0 + 3 * kG44Rows, afut);
+      const int64_t rc0 = r_begin + c * cs;
+      if constexpr (GL) dma_x((int)((c + 1) & 1), rc0 + cs);
+      else load_x(rc0 + cs, xr);
+      load_a(rc0 + 3 * cs, afut);
       if (active && c < nchunks) mma(xs[c & 1], acur);
-      if constexpr (!GL) store_x((int)((c + 1) & 1), rc0 + kG44Rows, xr);
+      if constexpr (!GL) store_x((int)((c + 1) & 1), rc0 + cs, xr);
       __syncthreads();
     };
     for (int64_t c = 0; c < nchunks; c += 4) {
@@ -279,7 +292,7 @@ __device__ __forceinline__ void gram44_body(int64_t r_begin, int64_t r_end, int6
       step(c + 3, a3, a2);
     }
     if constexpr (GL) {
-      const int64_t rc0 = r_begin + nchunks * kG44Rows;
+      const int64_t rc0 = r_begin + nchunks * cs;
       if (rc0 < r_end) {
         load_x(rc0, xr);
         load_a(rc0, a0);
@@ -304,16 +317,16 @@ __device__ __forceinline__ void gram44_body(int64_t r_begin, int64_t r_end, int6
       store_x(0, r_begin, xr);
     }
     load_a(r_begin, a0);
-    load_a(r_begin + kG44Rows, a1);
+    load_a(r_begin + cs, a1);
   }
   __syncthreads();
   auto step = [&](int64_t c, const double (&acur)[KS][AG], double (&afut)[KS][AG]) {
-    const int64_t rc0 = r_begin + c * kG44Rows;
-    if constexpr (GL) dma_x((int)((c + 1) & 1), rc0 + kG44Rows);
-    else load_x(rc0 + kG44Rows, xr);
-    load_a(rc0 + 2 * kG44Rows, afut);
+    const int64_t rc0 = r_begin + c * cs;
+    if constexpr (GL) dma_x((int)((c + 1) & 1), rc0 + cs);
+    else load_x(rc0 + cs, xr);
+    load_a(rc0 + 2 * cs, afut);
     if (active && c < nchunks) mma(xs[c & 1], acur);  // no loads inside: vmcnt bookkeeping unaffected
-    if constexpr (!GL) store_x((int)((c + 1) & 1), rc0 + kG44Rows, xr);
+    if constexpr (!GL) store_x((int)((c + 1) & 1), rc0 + cs, xr);
     __syncthreads();
   };
   for (int64_t c = 0; c < nchunks; c += 3) {
@@ -322,7 +335,7 @@ __device__ __forceinline__ void gram44_body(int64_t r_begin, int64_t r_end, int6
     step(c + 2, a2, a1);
   }
   if constexpr (GL) {
-    const int64_t rc0 = r_begin + nchunks * kG44Rows;
+    const int64_t rc0 = r_begin + nchunks * cs;
     if (rc0 < r_end) {  // every DMA has landed (closing barrier of the last step)
       load_x(rc0, xr);
       load_a(rc0, a0);
@@ -345,15 +358,15 @@ __device__ __forceinline__ void gram44_body(int64_t r_begin, int64_t r_end, int6
   }
   __syncthreads();
   for (int64_t c = 0; c < nchunks; ++c) {
-    const int64_t rc0 = r_begin + c * kG44Rows;
+    const int64_t rc0 = r_begin + c * cs;
     // unconditional (clamped on the last chunk): a uniform branch here would make the
     // waitcnt pass merge a no-load path and drain the prefetch before the MFMAs
-    load_x(rc0 + kG44Rows, xr);
-    if (!(RBL_REORTH_ABL & 1)) load_a(rc0 + kG44Rows, anext);
+    load_x(rc0 + cs, xr);
+    if (!(RBL_REORTH_ABL & 1)) load_a(rc0 + cs, anext);
     if (active) mma(xs[c & 1], acur);  // idle waves (a 3-panel group) only help stage X
     // unconditional as well: a consumer under `if (more)` lets LLVM sink the loads into it
     // (after the MFMAs); on the last chunk this writes the dead spare buffer
-    if (!(RBL_REORTH_ABL & 4)) store_x((int)((c + 1) & 1), rc0 + kG44Rows, xr);
+    if (!(RBL_REORTH_ABL & 4)) store_x((int)((c + 1) & 1), rc0 + cs, xr);
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
@@ -393,13 +406,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(DUO ? RBL_G
   const int xcd = bid & 7, t = bid >> 3;
   const int pg = t % npg;
   const int64_t s = (int64_t)(t / npg) * 8 + xcd;
-  const int64_t r_begin = s * rows_per;
-  const int64_t r_end = r_begin + rows_per < nrows ? r_begin + rows_per : nrows;
+  // RBL_G44_INTER(16): interleaved splits (split s takes chunks s, s + S, ...; S = splits)
+  constexpr bool kInter = B == 16 ? RBL_G44_INTER16 : RBL_G44_INTER;
+  const int64_t S = gridDim.x / npg;
+  const int64_t r_begin = kInter ? s * kG44Rows : s * rows_per;
+  const int64_t r_end = kInter ? nrows : (r_begin + rows_per < nrows ? r_begin + rows_per : nrows);
+  const int64_t cs = kInter ? S * kG44Rows : kG44Rows;
   const int rem = (PAIR || DUO ? W.count / 2 : W.count) - pg * kG44Waves;
   const int r = rem < kG44Waves ? rem : kG44Waves;  // panels in this group (workgroup-uniform)
-  if (r >= 3) gram44_body<B, NX, 1, PAIR, GL, DUO>(r_begin, r_end, s, pg, r, W, X, slab, xs);
-  else if (r == 2) gram44_body<B, NX, NPH2, PAIR, GL, DUO>(r_begin, r_end, s, pg, r, W, X, slab, xs);
-  else gram44_body<B, NX, NPH4, PAIR, GL, DUO>(r_begin, r_end, s, pg, r, W, X, slab, xs);
+  if (r >= 3) gram44_body<B, NX, 1, PAIR, GL, DUO>(r_begin, r_end, cs, s, pg, r, W, X, slab, xs);
+  else if (r == 2) gram44_body<B, NX, NPH2, PAIR, GL, DUO>(r_begin, r_end, cs, s, pg, r, W, X, slab, xs);
+  else gram44_body<B, NX, NPH4, PAIR, GL, DUO>(r_begin, r_end, cs, s, pg, r, W, X, slab, xs);
 }
 
 bool gram44_ok(int64_t nrows, int nW, int w, int xcount, int xw) {
