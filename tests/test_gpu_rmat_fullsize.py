@@ -1,7 +1,13 @@
 """GPU: BASELINE config 4 at full size (C4b: R-MAT scale 24, n = 1e7, ~1e9 nonzeros, b = 32,
-k = 20 — the bench's `c4b_rmat` workload), checked through size-independent properties, since
-the oracle cannot run at this size in a test (it ran at n = 1e6: test_gpu_c2_c3.py
-test_c4b_rmat_1e6_vs_oracle):
+k = 20 — the bench's `c4b_rmat` workload, as drawn).
+
+Against the oracle at full size: tests/golden/make_fullsize.py c4b_full ran the oracle on this
+very matrix offline in the build container (the R-MAT CSR built in chunks, bit-exact with
+matgen.rmat_csr; block CGS evaluated block by block) and committed golden_c4b_full.npz;
+test_c4b_full_size_vs_oracle feeds the fixture's Omega and checks the step count, the
+eigenvalues (< 1e-10 relative) and each Ritz vector's 16 largest entries (1e-6, up to sign).
+
+Beside it, size-independent properties:
 
   * SpMM (`rbl_apply`: the segmented gather + long-row fixup the bench runs) on sampled rows
     against SciPy's product of the same CSR rows downloaded from the device: the 64 highest-
@@ -107,3 +113,29 @@ def test_c4b_fullsize_rbl_gpu(full):
     assert np.abs(G - np.eye(K)).max() < ORTH_TOL, np.abs(G - np.eye(K)).max()
     rq = np.einsum("ij,ij->j", V, AV) / np.einsum("ij,ij->j", V, V)
     assert np.all(np.abs(rq - D) <= RAYLEIGH_TOL * np.abs(D)), np.abs(rq - D) / np.abs(D)
+
+
+def test_c4b_full_size_vs_oracle(full):
+    """BASELINE config 4 against the oracle's own run at n = 1e7 (golden_c4b_full.npz): the
+    device-generated R-MAT matrix (relabel off: the matrix as drawn) is the fixture's (same
+    nonzero count; the generator is bit-exact, test_gpu_rmat), the fixture's Omega, the same
+    number of block steps to convergence, eigenvalues within 1e-10 relative, Ritz vectors'
+    largest entries within 1e-6 up to sign."""
+    import os
+    rbl, ctx, A = full
+    g = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "golden_c4b_full.npz"))
+    cfg = {k[4:]: g[k].item() for k in g.files if k.startswith("cfg_")}
+    assert (cfg["n"], cfg["scale"], cfg["edges"], cfg["seed"], cfg["b"], cfg["k"]) == (N, SCALE, EDGES, SEED, B, K)
+    assert A.nnz == int(g["nnz"])
+    omega = np.random.default_rng(cfg["omega_seed"]).standard_normal((N, B))
+    D, V, info = rbl.lanczos(ctx, K, B, omega=omega)
+    del omega
+    _log(f"vs oracle: {info.iters} steps")
+    assert info.converged and info.iters == int(g["iters"])
+    rel = np.abs(D - g["D"]) / np.abs(g["D"])
+    assert rel.max() < 1e-10, rel
+    idx, val = g["top_idx"], g["top_val"]
+    for j in range(K):
+        v = V[idx[:, j], j]
+        s = np.sign(v @ val[:, j])
+        assert np.abs(s * v - val[:, j]).max() < 1e-6, (j, np.abs(s * v - val[:, j]).max())
