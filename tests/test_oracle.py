@@ -137,3 +137,22 @@ def test_rmat_relabel_is_a_symmetric_permutation():
     # the hubs (R-MAT's low ids) no longer sit in the first rows
     deg = np.diff(B.indptr)
     assert deg[: n // 8].sum() < 0.3 * deg.sum() < np.diff(A.indptr)[: n // 8].sum()
+
+
+def test_mixed_mode_step_suite_spurious_pairs():
+    """Documents a property of the reference's mixed mode (FLOAT = Float32, README.md:69) on its
+    own step suite (test.jl:40-50, n = 1e5): the T-based convergence test (common.jl:56-65)
+    passes while the returned top-k holds spurious values beside the true 10n, 9n, 8n — the
+    fp32 basis loses orthogonality against eigenvectors 1e5 times the bulk.  The fp64 oracle
+    meets the suite's 1e-13 on the same Omega."""
+    n = 100_000
+    A, eig = o.step_decay_matrix(n, 5)
+    om = np.random.default_rng(1).standard_normal((n, 5))
+    r32 = o.RBL_gpu_mixed(A, 5, 5, omega=om)
+    r64 = o.RBL_gpu_semantics(A, 5, 5, omega=om, qr_mode="posdiag", reorth_mode="cgs")
+    assert r32.converged and r64.converged
+    assert np.linalg.norm((r64.D - eig) / eig) < o.KNOWN_ANSWER_TOL
+    assert np.linalg.norm((r32.D - eig) / eig) > 1e-2           # spurious values in the top 5
+    assert abs(r32.D[0] - eig[0]) < 1e-6 * eig[0]                # the top one is right
+    res = np.linalg.norm(A @ r32.V - r32.V * r32.D, axis=0) / np.abs(r32.D)
+    assert res.max() > 1e-5                                      # ... and not eigenpairs of A
