@@ -5,6 +5,8 @@
 // (nearly) rank deficient — Krylov exhaustion in the reference's own tests —
 // shifted CholQR3 (Fukaya et al. 2020: shift s = 11 (n b + b (b+1)) u ||U||^2, then two
 // unshifted passes).  R has a non-negative diagonal.
+#include <cstdlib>
+
 #include "kernels.hpp"
 
 namespace rbl {
@@ -137,9 +139,137 @@ __global__ __launch_bounds__(256) void k_chol(const double* __restrict__ G, int 
   }
 }
 
+// The same factorisation for b = 16 / 32 on ONE wave with the matrix in registers: lane c holds
+// column c of M (then of R^-1, then of Rtot), and the row elements another lane holds come over
+// v_readlane (lane index a compile-time constant: the loops are unrolled).  k_chol spends its
+// time in ~3 four-wave barriers per column and a serial pivot on thread 0 (26 us per call at
+// b = 32, ~7 calls per block step); here there is no barrier at all.  Every entry is formed
+// by the same operations in the same order as k_chol (terms that k_chol skips are exact zeros
+// here, added at the end of a sum), so R, R^-1 and Rtot come out the same.
+__device__ __forceinline__ double bcast(double v, int lane) {
+  const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)u, lane);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(u >> 32), lane);
+  return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+
+template <int B>
+__global__ __launch_bounds__(64) void k_chol_reg(const double* __restrict__ G, int64_t nglob, int mode,
+                                                 double* R, double* Rinv, double* Rtot, int* need3,
+                                                 int* status, const int* skip) {
+  if (skip && *skip) return;
+  const int c = threadIdx.x;           // the column this lane holds (lanes >= B hold nothing)
+  const int cc = c < B ? c : B - 1;    // clamped for loads
+  double tr = 0.0;
+#pragma unroll
+  for (int j = 0; j < B; ++j) tr += G[j * B + j];
+  const bool zero = !(tr > 0.0);
+  const double shift = zero ? 0.0 : 11.0 * ((double)nglob * B + (double)B * (B + 1)) * 0x1.0p-53 * tr;
+  double m[B];
+  int fail = 0, shifted = 0;
+  if (!zero) {
+    for (int attempt = 0; attempt < 2; ++attempt) {
+      const double sh = attempt ? shift : 0.0;
+#pragma unroll
+      for (int r = 0; r < B; ++r) m[r] = (r <= c) ? G[r * B + cc] + (r == c ? sh : 0.0) : 0.0;
+      fail = 0;
+#pragma unroll
+      for (int j = 0; j < B; ++j) {
+        const double d = bcast(m[j], j);  // M(j, j), held by lane j
+        const double gjj = G[j * B + j] + sh;
+        if (!(d > 0.0) || !isfinite(d)) {
+          fail = 1;
+        } else if (attempt == 0 && mode == 0 && d < 1e-15 * gjj) {
+          fail = 2;
+        }
+        if (fail) break;
+        const double rjj = sqrt(d);
+        if (c == j) m[j] = rjj;
+        if (c > j) m[j] /= rjj;            // M(j, c) /= rjj
+#pragma unroll
+        for (int r = j + 1; r < B; ++r) {  // M(r, c) -= M(j, r) M(j, c), r <= c
+          const double mjr = bcast(m[j], r);
+          if (r <= c) m[r] -= mjr * m[j];
+        }
+      }
+      if (!fail) break;
+      shifted = 1;
+    }
+  }
+  const bool bad = !zero && fail;
+  const bool ok = !zero && !bad;
+  // R^-1, column c: X(c, c) = 1 / M(c, c); X(i, c) = -sum_{k = i+1..c} M(i, k) X(k, c) / M(i, i)
+  double x[B];
+#pragma unroll
+  for (int i = 0; i < B; ++i) x[i] = 0.0;
+  if (ok) {
+#pragma unroll
+    for (int i = B - 1; i >= 0; --i) {
+      const double mii = bcast(m[i], i);
+      if (i == c) x[i] = 1.0 / mii;
+      double acc = 0.0;
+#pragma unroll
+      for (int k = i + 1; k < B; ++k) acc += bcast(m[i], k) * x[k];  // x[k] = 0 for k > c
+      if (i < c) x[i] = -acc / mii;
+    }
+  }
+  if (c < B) {
+#pragma unroll
+    for (int r = 0; r < B; ++r) {
+      const bool up = r <= c && ok;
+      R[r * B + c] = up ? m[r] : 0.0;
+      Rinv[r * B + c] = up ? x[r] : 0.0;
+    }
+  }
+  // Rtot = R (mode 0) or R Rtot_prev (mode 1), column c; Rtot_prev is upper triangular
+  if (mode == 0) {
+    if (c < B) {
+#pragma unroll
+      for (int r = 0; r < B; ++r) Rtot[r * B + c] = (r <= c && ok) ? m[r] : 0.0;
+    }
+  } else {
+    double p[B];
+#pragma unroll
+    for (int k = 0; k < B; ++k) p[k] = Rtot[k * B + cc];
+    __syncthreads();  // every lane has read Rtot_prev before any lane overwrites it
+    double out[B];
+#pragma unroll
+    for (int r = 0; r < B; ++r) {
+      double acc = 0.0;
+#pragma unroll
+      for (int k = r; k < B; ++k) acc += bcast(m[r], k) * p[k];  // p[k] = 0 for k > c
+      out[r] = (r <= c && ok) ? acc : 0.0;
+    }
+    if (c < B) {
+#pragma unroll
+      for (int r = 0; r < B; ++r) Rtot[r * B + c] = out[r];
+    }
+  }
+  if (c == 0) {
+    if (mode == 0) { need3[0] = shifted; need3[1] = !shifted; }
+    if (bad) status[0] = 1;
+    if (shifted) status[1] += 1;
+  }
+}
+
+// RBL_CHOL_REG=0: the four-wave kernel at b = 16 / 32 as well (A/B; read per call, tests switch it)
+static bool chol_reg_on() {
+  const char* e = getenv("RBL_CHOL_REG");
+  return !e || atoi(e) != 0;
+}
+
 void chol_step(const double* G, int b, int64_t nglobal, int mode, double* R, double* Rinv,
                double* Rtot, int* need3, int* status, const int* skip, hipStream_t s,
                double* scratch) {
+  if ((b == 32 || b == 16) && chol_reg_on()) {
+    if (b == 32)
+      hipLaunchKernelGGL(k_chol_reg<32>, dim3(1), dim3(64), 0, s, G, nglobal, mode, R, Rinv, Rtot,
+                         need3, status, skip);
+    else
+      hipLaunchKernelGGL(k_chol_reg<16>, dim3(1), dim3(64), 0, s, G, nglobal, mode, R, Rinv, Rtot,
+                         need3, status, skip);
+    return;
+  }
   if (b <= kMaxB)
     hipLaunchKernelGGL(k_chol<true>, dim3(1), dim3(256), 0, s, G, b, nglobal, mode, R, Rinv, Rtot,
                        need3, status, skip, scratch);

@@ -351,3 +351,25 @@ def test_speculative_steps_change_nothing(rbl, case):
     assert np.array_equal(D0, D1) and np.array_equal(V0, V1)
     assert all(np.array_equal(a, c) for a, c in zip(i0.trace_A, i1.trace_A))
     assert all(np.array_equal(a, c) for a, c in zip(i0.trace_B, i1.trace_B))
+
+
+@pytest.mark.parametrize("b,bits", [(16, 64), (32, 64), (32, 32)])
+def test_cholqr_register_kernel_bit_identical(rbl, monkeypatch, b, bits):
+    """The one-wave register Cholesky (k_chol_reg, b = 16 / 32) against the four-wave LDS kernel
+    (RBL_CHOL_REG=0): the same R, R^-1 and Rtot, so 12-step A_i / B_{i+1} traces are bit-identical
+    — on the C1-like matrix and through Krylov exhaustion (the reference's slow-decay matrix at
+    n = 9 b: the last step factors a numerically zero block, the shifted / zero paths)."""
+    A1 = c1_matrix(4000, 10)
+    A2, _ = o.slow_decay_matrix(9 * b, 5)
+    for A, steps in ((A1, 12), (A2, 9)):
+        n = A.shape[0]
+        omega = np.random.default_rng(b).standard_normal((n, b))
+        out = {}
+        for reg in ("0", "1"):
+            monkeypatch.setenv("RBL_CHOL_REG", reg)
+            with rbl.Context(0) as ctx:
+                ctx.set_matrix(A)
+                _, _, info = rbl.lanczos(ctx, 5, b, omega=omega, check=False, max_steps=steps,
+                                         trace=True, ritz=False, basis_bits=bits)
+            out[reg] = (np.array(info.trace_A), np.array(info.trace_B))
+        assert np.array_equal(out["0"][0], out["1"][0]) and np.array_equal(out["0"][1], out["1"][1])
