@@ -62,6 +62,11 @@ def parse():
                     help="n of the CPU baseline's fixed-step cross-check (0 skips it): the first "
                          "--cpu-check-steps block steps timed at the sample's n and at this n")
     ap.add_argument("--cpu-check-steps", type=int, default=8)
+    ap.add_argument("--cpu-fixed-n", type=int, default=0,
+                    help="also time the oracle's first --cpu-check-steps block steps at this n (SURVEY "
+                         "§8(d)'s fixed-step form at the config's own n, e.g. 10000000: the 1e9-nnz "
+                         "CSR built in row chunks, ~45 GB of host memory, several minutes; off by "
+                         "default)")
     ap.add_argument("--no-ttk", action="store_true")
     ap.add_argument("--no-ttk-slow", action="store_true",
                     help="skip the second time-to-k on a slowly decaying planted spectrum "
@@ -917,7 +922,45 @@ def cpu_baseline(args, m_max, plant):
                     "sample_seconds_1thread": round(t1, 3)})
     if args.cpu_check_n and args.matrix == "hashwindow" and args.basis_bits == 64:
         out["linear_scaling_check"] = cpu_scaling_check(args, plant, A, omega)
+    if args.cpu_fixed_n and args.matrix == "hashwindow" and args.basis_bits == 64:
+        out["fixed_steps_at_n"] = cpu_fixed_steps(args, plant)
     return out
+
+
+def cpu_fixed_steps(args, plant):
+    """the oracle at the config's own n for a fixed number of block steps (rbl_start
+    + the first --cpu-check-steps steps, convergence checks off), per-step time stated as such —
+    not extrapolated.  The partial reorth grows with the step, so a 38-step run costs more per
+    step than these first steps."""
+    import threading
+    from oracle import matgen
+    from oracle import rbl_oracle as o
+    n, steps = args.cpu_fixed_n, args.cpu_check_steps
+    done = threading.Event()
+
+    def heartbeat():  # minutes of CPU work: keep stderr alive
+        while not done.wait(30.0):
+            progress(f"CPU fixed-step run at n={n} in progress")
+    hb = threading.Thread(target=heartbeat, daemon=True)
+    hb.start()
+    try:
+        t0 = time.perf_counter()
+        A = matgen.hashwindow_csr_chunked(n, args.halfwidth, args.density, args.seed, plant)
+        gen_s = time.perf_counter() - t0
+        progress(f"CPU fixed-step run: matrix built ({gen_s:.0f} s)")
+        omega = np.random.default_rng(0).standard_normal((n, args.b))
+        t0 = time.perf_counter()
+        o.RBL_gpu_semantics(A, args.k, args.b, omega=omega, kryl_sz=args.kryl, check=False,
+                            max_steps=steps)
+        t = time.perf_counter() - t0
+    finally:
+        done.set()
+    return {"n": n, "nnz": int(A.nnz), "block_steps": steps, "seconds": round(t, 2),
+            "ms_per_block_step": round(t / steps * 1e3, 1),
+            "block_iters_per_s_first_steps": round(steps / t, 5),
+            "matrix_build_s": round(gen_s, 1),
+            "note": "the oracle's rbl_start + first block steps at this n, measured in this run; the "
+                    "38-step figure (`value`) is extrapolated from the n = 1e5 sample"}
 
 
 def cpu_scaling_check(args, plant, A_small, omega_small):

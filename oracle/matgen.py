@@ -67,6 +67,25 @@ def hashwindow_csr(n: int, W: int, p: float, seed: int, plant=None, row_begin=0,
     return A
 
 
+def hashwindow_csr_chunked(n: int, W: int, p: float, seed: int, plant=None, chunk: int = 200_000):
+    """hashwindow_csr over all n rows built [chunk] rows at a time (the one-shot form needs ~10 GB
+    per candidate array at n = 1e7): the same matrix bit for bit, int32 indices (nnz < 2^31)."""
+    vals, cols, counts = [], [], []
+    for r0 in range(0, n, chunk):
+        A = hashwindow_csr(n, W, p, seed, plant, r0, min(n, r0 + chunk))
+        vals.append(A.data)
+        cols.append(A.indices.astype(np.int32))
+        counts.append(np.diff(A.indptr))
+    rowptr = np.zeros(n + 1, dtype=np.int64)
+    np.cumsum(np.concatenate(counts), out=rowptr[1:])
+    val = np.concatenate(vals)
+    del vals
+    col = np.concatenate(cols)
+    del cols
+    assert rowptr[-1] < 2 ** 31
+    return sp.csr_matrix((val, col, rowptr.astype(np.int32)), shape=(n, n))
+
+
 _RMAT_K = np.uint64(0xD1B54A32D192ED03)
 
 

@@ -67,24 +67,9 @@ def c4b_matrix():
 
 
 def c4a_matrix(chunk=200_000):
-    """C4a's CSR built in row chunks (the one-shot generator would need ~10 GB per candidate
-    array at n = 1e7); the chunks are matgen.hashwindow_csr's own rows, so the result is the
-    same matrix bit for bit.  int32 indices: nnz < 2^31."""
-    import scipy.sparse as sp
-    n, W, p, seed = C4A["n"], C4A["halfwidth"], C4A["density"], C4A["seed"]
-    plant = matgen.planted_spectrum(C4A["k"])
-    vals, cols, counts = [], [], []
-    for r0 in range(0, n, chunk):
-        A = matgen.hashwindow_csr(n, W, p, seed, plant, r0, min(n, r0 + chunk))
-        vals.append(A.data)
-        cols.append(A.indices.astype(np.int32))
-        counts.append(np.diff(A.indptr))
-    rowptr = np.zeros(n + 1, dtype=np.int64)
-    np.cumsum(np.concatenate(counts), out=rowptr[1:])
-    val = np.concatenate(vals); del vals
-    col = np.concatenate(cols); del cols
-    assert rowptr[-1] < 2 ** 31
-    return sp.csr_matrix((val, col, rowptr.astype(np.int32)), shape=(n, n))
+    """C4a's CSR built in row chunks (matgen.hashwindow_csr_chunked: the same matrix bit for bit)."""
+    return matgen.hashwindow_csr_chunked(C4A["n"], C4A["halfwidth"], C4A["density"], C4A["seed"],
+                                         matgen.planted_spectrum(C4A["k"]), chunk)
 
 
 # C4b at BASELINE's full size (the bench's sub-record, as drawn: RBL_OPT_RELABEL 0)

@@ -156,3 +156,14 @@ def test_mixed_mode_step_suite_spurious_pairs():
     assert abs(r32.D[0] - eig[0]) < 1e-6 * eig[0]                # the top one is right
     res = np.linalg.norm(A @ r32.V - r32.V * r32.D, axis=0) / np.abs(r32.D)
     assert res.max() > 1e-5                                      # ... and not eigenpairs of A
+
+
+def test_hashwindow_chunked_is_the_same_matrix():
+    """matgen.hashwindow_csr_chunked (the form the full-size fixtures and bench --cpu-fixed-n use)
+    builds hashwindow_csr's matrix bit for bit, chunk boundaries anywhere."""
+    plant = matgen.planted_spectrum(20)
+    A = matgen.hashwindow_csr(30000, 64, 0.7734, 11, plant)
+    for chunk in (997, 30000, 4096):
+        B = matgen.hashwindow_csr_chunked(30000, 64, 0.7734, 11, plant, chunk)
+        assert np.array_equal(A.indptr, B.indptr) and np.array_equal(A.indices, B.indices)
+        assert np.array_equal(A.data, B.data)
