@@ -252,16 +252,135 @@ __global__ __launch_bounds__(64) void k_chol_reg(const double* __restrict__ G, i
   }
 }
 
-// RBL_CHOL_REG=0: the four-wave kernel at b = 16 / 32 as well (A/B; read per call, tests switch it)
-static bool chol_reg_on() {
+// The same Cholesky on one wave with R^-1 formed in the same sweep: every row operation of the
+// right-looking factorisation (row j scaled by 1 / r_jj, row r minus M(j, r) times row j) is also
+// applied to X = I, which therefore ends as R^-T — no separate back substitution, whose 32
+// dependent divisions and sums made up half of k_chol_reg's time.  Row j goes to the other lanes
+// through LDS (a wave's LDS operations complete in issue order: one write, then broadcast reads;
+// no barrier), and R is staged in LDS once for the Rtot product.  R and Rtot have k_chol's bits;
+// R^-1 differs from the back substitution's at rounding level (both paths of every comparison in
+// the tests run this kernel).
+template <int B>
+__global__ __launch_bounds__(64) void k_chol_elim(const double* __restrict__ G, int64_t nglob, int mode,
+                                                  double* R, double* Rinv, double* Rtot, int* need3,
+                                                  int* status, const int* skip) {
+  if (skip && *skip) return;
+  __shared__ double rowj[2][64];
+  __shared__ __attribute__((aligned(16))) double Ms[B][B + 2];
+  const int c = threadIdx.x;
+  const int cc = c < B ? c : B - 1;
+  double tr = 0.0;
+#pragma unroll
+  for (int j = 0; j < B; ++j) tr += G[j * B + j];
+  const bool zero = !(tr > 0.0);
+  const double shift = zero ? 0.0 : 11.0 * ((double)nglob * B + (double)B * (B + 1)) * 0x1.0p-53 * tr;
+  double m[B], x[B];
+  int fail = 0, shifted = 0;
+  if (!zero) {
+    for (int attempt = 0; attempt < 2; ++attempt) {
+      const double sh = attempt ? shift : 0.0;
+#pragma unroll
+      for (int r = 0; r < B; ++r) {
+        m[r] = (r <= c) ? G[r * B + cc] + (r == c ? sh : 0.0) : 0.0;
+        x[r] = r == c ? 1.0 : 0.0;
+      }
+      fail = 0;
+#pragma unroll
+      for (int j = 0; j < B; ++j) {
+        const double d = bcast(m[j], j);  // M(j, j), held by lane j
+        const double gjj = G[j * B + j] + sh;
+        if (!(d > 0.0) || !isfinite(d)) {
+          fail = 1;
+        } else if (attempt == 0 && mode == 0 && d < 1e-15 * gjj) {
+          fail = 2;
+        }
+        if (fail) break;
+        const double rjj = sqrt(d);
+        if (c == j) m[j] = rjj;
+        if (c > j) m[j] /= rjj;  // M(j, c) /= rjj
+        x[j] /= rjj;             // row j of X (zero for c > j)
+        if (j + 1 < B) {
+          rowj[j & 1][c] = m[j];  // row j of M to every lane
+          __builtin_amdgcn_wave_barrier();
+#pragma unroll
+          for (int r = j + 1; r < B; ++r) {
+            const double mjr = rowj[j & 1][r];
+            if (r <= c) m[r] -= mjr * m[j];  // M(r, c) -= M(j, r) M(j, c)
+            x[r] -= mjr * x[j];              // X(r, c) -= M(j, r) X(j, c)
+          }
+        }
+      }
+      if (!fail) break;
+      shifted = 1;
+    }
+  }
+  const bool bad = !zero && fail;
+  const bool ok = !zero && !bad;
+  if (c < B) {
+#pragma unroll
+    for (int r = 0; r < B; ++r) {
+      const bool up = r <= c && ok;
+      R[r * B + c] = up ? m[r] : 0.0;
+      Rinv[c * B + r] = (ok && r >= c) ? x[r] : 0.0;  // R^-1 (c, r) = X(r, c)
+    }
+  }
+  if (mode == 0) {
+    if (c < B) {
+#pragma unroll
+      for (int r = 0; r < B; ++r) Rtot[r * B + c] = (r <= c && ok) ? m[r] : 0.0;
+    }
+  } else {
+    // Rtot = R Rtot_prev, column c: sum_{k = r..c} R(r, k) Rtot_prev(k, c) (Rtot_prev upper
+    // triangular: the terms past c are exact zeros), R(r, k) broadcast from LDS
+    double p[B];
+#pragma unroll
+    for (int k = 0; k < B; ++k) p[k] = Rtot[k * B + cc];
+    if (c < B) {
+#pragma unroll
+      for (int r = 0; r < B; ++r) Ms[r][c] = m[r];
+    }
+    __syncthreads();  // one wave: R staged, and every lane has read Rtot_prev
+    double out[B];
+#pragma unroll
+    for (int r = 0; r < B; ++r) {
+      double acc = 0.0;
+#pragma unroll
+      for (int k = r; k < B; ++k) acc += Ms[r][k] * p[k];
+      out[r] = (r <= c && ok) ? acc : 0.0;
+    }
+    if (c < B) {
+#pragma unroll
+      for (int r = 0; r < B; ++r) Rtot[r * B + c] = out[r];
+    }
+  }
+  if (c == 0) {
+    if (mode == 0) { need3[0] = shifted; need3[1] = !shifted; }
+    if (bad) status[0] = 1;
+    if (shifted) status[1] += 1;
+  }
+}
+
+// RBL_CHOL_REG: 0 the four-wave kernel at b = 16 / 32 as well, 1 k_chol_reg, 2 k_chol_elim
+// (A/B; read per call, tests switch it)
+static int chol_reg_mode() {
   const char* e = getenv("RBL_CHOL_REG");
-  return !e || atoi(e) != 0;
+  return e ? atoi(e) : 1;
 }
 
 void chol_step(const double* G, int b, int64_t nglobal, int mode, double* R, double* Rinv,
                double* Rtot, int* need3, int* status, const int* skip, hipStream_t s,
                double* scratch) {
-  if ((b == 32 || b == 16) && chol_reg_on()) {
+  const int cm = (b == 32 || b == 16) ? chol_reg_mode() : 0;
+  if (cm == 2) {
+    if (b == 32)
+      hipLaunchKernelGGL(k_chol_elim<32>, dim3(1), dim3(64), 0, s, G, nglobal, mode, R, Rinv, Rtot,
+                         need3, status, skip);
+    else
+      hipLaunchKernelGGL(k_chol_elim<16>, dim3(1), dim3(64), 0, s, G, nglobal, mode, R, Rinv, Rtot,
+                         need3, status, skip);
+    return;
+  }
+  if (cm == 1) {
     if (b == 32)
       hipLaunchKernelGGL(k_chol_reg<32>, dim3(1), dim3(64), 0, s, G, nglobal, mode, R, Rinv, Rtot,
                          need3, status, skip);
