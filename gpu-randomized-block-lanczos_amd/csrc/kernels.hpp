@@ -325,6 +325,9 @@ void chol_step(const double* G, int b, int64_t nglobal, int mode, double* R, dou
 void copy_small(const double* src, double* dst, int64_t len, hipStream_t s, const int* skip = nullptr);
 // dst = src^T (b x b row-major).
 void transpose_small(const double* src, double* dst, int b, hipStream_t s);
+// stash = [A_i (b x b) | R_tot (b x b) | 4 int flags], Bprev = R_tot, flags cleared (k_stash)
+void stash_step(const double* Ai, const double* Rtot, double* Bprev, int* flags, double* stash,
+                int b, hipStream_t s);
 
 // --- gen_rmat.hip (R-MAT generator) -------------------------------------
 struct RmatParams {

@@ -169,8 +169,16 @@ struct rbl_ctx {
   double* h_pin = nullptr;    // pinned staging: Ai, Rtot (2 b x b)
   void* h_d2h[2] = {nullptr, nullptr};  // pinned slots of the staged D2H (d2h_staged)
   hipEvent_t ev_d2h_slot[2] = {nullptr, nullptr};
-  double* h_hist = nullptr;   // rbl_step_async stash: per step i, Ai and Rtot (2 b x b)
-  int* h_hflags = nullptr;    //   and the step's 4 flags
+  double* h_hist = nullptr;   // rbl_step_async stash: per step i, Ai and Rtot (2 b x b) and the
+                              //   step's 4 flags (2 doubles' room): stash_rec(b) doubles each
+  double* d_stash = nullptr;  // the device side of one such record (k_stash; RBL_STASH_COPY=1)
+  // k_stash writes the record straight into h_pin / h_hist (coherent pinned memory, these are
+  // their device addresses) instead of a device record plus a D2H copy, which the SDMA engine
+  // ran ~60-80 us after the kernel, on the step's critical path
+  bool stash_direct = true;
+  double* dv_pin = nullptr;
+  double* dv_hist = nullptr;
+  bool flags_clean = false;   // d_flags already zero (the last step's k_stash cleared them)
   int fetched = 1;            // steps < fetched have been returned by rbl_fetch
   bool have_bprev = false;
   // locked Ritz vectors of the restarted variants (restarted.jl: Qlock / Qlock_gpu), fp64,
@@ -1554,6 +1562,7 @@ int rowop_ex(rbl_ctx* ctx, RowOpArgs a, double* G, double* Gx, bool reduce_x) {
 int tsqr(rbl_ctx* ctx, const double* U, double* Qout, bool g1_ready = false, float* Qout32 = nullptr,
          const double* Zloc = nullptr) {
   StageScope t(ctx, RBL_STAGE_QR);
+  ctx->flags_clean = false;  // the flags below start from zero only after a memset or k_stash
   const int b = ctx->b;
   int* need3 = ctx->d_flags;      // [need3, skip3]
   int* status = ctx->d_flags + 2; // [breakdown, shifted count]
@@ -1742,6 +1751,9 @@ int halo_exchange32(rbl_ctx* ctx, const float* Q, const float** Qin, int64_t* of
   return RBL_OK;
 }
 
+// one step's record in the async stash: A_i, R_tot (b x b each) and 4 int flags (2 doubles)
+size_t stash_rec(int b) { return (size_t)2 * b * b + 2; }
+
 // ---- the pushed half of the split halo (prepare_push) ----
 bool push_on(const rbl_ctx* ctx) { return ctx->push && ctx->ghost_active && ctx->nranks > 1; }
 
@@ -1845,8 +1857,9 @@ void free_run(rbl_ctx* ctx) {
   ctx->h_pin = nullptr;
   if (ctx->h_hist) hipHostFree(ctx->h_hist);
   ctx->h_hist = nullptr;
-  if (ctx->h_hflags) hipHostFree(ctx->h_hflags);
-  ctx->h_hflags = nullptr;
+  hipFree(ctx->d_stash);
+  ctx->d_stash = nullptr;
+  ctx->dv_pin = ctx->dv_hist = nullptr;
   ctx->nblocks = 0;
   ctx->b = 0;
   ctx->have_bprev = false;
@@ -2731,9 +2744,19 @@ int rbl_start(rbl_ctx* ctx, int b, int max_blocks, int basis_bits, const double*
   HIPC(hipMalloc(&ctx->d_small, (size_t)S_NSMALL * b * b * sizeof(double)));
   HIPC(hipMalloc(&ctx->d_flags, 4 * sizeof(int)));
   HIPC(hipMemset(ctx->d_flags, 0, 4 * sizeof(int)));
-  HIPC(hipHostMalloc(&ctx->h_pin, 2 * b * b * sizeof(double), hipHostMallocDefault));
-  HIPC(hipHostMalloc(&ctx->h_hist, (size_t)(max_blocks + 2) * 2 * b * b * sizeof(double), hipHostMallocDefault));
-  HIPC(hipHostMalloc(&ctx->h_hflags, (size_t)(max_blocks + 2) * 4 * sizeof(int), hipHostMallocDefault));
+  {
+    const char* e = std::getenv("RBL_STASH_COPY");  // A/B: 1 = device record + D2H copy
+    ctx->stash_direct = !(e && std::atoi(e) == 1);
+    const unsigned hf = ctx->stash_direct ? (hipHostMallocMapped | hipHostMallocCoherent) : hipHostMallocDefault;
+    HIPC(hipHostMalloc(&ctx->h_pin, stash_rec(b) * sizeof(double), hf));
+    HIPC(hipHostMalloc(&ctx->h_hist, (size_t)(max_blocks + 2) * stash_rec(b) * sizeof(double), hf));
+    if (ctx->stash_direct) {
+      HIPC(hipHostGetDevicePointer(reinterpret_cast<void**>(&ctx->dv_pin), ctx->h_pin, 0));
+      HIPC(hipHostGetDevicePointer(reinterpret_cast<void**>(&ctx->dv_hist), ctx->h_hist, 0));
+    } else {
+      HIPC(hipMalloc(&ctx->d_stash, stash_rec(b) * sizeof(double)));
+    }
+  }
   }
   // the push/pull split's partial-row buffers (sized by the matrix held, so also on a reused
   // plan): allocated here, inside the vote, not lazily in the first push exchange — a rank
@@ -2829,8 +2852,8 @@ int rbl_fetch(rbl_ctx* ctx, int i0, int i1, double* A_out, double* B_out, int* s
   const int b = ctx->b;
   int rc = RBL_OK;
   for (int j = i0; j < i1; ++j) {
-    const double* h = ctx->h_hist + (size_t)j * 2 * b * b;
-    const int* fl = ctx->h_hflags + 4 * j;
+    const double* h = ctx->h_hist + (size_t)j * stash_rec(b);
+    const int* fl = reinterpret_cast<const int*>(h + 2 * b * b);
     double* A = A_out ? A_out + (size_t)(j - i0) * b * b : nullptr;
     double* B = B_out ? B_out + (size_t)(j - i0) * b * b : nullptr;
     for (int r = 0; r < b; ++r)
@@ -2854,7 +2877,8 @@ int step_impl(rbl_ctx* ctx, int i, int part_reorth, double* A_out, double* B_out
   HIPC(hipSetDevice(ctx->device));
   const int b = ctx->b;
   const bool f32 = ctx->basis_bits == 32;
-  HIPC(hipMemsetAsync(ctx->d_flags, 0, 4 * sizeof(int), ctx->stream));
+  if (!ctx->flags_clean) HIPC(hipMemsetAsync(ctx->d_flags, 0, 4 * sizeof(int), ctx->stream));
+  ctx->flags_clean = false;  // until this step's k_stash has run
   if (f32 && (part_reorth & 2))
     return fail(ctx, RBL_ERR_INVALID, "rbl_step: locked-vector reorth needs the fp64 basis");
   // fp32 basis with the band-tile SpMM: A Q_i (after an fp32 halo exchange) and the 3-term
@@ -3085,13 +3109,19 @@ int step_impl(rbl_ctx* ctx, int i, int part_reorth, double* A_out, double* B_out
   } else {  // Qg = FLOAT(Qg_d) (RBL_gpu.jl:182): the new block enters the basis rounded to fp32
     CHK(tsqr(ctx, ctx->d_U, ctx->d_Qi64, fused, slotp32(ctx, i)));
   }
-  copy_small(smallp(ctx, S_RTOT), smallp(ctx, S_BPREV), (int64_t)b * b, ctx->stream);
+  // B_prev = R_tot, and A_i, R_tot, flags as one record: written to the host by k_stash itself
+  // (or one D2H copy of the device record, RBL_STASH_COPY=1)
+  const size_t rec = stash_rec(b);
+  double* rec_dev = !ctx->stash_direct ? ctx->d_stash
+                    : async            ? ctx->dv_hist + (size_t)i * rec
+                                       : ctx->dv_pin;
+  stash_step(smallp(ctx, S_AI), smallp(ctx, S_RTOT), smallp(ctx, S_BPREV), ctx->d_flags, rec_dev,
+             b, ctx->stream);
+  ctx->flags_clean = true;
   if (async) {  // stash A_i, R_tot and the flags for rbl_fetch; no host round trip
-    double* h = ctx->h_hist + (size_t)i * 2 * b * b;
-    HIPC(hipMemcpyAsync(h, smallp(ctx, S_AI), (size_t)b * b * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
-    HIPC(hipMemcpyAsync(h + b * b, smallp(ctx, S_RTOT), (size_t)b * b * sizeof(double),
-                        hipMemcpyDeviceToHost, ctx->stream));
-    HIPC(hipMemcpyAsync(ctx->h_hflags + 4 * i, ctx->d_flags, 4 * sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+    if (!ctx->stash_direct)
+      HIPC(hipMemcpyAsync(ctx->h_hist + (size_t)i * rec, ctx->d_stash, rec * sizeof(double),
+                          hipMemcpyDeviceToHost, ctx->stream));
     if ((int)ctx->step_ev.size() <= i) ctx->step_ev.resize(i + 1, nullptr);
     if (!ctx->step_ev[i]) HIPC(hipEventCreateWithFlags(&ctx->step_ev[i], hipEventDisableTiming));
     HIPC(hipEventRecord(ctx->step_ev[i], ctx->stream));
@@ -3099,13 +3129,11 @@ int step_impl(rbl_ctx* ctx, int i, int part_reorth, double* A_out, double* B_out
     ctx->nblocks = i + 1;
     return RBL_OK;
   }
-  HIPC(hipMemcpyAsync(ctx->h_pin, smallp(ctx, S_AI), (size_t)b * b * sizeof(double),
-                      hipMemcpyDeviceToHost, ctx->stream));
-  HIPC(hipMemcpyAsync(ctx->h_pin + b * b, smallp(ctx, S_RTOT), (size_t)b * b * sizeof(double),
-                      hipMemcpyDeviceToHost, ctx->stream));
-  int flags[4];
-  HIPC(hipMemcpyAsync(flags, ctx->d_flags, sizeof(flags), hipMemcpyDeviceToHost, ctx->stream));
+  if (!ctx->stash_direct)
+    HIPC(hipMemcpyAsync(ctx->h_pin, ctx->d_stash, rec * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
   HIPC(hipStreamSynchronize(ctx->stream));
+  int flags[4];
+  memcpy(flags, ctx->h_pin + 2 * b * b, sizeof(flags));
   harvest_timers(ctx);
   // row-major device -> column-major host
   for (int r = 0; r < b; ++r)

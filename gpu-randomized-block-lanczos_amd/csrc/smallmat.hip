@@ -360,11 +360,11 @@ __global__ __launch_bounds__(64) void k_chol_elim(const double* __restrict__ G, 
   }
 }
 
-// RBL_CHOL_REG: 0 the four-wave kernel at b = 16 / 32 as well, 1 k_chol_reg, 2 k_chol_elim
+// RBL_CHOL_REG: 0 the four-wave kernel at b = 16 / 32 as well, 1 k_chol_reg, 2 k_chol_elim (default)
 // (A/B; read per call, tests switch it)
 static int chol_reg_mode() {
   const char* e = getenv("RBL_CHOL_REG");
-  return e ? atoi(e) : 1;
+  return e ? atoi(e) : 2;
 }
 
 void chol_step(const double* G, int b, int64_t nglobal, int mode, double* R, double* Rinv,
@@ -409,6 +409,30 @@ void copy_small(const double* src, double* dst, int64_t len, hipStream_t s, cons
   if (blocks > 8192) blocks = 8192;
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(k_copy, dim3((unsigned)blocks), dim3(256), 0, s, src, dst, len, skip);
+}
+
+// End of a block step: A_i, R_tot (= B_{i+1}) and the four step flags into one contiguous
+// record for a single D2H copy, R_tot into B_prev for the next step's 3-term epilogue, and the
+// flags cleared for the next step — one launch where a copy kernel, three small D2H copies (a
+// blit each) and the next step's flag memset ran.
+__global__ void k_stash(const double* __restrict__ Ai, const double* __restrict__ Rtot,
+                        double* __restrict__ Bprev, int* __restrict__ flags,
+                        double* __restrict__ stash, int bb) {
+  for (int e = threadIdx.x; e < bb; e += blockDim.x) {
+    stash[e] = Ai[e];
+    const double r = Rtot[e];
+    stash[bb + e] = r;
+    Bprev[e] = r;
+  }
+  if (threadIdx.x < 4) {
+    reinterpret_cast<int*>(stash + 2 * bb)[threadIdx.x] = flags[threadIdx.x];
+    flags[threadIdx.x] = 0;
+  }
+  __threadfence_system();  // the record may be coherent host memory, read after the step's event
+}
+void stash_step(const double* Ai, const double* Rtot, double* Bprev, int* flags, double* stash,
+                int b, hipStream_t s) {
+  hipLaunchKernelGGL(k_stash, dim3(1), dim3(256), 0, s, Ai, Rtot, Bprev, flags, stash, b * b);
 }
 
 // dst = src^T (b x b row-major): B_i^T for the dense path's 3-term epilogue
