@@ -323,6 +323,8 @@ void chol_step(const double* G, int b, int64_t nglobal, int mode, double* R, dou
 // dst = src (len doubles): B_i stashed for the next step's epilogue, and the out-of-place
 // CholQR applies at b > 64; nothing when *skip != 0.
 void copy_small(const double* src, double* dst, int64_t len, hipStream_t s, const int* skip = nullptr);
+// C = C Rinv (b x b, Rinv upper triangular) unless *skip (k_cloc_rinv)
+void cloc_rinv(double* C, const double* Rinv, int b, const int* skip, hipStream_t s);
 // dst = src^T (b x b row-major).
 void transpose_small(const double* src, double* dst, int b, hipStream_t s);
 // stash = [A_i (b x b) | R_tot (b x b) | 4 int flags], Bprev = R_tot, flags cleared (k_stash)

@@ -1122,8 +1122,9 @@ void count_exchange(rbl_ctx* ctx, const std::vector<Comm::Xfer>& x) {
   }
 }
 
-// Gram C = W^T X over all ranks.  C layout [nW*w][X.count*X.w].
-int gram(rbl_ctx* ctx, const PanelRun& W, const Panels& X, double* C, const int* skip) {
+// Gram C = W^T X over all ranks.  C layout [nW*w][X.count*X.w].  (comm = false: this rank's
+// share only, for a caller that all-reduces it together with another buffer)
+int gram(rbl_ctx* ctx, const PanelRun& W, const Panels& X, double* C, const int* skip, bool comm = true) {
   const int xcols = X.count * X.w;
   const int splits = gram_splits(ctx->nloc, W.count, W.w, xcols);
   const int64_t len = (int64_t)W.count * W.w * xcols;
@@ -1136,7 +1137,7 @@ int gram(rbl_ctx* ctx, const PanelRun& W, const Panels& X, double* C, const int*
     HIPC(hipMemsetAsync(C, 0, len * sizeof(double), ctx->stream));
   }
   HIPC(hipGetLastError());
-  return allreduce(ctx, C, (size_t)len);
+  return comm ? allreduce(ctx, C, (size_t)len) : RBL_OK;
 }
 
 PanelRun run1(const double* p, int w) {
@@ -1166,7 +1167,9 @@ Panels pan2(const double* p0, const double* p1, int w) {
 // small-buffer carve (b x b each)
 // S_CHS*: chol scratch (b > 64); S_RINV1: R1^-1 kept for the 3-pass CholQR; S_CLOC: the next
 // step's local-reorth Gram
-enum { S_R = 0, S_RINV, S_RTOT, S_BPREV, S_AI, S_G, S_BT, S_CHS0, S_CHS1, S_RINV1, S_CLOC, S_NSMALL };
+// (S_CLOC follows S_G: CholQR's pass-3 Gram and the next step's local-reorth Gram share one
+// all-reduce of 2 b^2)
+enum { S_R = 0, S_RINV, S_RTOT, S_BPREV, S_AI, S_G, S_CLOC, S_BT, S_CHS0, S_CHS1, S_RINV1, S_NSMALL };
 double* smallp(rbl_ctx* ctx, int which) { return ctx->d_small + (int64_t)which * ctx->b * ctx->b; }
 
 int tsmm_checked(rbl_ctx* ctx, const PanelRun& X, const double* C, int ldc, const Panels& Y,
@@ -1518,7 +1521,7 @@ int upd32(rbl_ctx* ctx, const float* Xb, int nX, const double* C, int ldc, float
 // Fused row op in one of the CholQR forms (RowOpArgs: mode 1 Gram only, mode 2 two-stage
 // apply, Z for a cross Gram).  G: the Gram (mode 1) over all ranks; Gx: Z^T Y over all ranks
 // (reduced only when reduce_x).
-int rowop_ex(rbl_ctx* ctx, RowOpArgs a, double* G, double* Gx, bool reduce_x) {
+int rowop_ex(rbl_ctx* ctx, RowOpArgs a, double* G, double* Gx, bool reduce_x, bool comm_x = true) {
   const int b = ctx->b;
   const int gmax = rowgram_grid(ctx->nloc, kRowgramMaxPerCu);
   if ((size_t)2 * gmax * b * b > ctx->slab_elems)
@@ -1546,7 +1549,7 @@ int rowop_ex(rbl_ctx* ctx, RowOpArgs a, double* G, double* Gx, bool reduce_x) {
   }
   if (Gx && reduce_x) {
     reduce_slab(ctx->d_slab + (size_t)gmax * b * b, xgrid, (int64_t)b * b, Gx, nullptr, ctx->stream);
-    CHK(allreduce(ctx, Gx, (size_t)b * b));
+    if (comm_x) CHK(allreduce(ctx, Gx, (size_t)b * b));
   }
   return RBL_OK;
 }
@@ -1578,21 +1581,21 @@ int tsqr(rbl_ctx* ctx, const double* U, double* Qout, bool g1_ready = false, flo
     copy_small(ctx->d_T, Qout, ctx->nloc * b, ctx->stream, skip);
     return RBL_OK;
   };
-  // pass 1 (shift decided on device)
+  // pass 1 (shift decided on device); the 3-pass form keeps R1^-1 (S_RINV1) for its last pass
+  const bool three = fused && (ctx->fuse & 1);
   if (!g1_ready) CHK(gram(ctx, run1(U, b), pan1(U, b), G, nullptr));
-  chol_step(G, b, ctx->n, 0, smallp(ctx, S_R), smallp(ctx, S_RINV), smallp(ctx, S_RTOT), need3,
-            status, nullptr, ctx->stream, smallp(ctx, S_CHS0));
-  if (fused && (ctx->fuse & 1)) {
+  chol_step(G, b, ctx->n, 0, smallp(ctx, S_R), smallp(ctx, three ? S_RINV1 : S_RINV), smallp(ctx, S_RTOT),
+            need3, status, nullptr, ctx->stream, smallp(ctx, S_CHS0));
+  if (three) {
     // 3 passes: G2 = Gram of Q1 = U R1^-1 without storing Q1; then Q = (U R1^-1) R2^-1 in
     // one pass (Q1 recomputed bit for bit) — the same bits as the 4-pass form below
     RowOpArgs a1;
     a1.X = U;
-    a1.C = smallp(ctx, S_RINV);
+    a1.C = smallp(ctx, S_RINV1);
     a1.ldc = b;
     a1.mode = 1;
     a1.tri = true;  // R^-1
     CHK(rowop_ex(ctx, a1, G, nullptr, false));
-    copy_small(smallp(ctx, S_RINV), smallp(ctx, S_RINV1), (int64_t)b * b, ctx->stream);
     chol_step(G, b, ctx->n, 1, smallp(ctx, S_R), smallp(ctx, S_RINV), smallp(ctx, S_RTOT), need3,
               status, nullptr, ctx->stream, smallp(ctx, S_CHS0));
     RowOpArgs a2;
@@ -1606,9 +1609,13 @@ int tsqr(rbl_ctx* ctx, const double* U, double* Qout, bool g1_ready = false, flo
     a2.f64flag = Qout32 ? need3 : nullptr;
     a2.Z = Zloc;
     a2.mode = 2;
-    CHK(rowop_ex(ctx, a2, nullptr, Zloc ? smallp(ctx, S_CLOC) : nullptr, false));
-    // pass 3 only after a shifted first pass (device flag; kernels early-exit otherwise)
-    CHK(gram(ctx, run1(Qout, b), pan1(Qout, b), G, skip3));
+    // Zloc: this rank's share of Zloc^T Q2 now, all-reduced below with the pass-3 Gram
+    CHK(rowop_ex(ctx, a2, nullptr, Zloc ? smallp(ctx, S_CLOC) : nullptr, Zloc != nullptr, false));
+    // pass 3 only after a shifted first pass (device flag; kernels early-exit otherwise).  Its
+    // Gram's all-reduce runs either way (the host does not know the flag) and carries Zloc^T Q2
+    // in the same call (S_CLOC follows S_G)
+    CHK(gram(ctx, run1(Qout, b), pan1(Qout, b), G, skip3, Zloc == nullptr));
+    if (Zloc) CHK(allreduce(ctx, G, (size_t)2 * b * b));
     chol_step(G, b, ctx->n, 1, smallp(ctx, S_R), smallp(ctx, S_RINV), smallp(ctx, S_RTOT), need3,
               status, skip3, ctx->stream, smallp(ctx, S_CHS0));
     RowOpArgs a3;
@@ -1619,9 +1626,10 @@ int tsqr(rbl_ctx* ctx, const double* U, double* Qout, bool g1_ready = false, flo
     a3.Y = Qout;
     a3.skip = skip3;
     a3.Y32 = Qout32;
-    a3.Z = Zloc;
     a3.mode = 0;
-    CHK(rowop_ex(ctx, a3, nullptr, Zloc ? smallp(ctx, S_CLOC) : nullptr, Zloc != nullptr));
+    CHK(rowop_ex(ctx, a3, nullptr, nullptr, false));
+    // after a third pass Q3 = Q2 R3^-1: Zloc^T Q3 = (Zloc^T Q2) R3^-1 (no-op unless it ran)
+    if (Zloc) cloc_rinv(smallp(ctx, S_CLOC), smallp(ctx, S_RINV), b, skip3, ctx->stream);
     HIPC(hipGetLastError());
     return RBL_OK;
   }

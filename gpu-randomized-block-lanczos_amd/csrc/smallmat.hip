@@ -435,6 +435,28 @@ void stash_step(const double* Ai, const double* Rtot, double* Bprev, int* flags,
   hipLaunchKernelGGL(k_stash, dim3(1), dim3(256), 0, s, Ai, Rtot, Bprev, flags, stash, b * b);
 }
 
+// C = C R^-1 (b x b row-major, R^-1 upper triangular) unless *skip: the next step's local-reorth
+// Gram Z^T Q after CholQR's third pass (Q3 = Q2 R3^-1, so Z^T Q3 = (Z^T Q2) R3^-1), formed from
+// the pass-2 Gram already all-reduced instead of a fourth collective
+__global__ void k_cloc_rinv(double* __restrict__ C, const double* __restrict__ Rinv, int b,
+                            const int* __restrict__ skip) {
+  if (skip && *skip) return;
+  __shared__ double c[kMaxB * kMaxB];
+  const int bb = b * b;
+  for (int e = threadIdx.x; e < bb; e += blockDim.x) c[e] = C[e];
+  __syncthreads();
+  for (int e = threadIdx.x; e < bb; e += blockDim.x) {
+    const int r = e / b, col = e % b;
+    double acc = 0.0;
+    for (int k = 0; k <= col; ++k) acc += c[r * b + k] * Rinv[k * b + col];
+    C[e] = acc;
+  }
+}
+void cloc_rinv(double* C, const double* Rinv, int b, const int* skip, hipStream_t s) {
+  if (getenv("RBL_DIAG_CLOC_NOFIX")) return;  // diagnostics: the test's negative control
+  hipLaunchKernelGGL(k_cloc_rinv, dim3(1), dim3(256), 0, s, C, Rinv, b, skip);
+}
+
 // dst = src^T (b x b row-major): B_i^T for the dense path's 3-term epilogue
 __global__ void k_transpose_small(const double* __restrict__ src, double* __restrict__ dst, int b) {
   for (int e = threadIdx.x; e < b * b; e += blockDim.x) dst[(e % b) * b + e / b] = src[e];

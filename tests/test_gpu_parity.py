@@ -405,3 +405,43 @@ def test_cholqr_elimination_kernel(rbl, monkeypatch, b, bits):
             A, eig = gen(300, 5)
             D, V, info = rbl.RBL_gpu(A, 5, b, seed=3, return_info=True)
             assert info.converged and np.linalg.norm((D - eig) / eig) < o.KNOWN_ANSWER_TOL
+
+
+@pytest.mark.parametrize("b", [16, 32])
+def test_local_reorth_gram_after_shifted_third_pass(rbl, monkeypatch, b):
+    """The next step's local-reorth Gram formed inside the QR (RBL_OPT_FUSE bit 1) when CholQR
+    takes its shifted third pass: Z^T Q3 = (Z^T Q2) R3^-1 (k_cloc_rinv), the partials of Z^T Q2
+    all-reduced with the pass-3 Gram.  A diagonal A of rank 4.5 b: the block Krylov space is
+    range(A) (Q_1 = qr(A Omega)), so step 4's U has b/2 directions above rounding and its QR is
+    shifted (an even step: the next one runs no partial reorth, so the Gram rides on this QR);
+    step 5's local reorth then removes the new block's (rounding-born) Q_4 components with it.  After 5 steps ||Q_4^T Q_5|| is at rounding (1e-12) with the Gram fused (3)
+    and separate (1); without the R3^-1 factor (RBL_DIAG_CLOC_NOFIX, the negative control) it is
+    not, so the test sees the factor."""
+    import scipy.sparse as sp
+    from rbl import _lib
+    n, D = 2000, 9 * b // 2
+    lam = np.zeros(n)
+    lam[:D] = np.linspace(1.0, 10.0, D)
+    A = sp.diags(lam).tocsc()
+    omega = np.random.default_rng(b).standard_normal((n, b))
+
+    def run(fuse):
+        with rbl.Context(0) as ctx:
+            ctx.set_option(_lib.RBL_OPT_FUSE, fuse)
+            ctx.set_matrix(A)
+            ctx.start(b, 8, omega=omega)
+            for i in range(1, 6):
+                ctx.step_async(i, i >= 2 and i % 2 == 0)
+            st = [s for _, _, s in ctx.fetch(1, 6)]
+            Q4, Q5 = ctx.get_block(4), ctx.get_block(5)
+        return st, np.abs(Q4.T @ Q5).max()
+
+    st3, e3 = run(3)
+    st1, e1 = run(1)
+    monkeypatch.setenv("RBL_DIAG_CLOC_NOFIX", "1")
+    st3n, e3n = run(3)
+    print(f"b={b}: statuses {st3} / {st1}; |Q4^T Q5| fused {e3:.2e}, separate {e1:.2e}, "
+          f"fused without R3^-1 {e3n:.2e}")
+    assert st3[3] == _lib.RBL_WARN_QR_SHIFTED and st1[3] == _lib.RBL_WARN_QR_SHIFTED
+    assert e3 < 1e-12 and e1 < 1e-12
+    assert e3n > 1e3 * e3
