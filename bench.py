@@ -294,12 +294,14 @@ def measure(ctx, args, matrix, K, W, nloc, nnz_loc, world, barrier, allmax):
         progress(f"{matrix} n={n} b={b}: warmup run {w_ + 1}/{W}")
     for key in host:
         host[key] = 0.0
-    # the timed region runs as a user's job does: stage timers off (each stage boundary is a
-    # pair of timestamped hipEvents on the stream, ~12 per block step, a few us of queue time
-    # each); the stage split and the rooflines come from a second pass of K runs with them on
-    ctx.set_option(_lib.RBL_OPT_TIMERS, 0)
+    # the timed region records hipEvents only around the two kernels priced against their
+    # rooflines (RBL_OPT_TIMERS 2: the SpMM's "AQ" and "part reorth" stages); every stage
+    # boundary timed (1) is ~12 timestamped events per block step, a few us of queue time each,
+    # so the full stage split comes from a second pass of the same K runs
+    ctx.set_option(_lib.RBL_OPT_TIMERS, 2)
     barrier()
     ctx.synchronize()
+    ctx.reset_timers()
     ctx.comm_stats(reset=True)
     barrier()
     t0 = time.perf_counter()
@@ -317,6 +319,7 @@ def measure(ctx, args, matrix, K, W, nloc, nnz_loc, world, barrier, allmax):
     run_spread = {"min": round(runs_ms[0], 2), "median": round(runs_ms[len(runs_ms) // 2], 2),
                   "max": round(runs_ms[-1], 2)} if runs_ms else None
     host_timed = dict(host)
+    stage_timed = ctx.timers()  # "AQ" and "part reorth" of the timed region
     ctx.set_option(_lib.RBL_OPT_TIMERS, 1)
     barrier()
     ctx.synchronize()
@@ -337,7 +340,7 @@ def measure(ctx, args, matrix, K, W, nloc, nnz_loc, world, barrier, allmax):
 
     # ---- roofline: SpMM (HBM) and partial reorth (fp64 MFMA), live from HIP events ----
     spmm_launches = K * (m_max + 1)               # rbl_start + one per block step
-    spmm_ms = stage["AQ"] / spmm_launches
+    spmm_ms = stage_timed["AQ"] / spmm_launches
     # algorithmic bytes: nnz*(8+4) + (n+1)*8 + read Q + write U
     # (+ read Q_{i-1} for the fused 3-term epilogue on the m_max step launches)
     bytes_step = nnz_loc * 12 + (nloc + 1) * 8 + 3 * nloc * b * 8
@@ -349,7 +352,7 @@ def measure(ctx, args, matrix, K, W, nloc, nnz_loc, world, barrier, allmax):
     spmm_bytes = (m_max * bytes_step + bytes_start + (m_max - 1) * nloc * b * 8 * lfused) / (m_max + 1)
     spmm_gbs = spmm_bytes / (spmm_ms * 1e-3) / 1e9
     reorth_flops = sum(8.0 * nloc * b * b * (i - 2) for i in range(4, m_max + 1, 2))
-    reorth_ms = stage_per_run["part reorth"]
+    reorth_ms = stage_timed["part reorth"] / K
     reorth_tf = reorth_flops / (reorth_ms * 1e-3) / 1e12 if reorth_ms > 0 else 0.0
     # HBM bytes from PMC counters (tools/pmc_traffic.sh -> tools/pmc_summarize.py; separate
     # FETCH_SIZE / WRITE_SIZE passes, gfx950 per-width calibration): a committed measurement of
@@ -421,7 +424,7 @@ def measure(ctx, args, matrix, K, W, nloc, nnz_loc, world, barrier, allmax):
                    **({"held_clock_ghz": round(held, 3),
                        "frac_of_peak_at_held_clock": round(reorth_tf / (mfma_peak * held / 2.4), 4)}
                       if held and mbound else {})}
-    if stage["part reorth"] > stage["AQ"]:
+    if stage_timed["part reorth"] > stage_timed["AQ"]:
         roofline, roofline2 = roof_reorth, roof_spmm
     else:
         roofline, roofline2 = roof_spmm, roof_reorth

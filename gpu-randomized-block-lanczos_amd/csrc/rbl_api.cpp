@@ -187,7 +187,7 @@ struct rbl_ctx {
   int nlock = 0, lock_cap = 0;
 
   // options
-  bool timers = false;
+  int timers = 0;  // RBL_OPT_TIMERS: 0 off, 1 every stage, 2 the SpMM and partial-reorth stages
   int reorth_order = 0;
   int spmm_variant = 0;
   int fuse = 7;               // RBL_OPT_FUSE
@@ -1072,13 +1072,14 @@ struct StageScope {
   hipStream_t st;
   StageScope(rbl_ctx* c, int s, hipStream_t on = nullptr) : ctx(c), stage(s), st(on ? on : c->stream) {
     roctxRangePushA(kStageNames[s]);
-    if (ctx->timers) {
+    if (ctx->timers == 1 ||
+        (ctx->timers == 2 && (s == RBL_STAGE_AQ || s == RBL_STAGE_PART_REORTH))) {
       a = next_event(ctx);
       if (a) hipEventRecord(a, st);
     }
   }
   ~StageScope() {
-    if (ctx->timers && a) {
+    if (a) {
       hipEvent_t b = next_event(ctx);
       if (b) {
         hipEventRecord(b, st);
@@ -2211,7 +2212,10 @@ int rbl_rccl_version(int* version, char* path, int path_len) {
 int rbl_set_option(rbl_ctx* ctx, int option, int64_t value) {
   if (!ctx) return RBL_ERR_INVALID;
   switch (option) {
-    case RBL_OPT_TIMERS: ctx->timers = value != 0; return RBL_OK;
+    case RBL_OPT_TIMERS:
+      if (value < 0 || value > 2) return fail(ctx, RBL_ERR_INVALID, "RBL_OPT_TIMERS: 0, 1 or 2");
+      ctx->timers = (int)value;
+      return RBL_OK;
     case RBL_OPT_REORTH_ORDER:
       if (value < 0 || value > 1) return fail(ctx, RBL_ERR_INVALID, "reorth order must be 0|1");
       ctx->reorth_order = (int)value;

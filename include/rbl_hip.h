@@ -57,7 +57,9 @@ extern "C" {
 #define RBL_NUM_STAGES        8
 
 /* Options for rbl_set_option(). */
-#define RBL_OPT_TIMERS        0   /* 1: record per-stage hipEvents (adds event records)         */
+#define RBL_OPT_TIMERS        0   /* 1: record per-stage hipEvents (adds event records);        */
+                                  /*    2: only the "AQ" and "part reorth" stages (the kernels  */
+                                  /*    the bench prices against their rooflines)               */
 #define RBL_OPT_REORTH_ORDER  1   /* 0: block-CGS (batched, default); 1: ascending-j block MGS  */
                                   /*    exactly as RBL.jl:30-48 / RBL_gpu.jl:65-67               */
 #define RBL_OPT_DEVICE_BLOCKS 3   /* Krylov blocks kept in HBM (the reference's hybrid buffer,

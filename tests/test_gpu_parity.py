@@ -190,6 +190,22 @@ def test_stage_timers(rbl):
         assert t[s] > 0.0, (s, t)
 
 
+def test_stage_timers_roofline_only(rbl):
+    """RBL_OPT_TIMERS 2 (the bench's timed region): events around "AQ" and "part reorth" only;
+    other values are refused."""
+    from rbl import _lib
+    A = c1_matrix(5000, 4)
+    with rbl.Context(0) as ctx:
+        ctx.set_matrix(A)
+        with pytest.raises(rbl.RBLError):
+            ctx.set_option(_lib.RBL_OPT_TIMERS, 3)
+        ctx.set_option(_lib.RBL_OPT_TIMERS, 2)
+        rbl.lanczos(ctx, 4, 8, seed=1, check=False, max_steps=8, ritz=True)
+        t = ctx.timers()
+    assert t["AQ"] > 0.0 and t["part reorth"] > 0.0, t
+    assert all(v == 0.0 for s, v in t.items() if s not in ("AQ", "part reorth")), t
+
+
 @pytest.mark.parametrize("b,k", [(16, 7), (32, 5)])
 def test_ritz_odd_k(rbl, b, k):
     """Ritz projection with an odd number of vectors on the b = 16 / 32 MFMA paths."""
