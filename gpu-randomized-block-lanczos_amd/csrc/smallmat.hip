@@ -360,7 +360,113 @@ __global__ __launch_bounds__(64) void k_chol_elim(const double* __restrict__ G, 
   }
 }
 
-// RBL_CHOL_REG: 0 the four-wave kernel at b = 16 / 32 as well, 1 k_chol_reg, 2 k_chol_elim (default)
+// k_chol_elim with the wave's other half at work: lanes [0, B) hold the columns of M, lanes
+// [B, 2B) those of X (= I, ending as R^-T), so a column step is one division and 31 - j fused
+// updates per lane instead of two and 2 (31 - j).  Every value is formed by the same operations
+// in the same order as k_chol_elim: the same bits.
+template <int B>
+__global__ __launch_bounds__(64) void k_chol_elim2(const double* __restrict__ G, int64_t nglob, int mode,
+                                                   double* R, double* Rinv, double* Rtot, int* need3,
+                                                   int* status, const int* skip) {
+  static_assert(2 * B <= 64, "two columns per lane pair");
+  if (skip && *skip) return;
+  __shared__ double rowj[2][B];
+  __shared__ __attribute__((aligned(16))) double Ms[B][B + 2];
+  const int c = threadIdx.x;
+  const bool isx = c >= B;                            // an X lane (or idle, c >= 2B)
+  const bool live = c < 2 * B;
+  const int col = c < B ? c : (live ? c - B : B - 1);  // the column this lane holds
+  double tr = 0.0;
+#pragma unroll
+  for (int j = 0; j < B; ++j) tr += G[j * B + j];
+  const bool zero = !(tr > 0.0);
+  const double shift = zero ? 0.0 : 11.0 * ((double)nglob * B + (double)B * (B + 1)) * 0x1.0p-53 * tr;
+  double v[B];
+  int fail = 0, shifted = 0;
+  if (!zero) {
+    for (int attempt = 0; attempt < 2; ++attempt) {
+      const double sh = attempt ? shift : 0.0;
+#pragma unroll
+      for (int r = 0; r < B; ++r) {  // loads on every lane, then selects: no branches
+        const double g = G[r * B + col];
+        v[r] = isx ? (r == col ? 1.0 : 0.0) : g + (r == col ? sh : 0.0);
+      }
+      fail = 0;
+#pragma unroll
+      for (int j = 0; j < B; ++j) {
+        const double d = bcast(v[j], j);  // M(j, j), held by lane j
+        const double gjj = G[j * B + j] + sh;
+        if (!(d > 0.0) || !isfinite(d)) {
+          fail = 1;
+        } else if (attempt == 0 && mode == 0 && d < 1e-15 * gjj) {
+          fail = 2;
+        }
+        if (fail) break;
+        const double rjj = sqrt(d);
+        // M lanes: M(j, c) /= rjj right of the diagonal, r_jj on it; X lanes: X(j, c) /= rjj
+        const double q = v[j] / rjj;
+        v[j] = (!isx && col == j) ? rjj : q;
+        if (j + 1 < B) {
+          if (!isx) rowj[j & 1][col] = v[j];  // row j of M to every lane
+          __builtin_amdgcn_wave_barrier();
+          // M(r, c) or X(r, c) -= M(j, r) (.)(j, c), every r on every lane: an M lane's entries
+          // below its diagonal (r > c) take values nothing reads (R, the rows sent through rowj
+          // and the Rtot product use only r <= c), so no lane masks are kept across the sweep
+#pragma unroll
+          for (int r = j + 1; r < B; ++r) {
+            const double mjr = rowj[j & 1][r];
+            v[r] -= mjr * v[j];
+          }
+        }
+      }
+      if (!fail) break;
+      shifted = 1;
+    }
+  }
+  const bool bad = !zero && fail;
+  const bool ok = !zero && !bad;
+  if (live) {
+#pragma unroll
+    for (int r = 0; r < B; ++r) {
+      if (!isx) R[r * B + col] = (r <= col && ok) ? v[r] : 0.0;
+      else Rinv[col * B + r] = (ok && r >= col) ? v[r] : 0.0;  // R^-1 (c, r) = X(r, c)
+    }
+  }
+  if (mode == 0) {
+    if (!isx) {
+#pragma unroll
+      for (int r = 0; r < B; ++r) Rtot[r * B + col] = (r <= col && ok) ? v[r] : 0.0;
+    }
+  } else {
+    // Rtot = R Rtot_prev, column c: sum_{k = r..c} R(r, k) Rtot_prev(k, c) on the M lanes (the
+    // terms past c are exact zeros), R(r, k) broadcast from LDS
+    double p[B];
+#pragma unroll
+    for (int k = 0; k < B; ++k) p[k] = Rtot[k * B + col];
+    if (!isx) {
+#pragma unroll
+      for (int r = 0; r < B; ++r) Ms[r][col] = v[r];
+    }
+    __syncthreads();  // one wave: R staged, and every lane has read Rtot_prev
+    if (!isx) {
+#pragma unroll
+      for (int r = 0; r < B; ++r) {
+        double acc = 0.0;
+#pragma unroll
+        for (int k = r; k < B; ++k) acc += Ms[r][k] * p[k];
+        Rtot[r * B + col] = (r <= col && ok) ? acc : 0.0;
+      }
+    }
+  }
+  if (c == 0) {
+    if (mode == 0) { need3[0] = shifted; need3[1] = !shifted; }
+    if (bad) status[0] = 1;
+    if (shifted) status[1] += 1;
+  }
+}
+
+// RBL_CHOL_REG: 0 the four-wave kernel at b = 16 / 32 as well, 1 k_chol_reg, 2 k_chol_elim2
+// (default), 3 k_chol_elim (the one-half-wave form, same bits as 2)
 // (A/B; read per call, tests switch it)
 static int chol_reg_mode() {
   const char* e = getenv("RBL_CHOL_REG");
@@ -372,6 +478,15 @@ void chol_step(const double* G, int b, int64_t nglobal, int mode, double* R, dou
                double* scratch) {
   const int cm = (b == 32 || b == 16) ? chol_reg_mode() : 0;
   if (cm == 2) {
+    if (b == 32)
+      hipLaunchKernelGGL(k_chol_elim2<32>, dim3(1), dim3(64), 0, s, G, nglobal, mode, R, Rinv, Rtot,
+                         need3, status, skip);
+    else
+      hipLaunchKernelGGL(k_chol_elim2<16>, dim3(1), dim3(64), 0, s, G, nglobal, mode, R, Rinv, Rtot,
+                         need3, status, skip);
+    return;
+  }
+  if (cm == 3) {
     if (b == 32)
       hipLaunchKernelGGL(k_chol_elim<32>, dim3(1), dim3(64), 0, s, G, nglobal, mode, R, Rinv, Rtot,
                          need3, status, skip);

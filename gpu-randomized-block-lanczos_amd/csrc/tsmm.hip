@@ -11,6 +11,8 @@
 // row = (lane>>4) + 4*reg).  Memory layout: every n x w panel is row-major, so a 16-lane
 // quad reads 128 contiguous bytes.  Gram partials go to a slab [split][a][c] reduced in a
 // fixed order by reduce_slab (bitwise reproducible, no atomics).
+#include <cstdlib>
+
 #include "kernels.hpp"
 
 namespace rbl {
@@ -226,8 +228,46 @@ __global__ __launch_bounds__(256) void k_reduce_chunks(const double* __restrict_
   part[(int64_t)c * len + e] = (a0 + a1) + (a2 + a3);
 }
 
+// The b x b Grams of a block step (len = b^2 <= 4096, one partial per row-op workgroup: ~500
+// at n = 1.25e6): 4 elements x 64 split lanes per workgroup, so len / 4 workgroups cover the
+// chip and a lane's sums are 2 rounds of 4 independent loads instead of k_reduce's 8 (a latency
+// kernel between two dependent launches, ~5 per step); then a fixed LDS tree over the 64 lanes.
+__global__ __launch_bounds__(256) void k_reduce_wide(const double* __restrict__ slab, int splits,
+                                                     int64_t len, double* __restrict__ out,
+                                                     const int* skip) {
+  if (skip && *skip) return;
+  __shared__ double part[64][5];
+  const int el = threadIdx.x & 3, j = threadIdx.x >> 2;
+  const int64_t e = (int64_t)blockIdx.x * 4 + el;
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+  if (e < len) {
+    int s = j;
+#pragma unroll 2
+    for (; s + 192 < splits; s += 256) {
+      a0 += slab[(int64_t)s * len + e];
+      a1 += slab[(int64_t)(s + 64) * len + e];
+      a2 += slab[(int64_t)(s + 128) * len + e];
+      a3 += slab[(int64_t)(s + 192) * len + e];
+    }
+    for (; s < splits; s += 64) a0 += slab[(int64_t)s * len + e];
+  }
+  part[j][el] = (a0 + a1) + (a2 + a3);
+  __syncthreads();
+  // 64 -> 1 in a fixed pairwise order: lane pairs (t, t + w) for w = 32, 16, ..., 1
+  for (int w = 32; w >= 1; w >>= 1) {
+    if (j < w) part[j][el] += part[j + w][el];
+    __syncthreads();
+  }
+  if (j == 0 && e < len) out[e] = part[0][el];
+}
+
 void reduce_slab(const double* slab, int splits, int64_t len, double* out, const int* skip,
                  hipStream_t s) {
+  if (len <= 4096 && splits > 64 && !std::getenv("RBL_REDUCE_NARROW")) {
+    hipLaunchKernelGGL(k_reduce_wide, dim3((unsigned)((len + 3) / 4)), dim3(256), 0, s, slab, splits, len,
+                       out, skip);
+    return;
+  }
   const int blocks = (int)((len + 15) / 16);
   hipLaunchKernelGGL(k_reduce, dim3(blocks), dim3(256), 0, s, slab, splits, len, out, skip);
 }

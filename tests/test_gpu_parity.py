@@ -393,24 +393,26 @@ def test_cholqr_register_kernel_bit_identical(rbl, monkeypatch, b, bits):
 
 @pytest.mark.parametrize("b,bits", [(16, 64), (32, 64), (32, 32)])
 def test_cholqr_elimination_kernel(rbl, monkeypatch, b, bits):
-    """The one-wave Cholesky that forms R^-1 in the factorisation's own sweep (k_chol_elim,
-    RBL_CHOL_REG=2): R and Rtot as the other kernels, R^-1 by forward elimination instead of back
-    substitution — 12-step A_i / B_{i+1} traces within 1e-12 of the four-wave kernel's on the
-    C1-like matrix and through Krylov exhaustion, and the reference's known-answer suites on it
-    (b = 16 / 32: moderate and slow decay at n = 300, k = 5) within the suites' 1e-13."""
+    """The one-wave Cholesky that forms R^-1 in the factorisation's own sweep (k_chol_elim2, the
+    default RBL_CHOL_REG=2): R and Rtot as the other kernels, R^-1 by forward elimination instead
+    of back substitution — 12-step A_i / B_{i+1} traces within 1e-12 of the four-wave kernel's on
+    the C1-like matrix and through Krylov exhaustion, and the reference's known-answer suites on
+    it (b = 16 / 32: moderate and slow decay at n = 300, k = 5) within the suites' 1e-13.  The
+    form on both halves of the wave (2) and on one half (k_chol_elim, 3): the same bits."""
     A1 = c1_matrix(4000, 10)
     A2, _ = o.slow_decay_matrix(9 * b, 5)
     for A, steps in ((A1, 12), (A2, 9)):
         n = A.shape[0]
         omega = np.random.default_rng(b).standard_normal((n, b))
         out = {}
-        for reg in ("0", "2"):
+        for reg in ("0", "2", "3"):
             monkeypatch.setenv("RBL_CHOL_REG", reg)
             with rbl.Context(0) as ctx:
                 ctx.set_matrix(A)
                 _, _, info = rbl.lanczos(ctx, 5, b, omega=omega, check=False, max_steps=steps,
                                          trace=True, ritz=False, basis_bits=bits)
             out[reg] = (np.array(info.trace_A), np.array(info.trace_B))
+        assert np.array_equal(out["2"][0], out["3"][0]) and np.array_equal(out["2"][1], out["3"][1])
         for t in (0, 1):
             scale = np.abs(out["0"][t]).max()
             d = np.abs(out["2"][t] - out["0"][t]).max() / scale
