@@ -196,11 +196,22 @@ __global__ __launch_bounds__(256) void k_reduce(const double* __restrict__ slab,
 }
 
 // Many splits (the partial-reorth update's local-reorth Gram: one partial per 128-row tile,
-// ~78 k at C4a): sum fixed chunks of splits in parallel (256 per chunk, then 16) until at most
+// ~78 k at C4a): sum fixed chunks of splits in parallel (red_chunk per chunk) until at most
 // 64 remain, each level into the scratch after the previous one, then k_reduce — a fixed order
 // (bitwise reproducible); one k_reduce pass over 78 k partials is latency-bound (16 split lanes
 // per element, 64 workgroups): 310 us against ~130 us.
-static int red_chunk(int splits) { return splits > 4096 ? 256 : 16; }
+// Chunk 32 (round 5): the first level's grid is then ~splits / 32 x len / 256 workgroups whose
+// threads sum 32 partials each (8 rounds of 4 loads) — at n = 1.25e6 (9,766 partials) 1,224
+// workgroups instead of 156 that summed 256 each (64 dependent rounds, 40 us).  RBL_RED_CHUNK=0:
+// the earlier rule (256 above 4,096 partials, else 16), for A/B.
+static int red_chunk(int splits) {
+  static const int mode = [] {
+    const char* e = std::getenv("RBL_RED_CHUNK");
+    return e ? std::atoi(e) : 32;
+  }();
+  if (mode <= 0) return splits > 4096 ? 256 : 16;
+  return mode;
+}
 int reduce_scratch_splits(int splits) {
   int tot = 0;
   while (splits > 64) {
