@@ -27,21 +27,33 @@ class TBand:
         self.b = b
         self.data = np.zeros((b + 1, b * max_blocks))
         self.nblocks = 0
+        # one block's entries as flat index arrays: one 1-D scatter per block instead of b slice
+        # assignments (~2.8 ms of host time per 38-step run at b = 32, between the GPU runs)
+        ncols = b * max_blocks
+        lr, lc = np.tril_indices(b)           # A_i[r, c], r >= c -> band (r - c, c)
+        self._a = ((lr - lc) * ncols + lc, lr * b + lc, lc * b + lr)
+        ur, uc = np.triu_indices(b)           # B_i[r, c], r <= c -> band (b - c + r, c)
+        self._b = ((b - uc + ur) * ncols + uc, ur * b + uc, uc * b + ur)
+        self._flat = self.data.reshape(-1)    # a view (C-contiguous)
+
+    @staticmethod
+    def _take(M: np.ndarray, src_c: np.ndarray, src_f: np.ndarray) -> np.ndarray:
+        if M.flags.f_contiguous:
+            return M.ravel(order="F")[src_f]
+        return np.ascontiguousarray(M).ravel()[src_c]
 
     def insert_A(self, Ai: np.ndarray) -> None:
         """common.jl:9-17: column (i-1)b+j receives A_i[j:b, j] (tril)."""
         b, i = self.b, self.nblocks
+        dst, src_c, src_f = self._a
         self.data[:, i * b:(i + 1) * b] = 0.0
-        for j in range(b):
-            self.data[: b - j, i * b + j] = Ai[j:, j]
+        self._flat[dst + i * b] = self._take(np.asarray(Ai, dtype=np.float64), src_c, src_f)
         self.nblocks += 1
 
     def insert_B(self, Bi: np.ndarray, it: int) -> None:
         """common.jl:20-26: the last j rows of column (it-1)b+j receive B[0:j, j] (triu)."""
-        b = self.b
-        start = (it - 1) * b
-        for j in range(1, b + 1):
-            self.data[b + 1 - j:, start + j - 1] = Bi[:j, j - 1]
+        dst, src_c, src_f = self._b
+        self._flat[dst + (it - 1) * self.b] = self._take(np.asarray(Bi, dtype=np.float64), src_c, src_f)
 
     def view(self) -> np.ndarray:
         return self.data[:, : self.nblocks * self.b]
