@@ -1171,6 +1171,7 @@ Panels pan2(const double* p0, const double* p1, int w) {
 // (S_CLOC follows S_G: CholQR's pass-3 Gram and the next step's local-reorth Gram share one
 // all-reduce of 2 b^2)
 enum { S_R = 0, S_RINV, S_RTOT, S_BPREV, S_AI, S_G, S_CLOC, S_BT, S_CHS0, S_CHS1, S_RINV1, S_NSMALL };
+static_assert(S_CLOC == S_G + 1, "tsqr all-reduces [S_G | S_CLOC] as one 2 b^2 buffer");
 double* smallp(rbl_ctx* ctx, int which) { return ctx->d_small + (int64_t)which * ctx->b * ctx->b; }
 
 int tsmm_checked(rbl_ctx* ctx, const PanelRun& X, const double* C, int ldc, const Panels& Y,
