@@ -205,10 +205,8 @@ __global__ __launch_bounds__(256) void k_reduce(const double* __restrict__ slab,
 // workgroups instead of 156 that summed 256 each (64 dependent rounds, 40 us).  RBL_RED_CHUNK=0:
 // the earlier rule (256 above 4,096 partials, else 16), for A/B.
 static int red_chunk(int splits) {
-  static const int mode = [] {
-    const char* e = std::getenv("RBL_RED_CHUNK");
-    return e ? std::atoi(e) : 32;
-  }();
+  const char* e = std::getenv("RBL_RED_CHUNK");  // read per call: the slab is sized by
+  const int mode = e ? std::atoi(e) : 32;          // rbl_start under the same setting
   if (mode <= 0) return splits > 4096 ? 256 : 16;
   return mode;
 }

@@ -463,3 +463,33 @@ def test_local_reorth_gram_after_shifted_third_pass(rbl, monkeypatch, b):
     assert st3[3] == _lib.RBL_WARN_QR_SHIFTED and st1[3] == _lib.RBL_WARN_QR_SHIFTED
     assert e3 < 1e-12 and e1 < 1e-12
     assert e3n > 1e3 * e3
+
+
+def test_latency_knobs_agree(rbl, monkeypatch):
+    """The A/B switches of round 5's latency work: RBL_STASH_COPY=1 (a device record and one D2H
+    copy instead of k_stash writing pinned memory) gives the same bits; RBL_REDUCE_NARROW=1 and
+    RBL_RED_CHUNK=0 (the earlier Gram-partial reductions: other summation trees) the same A_i /
+    B_{i+1} to 1e-12 — at n = 40,000, where the b x b Grams have > 64 partials (k_reduce_wide) and
+    the update's local-reorth Gram one per 128 rows (chunked levels)."""
+    A = c1_matrix(40000, 10)
+    b = 32
+    omega = np.random.default_rng(4).standard_normal((A.shape[0], b))
+
+    def run():
+        with rbl.Context(0) as ctx:
+            ctx.set_matrix(A)
+            _, _, info = rbl.lanczos(ctx, 10, b, omega=omega, check=False, max_steps=12,
+                                     trace=True, ritz=False)
+        return np.array(info.trace_A), np.array(info.trace_B)
+
+    ref = run()
+    for knob, exact in (("RBL_STASH_COPY", True), ("RBL_REDUCE_NARROW", False), ("RBL_RED_CHUNK", False)):
+        monkeypatch.setenv(knob, "0" if knob == "RBL_RED_CHUNK" else "1")
+        out = run()
+        monkeypatch.delenv(knob)
+        for t in (0, 1):
+            if exact:
+                assert np.array_equal(out[t], ref[t]), knob
+            else:
+                d = np.abs(out[t] - ref[t]).max() / np.abs(ref[t]).max()
+                assert d < 1e-12, (knob, t, d)
