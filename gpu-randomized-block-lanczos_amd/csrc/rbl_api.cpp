@@ -12,6 +12,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <chrono>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -1763,6 +1764,18 @@ int halo_exchange32(rbl_ctx* ctx, const float* Q, const float** Qin, int64_t* of
 
 // one step's record in the async stash: A_i, R_tot (b x b each) and 4 int flags (2 doubles)
 size_t stash_rec(int b) { return (size_t)2 * b * b + 2; }
+// The staged D2H of the Ritz vectors (d2h_staged): two pinned 64 MiB slots and their events,
+// kept for the context's life.  Pinning them costs ~20-30 ms, so rbl_start allocates them with
+// the run's buffers when a Ritz result will take the staged path (one basis block >= 256 MiB),
+// instead of the first rbl_ritz of the context paying it (profiles/r05_ttk_probe.log).
+constexpr size_t kD2HPiece = size_t(64) << 20;
+int ensure_d2h_slots(rbl_ctx* ctx) {
+  for (int s = 0; s < 2; ++s) {
+    if (!ctx->h_d2h[s]) HIPC(hipHostMalloc(&ctx->h_d2h[s], kD2HPiece, hipHostMallocDefault));
+    if (!ctx->ev_d2h_slot[s]) HIPC(hipEventCreateWithFlags(&ctx->ev_d2h_slot[s], hipEventDisableTiming));
+  }
+  return RBL_OK;
+}
 
 // ---- the pushed half of the split halo (prepare_push) ----
 bool push_on(const rbl_ctx* ctx) { return ctx->push && ctx->ghost_active && ctx->nranks > 1; }
@@ -2763,6 +2776,8 @@ int rbl_start(rbl_ctx* ctx, int b, int max_blocks, int basis_bits, const double*
     const unsigned hf = ctx->stash_direct ? (hipHostMallocMapped | hipHostMallocCoherent) : hipHostMallocDefault;
     HIPC(hipHostMalloc(&ctx->h_pin, stash_rec(b) * sizeof(double), hf));
     HIPC(hipHostMalloc(&ctx->h_hist, (size_t)(max_blocks + 2) * stash_rec(b) * sizeof(double), hf));
+    if ((size_t)ctx->nloc * b * sizeof(double) >= 4 * kD2HPiece && !std::getenv("RBL_D2H_DIRECT"))
+      CHK(ensure_d2h_slots(ctx));
     if (ctx->stash_direct) {
       HIPC(hipHostGetDevicePointer(reinterpret_cast<void**>(&ctx->dv_pin), ctx->h_pin, 0));
       HIPC(hipHostGetDevicePointer(reinterpret_cast<void**>(&ctx->dv_hist), ctx->h_hist, 0));
@@ -3164,16 +3179,12 @@ int step_impl(rbl_ctx* ctx, int i, int part_reorth, double* A_out, double* B_out
 // through the runtime's own bounce buffer on one thread, well under the PCIe rate (§2: 49-56 GB/s
 // pinned).  Every earlier piece's host copy has finished before its slot is refilled.
 // RBL_D2H_DIRECT=1 restores the plain copy (A/B).
-constexpr size_t kD2HPiece = size_t(64) << 20;
 int d2h_staged(rbl_ctx* ctx, void* dst, const void* src, size_t bytes) {
   if (bytes < 4 * kD2HPiece || std::getenv("RBL_D2H_DIRECT")) {
     HIPC(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
     return RBL_OK;
   }
-  for (int s = 0; s < 2; ++s) {
-    if (!ctx->h_d2h[s]) HIPC(hipHostMalloc(&ctx->h_d2h[s], kD2HPiece, hipHostMallocDefault));
-    if (!ctx->ev_d2h_slot[s]) HIPC(hipEventCreateWithFlags(&ctx->ev_d2h_slot[s], hipEventDisableTiming));
-  }
+  CHK(ensure_d2h_slots(ctx));
   const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
   const char* envt = std::getenv("RBL_D2H_THREADS");
   const int nthr = (int)std::min(envt ? std::max(1u, (unsigned)atoi(envt)) : 8u, hw);
@@ -3224,10 +3235,17 @@ int rbl_ritz(rbl_ctx* ctx, int nblocks, int k, const double* S, double* V_out) {
   const int kcp = (kc + 1) & ~1;  // even panel width (16-B row stores), zero-padded column
   if (chunk_bytes(kc) > 0.7 * (double)free_b)
     return fail(ctx, RBL_ERR_OOM, "rbl_ritz: no room for one Ritz column");
+  // RBL_RITZ_TRACE=1: host-side split of the call on stderr (diagnostics)
+  const bool trace = std::getenv("RBL_RITZ_TRACE") != nullptr;
+  auto tnow = [] { return std::chrono::duration<double, std::milli>(
+                       std::chrono::steady_clock::now().time_since_epoch()).count(); };
+  const double t0 = trace ? tnow() : 0.0;
+  double t_alloc = 0.0, t_comp = 0.0, t_d2h = 0.0;
   DevBuf d_S, d_V, d_Vcm;
   HIPC(hipMalloc(&d_S.p, rows * kcp * sizeof(double)));
   HIPC(hipMalloc(&d_V.p, nl * kcp * sizeof(double)));
   HIPC(hipMalloc(&d_Vcm.p, nl * kcp * sizeof(double)));
+  if (trace) t_alloc = tnow() - t0;
   std::vector<double> srm((size_t)rows * kcp);
   for (int c0 = 0; c0 < k; c0 += kc) {
     const int w = std::min(kc, k - c0);
@@ -3245,11 +3263,24 @@ int rbl_ritz(rbl_ctx* ctx, int nblocks, int k, const double* S, double* V_out) {
     }
     if (ctx->nloc > 0) rowmajor_to_colmajor(d_V.d(), ctx->nloc, kcp, d_Vcm.d(), ctx->stream);
     HIPC(hipGetLastError());
+    double tc = 0.0;
+    if (trace) {
+      HIPC(hipStreamSynchronize(ctx->stream));
+      tc = tnow();
+      t_comp += tc - t0 - t_alloc - t_comp - t_d2h;
+    }
     if (V_out && ctx->nloc > 0)
       CHK(d2h_staged(ctx, V_out + (size_t)c0 * ctx->nloc, d_Vcm.p, ctx->nloc * w * sizeof(double)));
+    if (trace) {
+      HIPC(hipStreamSynchronize(ctx->stream));
+      t_d2h += tnow() - tc;
+    }
   }
   HIPC(hipStreamSynchronize(ctx->stream));
   harvest_timers(ctx);
+  if (trace)
+    fprintf(stderr, "rbl_ritz: alloc %.2f ms, S + combine + transpose %.2f ms, D2H %.2f ms, total %.2f ms\n",
+            t_alloc, t_comp, t_d2h, tnow() - t0);
   return RBL_OK;
 }
 

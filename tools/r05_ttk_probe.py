@@ -1,0 +1,26 @@
+#!/usr/bin/env python3
+"""Time-to-k at C4a three times on one context, after one full-length run without Ritz vectors
+(as bench.py measures it): the host split (start / fetch wait / eig / Ritz + D2H) per run — does
+the first Ritz call pay one-off costs (the pinned staging slots)?"""
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "gpu-randomized-block-lanczos_amd")]
+import numpy as np  # noqa: E402
+import rbl  # noqa: E402
+
+n, b, k = 10_000_000, 32, 20
+plant = np.array([100.0 * (2 * k + 1 - l) for l in range(1, 2 * k + 1)])
+with rbl.Context(0) as ctx:
+    ctx.gen_hashwindow(n, 64, 0.7734, 20261015, plant)
+    rbl.lanczos(ctx, k, b, check=False, ritz=False)  # as bench.py's timed runs: full-length, no Ritz
+    for rep in range(3):
+        ctx.synchronize()
+        t = time.perf_counter()
+        D, V, info = rbl.lanczos(ctx, k, b, seed=rep + 1)
+        dt = time.perf_counter() - t
+        print(f"rep {rep}: {dt * 1e3:7.1f} ms iters={info.iters} start={info.start_ms:.1f} "
+              f"fetch={info.fetch_ms:.1f} eig={info.eig_ms:.1f} ritz+d2h={info.ritz_ms:.1f}", flush=True)
+        del V
