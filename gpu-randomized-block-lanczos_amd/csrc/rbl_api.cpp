@@ -3241,10 +3241,24 @@ int rbl_ritz(rbl_ctx* ctx, int nblocks, int k, const double* S, double* V_out) {
                        std::chrono::steady_clock::now().time_since_epoch()).count(); };
   const double t0 = trace ? tnow() : 0.0;
   double t_alloc = 0.0, t_comp = 0.0, t_d2h = 0.0;
-  DevBuf d_S, d_V, d_Vcm;
-  HIPC(hipMalloc(&d_S.p, rows * kcp * sizeof(double)));
-  HIPC(hipMalloc(&d_V.p, nl * kcp * sizeof(double)));
-  HIPC(hipMalloc(&d_Vcm.p, nl * kcp * sizeof(double)));
+  // the run's scratch blocks hold a chunk when it is at most b wide (k <= b: every chunk): U
+  // (n_local x b) takes V, T the column-major copy, the coefficient buffer (max_blocks b x 2b)
+  // the S rows — no 2 x n_local x kcp allocation per call (at C4a 3.2 GB, whose hipMalloc +
+  // first touch cost up to ~20 ms of a time-to-k)
+  DevBuf own_S, own_V, own_Vcm;
+  double *pS = nullptr, *pV = nullptr, *pVcm = nullptr;
+  if (kcp <= b && ctx->d_U && ctx->d_T && ctx->d_C && (size_t)rows * kcp <= ctx->C_elems) {
+    pS = ctx->d_C;
+    pV = ctx->d_U;
+    pVcm = ctx->d_T;
+  } else {
+    HIPC(hipMalloc(&own_S.p, rows * kcp * sizeof(double)));
+    HIPC(hipMalloc(&own_V.p, nl * kcp * sizeof(double)));
+    HIPC(hipMalloc(&own_Vcm.p, nl * kcp * sizeof(double)));
+    pS = own_S.d();
+    pV = own_V.d();
+    pVcm = own_Vcm.d();
+  }
   if (trace) t_alloc = tnow() - t0;
   std::vector<double> srm((size_t)rows * kcp);
   for (int c0 = 0; c0 < k; c0 += kc) {
@@ -3255,13 +3269,13 @@ int rbl_ritz(rbl_ctx* ctx, int nblocks, int k, const double* S, double* V_out) {
     // S columns [c0, c0 + w) (column-major, ld = rows) -> row-major rows x kcp, zero-padded
     for (int64_t r = 0; r < rows; ++r)
       for (int c = 0; c < kcp; ++c) srm[(size_t)r * kcp + c] = c < w ? S[(size_t)(c0 + c) * rows + r] : 0.0;
-    HIPC(hipMemcpyAsync(d_S.p, srm.data(), rows * kcp * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+    HIPC(hipMemcpyAsync(pS, srm.data(), rows * kcp * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
     {
       StageScope t(ctx, RBL_STAGE_RITZ);
-      if (ctx->basis_bits == 64) CHK(combine_blocks(ctx, nblocks, kcp, d_S.d(), d_V.d()));
-      else CHK(combine_blocks32(ctx, nblocks, kcp, d_S.d(), d_V.d()));
+      if (ctx->basis_bits == 64) CHK(combine_blocks(ctx, nblocks, kcp, pS, pV));
+      else CHK(combine_blocks32(ctx, nblocks, kcp, pS, pV));
     }
-    if (ctx->nloc > 0) rowmajor_to_colmajor(d_V.d(), ctx->nloc, kcp, d_Vcm.d(), ctx->stream);
+    if (ctx->nloc > 0) rowmajor_to_colmajor(pV, ctx->nloc, kcp, pVcm, ctx->stream);
     HIPC(hipGetLastError());
     double tc = 0.0;
     if (trace) {
@@ -3270,7 +3284,7 @@ int rbl_ritz(rbl_ctx* ctx, int nblocks, int k, const double* S, double* V_out) {
       t_comp += tc - t0 - t_alloc - t_comp - t_d2h;
     }
     if (V_out && ctx->nloc > 0)
-      CHK(d2h_staged(ctx, V_out + (size_t)c0 * ctx->nloc, d_Vcm.p, ctx->nloc * w * sizeof(double)));
+      CHK(d2h_staged(ctx, V_out + (size_t)c0 * ctx->nloc, pVcm, ctx->nloc * w * sizeof(double)));
     if (trace) {
       HIPC(hipStreamSynchronize(ctx->stream));
       t_d2h += tnow() - tc;

@@ -13,7 +13,11 @@ import rbl  # noqa: E402
 
 n, b, k = 10_000_000, 32, 20
 plant = np.array([100.0 * (2 * k + 1 - l) for l in range(1, 2 * k + 1)])
+if len(sys.argv) > 1 and sys.argv[1] == "slow":  # bench.py's slowly decaying spectrum
+    plant = np.array([12.0 + 0.25 * (2 * k + 1 - l) for l in range(1, 2 * k + 1)])
 with rbl.Context(0) as ctx:
+    if "timers" in sys.argv[1:]:  # every stage timed, as bench.py's time-to-k runs
+        ctx.set_option(0, 1)
     ctx.gen_hashwindow(n, 64, 0.7734, 20261015, plant)
     rbl.lanczos(ctx, k, b, check=False, ritz=False)  # as bench.py's timed runs: full-length, no Ritz
     for rep in range(3):
