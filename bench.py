@@ -566,7 +566,8 @@ def main():
                "host_eig_ms": round(info.eig_ms, 3),
                "host_ms": {"start": round(info.start_ms, 1), "fetch_wait": round(info.fetch_ms, 1),
                            "eig": round(info.eig_ms, 1), "ritz_and_d2h": round(info.ritz_ms, 1)},
-               "stage_ms": {s_: round(v, 3) for s_, v in ttk_stage.items()}}
+               "stage_ms": {s_: round(v, 3) for s_, v in ttk_stage.items()},
+               "speculated_steps": info.spec_steps, "speculated_discarded": info.spec_wasted}
 
     # ---- time-to-k on a slowly decaying spectrum (same generator and n, another plant) ----
     ttk_slow = None
@@ -597,7 +598,9 @@ def main():
                     "host_eig_ms": round(info.eig_ms, 3),
                     "host_ms": {"start": round(info.start_ms, 1), "fetch_wait": round(info.fetch_ms, 1),
                                 "eig": round(info.eig_ms, 1), "ritz_and_d2h": round(info.ritz_ms, 1)},
-                    "stage_ms": {s_: round(v, 3) for s_, v in st_.items()}}
+                    "stage_ms": {s_: round(v, 3) for s_, v in st_.items()},
+                    "speculated_steps": info.spec_steps, "speculated_discarded": info.spec_wasted,
+                    "max_residual_per_check": [float("%.3g" % r) for r in info.resid]}
 
     # ---- BASELINE config 4 (C4b): the R-MAT pattern at the same n, b, k, same ranks ----
     # A sub-record that raises on one rank leaves the headline line unprinted; on one rank

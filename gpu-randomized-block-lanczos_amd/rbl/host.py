@@ -133,10 +133,32 @@ def sort_eig_abs(D: np.ndarray, V: np.ndarray, k: int):
     return D[perm], V[:, perm]
 
 
+def residual_norms(B: np.ndarray, V: np.ndarray, b: int, k: int) -> np.ndarray:
+    """The k residual bounds ||B_{i+1} S[end-b+1:end, l]||_2 of common.jl:56-65."""
+    return np.linalg.norm(B @ V[V.shape[0] - b:, :k], axis=0)
+
+
+def speculation_depth(resid: list, tol: float, margin: float = 100.0) -> int:
+    """How many steps rbl.lanczos(speculate="auto") enqueues ahead of the next convergence check,
+    from the max residual bounds of the earlier checks.  The next bound is predicted as the last
+    one times the last ratio (clamped to <= 1: geometric decay, the Lanczos rate; measured at C4a
+    on the slow spectrum the prediction lands within 1.1x of the bound once the decay is steady,
+    and overestimates it while the decay still accelerates).  Predicted above margin x tol: the
+    check is expected to fail, so the 4 steps up to the next check (the next check's stride).
+    Between tol and margin x tol: 1 step (an odd step: no partial reorth, cheaper than the
+    eigensolve it hides once the T band is large).  Otherwise, or with fewer than two earlier
+    checks (no rate), none."""
+    if len(resid) < 2 or not (resid[-1] > 0.0 and resid[-2] > 0.0):
+        return 0
+    pred = resid[-1] * min(1.0, resid[-1] / resid[-2])
+    if pred > margin * tol:
+        return 4
+    return 1 if pred > tol else 0
+
+
 def check_convergence(B: np.ndarray, V: np.ndarray, b: int, k: int, tol: float) -> bool:
     """common.jl:56-65 — every ||B_{i+1} S[end-b+1:end, l]||_2 <= tol (absolute)."""
-    Y = B @ V[V.shape[0] - b:, :k]
-    return bool(np.all(np.linalg.norm(Y, axis=0) <= tol))
+    return bool(np.all(residual_norms(B, V, b, k) <= tol))
 
 
 def fix_signs(S: np.ndarray) -> np.ndarray:

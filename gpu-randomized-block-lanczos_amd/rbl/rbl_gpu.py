@@ -27,7 +27,8 @@ import scipy.sparse as sp
 
 from . import _lib
 from ._lib import RBLError, dptr, i32ptr, i64ptr, lib, u8ptr
-from .host import TBand, check_convergence, dsbev, eig_topk, fix_signs, sort_eig_abs
+from .host import (TBand, check_convergence, dsbev, eig_topk, fix_signs,
+                   residual_norms, sort_eig_abs, speculation_depth)
 
 KRYL_SZ_GPU = 1200          # RBL_gpu.jl:211
 RESIDUAL_TOL = 1e-7         # RBL_gpu.jl:189
@@ -349,6 +350,9 @@ class RBLInfo:
     ritz_ms: float = 0.0         # host wall time of rbl_ritz (device work + D2H of V)
     start_ms: float = 0.0        # host wall time of rbl_start (A Omega + QR)
     enqueue_ms: float = 0.0      # host time inside rbl_step_async (enqueueing the steps)
+    spec_steps: int = 0          # steps enqueued ahead of a convergence check (speculate)
+    spec_wasted: int = 0         # of those, steps past the converging check (discarded)
+    resid: list = field(default_factory=list)   # max residual bound at each check
     trace_A: list = field(default_factory=list)
     trace_B: list = field(default_factory=list)
 
@@ -377,7 +381,7 @@ def max_steps_for(kryl_sz: int, b: int) -> int:
 def lanczos(ctx: Context, k: int, b: int, *, kryl_sz: int = KRYL_SZ_GPU, omega=None, seed=0,
             check: bool = True, max_steps: int | None = None, tol: float = RESIDUAL_TOL,
             trace: bool = False, ritz: bool = True, basis_bits: int = 64,
-            speculate: "bool | int" = False):
+            speculate: "bool | int | str" = "auto"):
     """RBL_gpu.jl:134-203 + :219 on an already-loaded context.  Returns (D, V_local, info)."""
     steps_cap = max_steps_for(kryl_sz, b)
     if max_steps is not None:
@@ -400,14 +404,17 @@ def lanczos(ctx: Context, k: int, b: int, *, kryl_sz: int = KRYL_SZ_GPU, omega=N
     # Steps are enqueued without a host round trip (rbl_step_async) and fetched where the host
     # needs the T band: at a convergence check (:186) and after the last step.  T receives the
     # same A_i / B_i in the same order as the reference's per-step pushes (:185, :193).
-    # Speculation: before blocking at a check the host enqueues as many further steps as its
-    # T-band eigensolve is expected to last (the previous one scaled by (N/N_prev)^2.7, over the
-    # measured time per step; at most up to the next check), so the GPU keeps working during
-    # dsbev.  The check reads only steps <= i, and steps after an even i touch no block <= i
-    # (partial reorth at even steps), so D, S and the Ritz vectors are unchanged; a converged
-    # run discards the extra steps.  Off by default: on the C4a slow-spectrum time-to-k (28
-    # steps, dsbevd) it hid ~60 ms of eigensolves and wasted as much on the steps after the
-    # converging check (0.91 s vs 0.87-0.89 s strict).
+    # Speculation: before the host blocks at a check and solves the T band (dsbev, up to ~35 ms at
+    # N = 896), it may enqueue further steps, so the GPU keeps working during the eigensolve.  The
+    # check reads only steps <= i, and steps after an even i touch no block <= i (partial reorth
+    # at even steps), so D, S and the Ritz vectors are unchanged; a converged run discards the
+    # extra steps, which is the cost.  speculate="auto" (default) enqueues up to the next check
+    # when the residual bounds of the previous two checks, extrapolated geometrically, put this
+    # check at least 100x above the tolerance, and one step when they put it above the tolerance
+    # (host.speculation_depth) — a decision every rank makes alike from the same T (the
+    # convergence test itself already relies on that), so ranks issue the same steps.
+    # True: as many steps as the eigensolve is expected to last (the previous one scaled by
+    # (N/N_prev)^2.7, over the measured time per step; one rank only); an int: a fixed count (tests).
     last_i = min(steps_cap, math.ceil(kryl_sz / b))
     enq = 0
 
@@ -434,12 +441,19 @@ def lanczos(ctx: Context, k: int, b: int, *, kryl_sz: int = KRYL_SZ_GPU, omega=N
         # (one rank only: the count comes from host timings, and every rank must issue the
         # same steps — their collectives pair up)
         # (speculate may also be a fixed count of extra steps per check: tests)
-        if speculate and ctx.nranks == 1 and is_check and not is_last and i % 2 == 0:
-            if speculate is True:
-                extra = int(last_eig * (i * b / last_n) ** 2.7 // step_ms) if last_eig and step_ms else 0
+        spec_to = i
+        if speculate is not False and is_check and not is_last and i % 2 == 0:
+            if speculate == "auto":
+                spec_to = i + speculation_depth(info.resid, tol)
+            elif speculate is True:
+                if ctx.nranks == 1 and last_eig and step_ms:
+                    spec_to = i + int(last_eig * (i * b / last_n) ** 2.7 // step_ms)
             else:
-                extra = int(speculate)
-            enqueue(min(last_i, i + 4, i + extra))
+                spec_to = i + int(speculate)
+            spec_to = min(last_i, i + 4, spec_to)
+            if spec_to > i:
+                info.spec_steps += spec_to - i
+                enqueue(spec_to)
         t0 = time.perf_counter()
         fetched = ctx.fetch(first, i + 1)
         t1 = time.perf_counter()
@@ -457,8 +471,11 @@ def lanczos(ctx: Context, k: int, b: int, *, kryl_sz: int = KRYL_SZ_GPU, omega=N
                 info.eig_ms += dt * 1e3
                 eig_prev = dt
                 last_eig, last_n = dt * 1e3, i * b
-                if check_convergence(Bj, S, b, k, tol):   # :189
+                res = residual_norms(Bj, S, b, k)
+                info.resid.append(float(res.max()) if res.size else 0.0)
+                if bool(np.all(res <= tol)):               # :189 (check_convergence)
                     info.converged = True
+                    info.spec_wasted += spec_to - i
                     break
             T.insert_B(Bj, j)                      # :193
         first = i + 1

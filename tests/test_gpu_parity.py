@@ -357,16 +357,20 @@ def test_speculative_steps_change_nothing(rbl, case):
         A = (A + matgen.hashwindow_csr(3000, 8, 0.5, 3, None) * 1e-3).tocsr()
     omega = np.random.default_rng(5).standard_normal((A.shape[0], b))
     out = []
-    for spec in (False, 3):
+    for spec in (False, 3, "auto"):
         with rbl.Context(0) as ctx:
             ctx.set_matrix(A)
             D, V, info = rbl.lanczos(ctx, k, b, omega=omega, trace=True, speculate=spec)
         out.append((D, V, info))
-    (D0, V0, i0), (D1, V1, i1) = out
-    assert i0.iters == i1.iters and i0.converged == i1.converged
-    assert np.array_equal(D0, D1) and np.array_equal(V0, V1)
-    assert all(np.array_equal(a, c) for a, c in zip(i0.trace_A, i1.trace_A))
-    assert all(np.array_equal(a, c) for a, c in zip(i0.trace_B, i1.trace_B))
+    D0, V0, i0 = out[0]
+    assert i0.spec_steps == 0 and out[1][2].spec_steps > 0
+    if case == "runs_out":   # residuals far above the tolerance: "auto" runs ahead from check 3 on
+        assert out[2][2].spec_steps > 0 and out[2][2].spec_wasted == 0
+    for D1, V1, i1 in out[1:]:
+        assert i0.iters == i1.iters and i0.converged == i1.converged
+        assert np.array_equal(D0, D1) and np.array_equal(V0, V1)
+        assert all(np.array_equal(a, c) for a, c in zip(i0.trace_A, i1.trace_A))
+        assert all(np.array_equal(a, c) for a, c in zip(i0.trace_B, i1.trace_B))
 
 
 @pytest.mark.parametrize("b,bits", [(16, 64), (32, 64), (32, 32)])

@@ -97,3 +97,27 @@ def test_fix_signs_makes_ritz_coefficients_solver_independent():
     assert np.all(F1[np.argmax(np.abs(F1), axis=0), np.arange(k)] > 0)
     neg = fix_signs(-S1)
     assert np.array_equal(neg, F1)
+
+
+def test_speculation_rule_from_residual_history():
+    """rbl.lanczos's speculate="auto": run ahead of a check by 4 steps when the geometric
+    extrapolation of the earlier checks' max residual bounds stays >= 100x above the tolerance,
+    by 1 between 1x and 100x, else not; the residual bounds are common.jl:56-65's norms
+    (check_convergence is their all-below-tol test)."""
+    from rbl.host import check_convergence, residual_norms, speculation_depth
+    tol = 1e-7
+    assert speculation_depth([], tol) == 0 and speculation_depth([1.0], tol) == 0
+    assert speculation_depth([1e-1, 1e-2], tol) == 4           # next ~1e-3
+    assert speculation_depth([1e-3, 2e-3], tol) == 4           # growth clamped: next ~2e-3
+    assert speculation_depth([2.8e-3, 4.0e-5], tol) == 1       # next ~5.7e-7 (C4a slow, check 24)
+    assert speculation_depth([4.0e-5, 6.0e-7], tol) == 0       # next ~9e-9: expected to converge
+    assert speculation_depth([0.0, 1e-3], tol) == 0 and speculation_depth([1.0, float("nan")], tol) == 0
+    # the C4a slow-spectrum bounds of profiles/r05_ttk_probe_b26.log: 4, 4, 4, 1, 0 from check 3 on
+    r = [4.8e+00, 2.5e+00, 1.9e-01, 2.8e-03, 4.0e-05, 6.0e-07, 8.9e-09]
+    assert [speculation_depth(r[:j], tol) for j in range(2, 7)] == [4, 4, 4, 1, 0]
+    rng = np.random.default_rng(0)
+    b, k = 4, 3
+    B, S = rng.standard_normal((b, b)), rng.standard_normal((20, 6))
+    r = residual_norms(B, S, b, k)
+    assert r.shape == (k,) and np.allclose(r, np.linalg.norm(B @ S[-b:, :k], axis=0))
+    assert check_convergence(B, S, b, k, r.max() * 1.001) and not check_convergence(B, S, b, k, r.max() * 0.999)

@@ -23,8 +23,12 @@ with rbl.Context(0) as ctx:
     for rep in range(3):
         ctx.synchronize()
         t = time.perf_counter()
-        D, V, info = rbl.lanczos(ctx, k, b, seed=rep + 1)
+        spec = os.environ.get("TTK_SPEC", "auto")
+        spec = {"0": False, "auto": "auto", "1": True}.get(spec, spec)
+        D, V, info = rbl.lanczos(ctx, k, b, seed=rep + 1, speculate=spec)
         dt = time.perf_counter() - t
         print(f"rep {rep}: {dt * 1e3:7.1f} ms iters={info.iters} start={info.start_ms:.1f} "
-              f"fetch={info.fetch_ms:.1f} eig={info.eig_ms:.1f} ritz+d2h={info.ritz_ms:.1f}", flush=True)
+              f"fetch={info.fetch_ms:.1f} eig={info.eig_ms:.1f} ritz+d2h={info.ritz_ms:.1f} "
+              f"spec={info.spec_steps}/{info.spec_wasted} resid={['%.1e' % r for r in info.resid]}",
+              flush=True)
         del V
