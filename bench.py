@@ -72,6 +72,9 @@ def parse():
                     help="skip the second time-to-k on a slowly decaying planted spectrum "
                          "(12 + 0.25 (2k+1-l), l = 1..2k: its top eigenvalues sit just above the "
                          "bulk, as the reference's slow_dec suite, so convergence takes ~24 steps)")
+    ap.add_argument("--speculate", choices=["auto", "off"], default="auto",
+                    help="time-to-k runs: steps enqueued ahead of a convergence check while the "
+                         "host solves the T band (rbl.lanczos speculate; 'off': the strict order)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     ap.add_argument("--spmm-kernel", type=int, default=0)
     ap.add_argument("--matrix", default="hashwindow", choices=("hashwindow", "rmat", "circuit"),
@@ -555,7 +558,8 @@ def main():
         ctx.reset_timers()
         t0 = time.perf_counter()
         D, V, info = rbl.lanczos(ctx, k, b, kryl_sz=args.kryl, seed=args.seed + 2, check=True,
-                                 ritz=True, basis_bits=args.basis_bits)
+                                 ritz=True, basis_bits=args.basis_bits,
+                                 speculate=args.speculate == "auto" and "auto")
         ctx.synchronize()
         barrier()
         ttk_s = allmax(time.perf_counter() - t0)
@@ -586,7 +590,8 @@ def main():
         ctx.reset_timers()
         t0 = time.perf_counter()
         D, V, info = rbl.lanczos(ctx, k, b, kryl_sz=args.kryl, seed=args.seed + 2, check=True,
-                                 ritz=True, basis_bits=args.basis_bits)
+                                 ritz=True, basis_bits=args.basis_bits,
+                                 speculate=args.speculate == "auto" and "auto")
         ctx.synchronize()
         barrier()
         ts = allmax(time.perf_counter() - t0)
