@@ -130,6 +130,12 @@ function RBL_hip(A::Union{SparseMatrixCSC{Float64},Matrix{Float64}}, k::Int64, b
                                  ctx, Cint(i0), Cint(i1), Ah, Bh, sts), "rbl_fetch")
             return Ah, Bh
         end
+        # steps enqueued ahead of a check while the host solves the T band (rbl.lanczos's
+        # speculate="auto", host.speculation_depth): the max residual bound of each check so far;
+        # the next one predicted as the last times the last ratio (<= 1): above 100 tol the 4 steps
+        # to the next check, above tol one step.  Steps after an even i touch no block <= i, so
+        # the result is unchanged; a converging check discards them.
+        resid = Float64[]
         T = zeros(Float64, b + 1, 0)
         D = zeros(Float64)
         V = zeros(Float64)
@@ -142,6 +148,11 @@ function RBL_hip(A::Union{SparseMatrixCSC{Float64},Matrix{Float64}}, k::Int64, b
             is_last = !(i * b < kryl_sz && i < m_max)              # :162
             (is_check || is_last) || continue
             enqueue!(i)
+            if is_check && !is_last && iseven(i) && length(resid) >= 2 && resid[end] > 0 && resid[end-1] > 0
+                pred = resid[end] * min(1.0, resid[end] / resid[end-1])
+                ahead = pred > 100 * 1e-7 ? 4 : (pred > 1e-7 ? 1 : 0)
+                enqueue!(min(i + ahead, m_max))
+            end
             Ah, Bh = fetch!(first, i + 1)
             for (jj, j) in enumerate(first:i)
                 Ai = Ah[:, :, jj]
@@ -154,6 +165,8 @@ function RBL_hip(A::Union{SparseMatrixCSC{Float64},Matrix{Float64}}, k::Int64, b
                         @timeit timer "eig" D, V = dsbev('V', 'L', T)
                     end
                     D, V = sort_eig_abs(D, V, k)                    # :188
+                    Y = Bi * V[end-b+1:end, :]
+                    push!(resid, maximum(norm(Y[:, l]) for l in 1:k))
                     if check_convergence(Bi, V, b, k, 1e-7)         # :189
                         converged = true
                         break
