@@ -27,7 +27,7 @@ import scipy.sparse as sp
 
 from . import _lib
 from ._lib import RBLError, dptr, i32ptr, i64ptr, lib, u8ptr
-from .host import (TBand, check_convergence, dsbev, eig_topk, fix_signs,
+from .host import (TBand, dsbev, eig_topk, fix_signs,
                    residual_norms, sort_eig_abs, speculation_depth)
 
 KRYL_SZ_GPU = 1200          # RBL_gpu.jl:211
