@@ -170,6 +170,8 @@ struct rbl_ctx {
   double* h_pin = nullptr;    // pinned staging: Ai, Rtot (2 b x b)
   void* h_d2h[2] = {nullptr, nullptr};  // pinned slots of the staged D2H (d2h_staged)
   hipEvent_t ev_d2h_slot[2] = {nullptr, nullptr};
+  hipStream_t rstream = nullptr;      // the Ritz row pieces (ritz_pipelined)
+  hipEvent_t ev_ritz[9] = {};         // S uploaded, then each row piece finished on rstream
   double* h_hist = nullptr;   // rbl_step_async stash: per step i, Ai and Rtot (2 b x b) and the
                               //   step's 4 flags (2 doubles' room): stash_rec(b) doubles each
   double* d_stash = nullptr;  // the device side of one such record (k_stash; RBL_STASH_COPY=1)
@@ -1777,6 +1779,22 @@ int ensure_d2h_slots(rbl_ctx* ctx) {
   return RBL_OK;
 }
 
+// The pipelined Ritz vectors' side stream and events (ritz_pipelined).  A stream's first launch
+// costs ~25 ms (measured: the first pipelined rbl_ritz of a process took 60 ms against 31 ms for
+// the next), so rbl_start creates them with the staging slots and runs one empty launch on the
+// stream, instead of a time-to-k's Ritz step paying it.
+int ensure_ritz_stream(rbl_ctx* ctx) {
+  if (!ctx->rstream) {
+    HIPC(hipStreamCreateWithFlags(&ctx->rstream, hipStreamNonBlocking));
+    copy_small(ctx->d_small, ctx->d_small, 0, ctx->rstream);
+    HIPC(hipGetLastError());
+    HIPC(hipStreamSynchronize(ctx->rstream));
+  }
+  for (hipEvent_t& e : ctx->ev_ritz)
+    if (!e) HIPC(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  return RBL_OK;
+}
+
 // ---- the pushed half of the split halo (prepare_push) ----
 bool push_on(const rbl_ctx* ctx) { return ctx->push && ctx->ghost_active && ctx->nranks > 1; }
 
@@ -2176,6 +2194,9 @@ int rbl_free(rbl_ctx* ctx) {
   if (ctx->stream) hipStreamDestroy(ctx->stream);
   if (ctx->cstream) hipStreamDestroy(ctx->cstream);
   if (ctx->hstream) hipStreamDestroy(ctx->hstream);
+  if (ctx->rstream) hipStreamDestroy(ctx->rstream);
+  for (hipEvent_t e : ctx->ev_ritz)
+    if (e) hipEventDestroy(e);
   if (ctx->ev_push_ready) hipEventDestroy(ctx->ev_push_ready);
   if (ctx->ev_push_done) hipEventDestroy(ctx->ev_push_done);
   for (hipEvent_t e : {ctx->ev_fin, ctx->ev_d2h[0], ctx->ev_d2h[1], ctx->ev_d2h_slot[0],
@@ -2776,8 +2797,10 @@ int rbl_start(rbl_ctx* ctx, int b, int max_blocks, int basis_bits, const double*
     const unsigned hf = ctx->stash_direct ? (hipHostMallocMapped | hipHostMallocCoherent) : hipHostMallocDefault;
     HIPC(hipHostMalloc(&ctx->h_pin, stash_rec(b) * sizeof(double), hf));
     HIPC(hipHostMalloc(&ctx->h_hist, (size_t)(max_blocks + 2) * stash_rec(b) * sizeof(double), hf));
-    if ((size_t)ctx->nloc * b * sizeof(double) >= 4 * kD2HPiece && !std::getenv("RBL_D2H_DIRECT"))
+    if ((size_t)ctx->nloc * b * sizeof(double) >= 4 * kD2HPiece && !std::getenv("RBL_D2H_DIRECT")) {
       CHK(ensure_d2h_slots(ctx));
+      CHK(ensure_ritz_stream(ctx));
+    }
     if (ctx->stash_direct) {
       HIPC(hipHostGetDevicePointer(reinterpret_cast<void**>(&ctx->dv_pin), ctx->h_pin, 0));
       HIPC(hipHostGetDevicePointer(reinterpret_cast<void**>(&ctx->dv_hist), ctx->h_hist, 0));
@@ -3214,6 +3237,103 @@ int d2h_staged(rbl_ctx* ctx, void* dst, const void* src, size_t bytes) {
   }
   return RBL_OK;
 }
+
+// The Ritz vectors in row pieces with the D2H behind them (rbl_ritz, one chunk of k <= b columns,
+// fp64 basis, every block resident, a result of >= 4 staging pieces).  V = [Q_1..Q_m] S and its
+// transpose run in kRitzPieces row pieces on a side stream; the staged D2H stays on the context's
+// stream, each 64 MiB staging piece issued once the host has seen the row pieces it covers
+// finish, so the PCIe copy
+// (1.6 GB at ~53 GB/s, 30 ms at C4a) overlaps the basis reads of the later pieces (5.5 ms at 8
+// blocks, 17.6 ms at 28) instead of following all of them.  (Copies ordered behind the pieces by
+// a device-side stream wait ran at half the PCIe rate in most calls, on either stream:
+// profiles/r05_ritz_pipelined_trace_b29.log.)  Piece p (rows [r_p, r_{p+1})) is stored column-major
+// with its own row count as leading dimension, so the pieces tile the column-major buffer
+// contiguously; the host scatters each staged byte range into V_out's columns.  Every row of V is
+// the same sum in the same order as in the one-pass form, so V is bit-identical
+// (test_ritz_pipelined_matches_one_pass).  RBL_RITZ_SERIAL=1 restores the one-pass form.
+constexpr int kRitzPieces = 8;
+int ritz_pipelined(rbl_ctx* ctx, int nblocks, int k, int kcp, const double* d_S, double* pV,
+                   double* pVcm, double* V_out) {
+  const int b = ctx->b;
+  const int64_t nl = ctx->nloc;
+  const int64_t pr = (nl / kRitzPieces) & ~int64_t(63);  // rows per piece; the last takes the rest
+  int64_t r0p[kRitzPieces + 1];
+  for (int p = 0; p < kRitzPieces; ++p) r0p[p] = p * pr;
+  r0p[kRitzPieces] = nl;
+  CHK(ensure_d2h_slots(ctx));
+  CHK(ensure_ritz_stream(ctx));
+  HIPC(hipEventRecord(ctx->ev_ritz[kRitzPieces], ctx->stream));  // S is on the device
+  HIPC(hipStreamWaitEvent(ctx->rstream, ctx->ev_ritz[kRitzPieces], 0));
+  {
+    StageScope t(ctx, RBL_STAGE_RITZ, ctx->rstream);
+    for (int p = 0; p < kRitzPieces; ++p) {
+      const int64_t r0 = r0p[p], m = r0p[p + 1] - r0;
+      PanelRun X;
+      X.base = slotp(ctx, 0) + r0 * b;
+      X.stride = ctx->slot;
+      X.count = nblocks;
+      X.w = b;
+      tsmm(m, X, d_S, kcp, pan1(pV + r0 * kcp, kcp), 1.0, 0.0, nullptr, ctx->rstream);
+      rowmajor_to_colmajor(pV + r0 * kcp, m, kcp, pVcm + r0 * kcp, ctx->rstream);
+      HIPC(hipEventRecord(ctx->ev_ritz[p], ctx->rstream));
+    }
+  }
+  HIPC(hipGetLastError());
+  const char* src = reinterpret_cast<const char*>(pVcm);
+  const size_t bytes = (size_t)nl * kcp * sizeof(double);
+  auto piece_of = [&](size_t o) {  // the row piece holding byte o of the column-major buffer
+    int p = 0;
+    while (p + 1 < kRitzPieces && (size_t)r0p[p + 1] * kcp * sizeof(double) <= o) ++p;
+    return p;
+  };
+  // device bytes [a, e) of staging piece q (slot q & 1) -> V_out's columns (padding column skipped)
+  auto scatter = [&](size_t q, size_t a, size_t e) {
+    const char* slot = static_cast<const char*>(ctx->h_d2h[q & 1]);
+    const size_t base = q * kD2HPiece;
+    for (size_t o = base + a; o < base + e;) {
+      const int p = piece_of(o);
+      const int64_t r0 = r0p[p], m = r0p[p + 1] - r0;
+      const size_t colb = (size_t)m * sizeof(double);
+      const size_t within = o - (size_t)r0 * kcp * sizeof(double);
+      const size_t c = within / colb, inr = within % colb;
+      const size_t run = std::min(base + e, o + (colb - inr));
+      if ((int)c < k)
+        memcpy(reinterpret_cast<char*>(V_out + (int64_t)c * nl + r0) + inr, slot + (o - base), run - o);
+      o = run;
+    }
+  };
+  const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+  const char* envt = std::getenv("RBL_D2H_THREADS");
+  const int nthr = (int)std::min(envt ? std::max(1u, (unsigned)atoi(envt)) : 8u, hw);
+  const size_t nq = (bytes + kD2HPiece - 1) / kD2HPiece;
+  int waited = -1;  // the last row piece the context's stream waits for
+  for (size_t q = 0; q <= nq; ++q) {
+    if (q < nq) {
+      const size_t off = q * kD2HPiece, len = std::min(kD2HPiece, bytes - off);
+      // the host waits for the pieces, so the copy carries no cross-stream dependency (copies
+      // queued behind a hipStreamWaitEvent ran at half the PCIe rate, ~28 GB/s)
+      for (const int pl = piece_of(off + len - 1); waited < pl;)
+        HIPC(hipEventSynchronize(ctx->ev_ritz[++waited]));
+      HIPC(hipMemcpyAsync(ctx->h_d2h[q & 1], src + off, len, hipMemcpyDeviceToHost, ctx->stream));
+      HIPC(hipEventRecord(ctx->ev_d2h_slot[q & 1], ctx->stream));
+    }
+    if (q > 0) {
+      const size_t pq = q - 1, len = std::min(kD2HPiece, bytes - pq * kD2HPiece);
+      HIPC(hipEventSynchronize(ctx->ev_d2h_slot[pq & 1]));
+      const size_t part = ((len + nthr - 1) / nthr + 4095) & ~size_t(4095);
+      std::vector<std::thread> th;
+      for (size_t o = part; o < len; o += part)
+        th.emplace_back([=, &scatter] { scatter(pq, o, std::min(len, o + part)); });
+      scatter(pq, 0, std::min(part, len));
+      for (auto& t : th) t.join();
+    }
+  }
+  // every piece has finished (the host waited for the last before its copy); later work on the
+  // context's stream (the next run's steps reuse U and T) follows the side stream's kernels
+  HIPC(hipStreamSynchronize(ctx->rstream));
+  HIPC(hipStreamSynchronize(ctx->stream));
+  return RBL_OK;
+}
 }  // namespace
 
 int rbl_ritz(rbl_ctx* ctx, int nblocks, int k, const double* S, double* V_out) {
@@ -3260,7 +3380,20 @@ int rbl_ritz(rbl_ctx* ctx, int nblocks, int k, const double* S, double* V_out) {
     pVcm = own_Vcm.d();
   }
   if (trace) t_alloc = tnow() - t0;
+  const bool pipelined = V_out && ctx->nloc > 0 && kc >= k && pV == ctx->d_U && ctx->basis_bits == 64 &&
+                         nblocks <= ctx->resident && ctx->nloc >= 64 * kRitzPieces &&
+                         (size_t)ctx->nloc * kcp * sizeof(double) >= 4 * kD2HPiece &&
+                         !std::getenv("RBL_D2H_DIRECT") && !std::getenv("RBL_RITZ_SERIAL");
   std::vector<double> srm((size_t)rows * kcp);
+  if (pipelined) {
+    for (int64_t r = 0; r < rows; ++r)
+      for (int c = 0; c < kcp; ++c) srm[(size_t)r * kcp + c] = c < k ? S[(size_t)c * rows + r] : 0.0;
+    HIPC(hipMemcpyAsync(pS, srm.data(), rows * kcp * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+    CHK(ritz_pipelined(ctx, nblocks, k, kcp, pS, pV, pVcm, V_out));
+    harvest_timers(ctx);
+    if (trace) fprintf(stderr, "rbl_ritz: pipelined, %d row pieces, total %.2f ms\n", kRitzPieces, tnow() - t0);
+    return RBL_OK;
+  }
   for (int c0 = 0; c0 < k; c0 += kc) {
     const int w = std::min(kc, k - c0);
     // the previous chunk's copy may still read srm (HIP does not promise a pageable source is

@@ -497,3 +497,30 @@ def test_latency_knobs_agree(rbl, monkeypatch):
             else:
                 d = np.abs(out[t] - ref[t]).max() / np.abs(ref[t]).max()
                 assert d < 1e-12, (knob, t, d)
+
+
+def test_ritz_pipelined_matches_one_pass(rbl, monkeypatch, capfd):
+    """rbl_ritz's pipelined form (the combination in 8 row pieces on a side stream, the staged D2H
+    behind them on the context's stream; RBL_gpu.jl:106-132 / :219) returns the one-pass form's
+    V bit for bit, at a size where it applies (n_local x k x 8 B >= 256 MiB), and takes that path
+    (RBL_RITZ_TRACE); a second run on the same context then gives the same D and V again (the side
+    stream's use of the run scratch is ordered before the next run's steps)."""
+    n, b, k = 2_000_000, 32, 20
+    monkeypatch.setenv("RBL_RITZ_TRACE", "1")
+    out = []
+    with rbl.Context(0) as ctx:
+        ctx.gen_hashwindow(n, 64, 0.7734, 5, matgen.planted_spectrum(k))
+        for serial in ("1", None, None):
+            if serial:
+                monkeypatch.setenv("RBL_RITZ_SERIAL", serial)
+            else:
+                monkeypatch.delenv("RBL_RITZ_SERIAL", raising=False)
+            capfd.readouterr()
+            D, V, info = rbl.lanczos(ctx, k, b, seed=2)
+            err = capfd.readouterr().err
+            assert info.converged and ("pipelined" in err) == (serial is None), err
+            out.append((D, V))
+    (D0, V0) = out[0]
+    for D1, V1 in out[1:]:
+        assert V1.shape == (n, k) and np.array_equal(D0, D1)
+        assert np.array_equal(V0, V1), np.abs(V0 - V1).max()
