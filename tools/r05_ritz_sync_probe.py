@@ -5,7 +5,8 @@ variant: bench   — planted full-length run, planted time-to-k (V kept), regene
                    step 1, drop V, timed slow time-to-k (bench.py's order)
          noplant — the same without the planted time-to-k
          early   — the planted V dropped right after its run
-         fresh   — the slow time-to-k in a fresh context (as the probe)"""
+         fresh   — the slow time-to-k in a fresh context (as the probe)
+         keepv   — bench, but the planted V stays referenced (no munmap before the slow run)"""
 import os
 import sys
 import time
@@ -32,6 +33,7 @@ with rbl.Context(0) as ctx:
     ctx.gen_hashwindow(n, 64, 0.7734, 20261015, slow)
     ctx.start(b, 38, seed=3)
     ctx.step(1, False)
+    keep = V if variant == "keepv" else None
     V = None
     for rep in range(2):
         ctx.synchronize()
