@@ -138,21 +138,24 @@ def residual_norms(B: np.ndarray, V: np.ndarray, b: int, k: int) -> np.ndarray:
     return np.linalg.norm(B @ V[V.shape[0] - b:, :k], axis=0)
 
 
-def speculation_depth(resid: list, tol: float, margin: float = 100.0) -> int:
+def speculation_depth(resid: list, tol: float, margin: float = 100.0, mid: float = 5.0) -> int:
     """How many steps rbl.lanczos(speculate="auto") enqueues ahead of the next convergence check,
     from the max residual bounds of the earlier checks.  The next bound is predicted as the last
     one times the last ratio (clamped to <= 1: geometric decay, the Lanczos rate; measured at C4a
     on the slow spectrum the prediction lands within 1.1x of the bound once the decay is steady,
-    and overestimates it while the decay still accelerates).  Predicted above margin x tol: the
-    check is expected to fail, so the 4 steps up to the next check (the next check's stride).
-    Between tol and margin x tol: 1 step (an odd step: no partial reorth, cheaper than the
-    eigensolve it hides once the T band is large).  Otherwise, or with fewer than two earlier
-    checks (no rate), none."""
+    and overestimates it by up to 5x while the decay still accelerates).  Predicted above
+    margin x tol: the check is expected to fail, so the 4 steps up to the next check (the next
+    check's stride).  Above mid x tol (mid = 5: beyond the largest overestimate seen): 2 steps —
+    an odd step and an even one, about the eigensolve's length at that size.  Above tol: 1 step
+    (an odd step: no partial reorth, cheap to discard).  Otherwise, or with fewer than two earlier
+    checks (no rate), none.  RBL_SPEC_MID=0 drops the 2-step tier (A/B)."""
     if len(resid) < 2 or not (resid[-1] > 0.0 and resid[-2] > 0.0):
         return 0
     pred = resid[-1] * min(1.0, resid[-1] / resid[-2])
     if pred > margin * tol:
         return 4
+    if pred > mid * tol and os.environ.get("RBL_SPEC_MID", "1") != "0":
+        return 2
     return 1 if pred > tol else 0
 
 

@@ -133,7 +133,7 @@ function RBL_hip(A::Union{SparseMatrixCSC{Float64},Matrix{Float64}}, k::Int64, b
         # steps enqueued ahead of a check while the host solves the T band (rbl.lanczos's
         # speculate="auto", host.speculation_depth): the max residual bound of each check so far;
         # the next one predicted as the last times the last ratio (<= 1): above 100 tol the 4 steps
-        # to the next check, above tol one step.  Steps after an even i touch no block <= i, so
+        # to the next check, above 5 tol two, above tol one.  Steps after an even i touch no block <= i, so
         # the result is unchanged; a converging check discards them.
         resid = Float64[]
         T = zeros(Float64, b + 1, 0)
@@ -150,7 +150,7 @@ function RBL_hip(A::Union{SparseMatrixCSC{Float64},Matrix{Float64}}, k::Int64, b
             enqueue!(i)
             if is_check && !is_last && iseven(i) && length(resid) >= 2 && resid[end] > 0 && resid[end-1] > 0
                 pred = resid[end] * min(1.0, resid[end] / resid[end-1])
-                ahead = pred > 100 * 1e-7 ? 4 : (pred > 1e-7 ? 1 : 0)
+                ahead = pred > 100 * 1e-7 ? 4 : pred > 5 * 1e-7 ? 2 : pred > 1e-7 ? 1 : 0
                 enqueue!(min(i + ahead, m_max))
             end
             Ah, Bh = fetch!(first, i + 1)

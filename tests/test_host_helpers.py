@@ -102,19 +102,20 @@ def test_fix_signs_makes_ritz_coefficients_solver_independent():
 def test_speculation_rule_from_residual_history():
     """rbl.lanczos's speculate="auto": run ahead of a check by 4 steps when the geometric
     extrapolation of the earlier checks' max residual bounds stays >= 100x above the tolerance,
-    by 1 between 1x and 100x, else not; the residual bounds are common.jl:56-65's norms
+    by 2 between 5x and 100x, by 1 between 1x and 5x, else not; the residual bounds are common.jl:56-65's norms
     (check_convergence is their all-below-tol test)."""
     from rbl.host import check_convergence, residual_norms, speculation_depth
     tol = 1e-7
     assert speculation_depth([], tol) == 0 and speculation_depth([1.0], tol) == 0
     assert speculation_depth([1e-1, 1e-2], tol) == 4           # next ~1e-3
     assert speculation_depth([1e-3, 2e-3], tol) == 4           # growth clamped: next ~2e-3
-    assert speculation_depth([2.8e-3, 4.0e-5], tol) == 1       # next ~5.7e-7 (C4a slow, check 24)
+    assert speculation_depth([2.8e-3, 4.0e-5], tol) == 2       # next ~5.7e-7 (C4a slow, check 24)
+    assert speculation_depth([1e-4, 4e-6], tol) == 1           # next ~1.6e-7: within 5x of tol
     assert speculation_depth([4.0e-5, 6.0e-7], tol) == 0       # next ~9e-9: expected to converge
     assert speculation_depth([0.0, 1e-3], tol) == 0 and speculation_depth([1.0, float("nan")], tol) == 0
-    # the C4a slow-spectrum bounds of profiles/r05_ttk_probe_b26.log: 4, 4, 4, 1, 0 from check 3 on
+    # the C4a slow-spectrum bounds of profiles/r05_ttk_probe_b26.log: 4, 4, 4, 2, 0 from check 3 on
     r = [4.8e+00, 2.5e+00, 1.9e-01, 2.8e-03, 4.0e-05, 6.0e-07, 8.9e-09]
-    assert [speculation_depth(r[:j], tol) for j in range(2, 7)] == [4, 4, 4, 1, 0]
+    assert [speculation_depth(r[:j], tol) for j in range(2, 7)] == [4, 4, 4, 2, 0]
     rng = np.random.default_rng(0)
     b, k = 4, 3
     B, S = rng.standard_normal((b, b)), rng.standard_normal((20, 6))
