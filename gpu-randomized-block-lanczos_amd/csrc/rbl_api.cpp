@@ -3239,7 +3239,8 @@ int d2h_staged(rbl_ctx* ctx, void* dst, const void* src, size_t bytes) {
 }
 
 // The Ritz vectors in row pieces with the D2H behind them (rbl_ritz, one chunk of k <= b columns,
-// fp64 basis, every block resident, a result of >= 4 staging pieces).  V = [Q_1..Q_m] S and its
+// every block resident — fp64, or fp32 where the fp32-input MFMA combination applies — and a
+// result of >= 4 staging pieces).  V = [Q_1..Q_m] S and its
 // transpose run in kRitzPieces row pieces on a side stream; the staged D2H stays on the context's
 // stream, each 64 MiB staging piece issued once the host has seen the row pieces it covers
 // finish, so the PCIe copy
@@ -3269,11 +3270,16 @@ int ritz_pipelined(rbl_ctx* ctx, int nblocks, int k, int kcp, const double* d_S,
     for (int p = 0; p < kRitzPieces; ++p) {
       const int64_t r0 = r0p[p], m = r0p[p + 1] - r0;
       PanelRun X;
-      X.base = slotp(ctx, 0) + r0 * b;
       X.stride = ctx->slot;
       X.count = nblocks;
       X.w = b;
-      tsmm(m, X, d_S, kcp, pan1(pV + r0 * kcp, kcp), 1.0, 0.0, nullptr, ctx->rstream);
+      if (ctx->basis_bits == 64) {
+        X.base = slotp(ctx, 0) + r0 * b;
+        tsmm(m, X, d_S, kcp, pan1(pV + r0 * kcp, kcp), 1.0, 0.0, nullptr, ctx->rstream);
+      } else {  // fp32 basis: the fp32-input MFMA form of combine_blocks32, widened on load
+        X.base32 = slotp32(ctx, 0) + r0 * b;
+        tsmm44_f32x(m, X, d_S, kcp, pan1(pV + r0 * kcp, kcp), 1.0, 0.0, ctx->rstream);
+      }
       rowmajor_to_colmajor(pV + r0 * kcp, m, kcp, pVcm + r0 * kcp, ctx->rstream);
       HIPC(hipEventRecord(ctx->ev_ritz[p], ctx->rstream));
     }
@@ -3380,7 +3386,8 @@ int rbl_ritz(rbl_ctx* ctx, int nblocks, int k, const double* S, double* V_out) {
     pVcm = own_Vcm.d();
   }
   if (trace) t_alloc = tnow() - t0;
-  const bool pipelined = V_out && ctx->nloc > 0 && kc >= k && pV == ctx->d_U && ctx->basis_bits == 64 &&
+  const bool pipelined = V_out && ctx->nloc > 0 && kc >= k && pV == ctx->d_U &&
+                         (ctx->basis_bits == 64 || tsmm44_ok(b, kcp, kcp)) &&
                          nblocks <= ctx->resident && ctx->nloc >= 64 * kRitzPieces &&
                          (size_t)ctx->nloc * kcp * sizeof(double) >= 4 * kD2HPiece &&
                          !std::getenv("RBL_D2H_DIRECT") && !std::getenv("RBL_RITZ_SERIAL");

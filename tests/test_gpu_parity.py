@@ -499,12 +499,14 @@ def test_latency_knobs_agree(rbl, monkeypatch):
                 assert d < 1e-12, (knob, t, d)
 
 
-def test_ritz_pipelined_matches_one_pass(rbl, monkeypatch, capfd):
+@pytest.mark.parametrize("bits", [64, 32])
+def test_ritz_pipelined_matches_one_pass(rbl, monkeypatch, capfd, bits):
     """rbl_ritz's pipelined form (the combination in 8 row pieces on a side stream, the staged D2H
     behind them on the context's stream; RBL_gpu.jl:106-132 / :219) returns the one-pass form's
     V bit for bit, at a size where it applies (n_local x k x 8 B >= 256 MiB), and takes that path
     (RBL_RITZ_TRACE); a second run on the same context then gives the same D and V again (the side
-    stream's use of the run scratch is ordered before the next run's steps)."""
+    stream's use of the run scratch is ordered before the next run's steps).  Both bases: fp64, and
+    the fp32 Krylov basis (FLOAT = Float32) whose combination widens on load."""
     n, b, k = 2_000_000, 32, 20
     monkeypatch.setenv("RBL_RITZ_TRACE", "1")
     out = []
@@ -516,7 +518,7 @@ def test_ritz_pipelined_matches_one_pass(rbl, monkeypatch, capfd):
             else:
                 monkeypatch.delenv("RBL_RITZ_SERIAL", raising=False)
             capfd.readouterr()
-            D, V, info = rbl.lanczos(ctx, k, b, seed=2)
+            D, V, info = rbl.lanczos(ctx, k, b, seed=2, basis_bits=bits)
             err = capfd.readouterr().err
             assert info.converged and ("pipelined" in err) == (serial is None), err
             out.append((D, V))
