@@ -62,11 +62,11 @@ def parse():
                     help="n of the CPU baseline's fixed-step cross-check (0 skips it): the first "
                          "--cpu-check-steps block steps timed at the sample's n and at this n")
     ap.add_argument("--cpu-check-steps", type=int, default=8)
-    ap.add_argument("--cpu-fixed-n", type=int, default=0,
+    ap.add_argument("--cpu-fixed-n", type=int, default=-1,
                     help="also time the oracle's first --cpu-check-steps block steps at this n (SURVEY "
-                         "§8(d)'s fixed-step form at the config's own n, e.g. 10000000: the 1e9-nnz "
-                         "CSR built in row chunks, ~45 GB of host memory, several minutes; off by "
-                         "default)")
+                         "§8(d)'s fixed-step form at the config's own n: the 1e9-nnz CSR built in "
+                         "row chunks, ~45 GB of host memory, ~3-4 minutes at n = 1e7 on 16 threads); "
+                         "-1 (default): the run's own n on the hash-window matrix; 0: off")
     ap.add_argument("--no-ttk", action="store_true")
     ap.add_argument("--no-ttk-slow", action="store_true",
                     help="skip the second time-to-k on a slowly decaying planted spectrum "
@@ -270,10 +270,88 @@ def progress(msg: str) -> None:
         print(f"[bench {time.perf_counter() - T_START:7.1f} s] {msg}", file=sys.stderr, flush=True)
 
 
-def measure(ctx, args, matrix, K, W, nloc, nnz_loc, world, barrier, allmax):
+def host_threads() -> dict:
+    """This process's threads by name (/proc/self/task/*/comm): RCCL's proxy / socket threads,
+    HIP's, BLAS workers, the Python main thread."""
+    names = {}
+    try:
+        for t in os.listdir("/proc/self/task"):
+            try:
+                with open(f"/proc/self/task/{t}/comm") as f:
+                    nm = f.read().strip()
+            except OSError:
+                continue
+            names[nm] = names.get(nm, 0) + 1
+    except OSError:
+        pass
+    return dict(sorted(names.items(), key=lambda kv: -kv[1]))
+
+
+def _read(path):
+    try:
+        with open(path) as f:
+            return f.read().strip()
+    except OSError:
+        return None
+
+
+def cgroup_cpu() -> dict:
+    """The CPU quota of this process's cgroup (v2 cpu.max or v1 cfs quota / period) and its
+    throttling counters: a rehearsal whose ranks together want more CPU than the quota is
+    throttled (every thread of the cgroup stopped until the next period) however many CPUs the
+    affinity mask lists."""
+    out = {}
+    mx = _read("/sys/fs/cgroup/cpu.max")
+    if mx:
+        q, _, per = mx.partition(" ")
+        out["quota_cpus"] = None if q == "max" else round(int(q) / int(per or 100000), 2)
+        st = _read("/sys/fs/cgroup/cpu.stat") or ""
+    else:
+        q, per = _read("/sys/fs/cgroup/cpu/cpu.cfs_quota_us"), _read("/sys/fs/cgroup/cpu/cpu.cfs_period_us")
+        if q and per:
+            out["quota_cpus"] = None if int(q) < 0 else round(int(q) / int(per), 2)
+        st = _read("/sys/fs/cgroup/cpu/cpu.stat") or ""
+    for line in st.splitlines():
+        k, _, v = line.partition(" ")
+        if k in ("nr_periods", "nr_throttled", "throttled_usec", "throttled_time", "usage_usec"):
+            out[k] = int(v)
+    return out
+
+
+def gpu_processes() -> dict:
+    """GPU processes the KFD driver knows on this node (/sys/class/kfd/kfd/proc: one entry per
+    process with a GPU context), this process's queues there, and the amdgpu scheduler's
+    limit on processes it runs at once (hws_max_conc_proc; past it the firmware time-slices
+    whole processes)."""
+    out = {}
+    base = "/sys/class/kfd/kfd/proc"
+    try:
+        procs = os.listdir(base)
+        out["kfd_processes"] = len(procs)
+        q = f"{base}/{os.getpid()}/queues"
+        out["own_queues"] = len(os.listdir(q)) if os.path.isdir(q) else None
+    except OSError:
+        pass
+    for prm in ("hws_max_conc_proc", "sched_policy", "mes", "cwsr_enable"):
+        v = _read(f"/sys/module/amdgpu/parameters/{prm}")
+        if v is not None:
+            out[prm] = v
+    return out
+
+
+def cpu_seconds() -> float:
+    import resource
+    ru = resource.getrusage(resource.RUSAGE_SELF)
+    return ru.ru_utime + ru.ru_stime
+
+
+def measure(ctx, args, matrix, K, W, nloc, nnz_loc, world, barrier, allmax, gather=None):
     """W untimed + K timed fixed-length runs (rbl_start + m_max block steps, convergence checks
     off) on the matrix the context holds; the max over ranks of the timed region, the stage
-    times (hipEvents) and the SpMM / partial-reorth rooflines priced from them."""
+    times (hipEvents) and the SpMM / partial-reorth rooflines priced from them.  On several
+    ranks (`gather`: an all-gather of a Python object) every rank's own record as well: its
+    run times, its stage split, its collectives (counts, bytes, host and device time per
+    call), and the CPU time its process used against the CPUs it may run on."""
     import rbl
     from rbl import _lib
     n, b, k = args.n, args.b, args.k
@@ -307,6 +385,8 @@ def measure(ctx, args, matrix, K, W, nloc, nnz_loc, world, barrier, allmax):
     ctx.reset_timers()
     ctx.comm_stats(reset=True)
     barrier()
+    cg0 = cgroup_cpu() if world > 1 else {}
+    cpu0 = cpu_seconds()
     t0 = time.perf_counter()
     marks = [t0]
     for k_ in range(K):
@@ -314,9 +394,15 @@ def measure(ctx, args, matrix, K, W, nloc, nnz_loc, world, barrier, allmax):
         marks.append(time.perf_counter())
         progress(f"{matrix} n={n} b={b}: timed run {k_ + 1}/{K} {(marks[-1] - marks[-2]) * 1e3:.1f} ms")
     ctx.synchronize()
+    local_elapsed = time.perf_counter() - t0
+    local_cpu = cpu_seconds() - cpu0
+    threads_timed = host_threads() if world > 1 else None
+    cg1 = cgroup_cpu() if world > 1 else {}
+    gpu_procs = gpu_processes() if world > 1 else {}
     barrier()
     elapsed = allmax(time.perf_counter() - t0)
-    comm = ctx.comm_stats()
+    comm_full = ctx.comm_stats(times=True)
+    comm = {k_: v for k_, v in comm_full.items() if not k_.endswith("_ns")}
     # the spread of the timed runs on this rank (rank 0's is reported): run-to-run variation
     runs_ms = sorted((b_ - a_) * 1e3 for a_, b_ in zip(marks, marks[1:]))
     run_spread = {"min": round(runs_ms[0], 2), "median": round(runs_ms[len(runs_ms) // 2], 2),
@@ -327,16 +413,58 @@ def measure(ctx, args, matrix, K, W, nloc, nnz_loc, world, barrier, allmax):
     barrier()
     ctx.synchronize()
     ctx.reset_timers()
+    ctx.comm_stats(reset=True)
     barrier()
     t1 = time.perf_counter()
     for k_ in range(K):
         one_run()
         progress(f"{matrix} n={n} b={b}: stage-timer run {k_ + 1}/{K}")
     ctx.synchronize()
+    local_staged = time.perf_counter() - t1
     barrier()
     elapsed_staged = allmax(time.perf_counter() - t1)
+    comm_staged = ctx.comm_stats(times=True)
     host = host_timed
     stage = ctx.timers()
+    per_rank = None
+    if gather is not None and world > 1 and K:
+        try:
+            aff = len(os.sched_getaffinity(0))
+        except (AttributeError, OSError):
+            aff = os.cpu_count()
+        calls_ar = max(1, comm_full["allreduce_calls"])
+        calls_x = max(1, comm_full["exchange_calls"])
+        mine = {
+            "rank": int(os.environ.get("RANK", "0")), "device": ctx.device,
+            "rows": int(nloc), "nnz": int(nnz_loc),
+            "timed_ms_per_run": round(local_elapsed * 1e3 / K, 2),
+            "run_ms_median": run_spread_median(marks),
+            "stage_pass_ms_per_run": round(local_staged * 1e3 / K, 2),
+            "stage_ms_per_run": {s_: round(v / K, 3) for s_, v in stage.items()},
+            "host_ms_per_run": {key: round(v / K, 1) for key, v in host_timed.items()},
+            "allreduce_calls_per_run": round(comm_full["allreduce_calls"] / K, 2),
+            "allreduce_bytes_per_run": int(comm_full["allreduce_bytes"] / K),
+            "exchange_calls_per_run": round(comm_full["exchange_calls"] / K, 2),
+            "send_bytes_per_run": int(comm_full["send_bytes"] / K),
+            "recv_bytes_per_run": int(comm_full["recv_bytes"] / K),
+            # timed region: host wall time inside the transport calls
+            "allreduce_host_us_per_call": round(comm_full["allreduce_host_ns"] / calls_ar / 1e3, 1),
+            "exchange_host_us_per_call": round(comm_full["exchange_host_ns"] / calls_x / 1e3, 1),
+            # stage pass: hipEvent span of each call on its stream (peers' lateness included)
+            "allreduce_dev_us_per_call": round(comm_staged["allreduce_dev_ns"]
+                                               / max(1, comm_staged["allreduce_calls"]) / 1e3, 1),
+            "exchange_dev_us_per_call": round(comm_staged["exchange_dev_ns"]
+                                              / max(1, comm_staged["exchange_calls"]) / 1e3, 1),
+            "cpu_s_per_run": round(local_cpu / K, 3),
+            "affinity_cpus": aff,
+            "threads": threads_timed,
+            "cgroup": {**{k_: cg1[k_] for k_ in ("quota_cpus",) if k_ in cg1},
+                       **{f"{k_}_timed": cg1[k_] - cg0.get(k_, 0) for k_ in cg1
+                          if k_ != "quota_cpus" and isinstance(cg1[k_], int)}},
+            "gpu": gpu_procs,
+        }
+        per_rank = gather(mine)
+    host = host_timed
     iters = K * m_max
     value = iters / elapsed
     stage_per_run = {s: v / K for s, v in stage.items()}
@@ -442,10 +570,85 @@ def measure(ctx, args, matrix, K, W, nloc, nnz_loc, world, barrier, allmax):
     # enqueueing the steps, and waiting in rbl_fetch for the last one
     host_ms = {key: round(v / K, 1) for key, v in host.items()}
     return {"elapsed": elapsed, "stage": stage, "value": value, "roofline": roofline,
+            "per_rank": per_rank,
             "host_ms_per_run": host_ms,
             "stage_pass_ms_per_run": round(elapsed_staged * 1e3 / K, 2) if K else None,
             "roofline_secondary": roofline2, "spmm_kernel": spmm_kernel,
             "comm_per_step": comm_per_step, "m_max": m_max, "run_ms": run_spread}
+
+
+def run_spread_median(marks) -> float:
+    runs = sorted((b_ - a_) * 1e3 for a_, b_ in zip(marks, marks[1:]))
+    return round(runs[len(runs) // 2], 2) if runs else 0.0
+
+
+def rank_arrays(per_rank):
+    """The ranks' own records as arrays indexed by rank (the multi-rank line's self-diagnosis):
+    each rank's stage split of the stage pass and what it leaves unattributed (host gaps: the
+    stream idle while the host enqueues or waits), its collectives' per-call host and device
+    times, its bytes, and the CPU time its process used — with the job's total CPU time per
+    wall second against the CPUs the ranks may run on (>= ~0.9: the host is saturated, and every
+    host-side step of every rank waits for a core)."""
+    if not per_rank:
+        return None
+    per_rank = sorted(per_rank, key=lambda r: r["rank"])
+    stages = list(per_rank[0]["stage_ms_per_run"])
+    out = {"ranks": [r["rank"] for r in per_rank], "devices": [r["device"] for r in per_rank]}
+    for key in ("rows", "nnz", "timed_ms_per_run", "run_ms_median", "stage_pass_ms_per_run",
+                "allreduce_calls_per_run", "allreduce_bytes_per_run", "exchange_calls_per_run",
+                "send_bytes_per_run", "recv_bytes_per_run", "allreduce_host_us_per_call",
+                "exchange_host_us_per_call", "allreduce_dev_us_per_call",
+                "exchange_dev_us_per_call", "cpu_s_per_run"):
+        out[key] = [r[key] for r in per_rank]
+    out["stage_ms_per_run"] = {s_: [r["stage_ms_per_run"][s_] for r in per_rank] for s_ in stages}
+    sums = [round(sum(r["stage_ms_per_run"].values()), 2) for r in per_rank]
+    out["stage_sum_ms"] = sums
+    out["stage_sum_over_run"] = [round(sm / r["stage_pass_ms_per_run"], 4) if r["stage_pass_ms_per_run"] else None
+                                 for sm, r in zip(sums, per_rank)]
+    out["unattributed_ms"] = [round(r["stage_pass_ms_per_run"] - sm, 2) for sm, r in zip(sums, per_rank)]
+    out["host_ms_per_run"] = {key: [r["host_ms_per_run"][key] for r in per_rank]
+                              for key in per_rank[0]["host_ms_per_run"]}
+    aff = max(r["affinity_cpus"] or 1 for r in per_rank)
+    cpu_total = sum(r["cpu_s_per_run"] for r in per_rank)
+    wall = max(r["timed_ms_per_run"] for r in per_rank) / 1e3
+    out["host_cpu"] = {"affinity_cpus": aff, "os_cpu_count": os.cpu_count(),
+                       "cpu_s_per_run_all_ranks": round(cpu_total, 3),
+                       "busy_cpus": round(cpu_total / wall, 2) if wall else None,
+                       "saturation": round(cpu_total / wall / aff, 3) if wall else None,
+                       "threads_rank0": per_rank[0]["threads"],
+                       "threads_per_rank": [sum((r["threads"] or {}).values()) for r in per_rank],
+                       # the cgroup's quota and its throttling over rank 0's timed region
+                       "cgroup_rank0": per_rank[0].get("cgroup")}
+    out["gpu_processes"] = {"rank0": per_rank[0].get("gpu"),
+                            "queues_per_rank": [(r.get("gpu") or {}).get("own_queues") for r in per_rank]}
+    busiest = max(range(len(per_rank)), key=lambda i: per_rank[i]["stage_pass_ms_per_run"])
+    out["slowest_rank"] = per_rank[busiest]["rank"]
+    return out
+
+
+# DESIGN §6's prediction for the driver's curve (block-iters/s, one MI355X per rank over xGMI):
+# per-rank compute = the N = 1 run / N, plus ~30 us per all-reduce and the halo per SpMM
+SCALING_MODEL = {"C4a hash-window SpMM-Lanczos": {1: 46.83, 2: 92.0, 4: 181.0, 8: 350.0},
+                 "C4b R-MAT SpMM-Lanczos": {1: 18.05, 2: 33.0, 4: 63.0, 8: 125.0}}
+
+
+def model_block(workload, world, value, shared_gpu):
+    """The §6 model's value for this N and workload beside the measured one.  When the ranks
+    share GPUs (a one-GPU rehearsal) the xGMI prediction does not apply: the ranks split one
+    GPU's time, so the expectation is the N = 1 value (the same total work), and the ratio
+    measures what sharing and the loopback transport cost."""
+    m = SCALING_MODEL.get(workload)
+    if not m:
+        return None
+    out = {"source": "DESIGN.md §6 (modelled, not measured): per-rank compute = N=1 run time / N, "
+                     "~30 us per RCCL all-reduce, halo bytes over the xGMI links (~55 GB/s each)",
+           "n_gpus": world, "predicted_xgmi": m.get(world)}
+    if shared_gpu:
+        out.update({"applies": False, "shared_gpu_expectation": m[1],
+                    "measured_over_shared_gpu_expectation": round(value / m[1], 3)})
+    elif m.get(world):
+        out.update({"applies": True, "measured_over_predicted": round(value / m[world], 3)})
+    return out
 
 
 def main():
@@ -484,6 +687,13 @@ def main():
         dist.all_reduce(t)
         return int(t.item())
 
+    def gather_obj(x) -> list:
+        if dist is None:
+            return [x]
+        out = [None] * world
+        dist.all_gather_object(out, x)
+        return out
+
     def allgather_i64(x: int) -> list:
         if dist is None:
             return [int(x)]
@@ -498,6 +708,8 @@ def main():
     shm_path = None
     device = local_rank
     ngpu = gpu_count_sysfs() or 1
+    # a one-GPU rehearsal (shm transport, or RCCL with a host id per rank): ranks share GPUs
+    shared_gpu = (args.transport == "shm" or rccl_host_per_rank()) and world > ngpu
     if world > 1 and args.transport == "shm":
         # one segment per job, named by rank 0; ranks beyond the GPU count share GPUs
         import uuid
@@ -543,7 +755,7 @@ def main():
     ctx.set_option(_lib.RBL_OPT_FUSE, args.fuse)
     m_max = rbl.rbl_gpu.max_steps_for(args.kryl, b)
     meas = measure(ctx, args, args.matrix, args.steps, args.warmup, nloc, nnz_loc, world,
-                   barrier, allmax)
+                   barrier, allmax, gather_obj)
     K = args.steps
     elapsed, stage, value = meas["elapsed"], meas["stage"], meas["value"]
     stage_per_run = {s: v / K for s, v in stage.items()}
@@ -627,13 +839,14 @@ def main():
     if args.matrix == "hashwindow" and args.rmat_steps > 0 and args.basis_bits == 64:
         progress("C4b sub-record")
         rmat_rec = guarded(rmat_subrecord, ctx, args, plant, world, barrier, allmax, allsum,
-                           allgather_i64)
+                           allgather_i64, gather_obj, shared_gpu)
 
     # ---- BASELINE config 3's shape: the circuit-like matrix at G3_circuit's n, b = 16 ----
     c3_rec = None
     if args.matrix == "hashwindow" and args.c3_steps > 0 and args.basis_bits == 64:
         progress("C3 sub-record")
-        c3_rec = guarded(c3_subrecord, ctx, args, world, barrier, allmax, allsum, allgather_i64)
+        c3_rec = guarded(c3_subrecord, ctx, args, world, barrier, allmax, allsum, allgather_i64,
+                         gather_obj)
 
     # ---- CPU baseline: the oracle (port of RBL.jl) on a bounded sample, rank 0, N = 1 ----
     cpu = None
@@ -690,6 +903,10 @@ def main():
         "matrix_gen_s": round(gen_s, 3),
         "cpu_baseline": cpu,
         "comm_per_step": meas["comm_per_step"], "run_ms_rank0": meas["run_ms"],
+        # several ranks: every rank's own record (arrays by rank) and the §6 model's value
+        **({"per_rank": rank_arrays(meas["per_rank"]),
+            "model": model_block(workload_name(args), world, value, shared_gpu)}
+           if world > 1 else {}),
         "c4b_rmat": rmat_rec,
         "c3_circuit": c3_rec,
         "c5_mixed": None,
@@ -718,7 +935,8 @@ def main():
         dist.destroy_process_group()
 
 
-def rmat_subrecord(ctx, args, plant, world, barrier, allmax, allsum, allgather_i64):
+def rmat_subrecord(ctx, args, plant, world, barrier, allmax, allsum, allgather_i64,
+                   gather_obj=None, shared_gpu=False):
     """BASELINE config 4 in the same driver run: the seeded R-MAT matrix
     ((a,b,c,d) = (0.57,0.19,0.19,0.05), scale 24, 0.66 n x 100 draws: ~1e9 nonzeros at n = 1e7)
     generated on the device in place of the headline matrix, nnz-balanced over the ranks; the
@@ -743,7 +961,7 @@ def rmat_subrecord(ctx, args, plant, world, barrier, allmax, allsum, allgather_i
     nloc = r1 - r0
     nnz = allsum(nnz_loc)
     meas = measure(ctx, ra, "rmat", args.rmat_steps, args.rmat_warmup, nloc, nnz_loc, world,
-                   barrier, allmax)
+                   barrier, allmax, gather_obj)
     K = args.rmat_steps
     barrier()
     ctx.synchronize()
@@ -785,6 +1003,10 @@ def rmat_subrecord(ctx, args, plant, world, barrier, allmax, allsum, allgather_i
             "roofline": meas["roofline"], "roofline_secondary": meas["roofline_secondary"],
             "stage_ms_per_run": {s_: round(v / K, 3) for s_, v in meas["stage"].items()},
             "comm_per_step": meas["comm_per_step"], "run_ms_rank0": meas["run_ms"],
+            **({"per_rank": rank_arrays(meas["per_rank"]),
+                "model": model_block("C4b R-MAT SpMM-Lanczos" if (args.n, args.b) == (10_000_000, 32)
+                                     else None, world, meas["value"], shared_gpu)}
+               if world > 1 else {}),
             "time_to_k": {"seconds": round(ttk_s, 4), "iters": info.iters,
                           "converged": info.converged, "k": args.k,
                           "top_eigenvalues": [round(float(x), 6) for x in D[:3]]},
@@ -792,7 +1014,7 @@ def rmat_subrecord(ctx, args, plant, world, barrier, allmax, allsum, allgather_i
             **({"as_drawn": as_drawn} if as_drawn else {})}
 
 
-def c3_subrecord(ctx, args, world, barrier, allmax, allsum, allgather_i64):
+def c3_subrecord(ctx, args, world, barrier, allmax, allsum, allgather_i64, gather_obj=None):
     """BASELINE config 3's shape in the same driver run: the seeded
     circuit-like SPD matrix of G3_circuit's size (n = 1,585,478, 7.66 M nonzeros, scattered: no
     band; the real G3_circuit is not in the image) generated on the device, b = 16, k = 20; the
@@ -809,7 +1031,7 @@ def c3_subrecord(ctx, args, world, barrier, allmax, allsum, allgather_i64):
     nloc = r1 - r0
     nnz = allsum(nnz_loc)
     K = args.c3_steps
-    meas = measure(ctx, ra, "circuit", K, 1, nloc, nnz_loc, world, barrier, allmax)
+    meas = measure(ctx, ra, "circuit", K, 1, nloc, nnz_loc, world, barrier, allmax, gather_obj)
     barrier()
     ctx.synchronize()
     ctx.reset_timers()
@@ -828,6 +1050,7 @@ def c3_subrecord(ctx, args, world, barrier, allmax, allsum, allgather_i64):
             "roofline": meas["roofline"], "roofline_secondary": meas["roofline_secondary"],
             "stage_ms_per_run": {s_: round(v / K, 3) for s_, v in meas["stage"].items()},
             "comm_per_step": meas["comm_per_step"], "run_ms_rank0": meas["run_ms"],
+            **({"per_rank": rank_arrays(meas["per_rank"])} if world > 1 else {}),
             "time_to_k": {"seconds": round(ttk_s, 4), "iters": info.iters,
                           "converged": info.converged, "k": ra.k,
                           "top_eigenvalues": [round(float(x), 6) for x in D[:3]]},
@@ -956,12 +1179,17 @@ def cpu_baseline(args, m_max, plant):
                     "sample_seconds_1thread": round(t1, 3)})
     if args.cpu_check_n and args.matrix == "hashwindow" and args.basis_bits == 64:
         out["linear_scaling_check"] = cpu_scaling_check(args, plant, A, omega)
-    if args.cpu_fixed_n and args.matrix == "hashwindow" and args.basis_bits == 64:
-        out["fixed_steps_at_n"] = cpu_fixed_steps(args, plant)
+    fixed_n = args.n if args.cpu_fixed_n < 0 else args.cpu_fixed_n
+    if fixed_n and args.matrix == "hashwindow" and args.basis_bits == 64:
+        out["fixed_steps_at_n"] = cpu_fixed_steps(args, plant, fixed_n)
+    out["value_is"] = ("the 38-step rate extrapolated linearly from the n = %d sample (sample, "
+                       "linear_scaling_check); fixed_steps_at_n is SURVEY §8(d)'s fixed-step form "
+                       "measured at the config's own n (the first steps only: the partial reorth "
+                       "grows with the step, so it is not the 38-step rate)" % ns)
     return out
 
 
-def cpu_fixed_steps(args, plant):
+def cpu_fixed_steps(args, plant, n):
     """the oracle at the config's own n for a fixed number of block steps (rbl_start
     + the first --cpu-check-steps steps, convergence checks off), per-step time stated as such —
     not extrapolated.  The partial reorth grows with the step, so a 38-step run costs more per
@@ -969,7 +1197,7 @@ def cpu_fixed_steps(args, plant):
     import threading
     from oracle import matgen
     from oracle import rbl_oracle as o
-    n, steps = args.cpu_fixed_n, args.cpu_check_steps
+    steps = args.cpu_check_steps
     done = threading.Event()
 
     def heartbeat():  # minutes of CPU work: keep stderr alive

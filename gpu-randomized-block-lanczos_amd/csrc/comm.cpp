@@ -21,7 +21,8 @@ namespace {
 // library is not linked against RCCL: with a DT_NEEDED entry, a process that imported torch
 // first had torch's bundled RCCL (same soname) serve every call, and one that did not had
 // ROCm's — the copy depended on import order.  Opened by path, ROCm's copy is the one used in
-// every process (a second copy beside torch's when torch is loaded; torch keeps its own).
+// every process (a second copy beside torch's when torch is loaded; torch keeps its own); if
+// that file does not load, RCCL is reported unavailable rather than looked up by soname.
 struct RcclApi {
   bool ok = false;
   std::string path, error;
@@ -44,15 +45,14 @@ const RcclApi& rccl() {
   static RcclApi api;
   static std::once_flag once;
   std::call_once(once, [] {
+    // by path only: a soname lookup ("librccl.so.1") in a process that imported torch first
+    // would return torch's copy, the import-order dependence this loader exists to remove
     const char* env = std::getenv("RBL_RCCL_LIB");
-    const char* cands[] = {env && *env ? env : "/opt/rocm/lib/librccl.so.1", "librccl.so.1"};
-    void* h = nullptr;
-    for (const char* c : cands) {
-      h = dlopen(c, RTLD_NOW | RTLD_LOCAL | RTLD_DEEPBIND);
-      if (h) break;
-      api.error += std::string(api.error.empty() ? "" : "; ") + dlerror();
+    void* h = dlopen(env && *env ? env : "/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_LOCAL | RTLD_DEEPBIND);
+    if (!h) {
+      api.error = dlerror();
+      return;
     }
-    if (!h) return;
     bool all = true;
     auto sym = [&](auto& fp, const char* name) {
       fp = reinterpret_cast<std::remove_reference_t<decltype(fp)>>(dlsym(h, name));

@@ -203,11 +203,20 @@ struct rbl_ctx {
   // collectives issued by this rank since the last reset (rbl_comm_stats): all-reduce calls and
   // bytes, grouped halo exchanges and the bytes sent / received in them
   int64_t comm_stats[RBL_COMM_NSTATS] = {0};
+  // time spent in this rank's collectives since the last rbl_comm_stats reset
+  // (RBL_COMM_*_HOST_NS / *_DEV_NS): host wall time inside the transport call, and the
+  // hipEvent span of the call on its stream (recorded while RBL_OPT_TIMERS is 1)
+  int64_t comm_host_ns[2] = {0, 0};  // [0] all-reduces, [1] halo exchanges
+  double comm_dev_ms[2] = {0.0, 0.0};
   // which code path each step took (rbl_path_stats): counted on the host as the work is issued,
   // so a test can assert the path itself instead of timing it
   int64_t path_stats[RBL_PATH_NSTATS] = {0};
-  struct Mark { int stage; hipEvent_t a, b; };
+  // parent: the stage whose span encloses this one on the same stream (a collective inside
+  // "3-term" / "qr" / "part reorth"), whose time excludes it; -1 none
+  struct Mark { int stage; hipEvent_t a, b; int parent = -1; };
   std::vector<Mark> marks;
+  struct OpenStage { int stage; hipStream_t st; };
+  std::vector<OpenStage> open_stages;  // StageScopes alive now, innermost last
   std::vector<hipEvent_t> ev_pool;
   size_t ev_used = 0;
 };
@@ -579,52 +588,65 @@ int prepare_push(rbl_ctx* ctx, const std::vector<int64_t>& rp) {
   // columns of tier 1 (the ghosts with the split) and of tiers 1 + 2 (without)
   const int64_t nz1 = m > 0 ? tier_nnz(ctx, 1) : 0, nz2 = m > 0 ? tier_nnz(ctx, 2) : 0;
   std::vector<int32_t> c1(std::max<int64_t>(nz1, 1)), c2(std::max<int64_t>(nz2, 1));
-  if (nz1) HIPC(hipMemcpy(c1.data(), ctx->seg_tier[1].col, nz1 * sizeof(int32_t), hipMemcpyDeviceToHost));
-  if (nz2) HIPC(hipMemcpy(c2.data(), ctx->seg_tier[2].col, nz2 * sizeof(int32_t), hipMemcpyDeviceToHost));
-  // [tier-1 entries by owner | tier-2 by owner | d1 | d12 | tier-1 hash by owner | tier-2 hash]
-  std::vector<int64_t> vote(4 * P + 2, 0);
-  std::vector<uint8_t> mark(std::max<int64_t>(n, 1), 0);
+  // [tier-1 entries by owner | tier-2 by owner | d1 | d12 | tier-1 hash by owner | tier-2 hash |
+  //  this rank's status]: a rank whose local part fails (a D2H copy) still takes part in the
+  // all-gather with its error code, and every rank then fails together instead of leaving its
+  // peers waiting in the collective
+  std::vector<int64_t> vote(4 * P + 3, 0);
   auto owner = [&](int64_t c) {
     return (int)(std::upper_bound(ctx->bounds.begin(), ctx->bounds.end(), c) - ctx->bounds.begin()) - 1;
   };
-  for (int64_t k = 0; k < nz1; ++k) {
-    ++vote[owner(c1[k])];
-    if (!mark[c1[k]]) { mark[c1[k]] = 1; ++vote[2 * P]; }
-  }
-  for (int64_t k = 0; k < nz2; ++k) {
-    ++vote[P + owner(c2[k])];
-    if (!mark[c2[k]]) { mark[c2[k]] = 2; ++vote[2 * P + 1]; }
-  }
-  vote[2 * P + 1] += vote[2 * P];
-  std::vector<uint8_t>().swap(mark);
-  // the entries themselves, not only their counts: the split forms A[r,c] Q[c] on c's rank from
-  // A[c,r], so p's tier-2 entries towards q must be q's tier-1 entries towards p transposed,
-  // values included.  Per peer an order-free hash (wrapping sum of mixed (row, col, value
-  // bits), tier 2 keyed transposed) is compared: a pattern or a value that is not symmetric
-  // keeps the pull-all halo (or fails under RBL_OPT_HALO_PUSH 1) instead of a wrong SpMM.
-  auto tier_hash = [&](int t, int64_t nz, const std::vector<int32_t>& cols, int64_t* out) -> int {
-    if (nz == 0) return RBL_OK;
-    std::vector<int64_t> trp(m + 1);
-    std::vector<double> tv(nz);
-    HIPC(hipMemcpy(trp.data(), ctx->seg_tier[t].rowptr, (m + 1) * sizeof(int64_t), hipMemcpyDeviceToHost));
-    HIPC(hipMemcpy(tv.data(), ctx->seg_tier[t].val, nz * sizeof(double), hipMemcpyDeviceToHost));
-    for (int64_t r = 0; r < m; ++r)
-      for (int64_t k = trp[r]; k < trp[r + 1]; ++k) {
-        const uint64_t row = (uint64_t)(ctx->r0 + r), col = (uint64_t)cols[k];
-        uint64_t vb;
-        memcpy(&vb, &tv[k], sizeof(vb));
-        const uint64_t a = t == 1 ? row : col, b2 = t == 1 ? col : row;  // tier 2: transposed
-        const uint64_t h = mix64(mix64(a * 0x9E3779B97F4A7C15ull ^ b2) ^ vb);
-        out[owner(cols[k])] = (int64_t)((uint64_t)out[owner(cols[k])] + h);
-      }
+  auto local_counts = [&]() -> int {
+    if (nz1) HIPC(hipMemcpy(c1.data(), ctx->seg_tier[1].col, nz1 * sizeof(int32_t), hipMemcpyDeviceToHost));
+    if (nz2) HIPC(hipMemcpy(c2.data(), ctx->seg_tier[2].col, nz2 * sizeof(int32_t), hipMemcpyDeviceToHost));
+    std::vector<uint8_t> mark(std::max<int64_t>(n, 1), 0);
+    for (int64_t k = 0; k < nz1; ++k) {
+      ++vote[owner(c1[k])];
+      if (!mark[c1[k]]) { mark[c1[k]] = 1; ++vote[2 * P]; }
+    }
+    for (int64_t k = 0; k < nz2; ++k) {
+      ++vote[P + owner(c2[k])];
+      if (!mark[c2[k]]) { mark[c2[k]] = 2; ++vote[2 * P + 1]; }
+    }
+    vote[2 * P + 1] += vote[2 * P];
+    std::vector<uint8_t>().swap(mark);
+    // the entries themselves, not only their counts: the split forms A[r,c] Q[c] on c's rank from
+    // A[c,r], so p's tier-2 entries towards q must be q's tier-1 entries towards p transposed,
+    // values included.  Per peer an order-free hash (wrapping sum of mixed (row, col, value
+    // bits), tier 2 keyed transposed) is compared: a pattern or a value that is not symmetric
+    // keeps the pull-all halo (or fails under RBL_OPT_HALO_PUSH 1) instead of a wrong SpMM.
+    auto tier_hash = [&](int t, int64_t nz, const std::vector<int32_t>& cols, int64_t* out) -> int {
+      if (nz == 0) return RBL_OK;
+      std::vector<int64_t> trp(m + 1);
+      std::vector<double> tv(nz);
+      HIPC(hipMemcpy(trp.data(), ctx->seg_tier[t].rowptr, (m + 1) * sizeof(int64_t), hipMemcpyDeviceToHost));
+      HIPC(hipMemcpy(tv.data(), ctx->seg_tier[t].val, nz * sizeof(double), hipMemcpyDeviceToHost));
+      for (int64_t r = 0; r < m; ++r)
+        for (int64_t k = trp[r]; k < trp[r + 1]; ++k) {
+          const uint64_t row = (uint64_t)(ctx->r0 + r), col = (uint64_t)cols[k];
+          uint64_t vb;
+          memcpy(&vb, &tv[k], sizeof(vb));
+          const uint64_t a = t == 1 ? row : col, b2 = t == 1 ? col : row;  // tier 2: transposed
+          const uint64_t h = mix64(mix64(a * 0x9E3779B97F4A7C15ull ^ b2) ^ vb);
+          out[owner(cols[k])] = (int64_t)((uint64_t)out[owner(cols[k])] + h);
+        }
+      return RBL_OK;
+    };
+    CHK(tier_hash(1, nz1, c1, vote.data() + 2 * P + 2));
+    CHK(tier_hash(2, nz2, c2, vote.data() + 3 * P + 2));
     return RBL_OK;
   };
-  CHK(tier_hash(1, nz1, c1, vote.data() + 2 * P + 2));
-  CHK(tier_hash(2, nz2, c2, vote.data() + 3 * P + 2));
+  const int lrc = local_counts();
   std::vector<int32_t>().swap(c2);
-  const int V = 4 * P + 2;
+  const int V = 4 * P + 3;
+  vote[4 * P + 2] = lrc;
   std::vector<int64_t> votes((size_t)P * V);
   COMMC(ctx->comm->allgather_host(vote.data(), votes.data(), V, ctx->stream, &ctx->err));
+  if (lrc < 0) return lrc;  // (ctx->err already says what failed here)
+  for (int p = 0; p < P; ++p)
+    if (votes[(size_t)p * V + 4 * P + 2] < 0)
+      return fail(ctx, (int)votes[(size_t)p * V + 4 * P + 2],
+                  "push/pull halo setup failed on rank " + std::to_string(p));
   bool sym = true;
   int64_t d1 = 0, d12 = 0;
   for (int p = 0; p < P; ++p) {
@@ -768,6 +790,11 @@ int prepare_tiers(rbl_ctx* ctx, const std::vector<int64_t>& rp) {
     return RBL_OK;
   }
   if (ctx->seg_ntasks == 0 || ctx->nnz == 0 || ctx->csr_dropped) return RBL_OK;
+#ifndef RBL_VARIANTS
+  return RBL_OK;
+#else
+  // (variants build only: the degree-ranked column tiers of one rank, measured no faster,
+  // DESIGN.md §3 round 3)
   const char* e = std::getenv("RBL_SEG_TIERS");
   if (!e || ctx->nloc != ctx->n) return RBL_OK;
   std::vector<int64_t> sz;
@@ -793,6 +820,7 @@ int prepare_tiers(rbl_ctx* ctx, const std::vector<int64_t>& rp) {
     for (int64_t k = 0; k < sz[t] && rank < n; ++k) tier_of[order[rank++]] = (uint8_t)t;
   (void)m;
   return build_tiers(ctx, tier_of, nt);
+#endif
 }
 
 // The tier CSRs and task tables for a column -> tier map (tier_of: n entries, < nt), or for
@@ -994,7 +1022,8 @@ int prepare_window_formats(rbl_ctx* ctx, const std::vector<int64_t>& rp) {
       HIPC(hipGetLastError());
       HIPC(hipStreamSynchronize(ctx->stream));
       ctx->bt_ng = NG;
-      // RBL_BT_PACK = 1: pack the tiles (zeros dropped; C4a: 13.1 KB per tile instead of
+#ifdef RBL_VARIANTS
+      // (variants build only) RBL_BT_PACK = 1: pack the tiles (zeros dropped; C4a: 13.1 KB per tile instead of
       // 18.4 KB, 3 GB less HBM at n = 1e7).  Off by default: the kernel is not bound by its
       // A bytes (one wave per SIMD, 60 % MFMA busy, fp64 MFMA and VALU do not co-issue) and
       // the index arithmetic of the packed loads costs more than the bytes save (3.56 vs
@@ -1026,6 +1055,7 @@ int prepare_window_formats(rbl_ctx* ctx, const std::vector<int64_t>& rp) {
           }
         }
       }
+#endif
     }
   }
   if (!ctx->keep_csr && ctx->bt_ng) {
@@ -1073,6 +1103,7 @@ struct StageScope {
   // every stage is also a roctx range named like the reference's TimerOutputs labels
   // (RBL_gpu.jl:152-187: "AQ", "3-term", ...): `rocprofv3 --marker-trace` shows them
   hipStream_t st;
+  int parent = -1;
   StageScope(rbl_ctx* c, int s, hipStream_t on = nullptr) : ctx(c), stage(s), st(on ? on : c->stream) {
     roctxRangePushA(kStageNames[s]);
     if (ctx->timers == 1 ||
@@ -1080,13 +1111,23 @@ struct StageScope {
       a = next_event(ctx);
       if (a) hipEventRecord(a, st);
     }
+    // a collective issued inside another stage on the same stream: its span is "comm" only, so
+    // the stages of a step sum to the step's stream time (the multi-rank line's per-rank split)
+    if (s == RBL_STAGE_COMM)
+      for (auto it = ctx->open_stages.rbegin(); it != ctx->open_stages.rend(); ++it)
+        if (it->st == st) {
+          parent = it->stage;
+          break;
+        }
+    ctx->open_stages.push_back({s, st});
   }
   ~StageScope() {
+    ctx->open_stages.pop_back();
     if (a) {
       hipEvent_t b = next_event(ctx);
       if (b) {
         hipEventRecord(b, st);
-        ctx->marks.push_back({stage, a, b});
+        ctx->marks.push_back({stage, a, b, parent});
       }
     }
     roctxRangePop();
@@ -1102,16 +1143,54 @@ void harvest_timers(rbl_ctx* ctx) {
       continue;
     }
     float ms = 0.f;
-    if (hipEventElapsedTime(&ms, m.a, m.b) == hipSuccess) ctx->stage_ms[m.stage] += ms;
+    if (hipEventElapsedTime(&ms, m.a, m.b) == hipSuccess) {
+      if (m.stage < RBL_NUM_STAGES) {
+        ctx->stage_ms[m.stage] += ms;
+        if (m.parent >= 0) ctx->stage_ms[m.parent] -= ms;  // (recorded whenever the child is)
+      } else {
+        ctx->comm_dev_ms[m.stage - RBL_NUM_STAGES] += ms;  // a CollScope's span
+      }
+    }
   }
   ctx->marks.swap(keep);
   if (ctx->marks.empty()) ctx->ev_used = 0;
 }
 
 // ---- collectives ---------------------------------------------------------------------
+// One collective call: the host wall time inside the transport (RCCL enqueues and returns;
+// the shm / in-process stand-ins block) and, while the full stage timers run, a hipEvent pair
+// around it on its stream — the span the collective holds that stream, waiting for the peers
+// included.  Read per rank through rbl_comm_stats (RBL_COMM_*_HOST_NS / *_DEV_NS).
+struct CollScope {
+  rbl_ctx* ctx;
+  int kind;  // 0 all-reduce, 1 exchange
+  hipStream_t st;
+  hipEvent_t a = nullptr;
+  std::chrono::steady_clock::time_point t0;
+  CollScope(rbl_ctx* c, int k, hipStream_t on) : ctx(c), kind(k), st(on) {
+    if (ctx->timers == 1) {
+      a = next_event(ctx);
+      if (a) hipEventRecord(a, st);
+    }
+    t0 = std::chrono::steady_clock::now();
+  }
+  ~CollScope() {
+    ctx->comm_host_ns[kind] += std::chrono::duration_cast<std::chrono::nanoseconds>(
+                                   std::chrono::steady_clock::now() - t0).count();
+    if (a) {
+      hipEvent_t b = next_event(ctx);
+      if (b) {
+        hipEventRecord(b, st);
+        ctx->marks.push_back({RBL_NUM_STAGES + kind, a, b});
+      }
+    }
+  }
+};
+
 int allreduce(rbl_ctx* ctx, double* buf, size_t count) {
   if (ctx->nranks == 1) return RBL_OK;
   StageScope t(ctx, RBL_STAGE_COMM);
+  CollScope c(ctx, 0, ctx->stream);
   COMMC(ctx->comm->allreduce_sum(buf, count, ctx->stream, &ctx->err));
   ctx->comm_stats[RBL_COMM_ALLREDUCE_CALLS] += 1;
   ctx->comm_stats[RBL_COMM_ALLREDUCE_BYTES] += (int64_t)(count * sizeof(double));
@@ -1124,6 +1203,14 @@ void count_exchange(rbl_ctx* ctx, const std::vector<Comm::Xfer>& x) {
     ctx->comm_stats[RBL_COMM_SEND_BYTES] += (int64_t)(t.nsend * sizeof(double));
     ctx->comm_stats[RBL_COMM_RECV_BYTES] += (int64_t)(t.nrecv * sizeof(double));
   }
+}
+
+// a step's grouped halo send/recv on `st`, timed and counted
+int exchange(rbl_ctx* ctx, const std::vector<Comm::Xfer>& x, hipStream_t st) {
+  CollScope c(ctx, 1, st);
+  COMMC(ctx->comm->exchange(x, st, &ctx->err));
+  count_exchange(ctx, x);
+  return RBL_OK;
 }
 
 // Gram C = W^T X over all ranks.  C layout [nW*w][X.count*X.w].  (comm = false: this rank's
@@ -1697,8 +1784,7 @@ int halo_exchange(rbl_ctx* ctx, const double* Q, const double** Qin, int64_t* of
       x[q].recv = ext + ctx->ghost_off[q] * b;
       x[q].nrecv = (size_t)ctx->ghost_cnt[q] * b;
     }
-    COMMC(ctx->comm->exchange(x, st, &ctx->err));
-    count_exchange(ctx, x);
+    CHK(exchange(ctx, x, st));
     ctx->ghost_local = Q;
     *Qin = ext;
     *off = 0;
@@ -1721,8 +1807,7 @@ int halo_exchange(rbl_ctx* ctx, const double* Q, const double** Qin, int64_t* of
       x[q].nrecv = (size_t)(nh - nl) * b;
     }
   }
-  COMMC(ctx->comm->exchange(x, st, &ctx->err));
-  count_exchange(ctx, x);
+  CHK(exchange(ctx, x, st));
   *Qin = ext;
   *off = ctx->ext_lo;
   return RBL_OK;
@@ -1757,12 +1842,21 @@ int halo_exchange32(rbl_ctx* ctx, const float* Q, const float** Qin, int64_t* of
       x[q].nrecv = (size_t)(nh - nl) * b / 2;
     }
   }
-  COMMC(ctx->comm->exchange(x, ctx->stream, &ctx->err));
-  count_exchange(ctx, x);
+  CHK(exchange(ctx, x, ctx->stream));
   *Qin = ext;
   *off = ctx->ext_lo;
   return RBL_OK;
 }
+
+// A/B switches of the variants build (tools/build_variant.sh with -DRBL_VARIANTS): the plain
+// D2H copy instead of the staged one (RBL_D2H_DIRECT), the one-pass Ritz (RBL_RITZ_SERIAL)
+#ifdef RBL_VARIANTS
+bool d2h_direct() { return std::getenv("RBL_D2H_DIRECT") != nullptr; }
+bool ritz_serial() { return std::getenv("RBL_RITZ_SERIAL") != nullptr; }
+#else
+constexpr bool d2h_direct() { return false; }
+constexpr bool ritz_serial() { return false; }
+#endif
 
 // one step's record in the async stash: A_i, R_tot (b x b each) and 4 int flags (2 doubles)
 size_t stash_rec(int b) { return (size_t)2 * b * b + 2; }
@@ -1846,8 +1940,7 @@ int push_exchange(rbl_ctx* ctx, int b, hipStream_t st) {
     x[q].recv = ctx->d_precv + ctx->send_off[q] * b;
     x[q].nrecv = (size_t)ctx->send_cnt[q] * b;
   }
-  COMMC(ctx->comm->exchange(x, st, &ctx->err));
-  count_exchange(ctx, x);
+  CHK(exchange(ctx, x, st));
   return RBL_OK;
 }
 
@@ -2066,6 +2159,13 @@ int halo_from_footprint(rbl_ctx* ctx) {
 extern "C" {
 
 int rbl_abi_version(void) { return RBL_ABI_VERSION; }
+int rbl_build_flags(void) {
+#ifdef RBL_VARIANTS
+  return RBL_BUILD_VARIANTS;
+#else
+  return 0;
+#endif
+}
 
 int rbl_create(rbl_ctx** out, int device) {
   if (!out) return RBL_ERR_INVALID;
@@ -2792,12 +2892,16 @@ int rbl_start(rbl_ctx* ctx, int b, int max_blocks, int basis_bits, const double*
   HIPC(hipMalloc(&ctx->d_flags, 4 * sizeof(int)));
   HIPC(hipMemset(ctx->d_flags, 0, 4 * sizeof(int)));
   {
+#ifdef RBL_VARIANTS
     const char* e = std::getenv("RBL_STASH_COPY");  // A/B: 1 = device record + D2H copy
     ctx->stash_direct = !(e && std::atoi(e) == 1);
+#else
+    ctx->stash_direct = true;
+#endif
     const unsigned hf = ctx->stash_direct ? (hipHostMallocMapped | hipHostMallocCoherent) : hipHostMallocDefault;
     HIPC(hipHostMalloc(&ctx->h_pin, stash_rec(b) * sizeof(double), hf));
     HIPC(hipHostMalloc(&ctx->h_hist, (size_t)(max_blocks + 2) * stash_rec(b) * sizeof(double), hf));
-    if ((size_t)ctx->nloc * b * sizeof(double) >= 4 * kD2HPiece && !std::getenv("RBL_D2H_DIRECT")) {
+    if ((size_t)ctx->nloc * b * sizeof(double) >= 4 * kD2HPiece && !d2h_direct()) {
       CHK(ensure_d2h_slots(ctx));
       CHK(ensure_ritz_stream(ctx));
     }
@@ -3203,7 +3307,7 @@ int step_impl(rbl_ctx* ctx, int i, int part_reorth, double* A_out, double* B_out
 // pinned).  Every earlier piece's host copy has finished before its slot is refilled.
 // RBL_D2H_DIRECT=1 restores the plain copy (A/B).
 int d2h_staged(rbl_ctx* ctx, void* dst, const void* src, size_t bytes) {
-  if (bytes < 4 * kD2HPiece || std::getenv("RBL_D2H_DIRECT")) {
+  if (bytes < 4 * kD2HPiece || d2h_direct()) {
     HIPC(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
     return RBL_OK;
   }
@@ -3265,6 +3369,12 @@ int ritz_pipelined(rbl_ctx* ctx, int nblocks, int k, int kcp, const double* d_S,
   CHK(ensure_ritz_stream(ctx));
   HIPC(hipEventRecord(ctx->ev_ritz[kRitzPieces], ctx->stream));  // S is on the device
   HIPC(hipStreamWaitEvent(ctx->rstream, ctx->ev_ritz[kRitzPieces], 0));
+  // on every exit, error paths included: the side stream's kernels write U / T and the run
+  // scratch, so nothing may leave here with them still queued behind the context's back
+  struct DrainSide {
+    hipStream_t s;
+    ~DrainSide() { (void)hipStreamSynchronize(s); }
+  } drain{ctx->rstream};
   {
     StageScope t(ctx, RBL_STAGE_RITZ, ctx->rstream);
     for (int p = 0; p < kRitzPieces; ++p) {
@@ -3362,7 +3472,11 @@ int rbl_ritz(rbl_ctx* ctx, int nblocks, int k, const double* S, double* V_out) {
   if (chunk_bytes(kc) > 0.7 * (double)free_b)
     return fail(ctx, RBL_ERR_OOM, "rbl_ritz: no room for one Ritz column");
   // RBL_RITZ_TRACE=1: host-side split of the call on stderr (diagnostics)
+#ifdef RBL_VARIANTS
   const bool trace = std::getenv("RBL_RITZ_TRACE") != nullptr;
+#else
+  const bool trace = false;
+#endif
   auto tnow = [] { return std::chrono::duration<double, std::milli>(
                        std::chrono::steady_clock::now().time_since_epoch()).count(); };
   const double t0 = trace ? tnow() : 0.0;
@@ -3390,12 +3504,13 @@ int rbl_ritz(rbl_ctx* ctx, int nblocks, int k, const double* S, double* V_out) {
                          (ctx->basis_bits == 64 || tsmm44_ok(b, kcp, kcp)) &&
                          nblocks <= ctx->resident && ctx->nloc >= 64 * kRitzPieces &&
                          (size_t)ctx->nloc * kcp * sizeof(double) >= 4 * kD2HPiece &&
-                         !std::getenv("RBL_D2H_DIRECT") && !std::getenv("RBL_RITZ_SERIAL");
+                         !d2h_direct() && !ritz_serial();
   std::vector<double> srm((size_t)rows * kcp);
   if (pipelined) {
     for (int64_t r = 0; r < rows; ++r)
       for (int c = 0; c < kcp; ++c) srm[(size_t)r * kcp + c] = c < k ? S[(size_t)c * rows + r] : 0.0;
     HIPC(hipMemcpyAsync(pS, srm.data(), rows * kcp * sizeof(double), hipMemcpyHostToDevice, ctx->stream));
+    ctx->path_stats[RBL_PATH_RITZ_PIECES] += 1;
     CHK(ritz_pipelined(ctx, nblocks, k, kcp, pS, pV, pVcm, V_out));
     harvest_timers(ctx);
     if (trace) fprintf(stderr, "rbl_ritz: pipelined, %d row pieces, total %.2f ms\n", kRitzPieces, tnow() - t0);
@@ -3543,6 +3658,18 @@ int rbl_timers(rbl_ctx* ctx, double* ms, int nstages) {
   for (int s = 0; s < nstages && s < RBL_NUM_STAGES; ++s) ms[s] = ctx->stage_ms[s];
   return RBL_OK;
 }
+int rbl_allgather_host(rbl_ctx* ctx, const int64_t* mine, int64_t* all, int n) {
+  if (!ctx || n < 0 || (n > 0 && (!mine || !all))) return fail(ctx, RBL_ERR_INVALID, "rbl_allgather_host: bad arguments");
+  if (n == 0) return RBL_OK;
+  HIPC(hipSetDevice(ctx->device));
+  if (ctx->nranks == 1) {
+    memcpy(all, mine, (size_t)n * sizeof(int64_t));
+    return RBL_OK;
+  }
+  COMMC(ctx->comm->allgather_host(mine, all, (size_t)n, ctx->stream, &ctx->err));
+  return RBL_OK;
+}
+
 int rbl_comm_stats(rbl_ctx* ctx, int64_t* out, int nstats, int reset) {
   if (!ctx || nstats < 0 || (nstats > 0 && !out)) return RBL_ERR_INVALID;
   for (int i = 0; i < nstats && i < RBL_COMM_NSTATS; ++i) out[i] = ctx->comm_stats[i];
@@ -3550,9 +3677,16 @@ int rbl_comm_stats(rbl_ctx* ctx, int64_t* out, int nstats, int reset) {
   if (nstats > RBL_COMM_HALO_PUSH) out[RBL_COMM_HALO_PUSH] = ctx->push ? 1 : 0;
   if (nstats > RBL_COMM_PUSH_ROWS) out[RBL_COMM_PUSH_ROWS] = ctx->push_pred_rows;
   if (nstats > RBL_COMM_PULL_ROWS) out[RBL_COMM_PULL_ROWS] = ctx->pull_pred_rows;
-  for (int i = RBL_COMM_PULL_ROWS + 1; i < nstats; ++i) out[i] = 0;
-  if (reset)
+  // the time in the collectives: host wall time in the calls, hipEvent spans on their streams
+  const int64_t tm[4] = {ctx->comm_host_ns[0], ctx->comm_host_ns[1],
+                         (int64_t)(ctx->comm_dev_ms[0] * 1e6), (int64_t)(ctx->comm_dev_ms[1] * 1e6)};
+  for (int i = RBL_COMM_PULL_ROWS + 1; i < nstats; ++i)
+    out[i] = i <= RBL_COMM_EXCHANGE_DEV_NS ? tm[i - RBL_COMM_ALLREDUCE_HOST_NS] : 0;
+  if (reset) {
     for (int64_t& v : ctx->comm_stats) v = 0;
+    ctx->comm_host_ns[0] = ctx->comm_host_ns[1] = 0;
+    ctx->comm_dev_ms[0] = ctx->comm_dev_ms[1] = 0.0;
+  }
   return RBL_OK;
 }
 

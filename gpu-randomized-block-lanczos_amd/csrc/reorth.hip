@@ -466,21 +466,27 @@ static void launch_gram44(int64_t nrows, const PanelRun& W, const Panels& X, dou
 void gram44_partial(int64_t nrows, const PanelRun& W, const Panels& X, double* slab, int splits,
                     const int* skip, hipStream_t st) {
   if (W.w == 32) {
-    // RBL_G44_DUO=1: panel pairs per wave (A/B; see gram44_body)
+#ifdef RBL_VARIANTS
+    // (variants build only) RBL_G44_DUO=1: panel pairs per wave (A/B; see gram44_body)
     static const bool duo_ok = [] {
       const char* e = getenv("RBL_G44_DUO");
       return e && atoi(e) != 0;
     }();
     if (duo_ok && X.count == 2 && W.count % 2 == 0)
       return launch_gram44<32, 2, false, true>(nrows, W, X, slab, splits, skip, st);
+#endif
     if (X.count == 2) return launch_gram44<32, 2>(nrows, W, X, slab, splits, skip, st);
     return launch_gram44<32, 1>(nrows, W, X, slab, splits, skip, st);
   }
   // b = 16 with an even panel count (partial reorth: i - 2 panels at even i): panel pairs
-  static const bool pair_ok = [] {
+#ifdef RBL_VARIANTS
+  static const bool pair_ok = [] {  // RBL_G44_PAIR=0: one panel per wave (A/B)
     const char* e = getenv("RBL_G44_PAIR");
     return !e || atoi(e) != 0;
   }();
+#else
+  constexpr bool pair_ok = true;
+#endif
   if (pair_ok && W.count % 2 == 0) {
     if (X.count == 2) return launch_gram44<16, 2, true>(nrows, W, X, slab, splits, skip, st);
     return launch_gram44<16, 1, true>(nrows, W, X, slab, splits, skip, st);
@@ -980,10 +986,14 @@ void tsmm44(int64_t nrows, const PanelRun& X, const double* C, int ldc, const Pa
             double alpha, double beta, const int* skip, hipStream_t st, double* xslab, int* xgrid) {
   if (xgrid) *xgrid = 0;
   const int KY = Y.count * Y.w;
-  static const bool fast_ok = [] {
+#ifdef RBL_VARIANTS
+  static const bool fast_ok = [] {  // RBL_TSMM44_FAST=0: the generic kernel (A/B)
     const char* e = getenv("RBL_TSMM44_FAST");
     return !e || atoi(e) != 0;
   }();
+#else
+  constexpr bool fast_ok = true;
+#endif
   // fast path: 64 or 32 output columns, K a multiple of 32, Y not aliasing the X panels (a
   // wave writes its rows after the whole k-loop; the shifted last tile re-reads rows below it)
   bool alias = false;
@@ -992,10 +1002,14 @@ void tsmm44(int64_t nrows, const PanelRun& X, const double* C, int ldc, const Pa
   // (KYP = 32 builds but stays off: at b = 16 the update is HBM-bound and the generic kernel
   // ran 4 % faster on C2, its cross-Gram form 6 % slower than the Gram pass it replaces —
   // tools/r02_c2_ab.sh; round 3 again 3 % faster on C2 and C3, profiles/r03_tsmm_fast32_ab.log)
+#ifdef RBL_VARIANTS
   static const bool fast32 = [] {  // RBL_TSMM44_FAST32=1: the 32-column form too (A/B)
     const char* e = getenv("RBL_TSMM44_FAST32");
     return e && atoi(e) != 0;
   }();
+#else
+  constexpr bool fast32 = false;
+#endif
   if (fast_ok && (KY == 64 || (KY == 32 && fast32)) && (X.count * X.w) % kT44K == 0 &&
       nrows >= kT44fRows && Y.w % 2 == 0 && !alias) {
     const int64_t wgs = (nrows + 4 * kT44fRows - 1) / (4 * kT44fRows);
@@ -1017,10 +1031,13 @@ void tsmm44(int64_t nrows, const PanelRun& X, const double* C, int ldc, const Pa
     if (KY == 64) {
       if (X.w == 32) { if (xg) RBL_T44F(32, true, 64); else RBL_T44F(32, false, 64); }
       else { if (xg) RBL_T44F(16, true, 64); else RBL_T44F(16, false, 64); }
-    } else {
+    }
+#ifdef RBL_VARIANTS
+    else {
       if (X.w == 32) { if (xg) RBL_T44F(32, true, 32); else RBL_T44F(32, false, 32); }
       else { if (xg) RBL_T44F(16, true, 32); else RBL_T44F(16, false, 32); }
     }
+#endif
 #undef RBL_T44F
     return;
   }

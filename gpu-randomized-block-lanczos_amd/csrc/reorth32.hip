@@ -418,6 +418,14 @@ __global__ __launch_bounds__(256) void k_tsmm32_any(int64_t nrows, const float* 
   *y = beta != 0.f ? beta * *y + alpha * acc : alpha * acc;
 }
 
+// RBL_LOC32_MFMA=1 (variants build only): the fp32-basis local reorth on the MFMA tile
+// kernels instead of the 4-wave Gram / row-streaming update (A/B)
+#ifdef RBL_VARIANTS
+static bool loc32_mfma() { return std::getenv("RBL_LOC32_MFMA") != nullptr; }
+#else
+static constexpr bool loc32_mfma() { return false; }
+#endif
+
 void gram32_partial(int64_t nrows, const float* Wb, int64_t wstride, int nW, int w, const float* X0,
                     const float* X1, int xcount, double* slab, int splits, hipStream_t st) {
   if (w != 16 && w != 32) {
@@ -427,7 +435,7 @@ void gram32_partial(int64_t nrows, const float* Wb, int64_t wstride, int nW, int
                        st, nrows, Wb, wstride, nW, w, X0, X1, xcount, slab, rows_per);
     return;
   }
-  if (w == 32 && nW == 1 && xcount == 1 && !std::getenv("RBL_LOC32_MFMA")) {
+  if (w == 32 && nW == 1 && xcount == 1 && !loc32_mfma()) {
     int64_t rows_per = (nrows + splits - 1) / splits;
     rows_per = (rows_per + 63) / 64 * 64;
     hipLaunchKernelGGL(k_gram32_one<32>, dim3((unsigned)splits), dim3(256), 0, st, nrows, Wb, X0, slab,
@@ -863,7 +871,7 @@ void tsmm32(int64_t nrows, const float* Xb, int64_t xstride, int nX, int w, cons
   if (nrows <= 0) return;
   const int KY = ycount * w;
   // the local reorth's shape (one panel, 32 columns, Y += X C); RBL_LOC32_MFMA=1: the tile kernel
-  if (w == 32 && nX == 1 && KY == 32 && beta == 1.f && !std::getenv("RBL_LOC32_MFMA")) {
+  if (w == 32 && nX == 1 && KY == 32 && beta == 1.f && !loc32_mfma()) {
     const int64_t groups = (nrows + 31) / 32;
     const int64_t grid = groups < 8 * (int64_t)window_grid() ? groups : 8 * (int64_t)window_grid();
     hipLaunchKernelGGL(k_upd32_rows, dim3((unsigned)grid), dim3(256), 0, st, nrows, Xb, C, ldc, Y0, alpha);

@@ -468,10 +468,15 @@ __global__ __launch_bounds__(64) void k_chol_elim2(const double* __restrict__ G,
 // RBL_CHOL_REG: 0 the four-wave kernel at b = 16 / 32 as well, 1 k_chol_reg, 2 k_chol_elim2
 // (default), 3 k_chol_elim (the one-half-wave form, same bits as 2)
 // (A/B; read per call, tests switch it)
+#ifdef RBL_VARIANTS
 static int chol_reg_mode() {
   const char* e = getenv("RBL_CHOL_REG");
   return e ? atoi(e) : 2;
 }
+#else
+// the product build: k_chol_elim2 at b = 16 / 32, the four-wave kernel for any other b
+static constexpr int chol_reg_mode() { return 2; }
+#endif
 
 void chol_step(const double* G, int b, int64_t nglobal, int mode, double* R, double* Rinv,
                double* Rtot, int* need3, int* status, const int* skip, hipStream_t s,
@@ -486,6 +491,7 @@ void chol_step(const double* G, int b, int64_t nglobal, int mode, double* R, dou
                          need3, status, skip);
     return;
   }
+#ifdef RBL_VARIANTS
   if (cm == 3) {
     if (b == 32)
       hipLaunchKernelGGL(k_chol_elim<32>, dim3(1), dim3(64), 0, s, G, nglobal, mode, R, Rinv, Rtot,
@@ -504,6 +510,7 @@ void chol_step(const double* G, int b, int64_t nglobal, int mode, double* R, dou
                          need3, status, skip);
     return;
   }
+#endif
   if (b <= kMaxB)
     hipLaunchKernelGGL(k_chol<true>, dim3(1), dim3(256), 0, s, G, b, nglobal, mode, R, Rinv, Rtot,
                        need3, status, skip, scratch);

@@ -504,11 +504,15 @@ __global__ __launch_bounds__(band::kThreads) void k_spmm_band(BandArgs a) {
 
 template <int B, bool EPI, bool AIG, bool PAIR>
 static void launch_band_t(const BandArgs& a0, int grid, hipStream_t s) {
+  ensure_lds_attr(reinterpret_cast<const void*>(&k_spmm_band<B, EPI, false, AIG, PAIR>), BandLayout<B>::kLds);
+#ifndef RBL_VARIANTS
+  hipLaunchKernelGGL((k_spmm_band<B, EPI, false, AIG, PAIR>), dim3(grid), dim3(band::kThreads),
+                     BandLayout<B>::kLds, s, a0);
+#else
   static const bool prof = [] {
     const char* e = getenv("RBL_SPMM_PROF");
     return e && atoi(e) != 0;
   }();
-  ensure_lds_attr(reinterpret_cast<const void*>(&k_spmm_band<B, EPI, false, AIG, PAIR>), BandLayout<B>::kLds);
   ensure_lds_attr(reinterpret_cast<const void*>(&k_spmm_band<B, EPI, true, AIG, PAIR>), BandLayout<B>::kLds);
   if (!prof) {
     hipLaunchKernelGGL((k_spmm_band<B, EPI, false, AIG, PAIR>), dim3(grid), dim3(band::kThreads),
@@ -532,6 +536,7 @@ static void launch_band_t(const BandArgs& a0, int grid, hipStream_t s) {
             B, (int)EPI, w, w < band::kConsumers ? "consumer" : "producer", hbuf[w * 4] / tiles,
             hbuf[w * 4 + 2] / tiles, hbuf[w * 4 + 1] / tiles);
   }
+#endif
 }
 
 bool spmm_band(const CsrDev& A, const double* Qin, int64_t col_off, int b, double* U,
@@ -552,11 +557,15 @@ bool spmm_band(const CsrDev& A, const double* Qin, int64_t col_off, int b, doubl
   a.U = U;
   a.Qprev = Qprev;
   a.Bi = Bi;
-  static const int ablate = [] {
+#ifdef RBL_VARIANTS
+  static const int ablate = [] {  // diagnostics: 1 skip compute, 2 skip data loads
     const char* e = getenv("RBL_SPMM_ABLATE");
     return e ? atoi(e) : 0;
   }();
   a.ablate = ablate;
+#else
+  a.ablate = 0;
+#endif
   a.prof = nullptr;
   a.row0 = A.row0;
   const int grid = (int)((A.ntiles + A.tiles_per_wg - 1) / A.tiles_per_wg);

@@ -628,7 +628,9 @@ void k_spmm_bt(BtArgs a) {
   }
 }
 
-// ---- two waves per SIMD (b = 32, fp64, dense or half tiles) ---------------------------------
+#ifdef RBL_VARIANTS
+// ---- (variants build only) two waves per SIMD (b = 32, fp64, dense or half tiles) -------------
+// measured no faster than k_spmm_bt
 // k_spmm_bt holds one wave per SIMD (256 VGPRs + AGPRs), so the SIMD idles whenever that wave
 // waits on memory: with whole tiles it streams at the HBM rate anyway, but with half tiles (5.1
 // GB less per launch at C4a) it becomes issue-bound at the same time.  Here eight
@@ -998,6 +1000,7 @@ static bool bt2_on() {
   const char* e = getenv("RBL_BT2");  // read per launch (tests switch it)
   return e ? atoi(e) != 0 : false;
 }
+#endif
 
 template <int B, int NG, bool EPI, bool AIG, int VAR>
 static void launch_bt_v(const BtArgs& a, int grid, hipStream_t s) {
@@ -1009,9 +1012,13 @@ static void launch_bt_v(const BtArgs& a, int grid, hipStream_t s) {
 template <int B, int NG, bool EPI, bool AIG>
 static void launch_bt_t(const BtArgs& a, int grid, hipStream_t s, bool f32) {
   // default: non-temporal A loads and U stores (VAR 3): the format is read once per launch
-  // and U only by the next kernel — measured 7 % faster at C4a than the default policy;
+  // and U only by the next kernel — measured 7 % faster at C4a than the default policy
+#ifndef RBL_VARIANTS
+  if (f32) return launch_bt_v<B, NG, EPI, AIG, 3 | 64>(a, grid, s);
+  launch_bt_v<B, NG, EPI, AIG, 3>(a, grid, s);
+#else
   // RBL_BT_VAR = 0 / 35 / 259 (diagnostics): default policy / loads-only ablation / no LDS
-  // read-ahead of the next group's B operands
+  // read-ahead of the next group's B operands; packed (a.hdr) and half (a.Ah) tiles
   static const int var = [] {
     const char* e = getenv("RBL_BT_VAR");
     return e ? atoi(e) : 3;
@@ -1039,6 +1046,7 @@ static void launch_bt_t(const BtArgs& a, int grid, hipStream_t s, bool f32) {
     if (var == 515) return launch_bt_v<B, NG, EPI, AIG, 515>(a, grid, s);
   }
   launch_bt_v<B, NG, EPI, AIG, 3>(a, grid, s);
+#endif
 }
 
 bool spmm_bt(const CsrDev& A, const double* Qin, int64_t col_off, int b, double* U,
@@ -1080,6 +1088,7 @@ bool spmm_bt(const CsrDev& A, const double* Qin, int64_t col_off, int b, double*
     if (b != 32 || f32 || a.hdr || !epi || !aig) return false;
     a.lf_lo = A.lfix_lo;
     a.lf_hi = A.lfix_hi;
+#ifdef RBL_VARIANTS
     if (bt2_on()) {
       if (A.two_wave) *A.two_wave = 1;
       if (a.Ah) {
@@ -1094,12 +1103,16 @@ bool spmm_bt(const CsrDev& A, const double* Qin, int64_t col_off, int b, double*
     if (a.Ah) {
       if (A.bt_ng == 9) launch_bt_v<32, 9, true, true, 3 | 1024 | 2048>(a, grid, s);
       else launch_bt_v<32, 5, true, true, 3 | 1024 | 2048>(a, grid, s);
-    } else {
+      return true;
+    }
+#endif
+    {
       if (A.bt_ng == 9) launch_bt_v<32, 9, true, true, 3 | 1024>(a, grid, s);
       else launch_bt_v<32, 5, true, true, 3 | 1024>(a, grid, s);
     }
     return true;
   }
+#ifdef RBL_VARIANTS
   if (bt2_on() && b == 32 && epi && aig && !f32 && !a.hdr) {
     if (A.two_wave) *A.two_wave = 1;
     a.lf_lo = 0;
@@ -1113,6 +1126,7 @@ bool spmm_bt(const CsrDev& A, const double* Qin, int64_t col_off, int b, double*
     }
     return true;
   }
+#endif
   const int key = (b == 32 ? 8 : 0) | (A.bt_ng == 9 ? 4 : 0) | (epi ? 2 : 0) | (aig ? 1 : 0);
   switch (key) {
 #define RBL_BT_CASE(K, BB, NG, E, G) \
@@ -1237,7 +1251,8 @@ __global__ void k_bt_fill(int64_t nrows, const int64_t* __restrict__ rowptr,
   }
 }
 
-// Half tiles (A symmetric): tile t's left group g equals the transpose of group NG-1-g of tile
+#ifdef RBL_VARIANTS
+// (variants build only) Half tiles (A symmetric): tile t's left group g equals the transpose of group NG-1-g of tile
 // t - NGL + g bit for bit, so only groups NGL..NG-1 (diagonal + right strip: 10 of 18.4 KB per
 // tile at H = 64) are stored and the kernel transposes the strip groups of the previous NGL
 // tiles back (L2-resident: read NGL tiles earlier).  U is bit-identical to the whole tiles'.
@@ -1309,6 +1324,8 @@ int bt_half(const double* full, int64_t ntiles, int64_t tpw, int NG, double** ha
   return (int)hipStreamSynchronize(s);
 }
 
+#endif
+
 int64_t bt_tile_slots(int64_t ntiles, int64_t tpw) {
   const int64_t grid = (ntiles + tpw - 1) / tpw;
   return ((tpw + 3) / 4) * grid * 4;
@@ -1322,7 +1339,8 @@ void bt_fill(const CsrDev& A, int H, int NG, double* out, hipStream_t s) {
                      A.rowptr, A.col, A.val, A.row0, H, NG, tpw, grid, out);
 }
 
-// Packed tiles (see k_spmm_bt, VAR bit 7): one wave per tile slot.  Pass 1 counts the
+#ifdef RBL_VARIANTS
+// (variants build only) Packed tiles (see k_spmm_bt, VAR bit 7): one wave per tile slot.  Pass 1 counts the
 // nonzero operand elements, an exclusive scan gives every run's first value, pass 2 writes
 // header and run (per block: element 0 of the lanes in lane order, then element 1).
 __global__ void k_btp_count(const double* __restrict__ dense, int64_t nslots, int NG,
@@ -1409,5 +1427,7 @@ int bt_pack(const double* dense, int64_t nslots, int NG, uint64_t* hdr, double**
   *nval_out = total;
   return 0;
 }
+
+#endif
 
 }  // namespace rbl

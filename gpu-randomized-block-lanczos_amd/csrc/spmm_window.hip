@@ -402,11 +402,15 @@ bool spmm_window(const CsrDev& A, const double* Qin, int64_t col_off, int b, dou
   a.U = U;
   a.Qprev = Qprev;
   a.Bi = Bi;
-  static const int ablate = [] {
+#ifdef RBL_VARIANTS
+  static const int ablate = [] {  // diagnostics: 1 skip compute, 2 skip data loads
     const char* e = getenv("RBL_SPMM_ABLATE");
     return e ? atoi(e) : 0;
   }();
   a.ablate = ablate;
+#else
+  a.ablate = 0;
+#endif
   const int grid = (int)((A.ntiles + A.tiles_per_wg - 1) / A.tiles_per_wg);
   const bool epi = Qprev != nullptr;
   if (b == 32) {

@@ -13,6 +13,8 @@
 // fixed order by reduce_slab (bitwise reproducible, no atomics).
 #include <cstdlib>
 
+#include <algorithm>
+
 #include "kernels.hpp"
 
 namespace rbl {
@@ -204,12 +206,16 @@ __global__ __launch_bounds__(256) void k_reduce(const double* __restrict__ slab,
 // threads sum 32 partials each (8 rounds of 4 loads) — at n = 1.25e6 (9,766 partials) 1,224
 // workgroups instead of 156 that summed 256 each (64 dependent rounds, 40 us).  RBL_RED_CHUNK=0:
 // the earlier rule (256 above 4,096 partials, else 16), for A/B.
+#ifdef RBL_VARIANTS
 static int red_chunk(int splits) {
   const char* e = std::getenv("RBL_RED_CHUNK");  // read per call: the slab is sized by
   const int mode = e ? std::atoi(e) : 32;          // rbl_start under the same setting
   if (mode <= 0) return splits > 4096 ? 256 : 16;
-  return mode;
+  return std::max(2, mode);                        // (1 would never shrink the level)
 }
+#else
+static constexpr int red_chunk(int) { return 32; }
+#endif
 int reduce_scratch_splits(int splits) {
   int tot = 0;
   while (splits > 64) {
@@ -272,7 +278,12 @@ __global__ __launch_bounds__(256) void k_reduce_wide(const double* __restrict__ 
 
 void reduce_slab(const double* slab, int splits, int64_t len, double* out, const int* skip,
                  hipStream_t s) {
-  if (len <= 4096 && splits > 64 && !std::getenv("RBL_REDUCE_NARROW")) {
+#ifdef RBL_VARIANTS
+  const bool narrow = std::getenv("RBL_REDUCE_NARROW") != nullptr;  // k_reduce for every len (A/B)
+#else
+  constexpr bool narrow = false;
+#endif
+  if (len <= 4096 && splits > 64 && !narrow) {
     hipLaunchKernelGGL(k_reduce_wide, dim3((unsigned)((len + 3) / 4)), dim3(256), 0, s, slab, splits, len,
                        out, skip);
     return;

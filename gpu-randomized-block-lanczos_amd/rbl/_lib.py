@@ -42,7 +42,9 @@ RBL_PATH_LOC_GRAM = 3
 RBL_PATH_LOCFIX_EDGES = 4
 RBL_PATH_LOCFIX_REST = 5
 RBL_PATH_SPMM_TWO_WAVE = 6
-RBL_PATH_NSTATS = 7
+RBL_PATH_RITZ_PIECES = 7
+RBL_PATH_NSTATS = 8
+RBL_BUILD_VARIANTS = 1
 
 _p = C.c_void_p
 _i64 = C.c_int64
@@ -55,6 +57,7 @@ _pu8 = C.POINTER(C.c_uint8)
 # name -> (restype, argtypes); the complete export list of include/rbl_hip.h
 SIGNATURES = {
     "rbl_abi_version": (C.c_int, []),
+    "rbl_build_flags": (C.c_int, []),
     "rbl_create": (C.c_int, [C.POINTER(_p), C.c_int]),
     "rbl_get_unique_id": (C.c_int, [_pu8]),
     "rbl_create_dist": (C.c_int, [C.POINTER(_p), C.c_int, C.c_int, C.c_int, _pu8]),
@@ -100,6 +103,7 @@ SIGNATURES = {
     "rbl_reset_timers": (C.c_int, [_p]),
     "rbl_comm_stats": (C.c_int, [_p, _pi64, C.c_int, C.c_int]),
     "rbl_path_stats": (C.c_int, [_p, _pi64, C.c_int, C.c_int]),
+    "rbl_allgather_host": (C.c_int, [_p, _pi64, _pi64, C.c_int]),
     "rbl_synchronize": (C.c_int, [_p]),
     "rbl_plan_row_partition": (C.c_int, [_i64, _pi64, C.c_int, _pi64]),
     "rbl_plan_halo": (C.c_int, [_i64, _pi64, _pi64, C.c_int, C.c_int, _pi64, _pi64, _pi64]),
@@ -127,6 +131,9 @@ def load() -> C.CDLL:
 
 
 lib = load()
+# compiled with -DRBL_VARIANTS (tools/build_variant.sh): the measured-and-rejected variants and
+# their A/B switches are in this copy (tests/test_gpu_variants.py runs only then)
+VARIANTS = bool(lib.rbl_build_flags() & RBL_BUILD_VARIANTS)
 
 
 def dptr(a: np.ndarray | None):

@@ -312,27 +312,42 @@ class Context:
             out.update(rccl_version())
         return out
 
-    def comm_stats(self, reset: bool = False) -> dict:
+    def comm_stats(self, reset: bool = False, times: bool = False) -> dict:
         """Collectives this rank issued since the last reset (rbl_comm_stats): all-reduce
         calls / bytes, halo exchanges, bytes sent / received; and the halo plan of the matrix
         held (not reset): halo_push (the push/pull split runs, RBL_OPT_HALO_PUSH) and the Q rows
-        per SpMM summed over ranks its setup predicted with the split / with the pull-all halo."""
-        out = np.zeros(8, np.int64)
-        self._check(lib.rbl_comm_stats(self._h, i64ptr(out), 8, int(reset)), "rbl_comm_stats")
-        return dict(zip(("allreduce_calls", "allreduce_bytes", "exchange_calls", "send_bytes",
-                         "recv_bytes", "halo_push", "push_rows_pred", "pull_rows_pred"),
-                        (int(x) for x in out)))
+        per SpMM summed over ranks its setup predicted with the split / with the pull-all halo;
+        with times=True also the time in the collectives (ns): host wall time inside the
+        transport calls, and their hipEvent spans on the streams (recorded only while
+        RBL_OPT_TIMERS is 1)."""
+        out = np.zeros(12, np.int64)
+        self._check(lib.rbl_comm_stats(self._h, i64ptr(out), 12, int(reset)), "rbl_comm_stats")
+        keys = ("allreduce_calls", "allreduce_bytes", "exchange_calls", "send_bytes",
+                "recv_bytes", "halo_push", "push_rows_pred", "pull_rows_pred")
+        if times:  # (timings differ run to run: counts-only dicts compare across runs)
+            keys += ("allreduce_host_ns", "exchange_host_ns", "allreduce_dev_ns", "exchange_dev_ns")
+        return dict(zip(keys, (int(x) for x in out)))
 
     def path_stats(self, reset: bool = False) -> dict:
         """Which code path the steps took since the last reset (rbl_path_stats), counted as the
         work is issued: SpMM launches, those that applied the local-reorth update, separate
-        local-reorth passes and Grams, the fused path's edge fix-ups, two-wave SpMM launches."""
+        local-reorth passes and Grams, the fused path's edge fix-ups, two-wave SpMM launches
+        (variants build only), and rbl_ritz calls that took the row-piece form."""
         from . import _lib as L
         out = np.zeros(L.RBL_PATH_NSTATS, np.int64)
         self._check(lib.rbl_path_stats(self._h, i64ptr(out), L.RBL_PATH_NSTATS, int(reset)),
                     "rbl_path_stats")
         return dict(zip(("spmm", "spmm_loc_fused", "loc_separate", "loc_gram", "locfix_edges",
-                         "locfix_rest", "spmm_two_wave"), (int(x) for x in out)))
+                         "locfix_rest", "spmm_two_wave", "ritz_pieces"), (int(x) for x in out)))
+
+    def allgather(self, values) -> np.ndarray:
+        """rbl_allgather_host: every rank's int64 values, shape (nranks, len(values)); ordered
+        after the work enqueued on this context (a collective: every rank calls it)."""
+        mine = np.ascontiguousarray(np.asarray(values, dtype=np.int64).ravel())
+        out = np.zeros(self.nranks * mine.size, np.int64)
+        self._check(lib.rbl_allgather_host(self._h, i64ptr(mine), i64ptr(out), mine.size),
+                    "rbl_allgather_host")
+        return out.reshape(self.nranks, mine.size)
 
     def synchronize(self) -> None:
         self._check(lib.rbl_synchronize(self._h), "rbl_synchronize")
@@ -411,12 +426,19 @@ def lanczos(ctx: Context, k: int, b: int, *, kryl_sz: int = KRYL_SZ_GPU, omega=N
     # extra steps, which is the cost.  speculate="auto" (default) enqueues up to the next check
     # when the residual bounds of the previous two checks, extrapolated geometrically, put this
     # check at least 100x above the tolerance, and one step when they put it above the tolerance
-    # (host.speculation_depth) — a decision every rank makes alike from the same T (the
-    # convergence test itself already relies on that), so ranks issue the same steps.
+    # (host.speculation_depth) — on several ranks agreed once per check together with the
+    # convergence test (rank 0's decisions, below), so ranks issue the same steps.
     # True: as many steps as the eigensolve is expected to last (the previous one scaled by
     # (N/N_prev)^2.7, over the measured time per step; one rank only); an int: a fixed count (tests).
     last_i = min(steps_cap, math.ceil(kryl_sz / b))
     enq = 0
+    # Several ranks: each rank solves the same T band on its own host, and every rank must
+    # enqueue the same steps (their collectives pair up).  So the two decisions a check takes —
+    # converged, and (auto) how far to speculate before the next check — are all-gathered once
+    # per check (rbl_allgather_host) and rank 0's are taken by every rank: eigensolves that
+    # differ in the last bit across ranks (BLAS threading) cannot split the ranks' step counts.
+    multi = ctx.nranks > 1
+    next_depth = 0                                 # agreed auto depth for the next check
 
     def enqueue(upto):
         nonlocal enq
@@ -444,7 +466,7 @@ def lanczos(ctx: Context, k: int, b: int, *, kryl_sz: int = KRYL_SZ_GPU, omega=N
         spec_to = i
         if speculate is not False and is_check and not is_last and i % 2 == 0:
             if speculate == "auto":
-                spec_to = i + speculation_depth(info.resid, tol)
+                spec_to = i + (next_depth if multi else speculation_depth(info.resid, tol))
             elif speculate is True:
                 if ctx.nranks == 1 and last_eig and step_ms:
                     spec_to = i + int(last_eig * (i * b / last_n) ** 2.7 // step_ms)
@@ -473,7 +495,12 @@ def lanczos(ctx: Context, k: int, b: int, *, kryl_sz: int = KRYL_SZ_GPU, omega=N
                 last_eig, last_n = dt * 1e3, i * b
                 res = residual_norms(Bj, S, b, k)
                 info.resid.append(float(res.max()) if res.size else 0.0)
-                if bool(np.all(res <= tol)):               # :189 (check_convergence)
+                conv = bool(np.all(res <= tol))            # :189 (check_convergence)
+                if multi:
+                    depth = speculation_depth(info.resid, tol) if speculate == "auto" else 0
+                    agreed = ctx.allgather([int(conv), depth])[0]   # rank 0's decisions
+                    conv, next_depth = bool(agreed[0]), int(agreed[1])
+                if conv:
                     info.converged = True
                     info.spec_wasted += spec_to - i
                     break

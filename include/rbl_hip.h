@@ -135,6 +135,11 @@ extern "C" {
 typedef struct rbl_ctx rbl_ctx;
 
 int rbl_abi_version(void);
+/* How this copy of the library was built: RBL_BUILD_VARIANTS set when it was compiled with
+ * -DRBL_VARIANTS (tools/build_variant.sh: the measured-and-rejected kernel variants and their
+ * A/B switches, for diagnostics only; the product build leaves them out). */
+#define RBL_BUILD_VARIANTS 1
+int rbl_build_flags(void);
 
 /* ---- context ------------------------------------------------------------------------
  * Replaces the implicit CUDA.jl device state of RBL_gpu.jl:1-6. */
@@ -331,7 +336,22 @@ int rbl_synchronize(rbl_ctx* ctx);
 #define RBL_COMM_HALO_PUSH       5
 #define RBL_COMM_PUSH_ROWS       6
 #define RBL_COMM_PULL_ROWS       7
+/* time in the collectives since the last reset, ns: host wall time inside the transport's calls
+ * (all-reduces / halo exchanges; RCCL only enqueues, the shm and in-process stand-ins block),
+ * and the hipEvent span each call holds its stream — the wait for the slowest peer included —
+ * summed (recorded only while RBL_OPT_TIMERS is 1) */
+#define RBL_COMM_ALLREDUCE_HOST_NS 8
+#define RBL_COMM_EXCHANGE_HOST_NS  9
+#define RBL_COMM_ALLREDUCE_DEV_NS  10
+#define RBL_COMM_EXCHANGE_DEV_NS   11
 int rbl_comm_stats(rbl_ctx* ctx, int64_t* out, int nstats, int reset);
+
+/* All-gather of n int64 per rank from host memory: all[p*n + i] = rank p's mine[i] (one rank: a
+ * copy).  A collective, ordered after the work already enqueued on the context (the host waits
+ * for it).  The host loop uses it to take one decision for every rank — the convergence test
+ * and the speculation depth of the next check (rbl.lanczos) — so that ranks whose host
+ * eigensolves differ in the last bit still enqueue the same steps and collectives. */
+int rbl_allgather_host(rbl_ctx* ctx, const int64_t* mine, int64_t* all, int n);
 
 /* Which code path the block steps took, counted as the work is issued (since the last reset;
  * nstats entries, missing ones 0).  Stage timers cannot show this when ranks share a GPU (a
@@ -342,8 +362,11 @@ int rbl_comm_stats(rbl_ctx* ctx, int64_t* out, int nstats, int reset);
 #define RBL_PATH_LOC_GRAM        3  /* local-reorth Grams not formed by the producing pass     */
 #define RBL_PATH_LOCFIX_EDGES    4  /* rank-edge rows corrected before the halo exchange       */
 #define RBL_PATH_LOCFIX_REST     5  /* range-edge rows corrected after a fused SpMM            */
-#define RBL_PATH_SPMM_TWO_WAVE   6  /* SpMM launches served by the two-waves-per-SIMD kernel   */
-#define RBL_PATH_NSTATS          7
+#define RBL_PATH_SPMM_TWO_WAVE   6  /* SpMM launches served by the two-waves-per-SIMD kernel
+                                       (variants build only; 0 in the product library)        */
+#define RBL_PATH_RITZ_PIECES     7  /* rbl_ritz calls that formed V in row pieces on the side
+                                       stream with the staged D2H behind them                  */
+#define RBL_PATH_NSTATS          8
 int rbl_path_stats(rbl_ctx* ctx, int64_t* out, int nstats, int reset);
 
 /* ---- host-only planning (callable without a GPU) -------------------------------------- */

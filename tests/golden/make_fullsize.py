@@ -29,7 +29,10 @@ Fixtures are data only: the generator parameters, Omega's seed, and the outputs.
 
 Each holds D (k, descending |lambda|), the iteration count, and per Ritz vector its 16
 largest-magnitude entries (row ids + values) — enough to compare vectors up to sign without
-storing n x k numbers — and the residual norms ||A v - lambda v|| / |lambda|.
+storing n x k numbers — the residual norms ||A v - lambda v|| / |lambda|, and the per-step
+block trace (trace_A[i] = A_{i+1}, trace_B[i] = B_{i+2}: RBL_gpu.jl:153-161 then :176-184 of
+every loop step), so the block-step semantics are pinned at full size, not only their end
+product (round 6 regenerated c4a and c4b_full with the traces; D and iters are unchanged).
 """
 import os
 import sys
@@ -138,7 +141,7 @@ def omega_for(cfg):
 def run(name, cfg, A, reorth_mode="cgs"):
     t0 = time.perf_counter()
     res = o.RBL_gpu_semantics(A, cfg["k"], cfg["b"], omega=omega_for(cfg), qr_mode="posdiag",
-                              reorth_mode=reorth_mode)
+                              reorth_mode=reorth_mode, trace=True)
     dt = time.perf_counter() - t0
     assert res.converged, name
     V = res.V
@@ -151,6 +154,9 @@ def run(name, cfg, A, reorth_mode="cgs"):
     np.savez_compressed(out, D=res.D, iters=res.iters, top_idx=idx.astype(np.int64), top_val=vals,
                         residual=r, nnz=A.nnz, oracle_seconds=dt, peak_rss_gb=peak_rss_gb,
                         reorth_mode=reorth_mode,
+                        # per block step i (rbl_start's step 1 first): A_i and B_{i+1}, b x b each
+                        # (positive-diagonal R, so B needs no sign normalisation)
+                        trace_A=np.array(res.trace["A"]), trace_B=np.array(res.trace["B"]),
                         **{f"cfg_{key}": v for key, v in cfg.items()})
     print(f"{name}: n={A.shape[0]} nnz={A.nnz} iters={res.iters} D[:3]={res.D[:3]} "
           f"max residual={r.max():.2e} ({dt:.1f} s, peak RSS {peak_rss_gb:.1f} GB) -> {out}",

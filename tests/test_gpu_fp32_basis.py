@@ -174,37 +174,6 @@ def test_fp32_basis_tiny_slices(rbl):
             assert np.abs(a - a1).max() <= 1e-5 * np.abs(a1).max()
 
 
-@pytest.mark.parametrize("dense", [False, True])
-def test_fp32_local_reorth_row_kernel_matches_tile_kernel(rbl, dense, monkeypatch):
-    """b = 32: the fp32 local reorth runs its Gram on four waves per split (k_gram32_one) and
-    its update as a row-streaming kernel (k_upd32_rows, k_tsmm32's MFMA k order);
-    RBL_LOC32_MFMA=1 restores both tile kernels.  Traces and every basis block agree to fp32
-    rounding (the Gram's per-split sum order differs)."""
-    b, steps = 32, 8
-    A = (matgen.hashwindow_csr(6000, 64, 0.7734, 7, matgen.planted_spectrum(10)) if dense
-         else c1_matrix(5000, 10))
-    n = A.shape[0]
-    omega = np.random.default_rng(11).standard_normal((n, b))
-    out = []
-    for tile in (False, True):
-        if tile:
-            monkeypatch.setenv("RBL_LOC32_MFMA", "1")
-        else:
-            monkeypatch.delenv("RBL_LOC32_MFMA", raising=False)
-        with rbl.Context(0) as ctx:
-            ctx.set_matrix(A)
-            _, _, info = rbl.lanczos(ctx, 10, b, omega=omega, check=False, max_steps=steps,
-                                     trace=True, ritz=False, basis_bits=32)
-            out.append((info, [ctx.get_block(j) for j in range(1, steps + 1)]))
-    anorm = abs(A).sum(axis=0).max()
-    (i1, q1), (i2, q2) = out
-    for a1, a2 in zip(i1.trace_A + i1.trace_B, i2.trace_A + i2.trace_B):
-        assert np.abs(a1 - a2).max() <= STEP_TOL * anorm
-    for x, y in zip(q1, q2):
-        assert np.abs(x - y).max() <= 1e-5
-    print("bit-identical blocks:", sum(np.array_equal(x, y) for x, y in zip(q1, q2)), "of", steps)
-
-
 KNOWN_TOL_MIXED = 1e-7   # relative error norm; the fp64 path meets the reference's 1e-13
 
 

@@ -4,9 +4,10 @@ k = 20 — the bench workload).
 Against the oracle at full size: tests/golden/make_fullsize.py ran the oracle (the CPU
 restatement of RBL.jl with the GPU driver's bounds) on this very matrix offline, in the build
 container (873 s, 44.7 GB peak RSS, block CGS evaluated block by block), and committed
-golden_c4a.npz.  test_c4a_full_size_vs_oracle feeds the fixture's Omega and checks the step
-count, the eigenvalues (< 1e-10 relative) and each Ritz vector's 16 largest entries (1e-6, up
-to sign).
+golden_c4a.npz (round 6: regenerated with the per-step traces, 617 s; D unchanged).
+test_c4a_full_size_vs_oracle feeds the fixture's Omega and checks the step count, every
+step's A_i and B_{i+1} (relative 1e-8), the eigenvalues (< 1e-10 relative) and each Ritz
+vector's 16 largest entries (1e-6, up to sign).
 
 Beside it, size-independent properties:
 
@@ -126,10 +127,19 @@ def test_c4a_full_size_vs_oracle(full):
         (N, HALFWIDTH, DENSITY, SEED, B, K)
     assert A.nnz == int(g["nnz"])
     omega = np.random.default_rng(cfg["omega_seed"]).standard_normal((N, B))
-    D, V, info = rbl.lanczos(ctx, K, B, omega=omega)
+    D, V, info = rbl.lanczos(ctx, K, B, omega=omega, trace=True)
     del omega
     print(f"[fullsize] vs oracle: {info.iters} steps {time.perf_counter() - T0:.1f} s", flush=True)
     assert info.converged and info.iters == int(g["iters"])
+    # the block-step semantics at full size (RBL_gpu.jl:153-161, 176-184): every step's A_i and
+    # B_{i+1} against the oracle's, relative 1e-8 of the block's largest entry (as the small-n
+    # trace tests); positive-diagonal R on both sides, so no sign normalisation
+    tA, tB = g["trace_A"], g["trace_B"]
+    assert len(info.trace_A) == len(info.trace_B) == tA.shape[0] == tB.shape[0] == info.iters
+    for i in range(info.iters):
+        da = np.abs(info.trace_A[i] - tA[i]).max() / np.abs(tA[i]).max()
+        db = np.abs(info.trace_B[i] - tB[i]).max() / np.abs(tB[i]).max()
+        assert da < 1e-8 and db < 1e-8, (i, da, db)
     rel = np.abs(D - g["D"]) / np.abs(g["D"])
     assert rel.max() < 1e-10, rel
     idx, val = g["top_idx"], g["top_val"]

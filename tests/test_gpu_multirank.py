@@ -182,11 +182,10 @@ def test_multirank_local_reorth_fused_into_spmm(rbl, P, n, W):
             assert d < 1e-12, d
 
 
-@pytest.mark.parametrize("bt2", ["0", "1"])
 @pytest.mark.parametrize("P", [1, 2])
-def test_multirank_fused_local_reorth_runs(rbl, monkeypatch, P, bt2):
-    """The fused path really replaces the separate pass on 1 and 2 ranks, with the one-wave
-    band-tile SpMM (RBL_BT2=0, default) and the two-waves-per-SIMD one (RBL_BT2=1).  Asserted on
+def test_multirank_fused_local_reorth_runs(rbl, P):
+    """The fused path really replaces the separate pass on 1 and 2 ranks (the one-wave band-tile
+    SpMM; the two-waves-per-SIMD form is a variants-build kernel: test_gpu_variants).  Asserted on
     the library's path counters (rbl_path_stats), not on stage times: with both ranks on one GPU
     a stage's events also span the other rank's kernels (round 4's RBL_BT2=1 run measured rank
     0's loc-reorth stage at 2.65 ms fused against 1.46 ms separate — about one of rank 1's SpMM
@@ -195,7 +194,6 @@ def test_multirank_fused_local_reorth_runs(rbl, monkeypatch, P, bt2):
     i = 2 on applies the update inside the SpMM, fixes the range edges after it (and on several
     ranks the rank edges before the exchange), and runs no separate pass; unfused (3): a
     separate pass per step and no fused SpMM.  Both give the same A_i / B_{i+1} to 1e-12."""
-    monkeypatch.setenv("RBL_BT2", bt2)
     n, W, k, b, steps = 2_000_000, 64, 10, 32, 8
     plant = matgen.planted_spectrum(k)
 
@@ -222,35 +220,9 @@ def test_multirank_fused_local_reorth_runs(rbl, monkeypatch, P, bt2):
         assert p7["locfix_edges"] == (loc_steps if P > 1 else 0)
         assert p3["spmm_loc_fused"] == 0 and p3["loc_separate"] == loc_steps
         assert p3["locfix_rest"] == p3["locfix_edges"] == 0
-        if bt2 == "1":   # every step launch (EPI + A_i partials) on the two-wave kernel
-            assert p7["spmm_two_wave"] >= loc_steps and p3["spmm_two_wave"] >= loc_steps
-        else:
-            assert p7["spmm_two_wave"] == p3["spmm_two_wave"] == 0
+        assert p7["spmm_two_wave"] == p3["spmm_two_wave"] == 0
         for a, a1 in zip(i7.trace_A + i7.trace_B, i3.trace_A + i3.trace_B):
             assert np.abs(a - a1).max() <= 1e-12 * np.abs(a1).max()
-
-
-def test_multirank_half_band_tiles_bit_identical(rbl, monkeypatch):
-    """Half band tiles on 3 ranks (each rank's first NGL tiles whole, their left groups reach
-    into the previous rank's rows) against whole tiles: A_i / B_{i+1} bit for bit."""
-    n, W, p, seed, k, b = 30001, 64, 0.7734, 23, 10, 32
-    plant = matgen.planted_spectrum(k)
-
-    def run(half):
-        monkeypatch.setenv("RBL_BT_HALF", half)
-
-        def fn(ctx, r):
-            ctx.gen_hashwindow(n, W, p, seed, plant)
-            assert ctx.matrix_format() == (3 if half == "1" else 1)
-            _, _, info = rbl.lanczos(ctx, k, b, seed=3, check=False, max_steps=10, trace=True,
-                                     ritz=False)
-            return info
-        return run_ranks(rbl, 3, fn)
-
-    h, w = run("1"), run("0")
-    for ih, iw in zip(h, w):
-        for a, a1 in zip(ih.trace_A + ih.trace_B, iw.trace_A + iw.trace_B):
-            assert np.array_equal(a, a1)
 
 
 def test_multirank_tiny_slices(rbl):

@@ -373,62 +373,6 @@ def test_speculative_steps_change_nothing(rbl, case):
         assert all(np.array_equal(a, c) for a, c in zip(i0.trace_B, i1.trace_B))
 
 
-@pytest.mark.parametrize("b,bits", [(16, 64), (32, 64), (32, 32)])
-def test_cholqr_register_kernel_bit_identical(rbl, monkeypatch, b, bits):
-    """The one-wave register Cholesky (k_chol_reg, b = 16 / 32) against the four-wave LDS kernel
-    (RBL_CHOL_REG=0): the same R, R^-1 and Rtot, so 12-step A_i / B_{i+1} traces are bit-identical
-    — on the C1-like matrix and through Krylov exhaustion (the reference's slow-decay matrix at
-    n = 9 b: the last step factors a numerically zero block, the shifted / zero paths)."""
-    A1 = c1_matrix(4000, 10)
-    A2, _ = o.slow_decay_matrix(9 * b, 5)
-    for A, steps in ((A1, 12), (A2, 9)):
-        n = A.shape[0]
-        omega = np.random.default_rng(b).standard_normal((n, b))
-        out = {}
-        for reg in ("0", "1"):
-            monkeypatch.setenv("RBL_CHOL_REG", reg)
-            with rbl.Context(0) as ctx:
-                ctx.set_matrix(A)
-                _, _, info = rbl.lanczos(ctx, 5, b, omega=omega, check=False, max_steps=steps,
-                                         trace=True, ritz=False, basis_bits=bits)
-            out[reg] = (np.array(info.trace_A), np.array(info.trace_B))
-        assert np.array_equal(out["0"][0], out["1"][0]) and np.array_equal(out["0"][1], out["1"][1])
-
-
-@pytest.mark.parametrize("b,bits", [(16, 64), (32, 64), (32, 32)])
-def test_cholqr_elimination_kernel(rbl, monkeypatch, b, bits):
-    """The one-wave Cholesky that forms R^-1 in the factorisation's own sweep (k_chol_elim2, the
-    default RBL_CHOL_REG=2): R and Rtot as the other kernels, R^-1 by forward elimination instead
-    of back substitution — 12-step A_i / B_{i+1} traces within 1e-12 of the four-wave kernel's on
-    the C1-like matrix and through Krylov exhaustion, and the reference's known-answer suites on
-    it (b = 16 / 32: moderate and slow decay at n = 300, k = 5) within the suites' 1e-13.  The
-    form on both halves of the wave (2) and on one half (k_chol_elim, 3): the same bits."""
-    A1 = c1_matrix(4000, 10)
-    A2, _ = o.slow_decay_matrix(9 * b, 5)
-    for A, steps in ((A1, 12), (A2, 9)):
-        n = A.shape[0]
-        omega = np.random.default_rng(b).standard_normal((n, b))
-        out = {}
-        for reg in ("0", "2", "3"):
-            monkeypatch.setenv("RBL_CHOL_REG", reg)
-            with rbl.Context(0) as ctx:
-                ctx.set_matrix(A)
-                _, _, info = rbl.lanczos(ctx, 5, b, omega=omega, check=False, max_steps=steps,
-                                         trace=True, ritz=False, basis_bits=bits)
-            out[reg] = (np.array(info.trace_A), np.array(info.trace_B))
-        assert np.array_equal(out["2"][0], out["3"][0]) and np.array_equal(out["2"][1], out["3"][1])
-        for t in (0, 1):
-            scale = np.abs(out["0"][t]).max()
-            d = np.abs(out["2"][t] - out["0"][t]).max() / scale
-            assert d < 1e-12, (t, d)
-    if bits == 64:
-        monkeypatch.setenv("RBL_CHOL_REG", "2")
-        for gen in (o.moderate_decay_matrix, o.slow_decay_matrix):
-            A, eig = gen(300, 5)
-            D, V, info = rbl.RBL_gpu(A, 5, b, seed=3, return_info=True)
-            assert info.converged and np.linalg.norm((D - eig) / eig) < o.KNOWN_ANSWER_TOL
-
-
 @pytest.mark.parametrize("b", [16, 32])
 def test_local_reorth_gram_after_shifted_third_pass(rbl, monkeypatch, b):
     """The next step's local-reorth Gram formed inside the QR (RBL_OPT_FUSE bit 1) when CholQR
@@ -469,60 +413,52 @@ def test_local_reorth_gram_after_shifted_third_pass(rbl, monkeypatch, b):
     assert e3n > 1e3 * e3
 
 
-def test_latency_knobs_agree(rbl, monkeypatch):
-    """The A/B switches of round 5's latency work: RBL_STASH_COPY=1 (a device record and one D2H
-    copy instead of k_stash writing pinned memory) gives the same bits; RBL_REDUCE_NARROW=1 and
-    RBL_RED_CHUNK=0 (the earlier Gram-partial reductions: other summation trees) the same A_i /
-    B_{i+1} to 1e-12 — at n = 40,000, where the b x b Grams have > 64 partials (k_reduce_wide) and
-    the update's local-reorth Gram one per 128 rows (chunked levels)."""
-    A = c1_matrix(40000, 10)
-    b = 32
-    omega = np.random.default_rng(4).standard_normal((A.shape[0], b))
 
-    def run():
-        with rbl.Context(0) as ctx:
-            ctx.set_matrix(A)
-            _, _, info = rbl.lanczos(ctx, 10, b, omega=omega, check=False, max_steps=12,
-                                     trace=True, ritz=False)
-        return np.array(info.trace_A), np.array(info.trace_B)
-
-    ref = run()
-    for knob, exact in (("RBL_STASH_COPY", True), ("RBL_REDUCE_NARROW", False), ("RBL_RED_CHUNK", False)):
-        monkeypatch.setenv(knob, "0" if knob == "RBL_RED_CHUNK" else "1")
-        out = run()
-        monkeypatch.delenv(knob)
-        for t in (0, 1):
-            if exact:
-                assert np.array_equal(out[t], ref[t]), knob
-            else:
-                d = np.abs(out[t] - ref[t]).max() / np.abs(ref[t]).max()
-                assert d < 1e-12, (knob, t, d)
+@pytest.mark.parametrize("b", [16, 32])
+def test_cholqr_default_kernel_known_answers(rbl, b):
+    """The product's CholQR small part (k_chol_elim2 at b = 16 / 32: R^-1 formed in the
+    factorisation's own sweep) on the reference's known-answer suites (moderate and slow decay,
+    n = 300, k = 5) within the suites' 1e-13 (test.jl:16-50), and through Krylov exhaustion (the
+    slow-decay matrix at n = 9 b: the last step factors a numerically zero block, the shifted /
+    zero paths) with finite A_i / B_{i+1}.  Its bit identity with the other Cholesky
+    kernels is a variants-build test (test_gpu_variants)."""
+    for gen in (o.moderate_decay_matrix, o.slow_decay_matrix):
+        A, eig = gen(300, 5)
+        D, V, info = rbl.RBL_gpu(A, 5, b, seed=3, return_info=True)
+        assert info.converged and np.linalg.norm((D - eig) / eig) < o.KNOWN_ANSWER_TOL
+    A, _ = o.slow_decay_matrix(9 * b, 5)
+    omega = np.random.default_rng(b).standard_normal((9 * b, b))
+    with rbl.Context(0) as ctx:
+        ctx.set_matrix(A)
+        _, _, info = rbl.lanczos(ctx, 5, b, omega=omega, check=False, max_steps=9, trace=True,
+                                 ritz=False)
+    assert len(info.trace_A) == 9
+    assert all(np.all(np.isfinite(t)) for t in info.trace_A + info.trace_B)
 
 
 @pytest.mark.parametrize("bits", [64, 32])
-def test_ritz_pipelined_matches_one_pass(rbl, monkeypatch, capfd, bits):
-    """rbl_ritz's pipelined form (the combination in 8 row pieces on a side stream, the staged D2H
-    behind them on the context's stream; RBL_gpu.jl:106-132 / :219) returns the one-pass form's
-    V bit for bit, at a size where it applies (n_local x k x 8 B >= 256 MiB), and takes that path
-    (RBL_RITZ_TRACE); a second run on the same context then gives the same D and V again (the side
-    stream's use of the run scratch is ordered before the next run's steps).  Both bases: fp64, and
-    the fp32 Krylov basis (FLOAT = Float32) whose combination widens on load."""
+def test_ritz_row_pieces(rbl, bits):
+    """rbl_ritz at a size where its row-piece form applies (n_local x k x 8 B >= 256 MiB: the
+    combination V = [Q] S in 8 row pieces on a side stream with the staged D2H behind them;
+    RBL_gpu.jl:106-132 / :219) takes that path (rbl_path_stats' ritz_pieces), returns Ritz
+    pairs with residual ||A v - lambda v|| / |lambda| < 1e-7 (1e-5 with the fp32 basis) and
+    orthonormal vectors, and two more runs on the same context return the same D and V bit for
+    bit (the side stream's use of the run scratch is ordered before the next run's steps)."""
+    import scipy.sparse as sp
     n, b, k = 2_000_000, 32, 20
-    monkeypatch.setenv("RBL_RITZ_TRACE", "1")
     out = []
     with rbl.Context(0) as ctx:
         ctx.gen_hashwindow(n, 64, 0.7734, 5, matgen.planted_spectrum(k))
-        for serial in ("1", None, None):
-            if serial:
-                monkeypatch.setenv("RBL_RITZ_SERIAL", serial)
-            else:
-                monkeypatch.delenv("RBL_RITZ_SERIAL", raising=False)
-            capfd.readouterr()
+        rowptr, col, val = ctx.get_matrix_csr()
+        A = sp.csr_matrix((val, col, rowptr.astype(np.int32)), shape=(n, n))
+        for _ in range(3):
+            ctx.path_stats(reset=True)
             D, V, info = rbl.lanczos(ctx, k, b, seed=2, basis_bits=bits)
-            err = capfd.readouterr().err
-            assert info.converged and ("pipelined" in err) == (serial is None), err
+            assert info.converged and ctx.path_stats()["ritz_pieces"] == 1
             out.append((D, V))
-    (D0, V0) = out[0]
+    D0, V0 = out[0]
+    res = np.linalg.norm(A @ V0 - V0 * D0, axis=0) / np.abs(D0)
+    assert res.max() < (RES_TOL if bits == 64 else 1e-5), res
+    assert np.abs(V0.T @ V0 - np.eye(k)).max() < 1e-9
     for D1, V1 in out[1:]:
-        assert V1.shape == (n, k) and np.array_equal(D0, D1)
-        assert np.array_equal(V0, V1), np.abs(V0 - V1).max()
+        assert np.array_equal(D0, D1) and np.array_equal(V0, V1)

@@ -115,34 +115,6 @@ def test_rmat_multirank_lanczos(rbl):
             assert np.abs(bb - bb1).max() <= 1e-9 * np.abs(bb1).max()
 
 
-@pytest.mark.parametrize("tiers", ["64", "64,1024"])
-def test_rmat_column_tiers(rbl, tiers, monkeypatch):
-    """Column-tiered segmented gather (RBL_SEG_TIERS: the highest-degree columns swept first,
-    each tier its own CSR + task table, accumulated into U): the SpMM within 1e-13 |A||X| of
-    SciPy, and a fixed-step Lanczos trace equal to the one-sweep kernel's to 1e-12 (only each
-    row's sum order differs)."""
-    A = matgen.rmat_csr(CASE["n"], CASE["scale"], CASE["edges"], CASE["seed"],
-                        matgen.planted_spectrum(5))
-    X = np.random.default_rng(11).standard_normal((A.shape[0], 32))
-    infos = []
-    for env in (None, tiers):
-        if env is None:
-            monkeypatch.delenv("RBL_SEG_TIERS", raising=False)
-        else:
-            monkeypatch.setenv("RBL_SEG_TIERS", env)
-        with rbl.Context(0) as ctx:
-            ctx.gen_rmat(CASE["n"], CASE["scale"], CASE["edges"], CASE["seed"],
-                         matgen.planted_spectrum(5))
-            Y = ctx.apply(X)
-            _, _, info = rbl.lanczos(ctx, 5, 32, seed=9, check=False, max_steps=8, trace=True,
-                                     ritz=False)
-            infos.append(info)
-        bound = (abs(A) @ np.abs(X)) * 1e-13 + 1e-300
-        assert np.all(np.abs(Y - A @ X) <= bound)
-    for a0, a1 in zip(infos[0].trace_A, infos[1].trace_A):
-        assert np.abs(a0 - a1).max() <= 1e-12 * np.abs(a0).max()
-
-
 @pytest.mark.parametrize("P", [2, 3])
 def test_rmat_multirank_halo_overlap_bit_identical(rbl, P):
     """Several ranks on an unbanded matrix: each rank's SpMM runs as two column tiers, the own

@@ -128,10 +128,19 @@ def test_c4b_full_size_vs_oracle(full):
     assert (cfg["n"], cfg["scale"], cfg["edges"], cfg["seed"], cfg["b"], cfg["k"]) == (N, SCALE, EDGES, SEED, B, K)
     assert A.nnz == int(g["nnz"])
     omega = np.random.default_rng(cfg["omega_seed"]).standard_normal((N, B))
-    D, V, info = rbl.lanczos(ctx, K, B, omega=omega)
+    D, V, info = rbl.lanczos(ctx, K, B, omega=omega, trace=True)
     del omega
     _log(f"vs oracle: {info.iters} steps")
     assert info.converged and info.iters == int(g["iters"])
+    # the block-step semantics at full size (RBL_gpu.jl:153-161, 176-184): every step's A_i and
+    # B_{i+1} against the oracle's, relative 1e-8 of the block's largest entry (as the small-n
+    # trace tests); positive-diagonal R on both sides, so no sign normalisation
+    tA, tB = g["trace_A"], g["trace_B"]
+    assert len(info.trace_A) == len(info.trace_B) == tA.shape[0] == tB.shape[0] == info.iters
+    for i in range(info.iters):
+        da = np.abs(info.trace_A[i] - tA[i]).max() / np.abs(tA[i]).max()
+        db = np.abs(info.trace_B[i] - tB[i]).max() / np.abs(tB[i]).max()
+        assert da < 1e-8 and db < 1e-8, (i, da, db)
     rel = np.abs(D - g["D"]) / np.abs(g["D"])
     assert rel.max() < 1e-10, rel
     idx, val = g["top_idx"], g["top_val"]

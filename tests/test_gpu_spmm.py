@@ -131,74 +131,6 @@ def test_spmm_band_tiles(rbl, n, W, p, ng, b):
 
 
 @pytest.mark.parametrize("b", [16, 32])
-@pytest.mark.parametrize("n,W,p", [(7000, 64, 0.7734), (5003, 30, 0.9), (300, 60, 1.0), (100, 30, 0.95)])
-def test_spmm_band_tiles_packed_bit_identical(rbl, monkeypatch, n, W, p, b):
-    """Packed band tiles (zeros dropped, RBL_BT_PACK=1) against the dense tiles (the
-    default): the MFMA operands are the same values, so U and every Lanczos block A_i
-    (fused epilogue + A_i partials) must agree bit for bit."""
-    A = matgen.hashwindow_csr(n, W, p, n + 11)
-    X = np.random.default_rng(n + 1).standard_normal((n, b))
-    out = []
-    monkeypatch.setenv("RBL_BT2", "0")  # packed tiles run k_spmm_bt only: compare like with like
-    for pack in ("0", "1"):
-        monkeypatch.setenv("RBL_BT_PACK", pack)
-        with rbl.Context(0) as ctx:
-            ctx.set_matrix(A)
-            assert ctx.spmm_kernel_for(b) == 5
-            Y = ctx.apply(X)
-            _, _, info = rbl.lanczos(ctx, 4, b, seed=2, check=False, max_steps=4, trace=True,
-                                     ritz=False)
-        out.append((Y, info.trace_A))
-    _check(A, out[1][0], X)
-    assert np.array_equal(out[0][0], out[1][0])
-    for a0, a1 in zip(out[0][1], out[1][1]):
-        assert np.array_equal(a0, a1)
-
-
-@pytest.mark.parametrize("n,W,b,bits", [(50003, 64, 32, 64), (20001, 32, 32, 64),
-                                         (30000, 64, 16, 64), (12345, 32, 16, 64),
-                                         (40000, 64, 32, 32), (300, 32, 16, 64)])
-def test_spmm_half_band_tiles_bit_identical(rbl, monkeypatch, n, W, b, bits):
-    """Half band tiles (A symmetric: diagonal block + right strip stored, the left groups
-    transposed back in the kernel from the previous tiles' strips) against the whole tiles
-    (RBL_BT_HALF=0): the MFMA operands are the same values in the same order, so U, every
-    Lanczos A_i / B_{i+1} (fused epilogue, A_i partials, fused local reorth, fp32 basis) and
-    the Ritz pairs agree bit for bit.  n = 300: a single workgroup range."""
-    plant = matgen.planted_spectrum(5)
-    A = matgen.hashwindow_csr(n, W, 0.7734, n + 5, plant)
-    X = np.random.default_rng(n + 2).standard_normal((n, b))
-    out = []
-    for half in ("0", "1"):
-        monkeypatch.setenv("RBL_BT_HALF", half)  # opt-in format
-        with rbl.Context(0) as ctx:
-            ctx.set_matrix(A)
-            assert ctx.spmm_kernel_for(b) == 5
-            assert ctx.matrix_format() == (3 if half == "1" else 1)
-            Y = ctx.apply(X)
-            D, V, info = rbl.lanczos(ctx, 5, b, seed=2, check=False, max_steps=min(8, n // b),
-                                     trace=True, basis_bits=bits)
-        out.append((Y, info, D, V))
-    _check(A, out[1][0], X)
-    assert np.array_equal(out[0][0], out[1][0])
-    for a0, a1 in zip(out[0][1].trace_A + out[0][1].trace_B, out[1][1].trace_A + out[1][1].trace_B):
-        assert np.array_equal(a0, a1)
-    assert np.array_equal(out[0][2], out[1][2]) and np.array_equal(out[0][3], out[1][3])
-
-
-def test_spmm_half_band_tiles_need_exact_symmetry(rbl, monkeypatch):
-    """One nonzero whose mirror differs in the last bit keeps the whole tiles (format 1)."""
-    monkeypatch.setenv("RBL_BT_HALF", "1")
-    A = matgen.hashwindow_csr(5000, 64, 0.7734, 3).tolil()
-    A[100, 140] = np.nextafter(A[140, 100], np.inf) if A[140, 100] != 0 else 1.0
-    A = sp.csr_matrix(A)
-    with rbl.Context(0) as ctx:
-        ctx.set_matrix(A)
-        assert ctx.spmm_kernel_for(32) == 5 and ctx.matrix_format() == 1
-        X = np.random.default_rng(0).standard_normal((5000, 32))
-        _check(A, ctx.apply(X), X)
-
-
-@pytest.mark.parametrize("b", [16, 32])
 @pytest.mark.parametrize("variant", [0, 6])
 def test_spmm_segmented_long_rows(rbl, b, variant):
     """Segmented gather (kernel id 6): an arrow matrix whose 3 hub rows/columns
@@ -240,28 +172,3 @@ def test_spmm_segmented_and_gather_agree_in_lanczos(rbl):
     for a1, a2 in zip(out[0].trace_A, out[1].trace_A):
         assert np.abs(a1 - a2).max() <= 1e-12 * np.abs(a1).max()
 
-
-@pytest.mark.parametrize("n,W,half,fuse", [(50003, 64, "0", 7), (50003, 64, "1", 7), (20001, 32, "0", 7),
-                                           (20001, 32, "1", 3), (300, 64, "0", 7), (4099, 64, "1", 3)])
-def test_spmm_band_tiles_two_waves_per_simd(rbl, monkeypatch, n, W, half, fuse):
-    """k_spmm_bt2 (RBL_BT2=1: eight waves share the Q ring, waves p and p + 4 of a SIMD split a
-    tile's band groups) against k_spmm_bt: the same products, the group sum associated as (left
-    groups) + (the rest), so per-step A_i / B_{i+1} agree to 1e-12 relative over a 10-step
-    Lanczos run (fused 3-term epilogue, A_i partials, with and without the fused local
-    reorth); whole and half tiles; H = 32 and 64; a matrix smaller than one round (its run kept
-    well short of Krylov exhaustion, where the trace amplifies rounding)."""
-    plant = matgen.planted_spectrum(5)
-    A = matgen.hashwindow_csr(n, W, 0.7734, n + 9, plant)
-    monkeypatch.setenv("RBL_BT_HALF", half)
-    runs = []
-    for v in ("0", "1"):
-        monkeypatch.setenv("RBL_BT2", v)
-        with rbl.Context(0) as ctx:
-            ctx.set_option(rbl._lib.RBL_OPT_FUSE, fuse)
-            ctx.set_matrix(A)
-            assert ctx.spmm_kernel_for(32) == 5
-            _, _, info = rbl.lanczos(ctx, 5, 32, seed=4, check=False, max_steps=min(10, n // 64),
-                                     trace=True, ritz=False)
-        runs.append(info)
-    for a0, a1 in zip(runs[0].trace_A + runs[0].trace_B, runs[1].trace_A + runs[1].trace_B):
-        assert np.abs(a0 - a1).max() <= 1e-12 * np.abs(a0).max()
