@@ -359,7 +359,7 @@ def measure(ctx, args, matrix, K, W, nloc, nnz_loc, world, barrier, allmax, gath
     spmm_kid = ctx.spmm_kernel_for(b)
     mat_fmt = ctx.matrix_format()
     spmm_kernel = {1: "gather", 2: "lds-window", 3: "lds-band-mfma", 5: "band-tile-mfma",
-                   6: "segmented-gather"}[spmm_kid]
+                   6: "segmented-gather", 7: "column-panel-csr"}[spmm_kid]
 
     host = {"start": 0.0, "enqueue": 0.0, "fetch_wait": 0.0}
 

@@ -40,6 +40,10 @@ struct rbl_ctx {
   int64_t* d_tcmin = nullptr;
   int64_t* d_tcmax = nullptr;
   int64_t* d_tinfo = nullptr;
+  // column-panel SpMM (spmm_panel.hip): per 256-row block its first and last 256-row Q panel
+  int32_t* d_panel_blk = nullptr;
+  int64_t panel_nblk = 0;
+  bool panel_auto = false;  // chosen by default: every staged Q row used >= 4 times on average
   uint16_t* d_bpos = nullptr;  // band kernel: per-nonzero dense-tile positions
   double* d_bt = nullptr;      // band-tile kernel: the CSR in MFMA-ordered 16-row band tiles
   int bt_ng = 0;               // its band groups (0: not applicable)
@@ -316,6 +320,10 @@ CsrDev csr(rbl_ctx* ctx) {
   A.tile_cmin = ctx->d_tcmin;
   A.tile_cmax = ctx->d_tcmax;
   A.tile_info = ctx->d_tinfo;
+  // (the indexed halo's buffer holds ghost slots, not a row range: the panels need the range)
+  A.panel_blk = ctx->ghost ? nullptr : ctx->d_panel_blk;
+  A.panel_nblk = ctx->ghost ? 0 : ctx->panel_nblk;
+  A.panel_auto = ctx->panel_auto;
   A.ntiles = ctx->ntiles;
   A.tiles_per_wg = ctx->tiles_per_wg;
   A.window_ok16 = ctx->window_ok16;
@@ -756,11 +764,12 @@ int prepare_tiers(rbl_ctx* ctx, const std::vector<int64_t>& rp) {
     // part in build_ghosts (with no requests), and a rank that released its CSR for band tiles
     // (RBL_OPT_KEEP_CSR = 0) votes banded, which stops every rank here
     const int64_t banded = (ctx->bt_ng || ctx->band_ok16 || ctx->band_ok32 || ctx->window_ok16 ||
-                            ctx->window_ok32 || ctx->dense || ctx->csr_dropped) ? 1 : 0;
+                            ctx->window_ok32 || ctx->panel_auto || ctx->dense || ctx->csr_dropped)
+                               ? 1 : 0;
     std::vector<int64_t> all(ctx->nranks);
     COMMC(ctx->comm->allgather_host(&banded, all.data(), 1, ctx->stream, &ctx->err));
     for (int64_t v : all)
-      if (v) return RBL_OK;  // a banded kernel runs: its halo is a few rows
+      if (v) return RBL_OK;  // a banded kernel runs: its halo is a range of rows
     std::vector<uint8_t> tier_of(ctx->n, 1);
     for (int64_t c = ctx->r0; c < ctx->r1; ++c) tier_of[c] = 0;
     if (ctx->halo_push_opt != 0) {  // the push/pull split, if it moves fewer rows (collective)
@@ -885,6 +894,8 @@ int build_tiers(rbl_ctx* ctx, const std::vector<uint8_t>& tier_of, int nt, const
 // fits its ring (spmm_window.hip): columns sorted per row, footprints non-decreasing, a
 // tile's nonzeros <= 2048, ring rows: 256 (b=32) / 512 (b=16), new rows per tile <= 32 / 64.
 int prepare_window_formats(rbl_ctx* ctx, const std::vector<int64_t>& rp);
+// the column-panel SpMM's limit: panels per row block (256-row panels: windows <= 16 K rows)
+constexpr int64_t kPanelMax = 64;
 // Every SpMM format of a freshly set CSR: the segmented-gather table, the window / band /
 // band-tile formats, then (unbanded only) the column tiers.
 int prepare_window(rbl_ctx* ctx, const std::vector<int64_t>& rp) {
@@ -932,6 +943,38 @@ int prepare_window_formats(rbl_ctx* ctx, const std::vector<int64_t>& rp) {
   }
   if (first < 0) return RBL_OK;
   for (int64_t t = 0; t < first; ++t) { cmin[t] = cmin[first]; cmax[t] = cmax[first]; }
+  {
+    // column-panel SpMM (spmm_panel.hip): per block of panel_rows() rows the panels its columns
+    // span; applicable when no block spans more than kPanelMax panels (a window of 16 K rows:
+    // beyond that the panels' re-reads cost more than the gathers they replace)
+    const int tpb = panel_rows() / kWindowTileRows, pw = panel_width();
+    const int64_t nb = (nt + tpb - 1) / tpb;
+    std::vector<int32_t> bp(2 * nb);
+    int64_t maxp = 0, staged = 0;
+    for (int64_t bk = 0; bk < nb; ++bk) {
+      int64_t lo = INT64_MAX, hi = -1;
+      for (int64_t t = bk * tpb; t < std::min(nt, (bk + 1) * tpb); ++t) {
+        lo = std::min(lo, cmin[t]);
+        hi = std::max(hi, cmax[t]);
+      }
+      bp[2 * bk] = (int32_t)(lo / pw);
+      bp[2 * bk + 1] = (int32_t)(hi / pw);
+      maxp = std::max(maxp, hi / pw - lo / pw + 1);
+      staged += (hi / pw - lo / pw + 1) * pw;
+    }
+    if (maxp <= kPanelMax && ctx->n / pw < INT32_MAX) {
+      HIPC(hipMalloc(&ctx->d_panel_blk, 2 * nb * sizeof(int32_t)));
+      HIPC(hipMemcpy(ctx->d_panel_blk, bp.data(), 2 * nb * sizeof(int32_t), hipMemcpyHostToDevice));
+      ctx->panel_nblk = nb;
+      // by default only where the panels pay: a staged Q row read >= 4 times from LDS on
+      // average (bands; a scattered pattern's blocks span the whole matrix: the gathers)
+      ctx->panel_auto = 4 * staged <= ctx->nnz;
+      if (!ctx->d_zrow) {  // the panel rows outside the Q range read it
+        HIPC(hipMalloc(&ctx->d_zrow, 64 * sizeof(double)));
+        HIPC(hipMemset(ctx->d_zrow, 0, 64 * sizeof(double)));
+      }
+    }
+  }
   bool ok = true;
   int64_t max_span = 0, max_new = 0;
   for (int64_t t = 0; t < nt && ok; ++t) {
@@ -1015,8 +1058,10 @@ int prepare_window_formats(rbl_ctx* ctx, const std::vector<int64_t>& rp) {
       const size_t elems = (size_t)bt_tile_slots(nt, ctx->tiles_per_wg) * NG * 256;
       HIPC(hipMalloc(&ctx->d_bt, elems * sizeof(double)));
       HIPC(hipMemsetAsync(ctx->d_bt, 0, elems * sizeof(double), ctx->stream));
-      HIPC(hipMalloc(&ctx->d_zrow, 64 * sizeof(double)));
-      HIPC(hipMemsetAsync(ctx->d_zrow, 0, 64 * sizeof(double), ctx->stream));
+      if (!ctx->d_zrow) {
+        HIPC(hipMalloc(&ctx->d_zrow, 64 * sizeof(double)));
+        HIPC(hipMemsetAsync(ctx->d_zrow, 0, 64 * sizeof(double), ctx->stream));
+      }
       CsrDev A3 = csr(ctx);
       bt_fill(A3, H, NG, ctx->d_bt, ctx->stream);
       HIPC(hipGetLastError());
@@ -2006,6 +2051,7 @@ void free_matrix(rbl_ctx* ctx) {
   hipFree(ctx->d_tcmin); ctx->d_tcmin = nullptr;
   hipFree(ctx->d_tcmax); ctx->d_tcmax = nullptr;
   hipFree(ctx->d_tinfo); ctx->d_tinfo = nullptr;
+  hipFree(ctx->d_panel_blk); ctx->d_panel_blk = nullptr; ctx->panel_nblk = 0; ctx->panel_auto = false;
   hipFree(ctx->d_bpos); ctx->d_bpos = nullptr;
   hipFree(ctx->d_bt); ctx->d_bt = nullptr;
   hipFree(ctx->d_bth); ctx->d_bth = nullptr;
@@ -2364,8 +2410,8 @@ int rbl_set_option(rbl_ctx* ctx, int option, int64_t value) {
       // option values are the kernel ids rbl_spmm_kernel_for reports (4, the dense panel GEMM,
       // follows from rbl_set_matrix_dense and is not selectable); internally the band tiles
       // are variant 4 and the segmented gather variant 5 (spmm.hip)
-      if (value < 0 || value > 6 || value == 4)
-        return fail(ctx, RBL_ERR_INVALID, "spmm kernel must be 0 (auto) or a kernel id 1, 2, 3, 5, 6");
+      if (value < 0 || value > 7 || value == 4)
+        return fail(ctx, RBL_ERR_INVALID, "spmm kernel must be 0 (auto) or a kernel id 1, 2, 3, 5, 6, 7");
       ctx->spmm_variant = value == 5 ? 4 : value == 6 ? 5 : (int)value;
       return RBL_OK;
     case RBL_OPT_SPLIT_HALO: ctx->split_halo = value != 0; return RBL_OK;
@@ -2704,8 +2750,10 @@ int rbl_spmm_kernel_for(rbl_ctx* ctx, int b) {
   const int v = ctx->spmm_variant;
   const bool band = ctx->ntiles > 0 && ((b == 16 && ctx->band_ok16) || (b == 32 && ctx->band_ok32));
   const bool win = ctx->ntiles > 0 && ((b == 16 && ctx->window_ok16) || (b == 32 && ctx->window_ok32));
+  const bool panel = b == 32 && ctx->panel_nblk > 0 && !ctx->csr_dropped && !ctx->ghost;
   if ((v == 0 || v == 4) && (b == 32 || b == 16) && (ctx->bt_ng == 5 || ctx->bt_ng == 9)) return 5;
   if ((v == 0 || v == 3 || v == 4) && band) return 3;
+  if (((v == 0 && ctx->panel_auto) || v == 7) && panel) return 7;
   if ((v == 0 || v == 2 || v == 3) && win) return 2;
   if ((v == 0 || v == 5) && ctx->seg_ntasks > 0 && (b == 16 || b == 32)) return 6;
   return 1;

@@ -76,6 +76,33 @@ def test_multirank_apply_matches_scipy(rbl, P):
     assert np.abs(Y - ref).max() <= 1e-12 * np.abs(ref).max()
 
 
+@pytest.mark.parametrize("P", [2, 3])
+def test_multirank_column_panels(rbl, P):
+    """The column-panel SpMM on P ranks (range halo of W = 600 rows per side): rbl_apply equals
+    SciPy to 1e-12, and 6 block steps equal the single rank's A_i / B_{i+1} to 1e-10."""
+    A = matgen.hashwindow_csr(20000, 600, 0.08, 21, matgen.planted_spectrum(5))
+    X = np.random.default_rng(P).standard_normal((A.shape[0], 32))
+    omega = np.random.default_rng(9).standard_normal((A.shape[0], 32))
+    _, _, single = _single(rbl, A, 5, 32, omega, steps=6, check=False)
+
+    def fn(ctx, r):
+        ctx.set_matrix(A)
+        n, r0, r1, _ = ctx.matrix_info()
+        assert ctx.spmm_kernel_for(32) == 7
+        Y = ctx.apply(X[r0:r1])
+        _, _, info = rbl.lanczos(ctx, 5, 32, omega=omega[r0:r1], check=False, max_steps=6,
+                                 trace=True, ritz=False)
+        return Y, info
+
+    parts = run_ranks(rbl, P, fn)
+    Y = np.vstack([y for y, _ in parts])
+    ref = A @ X
+    assert np.abs(Y - ref).max() <= 1e-12 * np.abs(ref).max()
+    for _, info in parts:
+        for a, a1 in zip(info.trace_A + info.trace_B, single.trace_A + single.trace_B):
+            assert np.abs(a - a1).max() <= 1e-10 * np.abs(a1).max()
+
+
 @pytest.mark.parametrize("P,b", [(2, 8), (3, 16), (4, 32)])
 def test_multirank_lanczos_matches_single_rank(rbl, P, b):
     """Full RBL run (convergence checks on, Ritz vectors) on P ranks == 1 rank == oracle."""

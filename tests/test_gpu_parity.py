@@ -441,8 +441,8 @@ def test_ritz_row_pieces(rbl, bits):
     """rbl_ritz at a size where its row-piece form applies (n_local x k x 8 B >= 256 MiB: the
     combination V = [Q] S in 8 row pieces on a side stream with the staged D2H behind them;
     RBL_gpu.jl:106-132 / :219) takes that path (rbl_path_stats' ritz_pieces), returns Ritz
-    pairs with residual ||A v - lambda v|| / |lambda| < 1e-7 (1e-5 with the fp32 basis) and
-    orthonormal vectors, and two more runs on the same context return the same D and V bit for
+    pairs with residual ||A v - lambda v|| / |lambda| < 1e-7 and orthonormal vectors to 1e-9
+    (1e-5 and 1e-6 with the fp32 basis), and two more runs on the same context return the same D and V bit for
     bit (the side stream's use of the run scratch is ordered before the next run's steps)."""
     import scipy.sparse as sp
     n, b, k = 2_000_000, 32, 20
@@ -459,6 +459,6 @@ def test_ritz_row_pieces(rbl, bits):
     D0, V0 = out[0]
     res = np.linalg.norm(A @ V0 - V0 * D0, axis=0) / np.abs(D0)
     assert res.max() < (RES_TOL if bits == 64 else 1e-5), res
-    assert np.abs(V0.T @ V0 - np.eye(k)).max() < 1e-9
+    assert np.abs(V0.T @ V0 - np.eye(k)).max() < (1e-9 if bits == 64 else 1e-6)
     for D1, V1 in out[1:]:
         assert np.array_equal(D0, D1) and np.array_equal(V0, V1)

@@ -92,7 +92,9 @@ def test_spmm_general_pattern_and_empty_rows(rbl, b):
     X = np.random.default_rng(1).standard_normal((3000, b))
     with rbl.Context(0) as ctx:
         ctx.set_matrix(A)
-        assert ctx.spmm_kernel_for(b) == (6 if b in (16, 32) else 1)  # segmented / plain gather
+        # segmented / plain gather; at b = 32 this small pattern also passes the column panels'
+        # reuse rule (every staged Q row read >= 4 times), so either may be chosen
+        assert ctx.spmm_kernel_for(b) in ({6, 7} if b == 32 else {6} if b == 16 else {1})
         Y = ctx.apply(X)
     _check(A, Y, X)
     assert np.all(Y[[0, 5, 2999]] == 0)
@@ -172,3 +174,75 @@ def test_spmm_segmented_and_gather_agree_in_lanczos(rbl):
     for a1, a2 in zip(out[0].trace_A, out[1].trace_A):
         assert np.abs(a1 - a2).max() <= 1e-12 * np.abs(a1).max()
 
+
+
+# ---- column-panel CSR kernel (spmm_panel.hip, kernel id 7, b = 32) ----------------------------
+PANEL_CASES = [(50003, 300, 0.165), (20000, 1024, 0.0483), (3000, 2048, 0.024), (70001, 130, 1.0),
+               (257, 100, 0.5), (40000, 90, 0.55)]
+
+
+@pytest.mark.parametrize("n,W,p", PANEL_CASES)
+def test_spmm_column_panels(rbl, n, W, p):
+    """Wide bands (half-width 90 .. 2048, beyond the band tiles' 64): the automatic choice is
+    the column-panel kernel, and U = A X within 1e-13 |A||X| of SciPy — ragged last blocks
+    (n not a multiple of 256), a window wider than the matrix, rows with up to 261 nonzeros in
+    one 256-row panel (the chunk reload path), a matrix of one block and one row."""
+    A = matgen.hashwindow_csr(n, W, p, n + 3, matgen.planted_spectrum(5))
+    X = np.random.default_rng(n).standard_normal((n, 32))
+    with rbl.Context(0) as ctx:
+        ctx.set_matrix(A)
+        assert ctx.spmm_kernel_for(32) == 7, (n, W)
+        Y = ctx.apply(X)
+    _check(A, Y, X)
+
+
+@pytest.mark.parametrize("case", ["random", "empty_rows", "planted_diag"])
+def test_spmm_column_panels_forced(rbl, case):
+    """Kernel 7 forced (RBL_OPT_SPMM_KERNEL) on patterns it would not be chosen for: a random
+    unbanded matrix (every block spans every panel), empty rows and columns (zero rows of U),
+    a diagonal matrix (one panel per block, one entry per row)."""
+    n = 5000
+    if case == "random":
+        A = _rand_sym(n, 0.002, 9)
+    elif case == "empty_rows":
+        A = _rand_sym(n, 0.004, 4, empty_rows=(0, 255, 256, 4999))
+    else:
+        A = sp.diags(np.arange(1.0, n + 1.0)).tocsr()
+    X = np.random.default_rng(3).standard_normal((n, 32))
+    with rbl.Context(0) as ctx:
+        ctx.set_matrix(A)
+        ctx.set_option(2, 7)
+        assert ctx.spmm_kernel_for(32) == 7
+        Y = ctx.apply(X)
+    _check(A, Y, X)
+    if case == "empty_rows":
+        assert np.all(Y[[0, 255, 256, 4999]] == 0)
+
+
+def test_spmm_column_panels_in_lanczos(rbl):
+    """Inside block steps (the 3-term epilogue U -= Q_{i-1} B_i^T fused in the kernel,
+    RBL_gpu.jl:176-177): 8 steps on a half-width-700 band against the oracle's A_i / B_{i+1}
+    (1e-9 relative, as the other trace tests) and against the plain gather kernel (1e-12)."""
+    from oracle import rbl_oracle as o
+    n, W, b = 30011, 700, 32
+    A = matgen.hashwindow_csr(n, W, 0.07, 13, matgen.planted_spectrum(10))
+    omega = np.random.default_rng(5).standard_normal((n, b))
+    steps = 8
+    ref = o.RBL_gpu_semantics(A, 10, b, omega=omega, qr_mode="posdiag", reorth_mode="cgs",
+                              check=False, max_steps=steps, trace=True)
+    out = {}
+    for kernel in (0, 1):
+        with rbl.Context(0) as ctx:
+            ctx.set_matrix(A)
+            ctx.set_option(2, kernel)
+            assert ctx.spmm_kernel_for(b) == (7 if kernel == 0 else 1)
+            _, _, info = rbl.lanczos(ctx, 10, b, omega=omega, check=False, max_steps=steps,
+                                     trace=True, ritz=False)
+        out[kernel] = info
+    for i in range(steps):
+        Ar, Br = ref.trace["A"][i], ref.trace["B"][i]
+        Ag, Bg = out[0].trace_A[i], out[0].trace_B[i]
+        assert np.abs(Ag - Ar).max() <= 1e-9 * np.abs(Ar).max(), i
+        assert np.abs(Bg - Br).max() <= 1e-9 * np.abs(Br).max(), i
+        for x, y in ((Ag, out[1].trace_A[i]), (Bg, out[1].trace_B[i])):
+            assert np.abs(x - y).max() <= 1e-12 * np.abs(y).max(), i
