@@ -47,9 +47,11 @@ struct CsrDev {
   int64_t tiles_per_wg = 0;
   // column-panel SpMM (spmm_panel.hip, b = 32): per block of panel_rows() local rows its first
   // and last panel of panel_width() Q rows (global ids); null: not applicable
-  const int32_t* panel_blk = nullptr;
+  const int32_t* panel_blk = nullptr;   // per block: first / last panel, count offset (int64)
+  const uint16_t* panel_cnt = nullptr;  // per block, panel and row: the row's entries there
   int64_t panel_nblk = 0;
-  bool panel_auto = false;  // the automatic choice takes it (else only when forced)
+  int panel_rpg = 4;         // rows per 16-lane group (blocks of 64 rpg rows): 4 or 8
+  bool panel_auto = false;   // the automatic choice takes it (else only when forced)
   bool window_ok16 = false;
   bool window_ok32 = false;
   bool band_ok16 = false;   // spmm_band.hip applicable (and dense enough to pay)
@@ -215,11 +217,13 @@ void spmm_seg_tier(const CsrDev::Tier& T, const double* Q, int64_t col_off, int 
 void push_add(const int64_t* rows, const int64_t* ptr, const int64_t* slot, int64_t nrows,
               const double* recv, int b, double* U, hipStream_t s);
 // spmm_panel.hip: column-panel CSR kernel for wide bands (b = 32, Q rows [q_lo, q_hi)); false
-// if not applicable.  panel_rows(): rows per block, panel_width(): Q rows per panel.
+// if not applicable.  panel_width(): Q rows per panel.
 bool spmm_panel(const CsrDev& A, const double* Qin, int64_t col_off, int b, double* U,
                 const double* Qprev, const double* Bi, hipStream_t s);
-int panel_rows();
 int panel_width();
+// the counts of the column-panel format: ncnt entries (zeroed, then filled), binfo on the device
+int panel_counts(const CsrDev& A, const int32_t* binfo, int R, uint16_t* cnt, int64_t ncnt,
+                 hipStream_t s);
 // spmm_window.hip: persistent LDS-window kernel (b in {16,32}); false if not applicable.
 bool spmm_window(const CsrDev& A, const double* Qin, int64_t col_off, int b, double* U,
                  const double* Qprev, const double* Bi, hipStream_t s);

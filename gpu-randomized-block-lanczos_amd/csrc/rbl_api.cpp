@@ -42,7 +42,9 @@ struct rbl_ctx {
   int64_t* d_tinfo = nullptr;
   // column-panel SpMM (spmm_panel.hip): per 256-row block its first and last 256-row Q panel
   int32_t* d_panel_blk = nullptr;
+  uint16_t* d_panel_cnt = nullptr;  // per block, panel and row: the row's entries in the panel
   int64_t panel_nblk = 0;
+  int panel_rpg = 4;        // rows per 16-lane group: blocks of 64 panel_rpg rows
   bool panel_auto = false;  // chosen by default: every staged Q row used >= 4 times on average
   uint16_t* d_bpos = nullptr;  // band kernel: per-nonzero dense-tile positions
   double* d_bt = nullptr;      // band-tile kernel: the CSR in MFMA-ordered 16-row band tiles
@@ -324,6 +326,8 @@ CsrDev csr(rbl_ctx* ctx) {
   A.panel_blk = ctx->ghost ? nullptr : ctx->d_panel_blk;
   A.panel_nblk = ctx->ghost ? 0 : ctx->panel_nblk;
   A.panel_auto = ctx->panel_auto;
+  A.panel_cnt = ctx->d_panel_cnt;
+  A.panel_rpg = ctx->panel_rpg;
   A.ntiles = ctx->ntiles;
   A.tiles_per_wg = ctx->tiles_per_wg;
   A.window_ok16 = ctx->window_ok16;
@@ -943,38 +947,6 @@ int prepare_window_formats(rbl_ctx* ctx, const std::vector<int64_t>& rp) {
   }
   if (first < 0) return RBL_OK;
   for (int64_t t = 0; t < first; ++t) { cmin[t] = cmin[first]; cmax[t] = cmax[first]; }
-  {
-    // column-panel SpMM (spmm_panel.hip): per block of panel_rows() rows the panels its columns
-    // span; applicable when no block spans more than kPanelMax panels (a window of 16 K rows:
-    // beyond that the panels' re-reads cost more than the gathers they replace)
-    const int tpb = panel_rows() / kWindowTileRows, pw = panel_width();
-    const int64_t nb = (nt + tpb - 1) / tpb;
-    std::vector<int32_t> bp(2 * nb);
-    int64_t maxp = 0, staged = 0;
-    for (int64_t bk = 0; bk < nb; ++bk) {
-      int64_t lo = INT64_MAX, hi = -1;
-      for (int64_t t = bk * tpb; t < std::min(nt, (bk + 1) * tpb); ++t) {
-        lo = std::min(lo, cmin[t]);
-        hi = std::max(hi, cmax[t]);
-      }
-      bp[2 * bk] = (int32_t)(lo / pw);
-      bp[2 * bk + 1] = (int32_t)(hi / pw);
-      maxp = std::max(maxp, hi / pw - lo / pw + 1);
-      staged += (hi / pw - lo / pw + 1) * pw;
-    }
-    if (maxp <= kPanelMax && ctx->n / pw < INT32_MAX) {
-      HIPC(hipMalloc(&ctx->d_panel_blk, 2 * nb * sizeof(int32_t)));
-      HIPC(hipMemcpy(ctx->d_panel_blk, bp.data(), 2 * nb * sizeof(int32_t), hipMemcpyHostToDevice));
-      ctx->panel_nblk = nb;
-      // by default only where the panels pay: a staged Q row read >= 4 times from LDS on
-      // average (bands; a scattered pattern's blocks span the whole matrix: the gathers)
-      ctx->panel_auto = 4 * staged <= ctx->nnz;
-      if (!ctx->d_zrow) {  // the panel rows outside the Q range read it
-        HIPC(hipMalloc(&ctx->d_zrow, 64 * sizeof(double)));
-        HIPC(hipMemset(ctx->d_zrow, 0, 64 * sizeof(double)));
-      }
-    }
-  }
   bool ok = true;
   int64_t max_span = 0, max_new = 0;
   for (int64_t t = 0; t < nt && ok; ++t) {
@@ -1101,6 +1073,66 @@ int prepare_window_formats(rbl_ctx* ctx, const std::vector<int64_t>& rp) {
         }
       }
 #endif
+    }
+  }
+  // column-panel SpMM (spmm_panel.hip; not when the band tiles serve the matrix): per block of
+  // R = 64 rpg rows the panels its columns span and every row's count in each of them;
+  // applicable when no block spans more than kPanelMax panels (a window of 16 K rows: beyond
+  // that the panels' re-reads cost more than the gathers they replace)
+  if (!ctx->bt_ng) {
+    const int pw = panel_width();
+    // 8 rows per group (16-entry chunks) when a row's count per panel is mostly small, else 4
+    // (32-entry chunks): the mean count per row and panel at 512-row blocks decides
+    auto plan = [&](int R, std::vector<int32_t>* bp, int64_t* maxp, int64_t* staged) {
+      const int tpb = R / kWindowTileRows;
+      const int64_t nb = (nt + tpb - 1) / tpb;
+      if (bp) bp->assign(4 * nb, 0);
+      *maxp = *staged = 0;
+      int64_t coff = 0;
+      for (int64_t bk = 0; bk < nb; ++bk) {
+        int64_t lo = INT64_MAX, hi = -1;
+        for (int64_t t = bk * tpb; t < std::min(nt, (bk + 1) * tpb); ++t) {
+          lo = std::min(lo, cmin[t]);
+          hi = std::max(hi, cmax[t]);
+        }
+        const int64_t np = hi / pw - lo / pw + 1;
+        if (bp) {
+          (*bp)[4 * bk] = (int32_t)(lo / pw);
+          (*bp)[4 * bk + 1] = (int32_t)(hi / pw);
+          (*bp)[4 * bk + 2] = (int32_t)(uint32_t)(coff & 0xffffffff);
+          (*bp)[4 * bk + 3] = (int32_t)(coff >> 32);
+        }
+        coff += np * R;
+        *maxp = std::max(*maxp, np);
+        *staged += np * pw;
+      }
+      return nb;
+    };
+    int64_t maxp = 0, staged = 0;
+    plan(512, nullptr, &maxp, &staged);
+    const int rpg = (double)ctx->nnz <= 12.0 * (double)(staged / pw) * 512 ? 8 : 4;
+    const int R = 64 * rpg;
+    std::vector<int32_t> bp;
+    const int64_t nb = plan(R, &bp, &maxp, &staged);
+    const int64_t ncnt = bp.empty() ? 0 : ((int64_t)(uint32_t)bp[4 * nb - 2] | ((int64_t)bp[4 * nb - 1] << 32)) +
+                                              ((int64_t)bp[4 * nb - 3] - bp[4 * nb - 4] + 1) * R;
+    if (maxp <= kPanelMax && ctx->n / pw < INT32_MAX) {
+      HIPC(hipMalloc(&ctx->d_panel_blk, 4 * nb * sizeof(int32_t)));
+      HIPC(hipMemcpy(ctx->d_panel_blk, bp.data(), 4 * nb * sizeof(int32_t), hipMemcpyHostToDevice));
+      HIPC(hipMalloc(&ctx->d_panel_cnt, std::max<int64_t>(ncnt, 1) * sizeof(uint16_t)));
+      CsrDev A2 = csr(ctx);
+      if (panel_counts(A2, ctx->d_panel_blk, R, ctx->d_panel_cnt, ncnt, ctx->stream) != 0)
+        return fail(ctx, RBL_ERR_HIP, "panel_counts");
+      HIPC(hipStreamSynchronize(ctx->stream));
+      ctx->panel_nblk = nb;
+      ctx->panel_rpg = rpg;
+      // by default only where the panels pay: a staged Q row read >= 4 times from LDS on
+      // average (bands; a scattered pattern's blocks span the whole matrix: the gathers)
+      ctx->panel_auto = 4 * staged <= ctx->nnz;
+      if (!ctx->d_zrow) {  // the panel rows outside the Q range read it
+        HIPC(hipMalloc(&ctx->d_zrow, 64 * sizeof(double)));
+        HIPC(hipMemset(ctx->d_zrow, 0, 64 * sizeof(double)));
+      }
     }
   }
   if (!ctx->keep_csr && ctx->bt_ng) {
@@ -2052,6 +2084,7 @@ void free_matrix(rbl_ctx* ctx) {
   hipFree(ctx->d_tcmax); ctx->d_tcmax = nullptr;
   hipFree(ctx->d_tinfo); ctx->d_tinfo = nullptr;
   hipFree(ctx->d_panel_blk); ctx->d_panel_blk = nullptr; ctx->panel_nblk = 0; ctx->panel_auto = false;
+  hipFree(ctx->d_panel_cnt); ctx->d_panel_cnt = nullptr;
   hipFree(ctx->d_bpos); ctx->d_bpos = nullptr;
   hipFree(ctx->d_bt); ctx->d_bt = nullptr;
   hipFree(ctx->d_bth); ctx->d_bth = nullptr;

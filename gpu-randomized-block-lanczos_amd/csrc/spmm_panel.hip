@@ -3,32 +3,38 @@
 // U = A * Q_i  (+ the 3-term epilogue U -= Q_{i-1} B_i^T), RBL_gpu.jl:176-177, for matrices
 // whose rows reach further than the band-tile (|c - r| <= 64) and LDS-window (a 256-row ring)
 // kernels allow — the FEM / circuit orderings of the reference's benchmark.jl:21-28 inputs,
-// bandwidths in the hundreds to thousands.  HBM-bound on the CSR stream: per launch
-// nnz * (8 + 4) + (n + 1) * 8 + n * b * 8 * (2 + EPI) bytes.
+// bandwidths in the hundreds to thousands.  HBM-bound: per launch nnz * (8 + 4) + (n + 1) * 8 +
+// n * b * 8 * (2 + EPI) bytes, plus the Q panels each row block stages.
 //
-// A workgroup (1024 threads, one per CU, persistent) owns row blocks of kRows = 256 rows.  A
+// A workgroup (1024 threads, one per CU, persistent) owns row blocks of R = 64 RPG rows.  A
 // block's columns span [cmin, cmax]; that window is walked in column panels of kPanel = 256 Q
-// rows (64 KiB at b = 32), double-buffered in LDS: while panel p is multiplied, panel p + 1 (or
-// the next block's first panel) is loaded into registers, written to the other buffer after,
-// and one barrier per panel swaps them.  Every Q row a block needs is read from L2 / HBM once
-// per block and then from LDS once per nonzero (the 256 B of a Q row per nonzero are the
-// kernel's main traffic: ds_read_b128, 256 B/clk/CU).
+// rows (64 KiB at b = 32), double-buffered in LDS and filled by LDS-DMA
+// (global_load_lds_dwordx4): while panel p is multiplied the next one streams into the other
+// buffer, and one barrier per panel swaps them.  A Q row is read from L2 / HBM once per block
+// and then from LDS once per nonzero (the 256 B per nonzero are the kernel's main on-chip
+// traffic: ds_read_b128, 256 B/clk/CU).  R trades registers for staging: the panels cost
+// (R + 2H) / R Q blocks of traffic per launch.
 //
-//   * rows: 16-lane group G = tid / 16 (64 per workgroup) owns rows G, G + 64, G + 128, G + 192
-//     of the block; lane li holds columns 2 li, 2 li + 1 of each row's accumulator (16 VGPRs)
-//   * a row's nonzeros are column-sorted, so its entries in panel p are a prefix of what is
-//     left: the group holds a chunk of the next 32 entries (lane li: entries li, 16 + li), a
-//     ballot against the panel's end gives the count, the cursor advances by it, and the
-//     chunk for the next panel is loaded right after (unconditionally: the row end is applied
-//     where the chunk is used) — one panel of latency cover
+//   * rows: 16-lane group G = tid / 16 (64 per workgroup) owns rows G + 64 k (k < RPG) of the
+//     block; lane li holds columns 2 li, 2 li + 1 of each row's accumulator
+//   * the format (panel_counts) counts every row's entries in every panel of its block's window
+//     (uint16): the kernel knows each row's count in panel p before it reads a column index,
+//     so it loads exactly those entries (buffer loads; lanes past the count are out of range:
+//     no traffic), CH per row per load (more in a loop) — the next step's right after the row's
+//     entries in this one, into the same registers — and the counts two steps ahead
 //   * per entry: v_add_u32_dpp forms the Q row's LDS address from the broadcast offset
 //     (row_newbcast), one ds_read_b128, and two v_fmac_f64_dpp with the broadcast value; the
 //     four groups of a wave step through their rows' counts together (the wave loops to the
-//     largest, masked entries multiply a zero row of finite data)
-//   * the epilogue (B_i^T as a per-lane LDS table) and the store of U end a block.
+//     largest; masked entries multiply a row of finite data by zero)
+//   * hipcc drains an in-flight LDS-DMA at the first use of any ordinary load's result, so a
+//     step first touches everything the step before loaded, then issues its DMA and the loads
+//     for the next steps; the barrier waits for the DMA with a counted vmcnt, leaving those in
+//     flight
+//   * the epilogue (B_i^T as a per-lane LDS table, Q_{i-1} rows one ahead) and the store of U
+//     end a block.
 // Work goes to the workgroups XCD by XCD: the 8 XCDs take contiguous eighths of the blocks and
 // an XCD's 32 workgroups sweep theirs side by side, so neighbouring blocks — whose windows
-// overlap by 2H rows — read their shared panels from the same L2.
+// overlap by 2H rows — read shared panels close together in time (L2 / Infinity Cache).
 #include <cstdint>
 #include <type_traits>
 #include <utility>
@@ -39,7 +45,7 @@ namespace rbl {
 
 namespace pnl {
 constexpr int kThreads = 1024;
-constexpr int kRows = 256;                       // rows per block
+constexpr int kGroups = 64;                      // 16-lane row groups per workgroup
 constexpr int kPanel = 256;                      // Q rows per panel
 constexpr int kB = 32;
 constexpr int kRowBytes = kB * 8;                // 256
@@ -47,6 +53,7 @@ constexpr int kPanelBytes = kPanel * kRowBytes;  // 64 KiB
 constexpr int kBtBytes = kB * 16 * 16;           // B_i^T table: [u][lane] double2
 constexpr size_t kLds = 2 * (size_t)kPanelBytes + kBtBytes;
 constexpr int kXcds = 8;
+constexpr unsigned kOob = 0x10000000u;           // an entry offset past any block's records
 }  // namespace pnl
 
 namespace {
@@ -74,16 +81,28 @@ __device__ __forceinline__ void pnl_fma(double& acc, double val, double q) {
       : "+v"(acc)
       : "v"(val), "v"(q), "n"(S));
 }
+// x from lane S of the lane's 16-lane row (after the 2 wait states a VALU-written x needs)
+template <int S>
+__device__ __forceinline__ int pnl_bcast(int x) {
+  int r;
+  asm("s_nop 1\n\tv_mov_b32_dpp %0, %1 row_newbcast:%2 row_mask:0xf bank_mask:0xf"
+      : "=v"(r) : "v"(x), "n"(S));
+  return r;
+}
+// make the compiler wait for a loaded register here (no instruction)
+__device__ __forceinline__ void touch(int x) { asm volatile("" ::"v"(x)); }
+__device__ __forceinline__ void touch(double x) { asm volatile("" ::"v"(x)); }
 
 }  // namespace
 
 struct PanelArgs {
   int64_t nrows;             // local rows
-  int64_t nblk;              // blocks of kRows rows
+  int64_t nblk;              // blocks of 64 RPG rows
   const int64_t* rowptr;
   const int32_t* col;
   const double* val;
-  const int32_t* bpan;       // per block: first and last panel (global panel ids)
+  const int32_t* binfo;      // per block: first panel, last panel, count offset (2 x int32)
+  const uint16_t* cnt;       // per block and panel of its window: R counts (entries per row)
   const double* Q;           // Q row c at Q + (c - col_off) * 32, rows [q_lo, q_hi)
   int64_t col_off, q_lo, q_hi;
   const double* zrow;        // >= 32 zeros: the panel rows outside [q_lo, q_hi)
@@ -92,9 +111,13 @@ struct PanelArgs {
   const double* Bi;          // b x b row-major (B_i), with Qprev
 };
 
-template <bool EPI>
+template <bool EPI, int RPG, int CH>
 __global__ __launch_bounds__(pnl::kThreads) void k_spmm_panel(PanelArgs a) {
   using namespace pnl;
+  constexpr int R = kGroups * RPG;
+  constexpr int NCR = CH / 16;  // chunk registers per row
+  static_assert(CH == 16 || CH == 32, "chunk of 16 or 32 entries per row");
+  constexpr int kVm = 2 * NCR * RPG;  // chunk loads per step (the barrier's vmcnt)
   typedef double d2v __attribute__((ext_vector_type(2)));
   typedef __attribute__((address_space(3))) const d2v lds_d2;
   typedef __attribute__((address_space(3))) unsigned char lds_u8;
@@ -102,228 +125,250 @@ __global__ __launch_bounds__(pnl::kThreads) void k_spmm_panel(PanelArgs a) {
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int li = lane & 15;
-  const int grp = tid >> 4;                  // 0..63
-  const int gw = lane >> 4;                  // group within the wave
+  const int grp = tid >> 4;  // 0..63
+  const int wave = tid >> 6;
 
   // ---- this workgroup's blocks: XCD x (= blockIdx % 8) takes blocks [x nblk / 8, (x+1) nblk / 8)
   // and its workgroups j = blockIdx / 8 take every (gridDim / 8)-th of them ----
   const int nper = gridDim.x / kXcds;
   const int xcd = blockIdx.x % kXcds, j = blockIdx.x / kXcds;
-  const int64_t xb0 = a.nblk * xcd / kXcds, xb1 = a.nblk * (xcd + 1) / kXcds;
-  int64_t blk = xb0 + j;
-  if (blk >= xb1) return;  // whole workgroup: uniform
+  const int64_t xb1 = a.nblk * (xcd + 1) / kXcds;
+  const int64_t blk0 = a.nblk * xcd / kXcds + j;
+  if (blk0 >= xb1) return;  // whole workgroup: uniform
 
-  // ---- LDS: the B_i^T table (the panel buffers are written whole, out-of-range rows as
-  // zeros, before any read: masked entries read finite data) ----
-  {
-    if constexpr (EPI) {
-      d2v* bt = reinterpret_cast<d2v*>(smem + 2 * kPanelBytes);
-      for (int e = tid; e < kB * 16; e += kThreads) {
-        const int u = e >> 4, l = e & 15;
-        bt[e] = d2v{a.Bi[(2 * l) * kB + u], a.Bi[(2 * l + 1) * kB + u]};
-      }
+  if constexpr (EPI) {  // B_i^T as a per-lane table: bt[u][l] = (B_i[2l][u], B_i[2l+1][u])
+    d2v* bt = reinterpret_cast<d2v*>(smem + 2 * kPanelBytes);
+    for (int e = tid; e < kB * 16; e += kThreads) {
+      const int u = e >> 4, l = e & 15;
+      bt[e] = d2v{a.Bi[(2 * l) * kB + u], a.Bi[(2 * l + 1) * kB + u]};
     }
   }
   const unsigned lds_base = (unsigned)(size_t)(lds_u8*)smem;
   const unsigned lane_off = (unsigned)(li * 16);
 
-  // ---- panel staging: LDS-DMA (global_load_lds_dwordx4), no staging registers.  Wave w's
-  // instruction i writes 1 KiB = rows 4 (w + 16 i) .. + 3 of the panel (lane l: row + l / 16,
-  // bytes 16 (l % 16)); rows outside [q_lo, q_hi) come from a zero row ----
-  const int wave = tid >> 6;
+  // ---- block-uniform values through the scalar cache (read-only here) ----
+  typedef __attribute__((address_space(4))) const int64_t c_i64;
+  typedef __attribute__((address_space(4))) const int32_t c_i32;
+  c_i64* rp_s = (c_i64*)a.rowptr;
+  c_i32* bi_s = (c_i32*)a.binfo;
+  const int* rp32 = reinterpret_cast<const int*>(a.rowptr);  // low words: offsets in a block
+
+  // a step of the workgroup's sweep: (block, panel index within the block's window)
+  struct Step {
+    int64_t blk;
+    int pi, np, p0;  // panel index, panels of the block, its first panel (global id)
+    int64_t coff;    // the block's counts
+  };
+  auto block_step = [&](int64_t b) -> Step {
+    Step s;
+    s.blk = b;
+    s.pi = 0;
+    s.p0 = s.np = 0;
+    s.coff = 0;
+    if (b < xb1) {
+      s.p0 = bi_s[4 * b];
+      s.np = bi_s[4 * b + 1] - s.p0 + 1;
+      s.coff = (int64_t)(uint32_t)bi_s[4 * b + 2] | ((int64_t)bi_s[4 * b + 3] << 32);
+    }
+    return s;
+  };
+  auto next_step = [&](const Step& s) -> Step {
+    if (s.blk < xb1 && s.pi + 1 < s.np) {
+      Step t = s;
+      t.pi = s.pi + 1;
+      return t;
+    }
+    return block_step(s.blk < xb1 ? s.blk + nper : s.blk);
+  };
+  auto block_base = [&](int64_t b) -> int64_t {
+    const int64_t r = b * R;
+    return rp_s[r < a.nrows ? r : a.nrows];
+  };
+  auto rsrc_of = [&](int64_t b, __amdgpu_buffer_rsrc_t& rc, __amdgpu_buffer_rsrc_t& rv) {
+    const int64_t z0 = block_base(b), z1 = block_base(b + 1);
+    const int64_t n = z1 - z0;
+    rc = __builtin_amdgcn_make_buffer_rsrc(const_cast<int32_t*>(a.col + z0), 0, (int)(n * 4), 0x00020000);
+    rv = __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(a.val + z0), 0, (int)(n * 8), 0x00020000);
+  };
+
+  // ---- panel staging: LDS-DMA, no staging registers.  Wave w's instruction i writes 1 KiB =
+  // rows 4 (w + 16 i) .. + 3 of the panel (lane l: row + l / 16, bytes 16 (l % 16)); rows
+  // outside [q_lo, q_hi) come from a zero row ----
   auto load_panel = [&](int p, int buf) {
-    const int64_t cb = (int64_t)p * kPanel;
+    const int64_t cb0 = (int64_t)p * kPanel;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int rl = 4 * (wave + 16 * i);
-      const int64_t c = cb + rl + (lane >> 4);
+      const int64_t c = cb0 + rl + (lane >> 4);
       const double* src = (c >= a.q_lo && c < a.q_hi) ? a.Q + (c - a.col_off) * kB + 2 * li
                                                       : a.zrow + 2 * li;
       __builtin_amdgcn_global_load_lds(src, smem + buf * kPanelBytes + rl * kRowBytes, 16, 0, 0);
     }
   };
-
-  // per row k of the group: cursor and end (relative to the block's first nonzero, nzb), the
-  // chunk (entries cur + li, cur + 16 + li), the accumulators
-  int cur[4], end[4];
-  int c0[4], c1[4];
-  double v0[4], v1[4];
-  double acc[4][2];
-  int ncur[4], nend[4];  // the next block's rows (loaded during the current block)
-  auto row_of = [&](int64_t b, int k) -> int64_t { return b * kRows + grp + 64 * k; };
-  // block-uniform values through the scalar cache (read-only here): a block's first nonzero
-  // and its panel range — s_load, so waiting for them never drains the vector loads in flight
-  typedef __attribute__((address_space(4))) const int64_t c_i64;
-  typedef __attribute__((address_space(4))) const int32_t c_i32;
-  c_i64* rp_s = (c_i64*)a.rowptr;
-  c_i32* bp_s = (c_i32*)a.bpan;
-  auto block_base = [&](int64_t b) -> int64_t {
-    const int64_t r = b * kRows;
-    return rp_s[r < a.nrows ? r : a.nrows];
-  };
-  // a block's row bounds, low 32 bits of rowptr (the differences to the block's first
-  // nonzero fit: a block holds < 2^31 nonzeros), made relative to the base where they are used
-  const int* rp32 = reinterpret_cast<const int*>(a.rowptr);
-  auto load_bounds = [&](int64_t b, int (&cu)[4], int (&en)[4]) {
+  // entries [c0, c0 + min(m, CH)) of a row into chunk registers (lane li: c0 + li, + 16);
+  // lanes past m load nothing (an offset past the block's records reads 0)
+  auto load_chunk = [&](int (&cc)[NCR], double (&vv)[NCR], int c0, int m, __amdgpu_buffer_rsrc_t rc,
+                        __amdgpu_buffer_rsrc_t rv) {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {  // (rows past the slice: an empty range)
-      const int64_t r = row_of(b, k);
-      const bool in = r < a.nrows;
-      cu[k] = rp32[2 * (in ? r : a.nrows)];
-      en[k] = rp32[2 * (in ? r + 1 : a.nrows)];
+    for (int r = 0; r < NCR; ++r) {
+      const int e = 16 * r + li;
+      const unsigned o = e < m ? (unsigned)(c0 + e) : kOob;
+      cc[r] = __builtin_amdgcn_raw_buffer_load_b32(rc, (int)(o * 4u), 0, 0);
+      vv[r] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rv, (int)(o * 8u), 0, 0));
     }
   };
-  int64_t nzb = block_base(blk), nzb_next = 0;
-  // unconditional loads (no branches, no early use: the row end is applied in phase A): past
-  // a row's end they read the next rows' entries or the CSR's kCsrPad padding, never past it
-  // Non-temporal: the CSR streams through once, so its lines leave L2 first and the Q panels
-  // — each read by the ~(2H + 256) / 256 workgroups whose windows hold it, a panel step apart —
-  // stay there for them.
-  auto load_chunk = [&](int k, int64_t base) {
-    const int64_t e = base + cur[k] + li;
-    c0[k] = __builtin_nontemporal_load(a.col + e);
-    v0[k] = __builtin_nontemporal_load(a.val + e);
-    c1[k] = __builtin_nontemporal_load(a.col + e + 16);
-    v1[k] = __builtin_nontemporal_load(a.val + e + 16);
+  // a step's counts: lane li < RPG holds row k = li's (rows past the slice were counted 0)
+  auto load_counts = [&](const Step& s) -> int {
+    if (s.blk >= xb1 || li >= RPG) return 0;
+    return a.cnt[s.coff + (int64_t)s.pi * R + grp + 64 * li];
+  };
+  // a block's row starts (low words of rowptr)
+  auto load_starts = [&](int64_t b, int (&c)[RPG]) {
+#pragma unroll
+    for (int k = 0; k < RPG; ++k) {
+      const int64_t r = b * R + grp + 64 * k;
+      c[k] = rp32[2 * (r < a.nrows ? r : a.nrows)];
+    }
   };
 
-  int p0 = bp_s[2 * blk], p1 = bp_s[2 * blk + 1];
-  int p = p0;
+  int cur[RPG];             // row cursors, relative to the block's first nonzero
+  int nxt[RPG] = {};        // the next block's row starts (raw low words), loaded a step early
+  double acc[RPG][2];
+  int cc[RPG][NCR];         // each row's chunk: the current step's entries, then the next's
+  double vv[RPG][NCR];
+#pragma unroll
+  for (int k = 0; k < RPG; ++k) acc[k][0] = acc[k][1] = 0.0;
+
+  // ---- prologue: step 0's counts, cursors, chunks and panel; step 1's counts (and its
+  // block's starts if it begins one) ----
+  Step st = block_step(blk0);
+  Step st1 = next_step(st);
+  int64_t nzb = block_base(blk0);
+  __amdgpu_buffer_rsrc_t rc, rv;
+  rsrc_of(blk0, rc, rv);
+  load_starts(blk0, cur);
+  int cnt_cur = load_counts(st);
+#pragma unroll
+  for (int k = 0; k < RPG; ++k) cur[k] -= (int)nzb;
+  pfor<0, RPG>([&](auto kc) {
+    constexpr int k = decltype(kc)::value;
+    load_chunk(cc[k], vv[k], cur[k], pnl_bcast<k>(cnt_cur), rc, rv);
+  });
+  int cnt_nxt = load_counts(st1);
+  if (st1.blk < xb1 && st1.pi == 0) load_starts(st1.blk, nxt);
+  load_panel(st.p0, 0);
+  __syncthreads();  // (drains everything: the prologue's loads and DMA)
+
   int buf = 0;
-  load_bounds(blk, cur, end);
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    cur[k] -= (int)nzb;
-    end[k] -= (int)nzb;
-    load_chunk(k, nzb);
-    acc[k][0] = acc[k][1] = 0.0;
-  }
-  load_panel(p, 0);
-  __syncthreads();  // (waits for the DMA: an LDS-DMA is a pending load)
-
   for (;;) {
-    // ---- the next step: panel p + 1 of this block, or the next block's first panel ----
-    const bool last_panel = p == p1;
-    const int64_t nblk = blk + nper;
-    const bool have_next = !last_panel || nblk < xb1;
-    int np0 = 0, np1 = 0;
-    if (last_panel && nblk < xb1) {
-      np0 = bp_s[2 * nblk];
-      np1 = bp_s[2 * nblk + 1];
-    }
-    const int pn = last_panel ? np0 : p + 1;
-    const int64_t pbase = (int64_t)p * kPanel, pend = pbase + kPanel;
+    const bool last_panel = st.pi + 1 == st.np;
+    const Step sn = st1;
+    const bool have_next = sn.blk < xb1;
+    const Step sn2 = next_step(sn);
+    const int p = st.p0 + st.pi;
+    const int64_t pbase = (int64_t)p * kPanel;
     const unsigned bufb = lds_base + (unsigned)(buf * kPanelBytes);
 
-    // ---- phase A: every row's chunk against the panel's end — counts, LDS offsets, masked
-    // values — before the next panel's DMA is issued (hipcc drains an in-flight LDS-DMA at the
-    // first use of an ordinary load's result, so the chunks are consumed first) ----
-    int m[4], mmax[4];
-    unsigned o0[4], o1[4];
-    double w0[4], w1[4];
-    bool ok0[4], ok1[4];
-    auto count = [&](int k) {
-      const uint64_t b0 = __ballot(ok0[k]), b1 = __ballot(ok1[k]);
-      const int sh = 16 * gw;
-      m[k] = __popcll((b0 >> sh) & 0xffffull) + __popcll((b1 >> sh) & 0xffffull);
-      int mx = 0;
+    // (1) everything the step before loaded, waited for here — before this step's DMA
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int mg = __popcll((b0 >> (16 * g)) & 0xffffull) + __popcll((b1 >> (16 * g)) & 0xffffull);
-        mx = mg > mx ? mg : mx;
+    for (int k = 0; k < RPG; ++k) {
+#pragma unroll
+      for (int r = 0; r < NCR; ++r) {
+        touch(cc[k][r]);
+        touch(vv[k][r]);
       }
-      mmax[k] = mx;
-      // LDS byte offsets of the entries' Q rows in this panel; masked: row 0, value 0
-      o0[k] = ok0[k] ? bufb + (unsigned)((c0[k] - pbase) * kRowBytes) : bufb;
-      o1[k] = ok1[k] ? bufb + (unsigned)((c1[k] - pbase) * kRowBytes) : bufb;
-      w0[k] = ok0[k] ? v0[k] : 0.0;
-      w1[k] = ok1[k] ? v1[k] : 0.0;
-    };
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      ok0[k] = cur[k] + li < end[k] && c0[k] < pend;
-      ok1[k] = cur[k] + 16 + li < end[k] && c1[k] < pend;
-      count(k);
+      touch(nxt[k]);
     }
+    touch(cnt_cur);
+    touch(cnt_nxt);
     __builtin_amdgcn_sched_barrier(0);
-    if (have_next) load_panel(pn, buf ^ 1);
-    asm volatile("" ::: "memory");  // the loads below stay younger than the DMA
-    if (p == p0 && nblk < xb1) {
-      nzb_next = block_base(nblk);
-      load_bounds(nblk, ncur, nend);
+
+    // (2) the next step's panel, then the loads the next steps need (younger than the DMA)
+    if (have_next) load_panel(sn.p0 + sn.pi, buf ^ 1);
+    asm volatile("" ::: "memory");
+    const int cnt_nn = have_next ? load_counts(sn2) : 0;
+    // where the next step's chunks come from: this block, or the next one
+    __amdgpu_buffer_rsrc_t rcn = rc, rvn = rv;
+    int64_t nzb_n = nzb;
+    if (have_next && last_panel) {
+      nzb_n = block_base(sn.blk);
+      rsrc_of(sn.blk, rcn, rvn);
     }
 
-    // ---- phase B: multiply panel p (buffer buf), row by row; each row's chunk for the next
-    // step is loaded as soon as its entries here are done ----
-    pfor<0, 4>([&](auto kc) {
+    // (3) multiply panel p, row by row; each row's chunk for the next step follows its entries
+    pfor<0, RPG>([&](auto kc) {
       constexpr int k = decltype(kc)::value;
-      for (;;) {
-        unsigned u0 = o0[k], u1 = o1[k];
-        double x0 = w0[k], x1 = w1[k];
+      const int m = pnl_bcast<k>(cnt_cur);  // this group's row k: entries in panel p
+      // the largest count of the wave's four groups (lanes 0, 16, 32, 48 hold them)
+      const int mmax = max(max(__builtin_amdgcn_readlane(m, 0), __builtin_amdgcn_readlane(m, 16)),
+                           max(__builtin_amdgcn_readlane(m, 32), __builtin_amdgcn_readlane(m, 48)));
+      double& a0 = acc[k][0];
+      double& a1 = acc[k][1];
+      // entries 2h, 2h + 1 of one chunk register: their two LDS reads, then their FMAs
+      auto pair = [&](unsigned off, double w, auto hh) {
+        constexpr int H = decltype(hh)::value;
+        d2v q[2];
+        pfor<0, 2>([&](auto ic) {
+          constexpr int S = 2 * H + decltype(ic)::value;
+          q[decltype(ic)::value] = *(lds_d2*)(size_t)pnl_addr<S>(off, lane_off);
+        });
+        __builtin_amdgcn_sched_barrier(0);  // both reads in flight before the FMAs
+        pfor<0, 2>([&](auto ic) {
+          constexpr int S = 2 * H + decltype(ic)::value;
+          pnl_fma<S>(a0, w, q[decltype(ic)::value][0]);
+          pnl_fma<S>(a1, w, q[decltype(ic)::value][1]);
+        });
+      };
+      auto run = [&](int done) {
+        unsigned u[NCR];
+        double x[NCR];
+#pragma unroll
+        for (int r = 0; r < NCR; ++r) {  // masked entries: row 0 (finite), value 0 (loaded)
+          const bool ok = done + 16 * r + li < m;
+          u[r] = ok ? bufb + (unsigned)((cc[k][r] - pbase) * kRowBytes) : bufb;
+          x[r] = vv[k][r];
+        }
         // VALU write -> DPP read needs 2 wait states; hipcc does not pad inside asm
-        asm volatile("s_nop 1" : "+v"(u0), "+v"(u1), "+v"(x0), "+v"(x1));
-        double& a0 = acc[k][0];
-        double& a1 = acc[k][1];
-        const int mx = mmax[k];
-        // entries 4h .. 4h + 3 of one chunk register (lanes 4h .. 4h + 3 of the group): their
-        // four LDS reads issued together, then their FMAs
-        auto quad = [&](unsigned off, double w, auto hh) {
-          constexpr int H = decltype(hh)::value;
-          d2v q[4];
-          pfor<0, 4>([&](auto ic) {
-            constexpr int S = 4 * H + decltype(ic)::value;
-            q[decltype(ic)::value] = *(lds_d2*)(size_t)pnl_addr<S>(off, lane_off);
+        if constexpr (NCR == 2) asm volatile("s_nop 1" : "+v"(u[0]), "+v"(u[1]), "+v"(x[0]), "+v"(x[1]));
+        else asm volatile("s_nop 1" : "+v"(u[0]), "+v"(x[0]));
+        const int left = mmax - done;
+        pfor<0, NCR>([&](auto rr) {
+          constexpr int RR = decltype(rr)::value;
+          pfor<0, 8>([&](auto hh) {
+            if (16 * RR + 2 * decltype(hh)::value < left) pair(u[RR], x[RR], hh);
           });
-          __builtin_amdgcn_sched_barrier(0);  // all four reads in flight before the FMAs
-          pfor<0, 4>([&](auto ic) {
-            constexpr int S = 4 * H + decltype(ic)::value;
-            pnl_fma<S>(a0, w, q[decltype(ic)::value][0]);
-            pnl_fma<S>(a1, w, q[decltype(ic)::value][1]);
-          });
-        };
-        pfor<0, 4>([&](auto hh) {
-          if (4 * decltype(hh)::value < mx) quad(u0, x0, hh);
         });
-        pfor<0, 4>([&](auto hh) {
-          if (16 + 4 * decltype(hh)::value < mx) quad(u1, x1, hh);
-        });
-        cur[k] += m[k];
-        // a full chunk may leave entries in this panel: that group loads the next 32 (rare at
-        // ~100 nonzeros per row over several panels)
-        const bool need = m[k] == 32 && cur[k] < end[k];
-        if (__ballot(need) == 0) break;
-        if (need) load_chunk(k, nzb);
-        ok0[k] = need && cur[k] + li < end[k] && c0[k] < pend;
-        ok1[k] = need && cur[k] + 16 + li < end[k] && c1[k] < pend;
-        count(k);
+      };
+      run(0);
+      // more than CH entries in this panel in some group: the next CH, loaded here (rare
+      // when CH covers the typical count)
+      for (int done = CH; done < mmax; done += CH) {
+        load_chunk(cc[k], vv[k], cur[k] + done, m - done, rc, rv);
+        run(done);
       }
-      // the row's entries for the next step: the next panel's (the rest of this chunk comes
-      // back from L1 / L2), or at a block's last panel the next block's row k
-      if (last_panel && nblk < xb1) {
-        cur[k] = ncur[k] - (int)nzb_next;
-        end[k] = nend[k] - (int)nzb_next;
-        load_chunk(k, nzb_next);
-      } else if (have_next) {
-        load_chunk(k, nzb);
+      // the next step's entries of this row
+      if (have_next) {
+        cur[k] = last_panel ? nxt[k] - (int)nzb_n : cur[k] + m;
+        load_chunk(cc[k], vv[k], cur[k], pnl_bcast<k>(cnt_nxt), rcn, rvn);
       }
     });
-    if (last_panel && nblk < xb1) nzb = nzb_next;
+    // the starts of the block the step after next begins, if it does
+    if (sn2.blk < xb1 && sn2.pi == 0) load_starts(sn2.blk, nxt);
 
-    // ---- block end: epilogue, store U, the next block's accumulators ----
+    // (4) block end: epilogue, store U
     if (last_panel) {
-      // the epilogue's Q_{i-1} rows, one row ahead
-      auto qprev_row = [&](int k) -> d2v {
-        const int64_t r = row_of(blk, k);
-        return __builtin_nontemporal_load(reinterpret_cast<const d2v*>(a.Qprev + (r < a.nrows ? r : a.nrows - 1) * kB) + li);
+      auto qprev_row = [&](int k) -> d2v {  // the epilogue's Q_{i-1} rows, one row ahead
+        const int64_t r = st.blk * R + grp + 64 * k;
+        return *(reinterpret_cast<const d2v*>(a.Qprev + (r < a.nrows ? r : a.nrows - 1) * kB) + li);
       };
       d2v qn = EPI ? qprev_row(0) : d2v{0.0, 0.0};
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int64_t r = row_of(blk, k);
+      for (int k = 0; k < RPG; ++k) {
+        const int64_t r = st.blk * R + grp + 64 * k;
         double u0 = acc[k][0], u1 = acc[k][1];
         if constexpr (EPI) {
           const d2v qc = qn;
-          if (k < 3) qn = qprev_row(k + 1);
+          if (k + 1 < RPG) qn = qprev_row(k + 1);
           if (r < a.nrows) {
             double n0 = -qc[0], n1 = -qc[1];
             asm volatile("s_nop 1" : "+v"(n0), "+v"(n1));
@@ -344,31 +389,37 @@ __global__ __launch_bounds__(pnl::kThreads) void k_spmm_panel(PanelArgs a) {
       }
     }
     if (!have_next) break;
-    // the next panel's DMA has landed — it is older than the 16 chunk loads just issued, and
-    // loads retire in order, so vmcnt(16) leaves those in flight across the barrier — and every
-    // wave is done reading this panel (lgkmcnt(0)); a plain __syncthreads() would drain them
-    asm volatile("s_waitcnt vmcnt(16)\n\ts_waitcnt lgkmcnt(0)" ::: "memory");
+    // (5) the DMA has landed — older than the step's other loads, which retire in order, so a
+    // counted vmcnt leaves those (at least the kVm chunk loads) in flight across the barrier —
+    // and every wave is done reading this panel (lgkmcnt(0)).  A plain __syncthreads() would
+    // drain them.
+    asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)" ::"n"(kVm) : "memory");
     __builtin_amdgcn_s_barrier();
     buf ^= 1;
-    if (last_panel) {
-      blk = nblk;
-      p0 = np0;
-      p1 = np1;
-    }
-    p = pn;
+    nzb = nzb_n;
+    rc = rcn;
+    rv = rvn;
+    cnt_cur = cnt_nxt;
+    cnt_nxt = cnt_nn;
+    st = sn;
+    st1 = sn2;
   }
 }
 
+// RPG / CH by the format's typical count per row and panel (panel_format): 16-entry chunks at
+// 8 rows per group (512-row blocks: half the panel staging of 256) where a row's count in a
+// panel is mostly <= 16, 32-entry chunks at 4 rows per group otherwise (registers)
 bool spmm_panel(const CsrDev& A, const double* Qin, int64_t col_off, int b, double* U,
                 const double* Qprev, const double* Bi, hipStream_t s) {
-  if (b != 32 || !A.panel_blk || A.panel_nblk <= 0 || !A.zrow) return false;
+  if (b != 32 || !A.panel_blk || A.panel_nblk <= 0 || !A.panel_cnt || !A.zrow) return false;
   PanelArgs a;
   a.nrows = A.nrows;
   a.nblk = A.panel_nblk;
   a.rowptr = A.rowptr;
   a.col = A.col;
   a.val = A.val;
-  a.bpan = A.panel_blk;
+  a.binfo = A.panel_blk;
+  a.cnt = A.panel_cnt;
   a.Q = Qin;
   a.col_off = col_off;
   a.q_lo = A.q_lo;
@@ -380,17 +431,51 @@ bool spmm_panel(const CsrDev& A, const double* Qin, int64_t col_off, int b, doub
   // one workgroup per CU, a multiple of the 8 XCDs
   const int cus = window_grid();
   const int grid = cus >= pnl::kXcds ? cus / pnl::kXcds * pnl::kXcds : pnl::kXcds;
-  if (Qprev) {
-    ensure_lds_attr(reinterpret_cast<const void*>(&k_spmm_panel<true>), (int)pnl::kLds);
-    hipLaunchKernelGGL(k_spmm_panel<true>, dim3(grid), dim3(pnl::kThreads), pnl::kLds, s, a);
+  auto go = [&](auto kern) {
+    ensure_lds_attr(reinterpret_cast<const void*>(kern), (int)pnl::kLds);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(pnl::kThreads), pnl::kLds, s, a);
+  };
+  if (A.panel_rpg == 8) {
+    if (Qprev) go(&k_spmm_panel<true, 8, 16>); else go(&k_spmm_panel<false, 8, 16>);
   } else {
-    ensure_lds_attr(reinterpret_cast<const void*>(&k_spmm_panel<false>), (int)pnl::kLds);
-    hipLaunchKernelGGL(k_spmm_panel<false>, dim3(grid), dim3(pnl::kThreads), pnl::kLds, s, a);
+    if (Qprev) go(&k_spmm_panel<true, 4, 32>); else go(&k_spmm_panel<false, 4, 32>);
   }
   return true;
 }
 
-int panel_rows() { return pnl::kRows; }
 int panel_width() { return pnl::kPanel; }
+
+// ---- the format: per block of R rows its panel range (binfo) and the count of every row's
+// entries in every panel of the range (cnt, zero-filled first) ----
+__global__ void k_panel_counts(int64_t nrows, const int64_t* __restrict__ rowptr,
+                               const int32_t* __restrict__ col, const int32_t* __restrict__ binfo,
+                               int R, uint16_t* __restrict__ cnt) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= nrows) return;
+  const int64_t b = r / R;
+  const int p0 = binfo[4 * b];
+  const int64_t coff = (int64_t)(uint32_t)binfo[4 * b + 2] | ((int64_t)binfo[4 * b + 3] << 32);
+  const int rl = (int)(r - b * R);
+  int pc = -1, n = 0;
+  for (int64_t e = rowptr[r]; e < rowptr[r + 1]; ++e) {
+    const int p = col[e] / pnl::kPanel;
+    if (p != pc) {
+      if (pc >= 0) cnt[coff + (int64_t)(pc - p0) * R + rl] = (uint16_t)n;
+      pc = p;
+      n = 0;
+    }
+    ++n;
+  }
+  if (pc >= 0) cnt[coff + (int64_t)(pc - p0) * R + rl] = (uint16_t)n;
+}
+
+int panel_counts(const CsrDev& A, const int32_t* binfo, int R, uint16_t* cnt, int64_t ncnt,
+                 hipStream_t s) {
+  if (hipMemsetAsync(cnt, 0, (size_t)ncnt * sizeof(uint16_t), s) != hipSuccess) return -1;
+  if (A.nrows > 0)
+    hipLaunchKernelGGL(k_panel_counts, dim3((unsigned)((A.nrows + 255) / 256)), dim3(256), 0, s,
+                       A.nrows, A.rowptr, A.col, binfo, R, cnt);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
 
 }  // namespace rbl
