@@ -75,7 +75,11 @@ extern "C" {
                                    * band on fp64 MFMA; 5 band-tile format (CSR densified once
                                    * into MFMA operand order, b in {16, 32}, |c - r| <= 64);
                                    * 6 segmented gather (power-law rows split / packed, b in
-                                   * {16, 32}).  Each falls back 5 -> 3 -> 2 -> 1 when the matrix
+                                   * {16, 32}); 7 column panels (CSR rows in blocks of 256 / 512,
+                                   * Q staged through LDS in 256-row panels of the columns a block
+                                   * touches, b = 32; the default where every staged Q row is
+                                   * read >= 4 times, i.e. bands wider than the band tiles' 64).
+                                   * Each falls back 5 -> 3 -> 2 -> 1 (7 -> 1) when the matrix
                                    * does not fit the kernel's limits.  4 (dense panels) follows
                                    * from rbl_set_matrix_dense and is rejected here.           */
 #define RBL_OPT_SPLIT_HALO    4   /* several ranks, band-tile SpMM: 1 (default) the kernel reads
