@@ -217,7 +217,23 @@ def launch_ranks(args) -> None:
            f"--nproc-per-node={args.gpus}", "--master-addr=127.0.0.1", f"--master-port={port}",
            os.path.abspath(__file__), "--argv-env"]
     env = dict(os.environ, RBL_BENCH_ARGV=json.dumps(sys.argv[1:]))
+    if have and have < args.gpus and "GPU_MAX_HW_QUEUES" not in env:
+        env["GPU_MAX_HW_QUEUES"] = str(shared_gpu_queues(-(-args.gpus // have)))
     sys.exit(subprocess.run(cmd, env=env).returncode)
+
+
+# Hardware queues the GPU's scheduler keeps mapped for all processes together in the one-GPU
+# rehearsals: measured, 6 processes x 4 queues (HIP's default) run at the P = 4 rate per
+# collective and 7 x 4 time-slice whole processes (every collective then waits ~13-44 ms);
+# DESIGN.md §6, profiles/r06_p8_*.
+SHARED_GPU_QUEUE_BUDGET = 24
+
+
+def shared_gpu_queues(ranks_per_gpu: int) -> int:
+    """GPU_MAX_HW_QUEUES for ranks that share a GPU (the rehearsal of an N-GPU job on fewer
+    GPUs; never set for one rank per GPU): HIP's default 4 while the ranks' queues fit the
+    scheduler's budget, fewer beyond (the streams of a process then share its queues)."""
+    return max(1, min(4, SHARED_GPU_QUEUE_BUDGET // max(1, ranks_per_gpu)))
 
 
 def rccl_host_per_rank() -> bool:
@@ -332,6 +348,7 @@ def gpu_processes() -> dict:
         out["own_queues"] = len(os.listdir(q)) if os.path.isdir(q) else None
     except OSError:
         pass
+    out["gpu_max_hw_queues"] = os.environ.get("GPU_MAX_HW_QUEUES")
     for prm in ("hws_max_conc_proc", "sched_policy", "mes", "cwsr_enable"):
         v = _read(f"/sys/module/amdgpu/parameters/{prm}")
         if v is not None:
