@@ -217,8 +217,9 @@ def launch_ranks(args) -> None:
            f"--nproc-per-node={args.gpus}", "--master-addr=127.0.0.1", f"--master-port={port}",
            os.path.abspath(__file__), "--argv-env"]
     env = dict(os.environ, RBL_BENCH_ARGV=json.dumps(sys.argv[1:]))
-    if have and have < args.gpus and "GPU_MAX_HW_QUEUES" not in env:
-        env["GPU_MAX_HW_QUEUES"] = str(shared_gpu_queues(-(-args.gpus // have)))
+    if have and have < args.gpus:  # (the box exports HIP's default 4: lowered, never raised)
+        cur = int(env.get("GPU_MAX_HW_QUEUES") or 4)
+        env["GPU_MAX_HW_QUEUES"] = str(min(cur, shared_gpu_queues(-(-args.gpus // have))))
     sys.exit(subprocess.run(cmd, env=env).returncode)
 
 

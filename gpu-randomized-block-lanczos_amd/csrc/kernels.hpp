@@ -49,6 +49,9 @@ struct CsrDev {
   // and last panel of panel_width() Q rows (global ids); null: not applicable
   const int32_t* panel_blk = nullptr;   // per block: first / last panel, count offset (int64)
   const uint16_t* panel_cnt = nullptr;  // per block, panel and row: the row's entries there
+  const uint32_t* panel_st = nullptr;   // ... and where they start (records from the block's base)
+  const uint8_t* panel_col = nullptr;   // the records, panel-major within a block: column - panel
+  const double* panel_val = nullptr;    //   base (one byte), value
   int64_t panel_nblk = 0;
   int panel_rpg = 4;         // rows per 16-lane group (blocks of 64 rpg rows): 4 or 8
   bool panel_auto = false;   // the automatic choice takes it (else only when forced)
@@ -221,9 +224,12 @@ void push_add(const int64_t* rows, const int64_t* ptr, const int64_t* slot, int6
 bool spmm_panel(const CsrDev& A, const double* Qin, int64_t col_off, int b, double* U,
                 const double* Qprev, const double* Bi, hipStream_t s);
 int panel_width();
-// the counts of the column-panel format: ncnt entries (zeroed, then filled), binfo on the device
-int panel_counts(const CsrDev& A, const int32_t* binfo, int R, uint16_t* cnt, int64_t ncnt,
-                 hipStream_t s);
+// the column-panel format (zeroed and filled on the device, stream-ordered): every row's count
+// (cnt) and first record (st) in every panel of its block's window, and the records themselves
+// regrouped panel-major within each block (pcol: column within the panel, pval: value); binfo
+// on the device; ncnt entries of cnt / st, nnz records
+int panel_format(const CsrDev& A, const int32_t* binfo, int R, int64_t nblk, uint16_t* cnt,
+                 uint32_t* st, int64_t ncnt, uint8_t* pcol, double* pval, hipStream_t s);
 // spmm_window.hip: persistent LDS-window kernel (b in {16,32}); false if not applicable.
 bool spmm_window(const CsrDev& A, const double* Qin, int64_t col_off, int b, double* U,
                  const double* Qprev, const double* Bi, hipStream_t s);

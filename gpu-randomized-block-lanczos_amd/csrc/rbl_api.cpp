@@ -43,9 +43,13 @@ struct rbl_ctx {
   // column-panel SpMM (spmm_panel.hip): per 256-row block its first and last 256-row Q panel
   int32_t* d_panel_blk = nullptr;
   uint16_t* d_panel_cnt = nullptr;  // per block, panel and row: the row's entries in the panel
+  uint32_t* d_panel_st = nullptr;   // ... and their first record (from the block's base)
+  uint8_t* d_panel_col = nullptr;   // the records panel-major within a block: column in the panel
+  double* d_panel_val = nullptr;    //   and value
   int64_t panel_nblk = 0;
   int panel_rpg = 4;        // rows per 16-lane group: blocks of 64 panel_rpg rows
   bool panel_auto = false;  // chosen by default: every staged Q row used >= 4 times on average
+  int64_t panel_span = 0;   // the widest block window, Q rows
   uint16_t* d_bpos = nullptr;  // band kernel: per-nonzero dense-tile positions
   double* d_bt = nullptr;      // band-tile kernel: the CSR in MFMA-ordered 16-row band tiles
   int bt_ng = 0;               // its band groups (0: not applicable)
@@ -327,6 +331,9 @@ CsrDev csr(rbl_ctx* ctx) {
   A.panel_nblk = ctx->ghost ? 0 : ctx->panel_nblk;
   A.panel_auto = ctx->panel_auto;
   A.panel_cnt = ctx->d_panel_cnt;
+  A.panel_st = ctx->d_panel_st;
+  A.panel_col = ctx->d_panel_col;
+  A.panel_val = ctx->d_panel_val;
   A.panel_rpg = ctx->panel_rpg;
   A.ntiles = ctx->ntiles;
   A.tiles_per_wg = ctx->tiles_per_wg;
@@ -759,6 +766,11 @@ int prepare_push(rbl_ctx* ctx, const std::vector<int64_t>& rp) {
 // Several ranks (unbanded A, the segmented gather): two tiers instead, the own columns
 // [r0, r1) and the halo columns, so the own part of the SpMM runs while the halo exchange is in
 // flight (step_impl); the sum order per row is the same with or without the overlap.
+// the column panels on several ranks need the range halo: taken where every block's window
+// is a small part of the matrix (a band), not where the windows span it (a small R-MAT's blocks
+// may pass panel_auto, and its indexed halo moves fewer rows)
+bool panel_banded(const rbl_ctx* ctx) { return ctx->panel_auto && 4 * ctx->panel_span <= ctx->n; }
+
 int prepare_tiers(rbl_ctx* ctx, const std::vector<int64_t>& rp) {
   free_tiers(ctx);
   ctx->push_pred_rows = ctx->pull_pred_rows = 0;
@@ -768,7 +780,7 @@ int prepare_tiers(rbl_ctx* ctx, const std::vector<int64_t>& rp) {
     // part in build_ghosts (with no requests), and a rank that released its CSR for band tiles
     // (RBL_OPT_KEEP_CSR = 0) votes banded, which stops every rank here
     const int64_t banded = (ctx->bt_ng || ctx->band_ok16 || ctx->band_ok32 || ctx->window_ok16 ||
-                            ctx->window_ok32 || ctx->panel_auto || ctx->dense || ctx->csr_dropped)
+                            ctx->window_ok32 || panel_banded(ctx) || ctx->dense || ctx->csr_dropped)
                                ? 1 : 0;
     std::vector<int64_t> all(ctx->nranks);
     COMMC(ctx->comm->allgather_host(&banded, all.data(), 1, ctx->stream, &ctx->err));
@@ -1110,25 +1122,50 @@ int prepare_window_formats(rbl_ctx* ctx, const std::vector<int64_t>& rp) {
     };
     int64_t maxp = 0, staged = 0;
     plan(512, nullptr, &maxp, &staged);
+#ifdef RBL_PANEL_RPG  // (probe builds: tools/build_variant.sh-style A/B of the kernel shape)
+    const int rpg = RBL_PANEL_RPG;
+#else
     const int rpg = (double)ctx->nnz <= 12.0 * (double)(staged / pw) * 512 ? 8 : 4;
+#endif
     const int R = 64 * rpg;
     std::vector<int32_t> bp;
     const int64_t nb = plan(R, &bp, &maxp, &staged);
     const int64_t ncnt = bp.empty() ? 0 : ((int64_t)(uint32_t)bp[4 * nb - 2] | ((int64_t)bp[4 * nb - 1] << 32)) +
                                               ((int64_t)bp[4 * nb - 3] - bp[4 * nb - 4] + 1) * R;
-    if (maxp <= kPanelMax && ctx->n / pw < INT32_MAX) {
+    // the kernel addresses a block's records with 32-bit buffer offsets: every block's
+    // values within 2 GiB (the block bases, rowptr[b R], read strided)
+    int64_t maxblk = 0;
+    if (maxp <= kPanelMax && ctx->n / pw < INT32_MAX && nb > 0) {
+      std::vector<int64_t> zb(nb + 1);
+      HIPC(hipMemcpy2D(zb.data(), sizeof(int64_t), ctx->d_rowptr, (size_t)R * sizeof(int64_t),
+                       sizeof(int64_t), (size_t)nb, hipMemcpyDeviceToHost));
+      zb[nb] = ctx->nnz;
+      for (int64_t bk = 0; bk < nb; ++bk) maxblk = std::max(maxblk, zb[bk + 1] - zb[bk]);
+    }
+    bool fits = maxp <= kPanelMax && ctx->n / pw < INT32_MAX && nb > 0 && maxblk * 8 < INT32_MAX;
+    // the records are a second copy of the matrix: without room for it, no panels (the gathers)
+    if (fits && hipMalloc(&ctx->d_panel_val, std::max<int64_t>(ctx->nnz, 1) * sizeof(double)) != hipSuccess) {
+      (void)hipGetLastError();
+      ctx->d_panel_val = nullptr;
+      fits = false;
+    }
+    if (fits) {
+      HIPC(hipMalloc(&ctx->d_panel_col, std::max<int64_t>(ctx->nnz, 1)));
       HIPC(hipMalloc(&ctx->d_panel_blk, 4 * nb * sizeof(int32_t)));
       HIPC(hipMemcpy(ctx->d_panel_blk, bp.data(), 4 * nb * sizeof(int32_t), hipMemcpyHostToDevice));
       HIPC(hipMalloc(&ctx->d_panel_cnt, std::max<int64_t>(ncnt, 1) * sizeof(uint16_t)));
+      HIPC(hipMalloc(&ctx->d_panel_st, std::max<int64_t>(ncnt, 1) * sizeof(uint32_t)));
       CsrDev A2 = csr(ctx);
-      if (panel_counts(A2, ctx->d_panel_blk, R, ctx->d_panel_cnt, ncnt, ctx->stream) != 0)
-        return fail(ctx, RBL_ERR_HIP, "panel_counts");
+      if (panel_format(A2, ctx->d_panel_blk, R, nb, ctx->d_panel_cnt, ctx->d_panel_st, ncnt,
+                       ctx->d_panel_col, ctx->d_panel_val, ctx->stream) != 0)
+        return fail(ctx, RBL_ERR_HIP, "panel_format");
       HIPC(hipStreamSynchronize(ctx->stream));
       ctx->panel_nblk = nb;
       ctx->panel_rpg = rpg;
       // by default only where the panels pay: a staged Q row read >= 4 times from LDS on
       // average (bands; a scattered pattern's blocks span the whole matrix: the gathers)
       ctx->panel_auto = 4 * staged <= ctx->nnz;
+      ctx->panel_span = maxp * pw;
       if (!ctx->d_zrow) {  // the panel rows outside the Q range read it
         HIPC(hipMalloc(&ctx->d_zrow, 64 * sizeof(double)));
         HIPC(hipMemset(ctx->d_zrow, 0, 64 * sizeof(double)));
@@ -2084,7 +2121,11 @@ void free_matrix(rbl_ctx* ctx) {
   hipFree(ctx->d_tcmax); ctx->d_tcmax = nullptr;
   hipFree(ctx->d_tinfo); ctx->d_tinfo = nullptr;
   hipFree(ctx->d_panel_blk); ctx->d_panel_blk = nullptr; ctx->panel_nblk = 0; ctx->panel_auto = false;
+  ctx->panel_span = 0;
   hipFree(ctx->d_panel_cnt); ctx->d_panel_cnt = nullptr;
+  hipFree(ctx->d_panel_st); ctx->d_panel_st = nullptr;
+  hipFree(ctx->d_panel_col); ctx->d_panel_col = nullptr;
+  hipFree(ctx->d_panel_val); ctx->d_panel_val = nullptr;
   hipFree(ctx->d_bpos); ctx->d_bpos = nullptr;
   hipFree(ctx->d_bt); ctx->d_bt = nullptr;
   hipFree(ctx->d_bth); ctx->d_bth = nullptr;

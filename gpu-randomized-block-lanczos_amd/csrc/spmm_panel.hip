@@ -1,10 +1,11 @@
-// spmm_panel.hip — column-panel CSR SpMM for wide bands (gfx950), b = 32, fp64.
+// spmm_panel.hip — column-panel SpMM for wide bands (gfx950), b = 32, fp64.
 //
 // U = A * Q_i  (+ the 3-term epilogue U -= Q_{i-1} B_i^T), RBL_gpu.jl:176-177, for matrices
 // whose rows reach further than the band-tile (|c - r| <= 64) and LDS-window (a 256-row ring)
 // kernels allow — the FEM / circuit orderings of the reference's benchmark.jl:21-28 inputs,
-// bandwidths in the hundreds to thousands.  HBM-bound: per launch nnz * (8 + 4) + (n + 1) * 8 +
-// n * b * 8 * (2 + EPI) bytes, plus the Q panels each row block stages.
+// bandwidths in the hundreds to thousands.  HBM-bound: SURVEY §8(d) prices a launch at
+// nnz * (8 + 4) + (n + 1) * 8 + n * b * 8 * (2 + EPI) bytes; this kernel streams nnz * (8 + 1)
+// record bytes plus the Q panels each row block stages.
 //
 // A workgroup (1024 threads, one per CU, persistent) owns row blocks of R = 64 RPG rows.  A
 // block's columns span [cmin, cmax]; that window is walked in column panels of kPanel = 256 Q
@@ -12,20 +13,26 @@
 // (global_load_lds_dwordx4): while panel p is multiplied the next one streams into the other
 // buffer, and one barrier per panel swaps them.  A Q row is read from L2 / HBM once per block
 // and then from LDS once per nonzero (the 256 B per nonzero are the kernel's main on-chip
-// traffic: ds_read_b128, 256 B/clk/CU).  R trades registers for staging: the panels cost
-// (R + 2H) / R Q blocks of traffic per launch.
+// traffic: ds_read_b128).  R trades registers for staging: the panels cost (R + 2H) / R Q
+// blocks of traffic per launch.
+//
+// The format (panel_format, built once per matrix): within a block the CSR records are
+// regrouped panel-major — panel by panel, and within a panel row by row, each row's entries in
+// column order (so every row's sum runs in the CSR's own order) — with the column stored as one
+// byte, its offset in the panel.  A step (block, panel) therefore reads one contiguous run of
+// records, and no cache line is fetched by two steps; per row and panel the format holds the
+// count (uint16) and the first record (uint32 from the block's base).
 //
 //   * rows: 16-lane group G = tid / 16 (64 per workgroup) owns rows G + 64 k (k < RPG) of the
 //     block; lane li holds columns 2 li, 2 li + 1 of each row's accumulator
-//   * the format (panel_counts) counts every row's entries in every panel of its block's window
-//     (uint16): the kernel knows each row's count in panel p before it reads a column index,
-//     so it loads exactly those entries (buffer loads; lanes past the count are out of range:
-//     no traffic), CH per row per load (more in a loop) — the next step's right after the row's
-//     entries in this one, into the same registers — and the counts two steps ahead
+//   * a row's records in panel p: CH per load (more in a loop) — the next step's right after the
+//     row's entries in this one, into the same registers; count and start two steps ahead.
+//     Lanes past the count load out of range (buffer loads: no traffic, value 0, column 0), so
+//     they multiply panel row 0 by zero with no mask
 //   * per entry: v_add_u32_dpp forms the Q row's LDS address from the broadcast offset
 //     (row_newbcast), one ds_read_b128, and two v_fmac_f64_dpp with the broadcast value; the
 //     four groups of a wave step through their rows' counts together (the wave loops to the
-//     largest; masked entries multiply a row of finite data by zero)
+//     largest)
 //   * hipcc drains an in-flight LDS-DMA at the first use of any ordinary load's result, so a
 //     step first touches everything the step before loaded, then issues its DMA and the loads
 //     for the next steps; the barrier waits for the DMA with a counted vmcnt, leaving those in
@@ -53,7 +60,7 @@ constexpr int kPanelBytes = kPanel * kRowBytes;  // 64 KiB
 constexpr int kBtBytes = kB * 16 * 16;           // B_i^T table: [u][lane] double2
 constexpr size_t kLds = 2 * (size_t)kPanelBytes + kBtBytes;
 constexpr int kXcds = 8;
-constexpr unsigned kOob = 0x10000000u;           // an entry offset past any block's records
+constexpr unsigned kOob = 0x10000000u;           // a record offset past any block's records
 }  // namespace pnl
 
 namespace {
@@ -98,11 +105,12 @@ __device__ __forceinline__ void touch(double x) { asm volatile("" ::"v"(x)); }
 struct PanelArgs {
   int64_t nrows;             // local rows
   int64_t nblk;              // blocks of 64 RPG rows
-  const int64_t* rowptr;
-  const int32_t* col;
-  const double* val;
+  const int64_t* rowptr;     // a block's base: rowptr[b R]
+  const uint8_t* pcol;       // the panel-major records: column within the panel
+  const double* pval;        //   and value
   const int32_t* binfo;      // per block: first panel, last panel, count offset (2 x int32)
   const uint16_t* cnt;       // per block and panel of its window: R counts (entries per row)
+  const uint32_t* st;        // ... and R first records (from the block's base)
   const double* Q;           // Q row c at Q + (c - col_off) * 32, rows [q_lo, q_hi)
   int64_t col_off, q_lo, q_hi;
   const double* zrow;        // >= 32 zeros: the panel rows outside [q_lo, q_hi)
@@ -116,7 +124,7 @@ __global__ __launch_bounds__(pnl::kThreads) void k_spmm_panel(PanelArgs a) {
   using namespace pnl;
   constexpr int R = kGroups * RPG;
   constexpr int NCR = CH / 16;  // chunk registers per row
-  static_assert(CH == 16 || CH == 32, "chunk of 16 or 32 entries per row");
+  static_assert(CH % 16 == 0 && CH <= 64, "chunks of 16 to 64 entries per row");
   constexpr int kVm = 2 * NCR * RPG;  // chunk loads per step (the barrier's vmcnt)
   typedef double d2v __attribute__((ext_vector_type(2)));
   typedef __attribute__((address_space(3))) const d2v lds_d2;
@@ -151,7 +159,6 @@ __global__ __launch_bounds__(pnl::kThreads) void k_spmm_panel(PanelArgs a) {
   typedef __attribute__((address_space(4))) const int32_t c_i32;
   c_i64* rp_s = (c_i64*)a.rowptr;
   c_i32* bi_s = (c_i32*)a.binfo;
-  const int* rp32 = reinterpret_cast<const int*>(a.rowptr);  // low words: offsets in a block
 
   // a step of the workgroup's sweep: (block, panel index within the block's window)
   struct Step {
@@ -175,7 +182,7 @@ __global__ __launch_bounds__(pnl::kThreads) void k_spmm_panel(PanelArgs a) {
   auto next_step = [&](const Step& s) -> Step {
     if (s.blk < xb1 && s.pi + 1 < s.np) {
       Step t = s;
-      t.pi = s.pi + 1;
+      ++t.pi;
       return t;
     }
     return block_step(s.blk < xb1 ? s.blk + nper : s.blk);
@@ -187,8 +194,8 @@ __global__ __launch_bounds__(pnl::kThreads) void k_spmm_panel(PanelArgs a) {
   auto rsrc_of = [&](int64_t b, __amdgpu_buffer_rsrc_t& rc, __amdgpu_buffer_rsrc_t& rv) {
     const int64_t z0 = block_base(b), z1 = block_base(b + 1);
     const int64_t n = z1 - z0;
-    rc = __builtin_amdgcn_make_buffer_rsrc(const_cast<int32_t*>(a.col + z0), 0, (int)(n * 4), 0x00020000);
-    rv = __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(a.val + z0), 0, (int)(n * 8), 0x00020000);
+    rc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(a.pcol + z0), 0, (int)n, 0x00020000);
+    rv = __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(a.pval + z0), 0, (int)(n * 8), 0x00020000);
   };
 
   // ---- panel staging: LDS-DMA, no staging registers.  Wave w's instruction i writes 1 KiB =
@@ -205,7 +212,7 @@ __global__ __launch_bounds__(pnl::kThreads) void k_spmm_panel(PanelArgs a) {
       __builtin_amdgcn_global_load_lds(src, smem + buf * kPanelBytes + rl * kRowBytes, 16, 0, 0);
     }
   };
-  // entries [c0, c0 + min(m, CH)) of a row into chunk registers (lane li: c0 + li, + 16);
+  // records [c0, c0 + min(m, CH)) of a row into chunk registers (lane li: c0 + li, + 16);
   // lanes past m load nothing (an offset past the block's records reads 0)
   auto load_chunk = [&](int (&cc)[NCR], double (&vv)[NCR], int c0, int m, __amdgpu_buffer_rsrc_t rc,
                         __amdgpu_buffer_rsrc_t rv) {
@@ -213,49 +220,39 @@ __global__ __launch_bounds__(pnl::kThreads) void k_spmm_panel(PanelArgs a) {
     for (int r = 0; r < NCR; ++r) {
       const int e = 16 * r + li;
       const unsigned o = e < m ? (unsigned)(c0 + e) : kOob;
-      cc[r] = __builtin_amdgcn_raw_buffer_load_b32(rc, (int)(o * 4u), 0, 0);
+      cc[r] = __builtin_amdgcn_raw_buffer_load_b8(rc, (int)o, 0, 0);
       vv[r] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rv, (int)(o * 8u), 0, 0));
     }
   };
-  // a step's counts: lane li < RPG holds row k = li's (rows past the slice were counted 0)
-  auto load_counts = [&](const Step& s) -> int {
-    if (s.blk >= xb1 || li >= RPG) return 0;
-    return a.cnt[s.coff + (int64_t)s.pi * R + grp + 64 * li];
-  };
-  // a block's row starts (low words of rowptr)
-  auto load_starts = [&](int64_t b, int (&c)[RPG]) {
-#pragma unroll
-    for (int k = 0; k < RPG; ++k) {
-      const int64_t r = b * R + grp + 64 * k;
-      c[k] = rp32[2 * (r < a.nrows ? r : a.nrows)];
-    }
+  // a step's counts and first records: lane li < RPG holds row k = li's (rows past the slice
+  // were counted 0)
+  auto load_cs = [&](const Step& s, int& m, int& c0) {
+    m = c0 = 0;
+    if (s.blk >= xb1 || li >= RPG) return;
+    const int64_t i = s.coff + (int64_t)s.pi * R + grp + 64 * li;
+    m = a.cnt[i];
+    c0 = (int)a.st[i];
   };
 
-  int cur[RPG];             // row cursors, relative to the block's first nonzero
-  int nxt[RPG] = {};        // the next block's row starts (raw low words), loaded a step early
   double acc[RPG][2];
-  int cc[RPG][NCR];         // each row's chunk: the current step's entries, then the next's
+  int cc[RPG][NCR];         // each row's chunk: the current step's records, then the next's
   double vv[RPG][NCR];
 #pragma unroll
   for (int k = 0; k < RPG; ++k) acc[k][0] = acc[k][1] = 0.0;
 
-  // ---- prologue: step 0's counts, cursors, chunks and panel; step 1's counts (and its
-  // block's starts if it begins one) ----
+  // ---- prologue: step 0's counts, starts, chunks and panel; step 1's counts and starts ----
   Step st = block_step(blk0);
   Step st1 = next_step(st);
-  int64_t nzb = block_base(blk0);
   __amdgpu_buffer_rsrc_t rc, rv;
   rsrc_of(blk0, rc, rv);
-  load_starts(blk0, cur);
-  int cnt_cur = load_counts(st);
-#pragma unroll
-  for (int k = 0; k < RPG; ++k) cur[k] -= (int)nzb;
+  int cnt_cur, s_cur;
+  load_cs(st, cnt_cur, s_cur);
   pfor<0, RPG>([&](auto kc) {
     constexpr int k = decltype(kc)::value;
-    load_chunk(cc[k], vv[k], cur[k], pnl_bcast<k>(cnt_cur), rc, rv);
+    load_chunk(cc[k], vv[k], pnl_bcast<k>(s_cur), pnl_bcast<k>(cnt_cur), rc, rv);
   });
-  int cnt_nxt = load_counts(st1);
-  if (st1.blk < xb1 && st1.pi == 0) load_starts(st1.blk, nxt);
+  int cnt_nxt, s_nxt;
+  load_cs(st1, cnt_nxt, s_nxt);
   load_panel(st.p0, 0);
   __syncthreads();  // (drains everything: the prologue's loads and DMA)
 
@@ -265,8 +262,6 @@ __global__ __launch_bounds__(pnl::kThreads) void k_spmm_panel(PanelArgs a) {
     const Step sn = st1;
     const bool have_next = sn.blk < xb1;
     const Step sn2 = next_step(sn);
-    const int p = st.p0 + st.pi;
-    const int64_t pbase = (int64_t)p * kPanel;
     const unsigned bufb = lds_base + (unsigned)(buf * kPanelBytes);
 
     // (1) everything the step before loaded, waited for here — before this step's DMA
@@ -277,28 +272,26 @@ __global__ __launch_bounds__(pnl::kThreads) void k_spmm_panel(PanelArgs a) {
         touch(cc[k][r]);
         touch(vv[k][r]);
       }
-      touch(nxt[k]);
     }
     touch(cnt_cur);
+    touch(s_cur);
     touch(cnt_nxt);
+    touch(s_nxt);
     __builtin_amdgcn_sched_barrier(0);
 
     // (2) the next step's panel, then the loads the next steps need (younger than the DMA)
     if (have_next) load_panel(sn.p0 + sn.pi, buf ^ 1);
     asm volatile("" ::: "memory");
-    const int cnt_nn = have_next ? load_counts(sn2) : 0;
+    int cnt_nn = 0, s_nn = 0;
+    if (have_next) load_cs(sn2, cnt_nn, s_nn);
     // where the next step's chunks come from: this block, or the next one
     __amdgpu_buffer_rsrc_t rcn = rc, rvn = rv;
-    int64_t nzb_n = nzb;
-    if (have_next && last_panel) {
-      nzb_n = block_base(sn.blk);
-      rsrc_of(sn.blk, rcn, rvn);
-    }
+    if (have_next && last_panel) rsrc_of(sn.blk, rcn, rvn);
 
-    // (3) multiply panel p, row by row; each row's chunk for the next step follows its entries
+    // (3) multiply the panel, row by row; each row's chunk for the next step follows its entries
     pfor<0, RPG>([&](auto kc) {
       constexpr int k = decltype(kc)::value;
-      const int m = pnl_bcast<k>(cnt_cur);  // this group's row k: entries in panel p
+      const int m = pnl_bcast<k>(cnt_cur);  // this group's row k: entries in the panel
       // the largest count of the wave's four groups (lanes 0, 16, 32, 48 hold them)
       const int mmax = max(max(__builtin_amdgcn_readlane(m, 0), __builtin_amdgcn_readlane(m, 16)),
                            max(__builtin_amdgcn_readlane(m, 32), __builtin_amdgcn_readlane(m, 48)));
@@ -323,14 +316,18 @@ __global__ __launch_bounds__(pnl::kThreads) void k_spmm_panel(PanelArgs a) {
         unsigned u[NCR];
         double x[NCR];
 #pragma unroll
-        for (int r = 0; r < NCR; ++r) {  // masked entries: row 0 (finite), value 0 (loaded)
-          const bool ok = done + 16 * r + li < m;
-          u[r] = ok ? bufb + (unsigned)((cc[k][r] - pbase) * kRowBytes) : bufb;
+        for (int r = 0; r < NCR; ++r) {  // lanes past the count: column 0, value 0 (loaded)
+          u[r] = bufb + ((unsigned)cc[k][r] << 8);
           x[r] = vv[k][r];
         }
         // VALU write -> DPP read needs 2 wait states; hipcc does not pad inside asm
+        if constexpr (NCR == 1) asm volatile("s_nop 1" : "+v"(u[0]), "+v"(x[0]));
         if constexpr (NCR == 2) asm volatile("s_nop 1" : "+v"(u[0]), "+v"(u[1]), "+v"(x[0]), "+v"(x[1]));
-        else asm volatile("s_nop 1" : "+v"(u[0]), "+v"(x[0]));
+        if constexpr (NCR == 3)
+          asm volatile("s_nop 1" : "+v"(u[0]), "+v"(u[1]), "+v"(u[2]), "+v"(x[0]), "+v"(x[1]), "+v"(x[2]));
+        if constexpr (NCR == 4)
+          asm volatile("s_nop 1" : "+v"(u[0]), "+v"(u[1]), "+v"(u[2]), "+v"(u[3]), "+v"(x[0]), "+v"(x[1]),
+                       "+v"(x[2]), "+v"(x[3]));
         const int left = mmax - done;
         pfor<0, NCR>([&](auto rr) {
           constexpr int RR = decltype(rr)::value;
@@ -343,17 +340,12 @@ __global__ __launch_bounds__(pnl::kThreads) void k_spmm_panel(PanelArgs a) {
       // more than CH entries in this panel in some group: the next CH, loaded here (rare
       // when CH covers the typical count)
       for (int done = CH; done < mmax; done += CH) {
-        load_chunk(cc[k], vv[k], cur[k] + done, m - done, rc, rv);
+        load_chunk(cc[k], vv[k], pnl_bcast<k>(s_cur) + done, m - done, rc, rv);
         run(done);
       }
-      // the next step's entries of this row
-      if (have_next) {
-        cur[k] = last_panel ? nxt[k] - (int)nzb_n : cur[k] + m;
-        load_chunk(cc[k], vv[k], cur[k], pnl_bcast<k>(cnt_nxt), rcn, rvn);
-      }
+      // the next step's records of this row
+      if (have_next) load_chunk(cc[k], vv[k], pnl_bcast<k>(s_nxt), pnl_bcast<k>(cnt_nxt), rcn, rvn);
     });
-    // the starts of the block the step after next begins, if it does
-    if (sn2.blk < xb1 && sn2.pi == 0) load_starts(sn2.blk, nxt);
 
     // (4) block end: epilogue, store U
     if (last_panel) {
@@ -396,11 +388,12 @@ __global__ __launch_bounds__(pnl::kThreads) void k_spmm_panel(PanelArgs a) {
     asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)" ::"n"(kVm) : "memory");
     __builtin_amdgcn_s_barrier();
     buf ^= 1;
-    nzb = nzb_n;
     rc = rcn;
     rv = rvn;
     cnt_cur = cnt_nxt;
+    s_cur = s_nxt;
     cnt_nxt = cnt_nn;
+    s_nxt = s_nn;
     st = sn;
     st1 = sn2;
   }
@@ -411,15 +404,18 @@ __global__ __launch_bounds__(pnl::kThreads) void k_spmm_panel(PanelArgs a) {
 // panel is mostly <= 16, 32-entry chunks at 4 rows per group otherwise (registers)
 bool spmm_panel(const CsrDev& A, const double* Qin, int64_t col_off, int b, double* U,
                 const double* Qprev, const double* Bi, hipStream_t s) {
-  if (b != 32 || !A.panel_blk || A.panel_nblk <= 0 || !A.panel_cnt || !A.zrow) return false;
+  if (b != 32 || !A.panel_blk || A.panel_nblk <= 0 || !A.panel_cnt || !A.panel_st || !A.panel_col ||
+      !A.panel_val || !A.zrow)
+    return false;
   PanelArgs a;
   a.nrows = A.nrows;
   a.nblk = A.panel_nblk;
   a.rowptr = A.rowptr;
-  a.col = A.col;
-  a.val = A.val;
+  a.pcol = A.panel_col;
+  a.pval = A.panel_val;
   a.binfo = A.panel_blk;
   a.cnt = A.panel_cnt;
+  a.st = A.panel_st;
   a.Q = Qin;
   a.col_off = col_off;
   a.q_lo = A.q_lo;
@@ -435,6 +431,11 @@ bool spmm_panel(const CsrDev& A, const double* Qin, int64_t col_off, int b, doub
     ensure_lds_attr(reinterpret_cast<const void*>(kern), (int)pnl::kLds);
     hipLaunchKernelGGL(kern, dim3(grid), dim3(pnl::kThreads), pnl::kLds, s, a);
   };
+#ifdef RBL_PANEL_RPG  // (probe builds: one shape for every matrix)
+  if (Qprev) go(&k_spmm_panel<true, RBL_PANEL_RPG, RBL_PANEL_CH>);
+  else go(&k_spmm_panel<false, RBL_PANEL_RPG, RBL_PANEL_CH>);
+  return true;
+#endif
   if (A.panel_rpg == 8) {
     if (Qprev) go(&k_spmm_panel<true, 8, 16>); else go(&k_spmm_panel<false, 8, 16>);
   } else {
@@ -445,8 +446,10 @@ bool spmm_panel(const CsrDev& A, const double* Qin, int64_t col_off, int b, doub
 
 int panel_width() { return pnl::kPanel; }
 
-// ---- the format: per block of R rows its panel range (binfo) and the count of every row's
-// entries in every panel of the range (cnt, zero-filled first) ----
+// ---- the format.  Per block of R rows: its panel range and count offset (binfo, host-made);
+// the count of every row's entries in every panel of the range (cnt, zero-filled first); their
+// first records, an exclusive scan of the block's counts in (panel, row) order (st); the
+// records regrouped in that order (pcol / pval) ----
 __global__ void k_panel_counts(int64_t nrows, const int64_t* __restrict__ rowptr,
                                const int32_t* __restrict__ col, const int32_t* __restrict__ binfo,
                                int R, uint16_t* __restrict__ cnt) {
@@ -469,12 +472,74 @@ __global__ void k_panel_counts(int64_t nrows, const int64_t* __restrict__ rowptr
   if (pc >= 0) cnt[coff + (int64_t)(pc - p0) * R + rl] = (uint16_t)n;
 }
 
-int panel_counts(const CsrDev& A, const int32_t* binfo, int R, uint16_t* cnt, int64_t ncnt,
-                 hipStream_t s) {
+// one workgroup (256 threads) per block: the exclusive scan of its counts, 256 at a time
+__global__ __launch_bounds__(256) void k_panel_starts(const int32_t* __restrict__ binfo, int R,
+                                                      const uint16_t* __restrict__ cnt,
+                                                      uint32_t* __restrict__ st) {
+  __shared__ uint32_t wsum[4];
+  const int64_t b = blockIdx.x;
+  const int np = binfo[4 * b + 1] - binfo[4 * b] + 1;
+  const int64_t coff = (int64_t)(uint32_t)binfo[4 * b + 2] | ((int64_t)binfo[4 * b + 3] << 32);
+  const int64_t len = (int64_t)np * R;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint32_t carry = 0;
+  for (int64_t i0 = 0; i0 < len; i0 += 256) {
+    const int64_t i = i0 + threadIdx.x;
+    const uint32_t v = i < len ? cnt[coff + i] : 0u;
+    uint32_t x = v;  // inclusive scan within the wave
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t y = __shfl_up(x, d, 64);
+      if (lane >= d) x += y;
+    }
+    if (lane == 63) wsum[w] = x;
+    __syncthreads();
+    uint32_t before = carry;
+    for (int k = 0; k < w; ++k) before += wsum[k];
+    const uint32_t total = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    if (i < len) st[coff + i] = before + x - v;
+    carry += total;
+    __syncthreads();
+  }
+}
+
+__global__ void k_panel_scatter(int64_t nrows, const int64_t* __restrict__ rowptr,
+                                const int32_t* __restrict__ col, const double* __restrict__ val,
+                                const int32_t* __restrict__ binfo, int R,
+                                const uint32_t* __restrict__ st, uint8_t* __restrict__ pcol,
+                                double* __restrict__ pval) {
+  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= nrows) return;
+  const int64_t b = r / R;
+  const int p0 = binfo[4 * b];
+  const int64_t coff = (int64_t)(uint32_t)binfo[4 * b + 2] | ((int64_t)binfo[4 * b + 3] << 32);
+  const int rl = (int)(r - b * R);
+  const int64_t zb = rowptr[b * R];
+  int pc = -1;
+  int64_t o = 0;
+  for (int64_t e = rowptr[r]; e < rowptr[r + 1]; ++e) {
+    const int c = col[e];
+    const int p = c / pnl::kPanel;
+    if (p != pc) {
+      pc = p;
+      o = zb + st[coff + (int64_t)(p - p0) * R + rl];
+    }
+    pcol[o] = (uint8_t)(c - p * pnl::kPanel);
+    pval[o] = val[e];
+    ++o;
+  }
+}
+
+int panel_format(const CsrDev& A, const int32_t* binfo, int R, int64_t nblk, uint16_t* cnt,
+                 uint32_t* st, int64_t ncnt, uint8_t* pcol, double* pval, hipStream_t s) {
   if (hipMemsetAsync(cnt, 0, (size_t)ncnt * sizeof(uint16_t), s) != hipSuccess) return -1;
-  if (A.nrows > 0)
-    hipLaunchKernelGGL(k_panel_counts, dim3((unsigned)((A.nrows + 255) / 256)), dim3(256), 0, s,
-                       A.nrows, A.rowptr, A.col, binfo, R, cnt);
+  if (A.nrows > 0) {
+    const dim3 g((unsigned)((A.nrows + 255) / 256));
+    hipLaunchKernelGGL(k_panel_counts, g, dim3(256), 0, s, A.nrows, A.rowptr, A.col, binfo, R, cnt);
+    hipLaunchKernelGGL(k_panel_starts, dim3((unsigned)nblk), dim3(256), 0, s, binfo, R, cnt, st);
+    hipLaunchKernelGGL(k_panel_scatter, g, dim3(256), 0, s, A.nrows, A.rowptr, A.col, A.val, binfo,
+                       R, st, pcol, pval);
+  }
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

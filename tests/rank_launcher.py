@@ -26,8 +26,8 @@ def run(req):
     env.update(req.get("env", {}))
     # every rank shares the one GPU: past 24 hardware queues in all its scheduler time-slices
     # whole processes (bench.py's shared_gpu_queues)
-    if "GPU_MAX_HW_QUEUES" not in env:
-        env["GPU_MAX_HW_QUEUES"] = str(max(1, min(4, 24 // max(1, len(req["cmds"])))))
+    cap = max(1, min(4, 24 // max(1, len(req["cmds"]))))
+    env["GPU_MAX_HW_QUEUES"] = str(min(int(env.get("GPU_MAX_HW_QUEUES") or 4), cap))
     procs, logs = [], []
     for argv in req["cmds"]:
         f = tempfile.TemporaryFile()
