@@ -223,18 +223,17 @@ def launch_ranks(args) -> None:
     sys.exit(subprocess.run(cmd, env=env).returncode)
 
 
-# Hardware queues the GPU's scheduler keeps mapped for all processes together in the one-GPU
-# rehearsals: measured, 6 processes x 4 queues (HIP's default) run at the P = 4 rate per
-# collective and 7 x 4 time-slice whole processes (every collective then waits ~13-44 ms);
-# DESIGN.md §6, profiles/r06_p8_*.
-SHARED_GPU_QUEUE_BUDGET = 24
+# Processes sharing one GPU in the rehearsals (measured, DESIGN.md §6, profiles/r06_p8_*): up to
+# 6 run at the P = 4 rate per collective with HIP's default 4 hardware queues each; 7 and 8
+# processes time-slice (every collective then waits ~10-45 ms) with 4 or 3 queues each, and run
+# at the P = 4 rate again with 1 (the streams of a process then share its one queue).
+SHARED_GPU_FULL_QUEUES_UP_TO = 6
 
 
 def shared_gpu_queues(ranks_per_gpu: int) -> int:
     """GPU_MAX_HW_QUEUES for ranks that share a GPU (the rehearsal of an N-GPU job on fewer
-    GPUs; never set for one rank per GPU): HIP's default 4 while the ranks' queues fit the
-    scheduler's budget, fewer beyond (the streams of a process then share its queues)."""
-    return max(1, min(4, SHARED_GPU_QUEUE_BUDGET // max(1, ranks_per_gpu)))
+    GPUs; never set for one rank per GPU)."""
+    return 4 if ranks_per_gpu <= SHARED_GPU_FULL_QUEUES_UP_TO else 1
 
 
 def rccl_host_per_rank() -> bool:

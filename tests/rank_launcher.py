@@ -24,9 +24,9 @@ import time
 def run(req):
     env = dict(os.environ)
     env.update(req.get("env", {}))
-    # every rank shares the one GPU: past 24 hardware queues in all its scheduler time-slices
-    # whole processes (bench.py's shared_gpu_queues)
-    cap = max(1, min(4, 24 // max(1, len(req["cmds"]))))
+    # every rank shares the one GPU: past 6 processes with HIP's default queues its scheduler
+    # time-slices whole processes (bench.py's shared_gpu_queues)
+    cap = 4 if len(req["cmds"]) <= 6 else 1
     env["GPU_MAX_HW_QUEUES"] = str(min(int(env.get("GPU_MAX_HW_QUEUES") or 4), cap))
     procs, logs = [], []
     for argv in req["cmds"]:
