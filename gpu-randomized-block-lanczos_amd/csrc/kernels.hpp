@@ -54,6 +54,7 @@ struct CsrDev {
   const double* panel_val = nullptr;    //   base (one byte), value
   int64_t panel_nblk = 0;
   int panel_rpg = 4;         // rows per 16-lane group (blocks of 64 rpg rows): 4 or 8
+  int panel_ch = 32;         // records per row and chunk load: 16 or 32
   bool panel_auto = false;   // the automatic choice takes it (else only when forced)
   bool window_ok16 = false;
   bool window_ok32 = false;

@@ -48,6 +48,7 @@ struct rbl_ctx {
   double* d_panel_val = nullptr;    //   and value
   int64_t panel_nblk = 0;
   int panel_rpg = 4;        // rows per 16-lane group: blocks of 64 panel_rpg rows
+  int panel_ch = 32;        // records per row and chunk load
   bool panel_auto = false;  // chosen by default: every staged Q row used >= 4 times on average
   int64_t panel_span = 0;   // the widest block window, Q rows
   uint16_t* d_bpos = nullptr;  // band kernel: per-nonzero dense-tile positions
@@ -335,6 +336,7 @@ CsrDev csr(rbl_ctx* ctx) {
   A.panel_col = ctx->d_panel_col;
   A.panel_val = ctx->d_panel_val;
   A.panel_rpg = ctx->panel_rpg;
+  A.panel_ch = ctx->panel_ch;
   A.ntiles = ctx->ntiles;
   A.tiles_per_wg = ctx->tiles_per_wg;
   A.window_ok16 = ctx->window_ok16;
@@ -1122,10 +1124,15 @@ int prepare_window_formats(rbl_ctx* ctx, const std::vector<int64_t>& rp) {
     };
     int64_t maxp = 0, staged = 0;
     plan(512, nullptr, &maxp, &staged);
+    // the kernel's shape by the mean count per row and panel at 512-row blocks: 8 rows per
+    // group with 16-record chunks up to a mean of 16, else 4 rows per group with 32-record
+    // chunks (profiles/r06_panel_shape_sweep_b13.txt)
+    const double mean_cnt = (double)ctx->nnz / std::max(1.0, (double)(staged / pw) * 512);
 #ifdef RBL_PANEL_RPG  // (probe builds: tools/build_variant.sh-style A/B of the kernel shape)
-    const int rpg = RBL_PANEL_RPG;
+    const int rpg = RBL_PANEL_RPG, pch = RBL_PANEL_CH;
 #else
-    const int rpg = (double)ctx->nnz <= 12.0 * (double)(staged / pw) * 512 ? 8 : 4;
+    const int rpg = mean_cnt <= 16.0 ? 8 : 4;
+    const int pch = rpg == 8 ? 16 : 32;
 #endif
     const int R = 64 * rpg;
     std::vector<int32_t> bp;
@@ -1162,6 +1169,7 @@ int prepare_window_formats(rbl_ctx* ctx, const std::vector<int64_t>& rp) {
       HIPC(hipStreamSynchronize(ctx->stream));
       ctx->panel_nblk = nb;
       ctx->panel_rpg = rpg;
+      ctx->panel_ch = pch;
       // by default only where the panels pay: a staged Q row read >= 4 times from LDS on
       // average (bands; a scattered pattern's blocks span the whole matrix: the gathers)
       ctx->panel_auto = 4 * staged <= ctx->nnz;

@@ -61,6 +61,17 @@ constexpr int kBtBytes = kB * 16 * 16;           // B_i^T table: [u][lane] doubl
 constexpr size_t kLds = 2 * (size_t)kPanelBytes + kBtBytes;
 constexpr int kXcds = 8;
 constexpr unsigned kOob = 0x10000000u;           // a record offset past any block's records
+// probe builds only (-DRBL_PANEL_ABLATE=mask, tools/build_variant.sh): 1 no FMAs, 2 no LDS
+// reads, 4 no panel DMA, 8 no record loads — wrong results, for timing what each part costs
+#ifndef RBL_PANEL_ABLATE
+#define RBL_PANEL_ABLATE 0
+#endif
+constexpr int kAbl = RBL_PANEL_ABLATE;
+// probe builds only (-DRBL_PANEL_STAMPS=1): workgroups 0 and 128 print the cycles their wave 0
+// spent in each phase of the step loop (s_memtime), once per launch
+#ifndef RBL_PANEL_STAMPS
+#define RBL_PANEL_STAMPS 0
+#endif
 }  // namespace pnl
 
 namespace {
@@ -96,6 +107,14 @@ __device__ __forceinline__ int pnl_bcast(int x) {
       : "=v"(r) : "v"(x), "n"(S));
   return r;
 }
+// the panel row at off (from lane S of the lane's 16-lane row) + lane_off: ds_read_b128 issued as
+// inline asm, so the compiler neither sinks it into the branch that uses it nor waits for it —
+// the caller waits (lgkmcnt) and keeps the destination live until then
+template <int S>
+__device__ __forceinline__ void pnl_read(double __attribute__((ext_vector_type(2)))& q, unsigned off,
+                                         unsigned lane_off) {
+  asm volatile("ds_read_b128 %0, %1" : "=v"(q) : "v"(pnl_addr<S>(off, lane_off)));
+}
 // make the compiler wait for a loaded register here (no instruction)
 __device__ __forceinline__ void touch(int x) { asm volatile("" ::"v"(x)); }
 __device__ __forceinline__ void touch(double x) { asm volatile("" ::"v"(x)); }
@@ -126,8 +145,9 @@ __global__ __launch_bounds__(pnl::kThreads) void k_spmm_panel(PanelArgs a) {
   constexpr int NCR = CH / 16;  // chunk registers per row
   static_assert(CH % 16 == 0 && CH <= 64, "chunks of 16 to 64 entries per row");
   constexpr int kVm = 2 * NCR * RPG;  // chunk loads per step (the barrier's vmcnt)
+  constexpr int QW = RPG == 8 ? 2 : 4;  // LDS reads per group in flight ahead (registers)
+  constexpr int NQ = 16 / QW;
   typedef double d2v __attribute__((ext_vector_type(2)));
-  typedef __attribute__((address_space(3))) const d2v lds_d2;
   typedef __attribute__((address_space(3))) unsigned char lds_u8;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x;
@@ -209,7 +229,8 @@ __global__ __launch_bounds__(pnl::kThreads) void k_spmm_panel(PanelArgs a) {
       const int64_t c = cb0 + rl + (lane >> 4);
       const double* src = (c >= a.q_lo && c < a.q_hi) ? a.Q + (c - a.col_off) * kB + 2 * li
                                                       : a.zrow + 2 * li;
-      __builtin_amdgcn_global_load_lds(src, smem + buf * kPanelBytes + rl * kRowBytes, 16, 0, 0);
+      if constexpr (!(kAbl & 4))
+        __builtin_amdgcn_global_load_lds(src, smem + buf * kPanelBytes + rl * kRowBytes, 16, 0, 0);
     }
   };
   // records [c0, c0 + min(m, CH)) of a row into chunk registers (lane li: c0 + li, + 16);
@@ -220,8 +241,13 @@ __global__ __launch_bounds__(pnl::kThreads) void k_spmm_panel(PanelArgs a) {
     for (int r = 0; r < NCR; ++r) {
       const int e = 16 * r + li;
       const unsigned o = e < m ? (unsigned)(c0 + e) : kOob;
-      cc[r] = __builtin_amdgcn_raw_buffer_load_b8(rc, (int)o, 0, 0);
-      vv[r] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rv, (int)(o * 8u), 0, 0));
+      if constexpr (kAbl & 8) {
+        cc[r] = (int)(o & 0xff);
+        vv[r] = 0.0;
+      } else {
+        cc[r] = __builtin_amdgcn_raw_buffer_load_b8(rc, (int)o, 0, 0);
+        vv[r] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rv, (int)(o * 8u), 0, 0));
+      }
     }
   };
   // a step's counts and first records: lane li < RPG holds row k = li's (rows past the slice
@@ -257,6 +283,20 @@ __global__ __launch_bounds__(pnl::kThreads) void k_spmm_panel(PanelArgs a) {
   __syncthreads();  // (drains everything: the prologue's loads and DMA)
 
   int buf = 0;
+#if RBL_PANEL_STAMPS
+  uint64_t ph[6] = {0, 0, 0, 0, 0, 0};
+  uint64_t tp = __builtin_readcyclecounter();
+  int nsteps = 0;
+  auto stamp = [&](int i) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const uint64_t t = __builtin_readcyclecounter();
+    ph[i] += t - tp;
+    tp = t;
+  };
+#define PNL_STAMP(i) stamp(i)
+#else
+#define PNL_STAMP(i) ((void)0)
+#endif
   for (;;) {
     const bool last_panel = st.pi + 1 == st.np;
     const Step sn = st1;
@@ -279,6 +319,7 @@ __global__ __launch_bounds__(pnl::kThreads) void k_spmm_panel(PanelArgs a) {
     touch(s_nxt);
     __builtin_amdgcn_sched_barrier(0);
 
+    PNL_STAMP(0);
     // (2) the next step's panel, then the loads the next steps need (younger than the DMA)
     if (have_next) load_panel(sn.p0 + sn.pi, buf ^ 1);
     asm volatile("" ::: "memory");
@@ -288,6 +329,7 @@ __global__ __launch_bounds__(pnl::kThreads) void k_spmm_panel(PanelArgs a) {
     __amdgpu_buffer_rsrc_t rcn = rc, rvn = rv;
     if (have_next && last_panel) rsrc_of(sn.blk, rcn, rvn);
 
+    PNL_STAMP(1);
     // (3) multiply the panel, row by row; each row's chunk for the next step follows its entries
     pfor<0, RPG>([&](auto kc) {
       constexpr int k = decltype(kc)::value;
@@ -297,20 +339,37 @@ __global__ __launch_bounds__(pnl::kThreads) void k_spmm_panel(PanelArgs a) {
                            max(__builtin_amdgcn_readlane(m, 32), __builtin_amdgcn_readlane(m, 48)));
       double& a0 = acc[k][0];
       double& a1 = acc[k][1];
-      // entries 2h, 2h + 1 of one chunk register: their two LDS reads, then their FMAs
-      auto pair = [&](unsigned off, double w, auto hh) {
-        constexpr int H = decltype(hh)::value;
-        d2v q[2];
-        pfor<0, 2>([&](auto ic) {
-          constexpr int S = 2 * H + decltype(ic)::value;
-          q[decltype(ic)::value] = *(lds_d2*)(size_t)pnl_addr<S>(off, lane_off);
+      // QW entries QW J .. QW J + QW - 1 of one chunk register: their LDS reads, issued one group
+      // ahead of their FMAs (a group's reads are in flight while the group before is multiplied)
+      auto readg = [&](d2v (&q)[QW], unsigned off, auto jc) {
+        constexpr int J = decltype(jc)::value;
+        pfor<0, QW>([&](auto ic) {
+          constexpr int S = QW * J + decltype(ic)::value;
+          if constexpr (kAbl & 2) {
+            q[decltype(ic)::value] = d2v{(double)pnl_addr<S>(off, lane_off), 0.0};
+          } else {
+            pnl_read<S>(q[decltype(ic)::value], off, lane_off);
+          }
         });
-        __builtin_amdgcn_sched_barrier(0);  // both reads in flight before the FMAs
-        pfor<0, 2>([&](auto ic) {
-          constexpr int S = 2 * H + decltype(ic)::value;
-          pnl_fma<S>(a0, w, q[decltype(ic)::value][0]);
-          pnl_fma<S>(a1, w, q[decltype(ic)::value][1]);
+      };
+      auto fmag = [&](const d2v (&q)[QW], double w, auto jc) {
+        constexpr int J = decltype(jc)::value;
+        pfor<0, QW>([&](auto ic) {
+          constexpr int S = QW * J + decltype(ic)::value;
+          if constexpr (kAbl & 1) {
+            touch(q[decltype(ic)::value][0]);
+            touch(q[decltype(ic)::value][1]);
+          } else {
+            pnl_fma<S>(a0, w, q[decltype(ic)::value][0]);
+            pnl_fma<S>(a1, w, q[decltype(ic)::value][1]);
+          }
         });
+      };
+      // wait until at most N LDS reads are in flight; q's registers count as written here
+      auto waitg = [&](d2v (&q)[QW], auto nc) {
+        constexpr int N = decltype(nc)::value;
+        if constexpr (QW == 2) asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(q[0]), "+v"(q[1]) : "n"(N));
+        else asm volatile("s_waitcnt lgkmcnt(%4)" : "+v"(q[0]), "+v"(q[1]), "+v"(q[2]), "+v"(q[3]) : "n"(N));
       };
       auto run = [&](int done) {
         unsigned u[NCR];
@@ -329,11 +388,38 @@ __global__ __launch_bounds__(pnl::kThreads) void k_spmm_panel(PanelArgs a) {
           asm volatile("s_nop 1" : "+v"(u[0]), "+v"(u[1]), "+v"(u[2]), "+v"(u[3]), "+v"(x[0]), "+v"(x[1]),
                        "+v"(x[2]), "+v"(x[3]));
         const int left = mmax - done;
+        // the wave's groups of QW entries (uniform branches): a group's reads are issued while
+        // the group before is multiplied, and lgkmcnt(QW) then waits for the older group only.
+        // The read-ahead is unconditional inside a taken group (past the count it reads panel
+        // row 0: harmless) — a read issued on one path only would leave its registers to a
+        // merge the compiler may resolve with a copy made before the data lands
         pfor<0, NCR>([&](auto rr) {
           constexpr int RR = decltype(rr)::value;
-          pfor<0, 8>([&](auto hh) {
-            if (16 * RR + 2 * decltype(hh)::value < left) pair(u[RR], x[RR], hh);
-          });
+          if (16 * RR < left) {
+            d2v qa[QW], qb[QW];
+            readg(qa, u[RR], std::integral_constant<int, 0>{});
+            pfor<0, NQ>([&](auto jc) {
+              constexpr int J = decltype(jc)::value;
+              if (16 * RR + QW * J < left) {
+                d2v(&cur)[QW] = J % 2 == 0 ? qa : qb;
+                d2v(&nxt)[QW] = J % 2 == 0 ? qb : qa;
+                if constexpr (J + 1 < NQ) {
+                  readg(nxt, u[RR], std::integral_constant<int, J + 1>{});
+                  waitg(cur, std::integral_constant<int, QW>{});
+                } else {
+                  waitg(cur, std::integral_constant<int, 0>{});
+                }
+                fmag(cur, x[RR], jc);
+              }
+            });
+            // the read-ahead past the last group taken may still be landing in qa / qb: wait for
+            // it while both are live (the compiler must not reuse their registers before)
+            if constexpr (QW == 2)
+              asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(qa[0]), "+v"(qa[1]), "+v"(qb[0]), "+v"(qb[1]));
+            else
+              asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(qa[0]), "+v"(qa[1]), "+v"(qa[2]), "+v"(qa[3]),
+                           "+v"(qb[0]), "+v"(qb[1]), "+v"(qb[2]), "+v"(qb[3]));
+          }
         });
       };
       run(0);
@@ -347,46 +433,57 @@ __global__ __launch_bounds__(pnl::kThreads) void k_spmm_panel(PanelArgs a) {
       if (have_next) load_chunk(cc[k], vv[k], pnl_bcast<k>(s_nxt), pnl_bcast<k>(cnt_nxt), rcn, rvn);
     });
 
-    // (4) block end: epilogue, store U
+    PNL_STAMP(2);
+    // (4) block end: epilogue, store U.  Q_{i-1} rows are loaded four at a time, and B_i^T's
+    // table is read once per four rows (two LDS reads per u pair), whose FMAs are independent;
+    // each row's sum runs in the same order as one row at a time
     if (last_panel) {
-      auto qprev_row = [&](int k) -> d2v {  // the epilogue's Q_{i-1} rows, one row ahead
-        const int64_t r = st.blk * R + grp + 64 * k;
-        return *(reinterpret_cast<const d2v*>(a.Qprev + (r < a.nrows ? r : a.nrows - 1) * kB) + li);
-      };
-      d2v qn = EPI ? qprev_row(0) : d2v{0.0, 0.0};
+      if constexpr (EPI) {
+        constexpr int EH = RPG < 4 ? RPG : 4;  // rows per pass (registers)
+        pfor<0, RPG / EH>([&](auto hc) {
+          constexpr int K0 = EH * decltype(hc)::value;
+          d2v qn[EH];  // -Q_{i-1} rows
+#pragma unroll
+          for (int k = 0; k < EH; ++k) {
+            const int64_t r = st.blk * R + grp + 64 * (K0 + k);
+            qn[k] = -*(reinterpret_cast<const d2v*>(a.Qprev + (r < a.nrows ? r : a.nrows - 1) * kB) + li);
+            asm volatile("s_nop 1" : "+v"(qn[k]));
+          }
+          const d2v* bt = reinterpret_cast<const d2v*>(smem + 2 * kPanelBytes);
+          pfor<0, 16>([&](auto sc) {
+            constexpr int S = decltype(sc)::value;  // u = 2 S (qn[.][0] of lane S), 2 S + 1 ([1])
+            const d2v be = bt[(2 * S) * 16 + li], bo = bt[(2 * S + 1) * 16 + li];
+#pragma unroll
+            for (int k = 0; k < EH; ++k) {
+              pnl_fma<S>(acc[K0 + k][0], qn[k][0], be[0]);
+              pnl_fma<S>(acc[K0 + k][1], qn[k][0], be[1]);
+              pnl_fma<S>(acc[K0 + k][0], qn[k][1], bo[0]);
+              pnl_fma<S>(acc[K0 + k][1], qn[k][1], bo[1]);
+            }
+          });
+        });
+      }
 #pragma unroll
       for (int k = 0; k < RPG; ++k) {
         const int64_t r = st.blk * R + grp + 64 * k;
-        double u0 = acc[k][0], u1 = acc[k][1];
-        if constexpr (EPI) {
-          const d2v qc = qn;
-          if (k + 1 < RPG) qn = qprev_row(k + 1);
-          if (r < a.nrows) {
-            double n0 = -qc[0], n1 = -qc[1];
-            asm volatile("s_nop 1" : "+v"(n0), "+v"(n1));
-            const d2v* bt = reinterpret_cast<const d2v*>(smem + 2 * kPanelBytes);
-            pfor<0, 16>([&](auto sc) {
-              constexpr int S = decltype(sc)::value;  // u = 2 S (n0 of lane S), 2 S + 1 (n1)
-              const d2v be = bt[(2 * S) * 16 + li], bo = bt[(2 * S + 1) * 16 + li];
-              pnl_fma<S>(u0, n0, be[0]);
-              pnl_fma<S>(u1, n0, be[1]);
-              pnl_fma<S>(u0, n1, bo[0]);
-              pnl_fma<S>(u1, n1, bo[1]);
-            });
-          }
-        }
         if (r < a.nrows)
-          __builtin_nontemporal_store(d2v{u0, u1}, reinterpret_cast<d2v*>(a.U + r * kB) + li);
+          __builtin_nontemporal_store(d2v{acc[k][0], acc[k][1]}, reinterpret_cast<d2v*>(a.U + r * kB) + li);
         acc[k][0] = acc[k][1] = 0.0;
       }
     }
+    PNL_STAMP(3);
+#if RBL_PANEL_STAMPS
+    ++nsteps;
+#endif
     if (!have_next) break;
     // (5) the DMA has landed — older than the step's other loads, which retire in order, so a
     // counted vmcnt leaves those (at least the kVm chunk loads) in flight across the barrier —
     // and every wave is done reading this panel (lgkmcnt(0)).  A plain __syncthreads() would
     // drain them.
     asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)" ::"n"(kVm) : "memory");
+    PNL_STAMP(4);
     __builtin_amdgcn_s_barrier();
+    PNL_STAMP(5);
     buf ^= 1;
     rc = rcn;
     rv = rvn;
@@ -397,11 +494,17 @@ __global__ __launch_bounds__(pnl::kThreads) void k_spmm_panel(PanelArgs a) {
     st = sn;
     st1 = sn2;
   }
+#if RBL_PANEL_STAMPS
+  if ((blockIdx.x == 0 || blockIdx.x == 128) && tid == 0)
+    printf("panel stamps wg %d steps %d: touch %llu issue %llu compute %llu epi %llu vmwait %llu barrier %llu\n",
+           (int)blockIdx.x, nsteps, (unsigned long long)ph[0], (unsigned long long)ph[1],
+           (unsigned long long)ph[2], (unsigned long long)ph[3], (unsigned long long)ph[4],
+           (unsigned long long)ph[5]);
+#endif
 }
 
-// RPG / CH by the format's typical count per row and panel (panel_format): 16-entry chunks at
-// 8 rows per group (512-row blocks: half the panel staging of 256) where a row's count in a
-// panel is mostly <= 16, 32-entry chunks at 4 rows per group otherwise (registers)
+// RPG / CH by the format's mean count per row and panel (rbl_api.cpp, prepare_window_formats):
+// <8, 16> up to 16, <4, 32> beyond (<8, 32> needs more than 128 VGPRs with the quad read-ahead)
 bool spmm_panel(const CsrDev& A, const double* Qin, int64_t col_off, int b, double* U,
                 const double* Qprev, const double* Bi, hipStream_t s) {
   if (b != 32 || !A.panel_blk || A.panel_nblk <= 0 || !A.panel_cnt || !A.panel_st || !A.panel_col ||
