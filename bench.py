@@ -1143,6 +1143,9 @@ def cpu_model() -> str:
     return "unknown"
 
 
+CPU_FIXED_START_BY_S = 240
+
+
 def cpu_baseline(args, m_max, plant):
     """Time the oracle (NumPy/SciPy restatement of RBL.jl) on n_s rows of the same generator
     for the same m_max fixed block steps (measured end to end, matrix generation excluded), and
@@ -1198,7 +1201,14 @@ def cpu_baseline(args, m_max, plant):
         out["linear_scaling_check"] = cpu_scaling_check(args, plant, A, omega)
     fixed_n = args.n if args.cpu_fixed_n < 0 else args.cpu_fixed_n
     if fixed_n and args.matrix == "hashwindow" and args.basis_bits == 64:
-        out["fixed_steps_at_n"] = cpu_fixed_steps(args, plant, fixed_n)
+        # ~3.5 minutes at n = 1e7 (the 1e9-nnz CSR build + 8 oracle steps): by default only while
+        # the run is young enough to finish well inside a 10-minute budget
+        elapsed = time.perf_counter() - T_START
+        if args.cpu_fixed_n < 0 and elapsed > CPU_FIXED_START_BY_S:
+            out["fixed_steps_at_n"] = {"n": fixed_n, "skipped": f"the run was {elapsed:.0f} s old "
+                                       f"(> {CPU_FIXED_START_BY_S} s); --cpu-fixed-n {fixed_n} forces it"}
+        else:
+            out["fixed_steps_at_n"] = cpu_fixed_steps(args, plant, fixed_n)
     out["value_is"] = ("the 38-step rate extrapolated linearly from the n = %d sample (sample, "
                        "linear_scaling_check); fixed_steps_at_n is SURVEY §8(d)'s fixed-step form "
                        "measured at the config's own n (the first steps only: the partial reorth "
