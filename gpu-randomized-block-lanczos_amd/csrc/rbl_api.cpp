@@ -1171,8 +1171,9 @@ int prepare_window_formats(rbl_ctx* ctx, const std::vector<int64_t>& rp) {
       ctx->panel_rpg = rpg;
       ctx->panel_ch = pch;
       // by default only where the panels pay: a staged Q row read >= 4 times from LDS on
-      // average (bands; a scattered pattern's blocks span the whole matrix: the gathers)
-      ctx->panel_auto = 4 * staged <= ctx->nnz;
+      // average (bands; a scattered pattern's blocks span the whole matrix: the gathers), and
+      // past what the LDS-window kernel takes (a 256-row ring: the narrow bands keep it)
+      ctx->panel_auto = 4 * staged <= ctx->nnz && !ctx->window_ok32;
       ctx->panel_span = maxp * pw;
       if (!ctx->d_zrow) {  // the panel rows outside the Q range read it
         HIPC(hipMalloc(&ctx->d_zrow, 64 * sizeof(double)));
