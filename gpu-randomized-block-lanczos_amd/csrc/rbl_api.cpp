@@ -1171,9 +1171,10 @@ int prepare_window_formats(rbl_ctx* ctx, const std::vector<int64_t>& rp) {
       ctx->panel_rpg = rpg;
       ctx->panel_ch = pch;
       // by default only where the panels pay: a staged Q row read >= 4 times from LDS on
-      // average (bands; a scattered pattern's blocks span the whole matrix: the gathers), and
-      // past what the LDS-window kernel takes (a 256-row ring: the narrow bands keep it)
-      ctx->panel_auto = 4 * staged <= ctx->nnz && !ctx->window_ok32;
+      // average (bands; a scattered pattern's blocks span the whole matrix: the gathers).  Ahead
+      // of the LDS-window kernel where both apply: 5.0 vs 7.6 ms at H = 72 and 96, n = 1e7
+      // (profiles/r06_panel_vs_window_b19.txt)
+      ctx->panel_auto = 4 * staged <= ctx->nnz;
       ctx->panel_span = maxp * pw;
       if (!ctx->d_zrow) {  // the panel rows outside the Q range read it
         HIPC(hipMalloc(&ctx->d_zrow, 64 * sizeof(double)));

@@ -428,7 +428,7 @@ static void launch_gather(const CsrDev& A, const double* Q, int64_t off, int b, 
 int spmm(const CsrDev& A, const double* Qin, int64_t col_off, int b, double* U,
          const double* Qprev, const double* Bi, int variant, hipStream_t s, double* ai_slab) {
   if (A.nrows <= 0) return 0;
-  // 0 auto: band tiles > band (MFMA) > column panels (past the window's ring) > window (DPP) > segmented gather >
+  // 0 auto: band tiles > band (MFMA) > column panels > window (DPP) > segmented gather >
   // gather;  1 gather;  2 window;  3 band;  4 band tiles;  5 segmented gather;  7 column panels
   int parts = 0;
   if ((variant == 0 || variant == 4) &&

@@ -66,7 +66,7 @@ def test_spmm_window_ragged_and_partial_tiles(rbl, b):
         _check(A, Y, X)
         tile_nnz = np.diff(A.indptr[np.r_[np.arange(0, n, 16), n]]).max()
         if W <= 64 and tile_nnz <= 2048:     # the window kernel's metadata cap per tile
-            assert k in (2, 3, 5), (n, W)
+            assert k in (2, 3, 5, 7), (n, W)   # (7: the column panels, ahead of the window)
         if tile_nnz > 2048:
             assert k in (1, 3, 5, 6), (n, W)
 
