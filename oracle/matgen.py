@@ -160,6 +160,24 @@ def planted_spectrum(k: int, scale: float = 100.0):
     return np.array([scale * (2 * k + 1 - l) for l in range(1, 2 * k + 1)], dtype=np.float64)
 
 
+def random_sym_csr(n: int = 10_000, density: float = 0.01, seed: int = 20261015, plant=None):
+    """SURVEY §8(d) C1 as defined there: A = R + R^T, R with `density` nonzeros at uniformly
+    random positions and N(0,1) values (numpy's PCG64 from `seed`), plus the planted diagonal at
+    rows 0 .. len(plant) - 1 (the top of the spectrum, so the top k converge).  Unbanded: every
+    row reaches the whole matrix (the GPU takes the segmented gather)."""
+    rng = np.random.default_rng(seed)
+    R = sp.random(n, n, density=density, format="csr", random_state=rng,
+                  data_rvs=rng.standard_normal)
+    A = (R + R.T).tocsr()
+    if plant is not None:
+        d = np.zeros(n)
+        d[:len(plant)] = plant
+        A = (A + sp.diags(d)).tocsr()
+    A.sort_indices()
+    A.eliminate_zeros()
+    return A
+
+
 _CIRC_K = np.uint64(0x9FB21C651E98DF25)
 _SCATTER_K = np.uint64(0xA0761D6478BD642F)
 

@@ -167,3 +167,21 @@ def test_hashwindow_chunked_is_the_same_matrix():
         B = matgen.hashwindow_csr_chunked(30000, 64, 0.7734, 11, plant, chunk)
         assert np.array_equal(A.indptr, B.indptr) and np.array_equal(A.indices, B.indices)
         assert np.array_equal(A.data, B.data)
+
+
+def test_c1_random_symmetric_as_defined():
+    """SURVEY §8(d) C1 as defined (A = R + R^T, 1 % density, N(0,1), planted diagonal): symmetric,
+    seeded (the same matrix twice), and the oracle's top k = 10 at b = 8 are the planted values to
+    the random part's perturbation, converged with small residuals."""
+    k = 10
+    plant = matgen.planted_spectrum(k)
+    A = matgen.random_sym_csr(10000, 0.01, 20261015, plant)
+    B = matgen.random_sym_csr(10000, 0.01, 20261015, plant)
+    assert (A - A.T).nnz == 0 and (A != B).nnz == 0
+    assert abs(A.nnz / 10000 - 2 * 0.01 * 10000) < 5   # ~200 per row (R + R^T)
+    omega = np.random.default_rng(1).standard_normal((10000, 8))
+    r = o.RBL_gpu_semantics(A, k, 8, omega=omega, qr_mode="posdiag")
+    assert r.converged
+    assert np.abs(r.D - plant[:k]).max() < 1.0
+    res = np.linalg.norm(A @ r.V - r.V * r.D, axis=0) / np.abs(r.D)
+    assert res.max() < 1e-8
