@@ -330,13 +330,14 @@ __global__ __launch_bounds__(pnl::kThreads) void k_spmm_panel(PanelArgs a) {
     if (have_next && last_panel) rsrc_of(sn.blk, rcn, rvn);
 
     PNL_STAMP(1);
+    // lane k (< RPG) of every group: the largest count of row k over the wave's four groups
+    int cmax4 = max(cnt_cur, __shfl_xor(cnt_cur, 16));
+    cmax4 = max(cmax4, __shfl_xor(cmax4, 32));
     // (3) multiply the panel, row by row; each row's chunk for the next step follows its entries
     pfor<0, RPG>([&](auto kc) {
       constexpr int k = decltype(kc)::value;
       const int m = pnl_bcast<k>(cnt_cur);  // this group's row k: entries in the panel
-      // the largest count of the wave's four groups (lanes 0, 16, 32, 48 hold them)
-      const int mmax = max(max(__builtin_amdgcn_readlane(m, 0), __builtin_amdgcn_readlane(m, 16)),
-                           max(__builtin_amdgcn_readlane(m, 32), __builtin_amdgcn_readlane(m, 48)));
+      const int mmax = __builtin_amdgcn_readlane(cmax4, k);  // the wave's largest (uniform)
       double& a0 = acc[k][0];
       double& a1 = acc[k][1];
       // QW entries QW J .. QW J + QW - 1 of one chunk register: their LDS reads, issued one group
