@@ -66,7 +66,11 @@ def main():
     # the partial-reorth pair: the Gram and the 64- (b = 32) or 32-column (b = 16) update
     upd = ("k_tsmm44<32, 64,", "k_tsmm44f") if wb == 32 else ("k_tsmm44<16, 32,",)
     reo = {k: v for k, v in kern.items() if k.startswith((f"k_gram44<{wb}, 2",) + upd)}
-    runs = 1  # bench.py --steps 1 --warmup 0: one 38-step run
+    # bench.py --steps 1 --warmup 0 runs the job once timed and (since round 6) once more with
+    # the stage timers: count the runs by the Gram's launches (len(range(4, m + 1, 2)) per run)
+    per_run = len(range(4, wm + 1, 2))
+    gl = sum(v["launches"] for k, v in reo.items() if k.startswith(f"k_gram44<{wb}, 2"))
+    runs = max(1, round(gl / per_run)) if per_run else 1
     reorth_bytes = sum(v["hbm_bytes_per_launch"] * v["launches"] for v in reo.values()) / runs
     # the kernels measured: the bench line of the FETCH pass names the fusions and the format
     extra = {}
