@@ -328,6 +328,23 @@ __global__ __launch_bounds__(pnl::kThreads) void k_spmm_panel(PanelArgs a) {
     // where the next step's chunks come from: this block, or the next one
     __amdgpu_buffer_rsrc_t rcn = rc, rvn = rv;
     if (have_next && last_panel) rsrc_of(sn.blk, rcn, rvn);
+    // the epilogue's Q_{i-1} rows, loaded here where registers allow (4 rows per group): their
+    // latency then runs under the step's multiply instead of before the epilogue's FMAs
+    // Issued on every step (from the zero row unless the block ends here) as inline asm: hipcc
+    // would wait vmcnt(0) for an ordinary load behind the in-flight DMA, draining the next
+    // step's record loads; the epilogue waits vmcnt(kVm) for these itself (the record loads of
+    // (3), kVm of them, are the only younger vector-memory ops; the "memory" clobbers keep them
+    // on their side of both asm statements).
+    constexpr bool kQpEarly = EPI && RPG == 4;
+    d2v qpe[kQpEarly ? RPG : 1];
+    if constexpr (kQpEarly) {
+#pragma unroll
+      for (int k = 0; k < RPG; ++k) {
+        const int64_t r = st.blk * R + grp + 64 * k;
+        const double* src = last_panel ? a.Qprev + (r < a.nrows ? r : a.nrows - 1) * kB + 2 * li : a.zrow;
+        asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(qpe[k]) : "v"(src) : "memory");
+      }
+    }
 
     PNL_STAMP(1);
     // lane k (< RPG) of every group: the largest count of row k over the wave's four groups
@@ -430,8 +447,9 @@ __global__ __launch_bounds__(pnl::kThreads) void k_spmm_panel(PanelArgs a) {
         load_chunk(cc[k], vv[k], pnl_bcast<k>(s_cur) + done, m - done, rc, rv);
         run(done);
       }
-      // the next step's records of this row
-      if (have_next) load_chunk(cc[k], vv[k], pnl_bcast<k>(s_nxt), pnl_bcast<k>(cnt_nxt), rcn, rvn);
+      // the next step's records of this row (past the last step the count is 0: every lane
+      // out of range — issued anyway, so the loads' order is the same on every path)
+      load_chunk(cc[k], vv[k], pnl_bcast<k>(s_nxt), pnl_bcast<k>(cnt_nxt), rcn, rvn);
     });
 
     PNL_STAMP(2);
@@ -443,11 +461,22 @@ __global__ __launch_bounds__(pnl::kThreads) void k_spmm_panel(PanelArgs a) {
         constexpr int EH = RPG < 4 ? RPG : 4;  // rows per pass (registers)
         pfor<0, RPG / EH>([&](auto hc) {
           constexpr int K0 = EH * decltype(hc)::value;
-          d2v qn[EH];  // -Q_{i-1} rows
+          d2v qn[EH];  // -Q_{i-1} rows: all loads first, then the negations (one wait)
 #pragma unroll
           for (int k = 0; k < EH; ++k) {
-            const int64_t r = st.blk * R + grp + 64 * (K0 + k);
-            qn[k] = -*(reinterpret_cast<const d2v*>(a.Qprev + (r < a.nrows ? r : a.nrows - 1) * kB) + li);
+            if constexpr (kQpEarly) {
+              if (k == 0)  // (the loads of (2): wait here, tied to their registers)
+                asm volatile("s_waitcnt vmcnt(%4)" : "+v"(qpe[0]), "+v"(qpe[1]), "+v"(qpe[2]), "+v"(qpe[3])
+                             : "n"(kVm) : "memory");
+              qn[k] = qpe[K0 + k];
+            } else {
+              const int64_t r = st.blk * R + grp + 64 * (K0 + k);
+              qn[k] = *(reinterpret_cast<const d2v*>(a.Qprev + (r < a.nrows ? r : a.nrows - 1) * kB) + li);
+            }
+          }
+#pragma unroll
+          for (int k = 0; k < EH; ++k) {
+            qn[k] = -qn[k];
             asm volatile("s_nop 1" : "+v"(qn[k]));
           }
           const d2v* bt = reinterpret_cast<const d2v*>(smem + 2 * kPanelBytes);
