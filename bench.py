@@ -81,6 +81,10 @@ def parse():
                     help="rmat: BASELINE config 4's power-law pattern (SURVEY §8(d) C4b); "
                          "circuit: BASELINE config 3's shape (G3_circuit-like SPD Laplacian, "
                          "scattered; use --n 1585478 --b 16)")
+    ap.add_argument("--wide-steps", type=int, default=2,
+                    help="timed runs of the wide-band sub-record (0: skip)")
+    ap.add_argument("--wide-halfwidth", type=int, default=1024,
+                    help="half-width of the wide-band sub-record's hash-window matrix")
     ap.add_argument("--c3-steps", type=int, default=6,
                     help="timed runs of the C3 circuit sub-record that follows a hash-window run "
                          "(n = 1,585,478, b = 16, k = 20: BASELINE config 3's shape; 0 skips it)")
@@ -865,6 +869,13 @@ def main():
         c3_rec = guarded(c3_subrecord, ctx, args, world, barrier, allmax, allsum, allgather_i64,
                          gather_obj)
 
+    # ---- a wide band (the FEM / circuit orderings benchmark.jl loads): the column panels ----
+    wide_rec = None
+    if args.matrix == "hashwindow" and args.wide_steps > 0 and args.basis_bits == 64 and args.b == 32:
+        progress("wide-band sub-record")
+        wide_rec = guarded(wide_subrecord, ctx, args, plant, world, barrier, allmax, allsum,
+                           allgather_i64, gather_obj)
+
     # ---- CPU baseline: the oracle (port of RBL.jl) on a bounded sample, rank 0, N = 1 ----
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -926,6 +937,7 @@ def main():
            if world > 1 else {}),
         "c4b_rmat": rmat_rec,
         "c3_circuit": c3_rec,
+        "c4w_wideband": wide_rec,
         "c5_mixed": None,
     }
 
@@ -1063,6 +1075,52 @@ def c3_subrecord(ctx, args, world, barrier, allmax, allsum, allgather_i64, gathe
             "value": round(meas["value"], 3), "unit": "block iterations/s",
             "steps": K, "warmup": 1, "ms_per_step": round(meas["elapsed"] / K * 1e3, 3),
             "n": ra.n, "nnz": nnz, "b": ra.b, "k": ra.k, "block_steps_per_run": meas["m_max"],
+            "nnz_per_rank": allgather_i64(nnz_loc),
+            "roofline": meas["roofline"], "roofline_secondary": meas["roofline_secondary"],
+            "stage_ms_per_run": {s_: round(v / K, 3) for s_, v in meas["stage"].items()},
+            "comm_per_step": meas["comm_per_step"], "run_ms_rank0": meas["run_ms"],
+            **({"per_rank": rank_arrays(meas["per_rank"])} if world > 1 else {}),
+            "time_to_k": {"seconds": round(ttk_s, 4), "iters": info.iters,
+                          "converged": info.converged, "k": ra.k,
+                          "top_eigenvalues": [round(float(x), 6) for x in D[:3]]},
+            "matrix_gen_s": round(gen_s, 3)}
+
+
+def wide_subrecord(ctx, args, plant, world, barrier, allmax, allsum, allgather_i64, gather_obj=None):
+    """A wide band in the same driver run: the headline's generator at the same n and ~100
+    nonzeros per row, but half-width --wide-halfwidth (default 1024, density 99 / 2H) — the regime
+    of the FEM / circuit orderings the reference's benchmark.jl:21-28 loads, past the band tiles'
+    64 — where the SpMM is the column-panel kernel (spmm_panel.hip); the same fixed-length runs
+    and a time-to-k."""
+    import copy
+    import rbl
+    ra = copy.copy(args)
+    ra.halfwidth = args.wide_halfwidth
+    ra.density = round(99.0 / (2 * ra.halfwidth), 6)
+    t0 = time.perf_counter()
+    ctx.gen_hashwindow(ra.n, ra.halfwidth, ra.density, ra.seed, plant)
+    gen_s = time.perf_counter() - t0
+    _, r0, r1, nnz_loc = ctx.matrix_info()
+    nloc = r1 - r0
+    nnz = allsum(nnz_loc)
+    K = args.wide_steps
+    meas = measure(ctx, ra, "hashwindow", K, 1, nloc, nnz_loc, world, barrier, allmax, gather_obj)
+    barrier()
+    ctx.synchronize()
+    ctx.reset_timers()
+    t0 = time.perf_counter()
+    D, V, info = rbl.lanczos(ctx, ra.k, ra.b, kryl_sz=ra.kryl, seed=ra.seed + 3, check=True,
+                             ritz=True)
+    ctx.synchronize()
+    barrier()
+    ttk_s = allmax(time.perf_counter() - t0)
+    return {"workload": f"wide-band hash-window SpMM-Lanczos (half-width {ra.halfwidth})",
+            "metric": f"RBL iters/sec, n={ra.n} nnz/row={nnz / ra.n:.1f} b={ra.b} (hashwindow, "
+                      f"halfwidth {ra.halfwidth})",
+            "value": round(meas["value"], 3), "unit": "block iterations/s",
+            "steps": K, "warmup": 1, "ms_per_step": round(meas["elapsed"] / K * 1e3, 3),
+            "n": ra.n, "nnz": nnz, "b": ra.b, "k": ra.k, "halfwidth": ra.halfwidth,
+            "density": ra.density, "block_steps_per_run": meas["m_max"],
             "nnz_per_rank": allgather_i64(nnz_loc),
             "roofline": meas["roofline"], "roofline_secondary": meas["roofline_secondary"],
             "stage_ms_per_run": {s_: round(v / K, 3) for s_, v in meas["stage"].items()},
