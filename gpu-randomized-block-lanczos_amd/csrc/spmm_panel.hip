@@ -18,7 +18,7 @@
 //
 // The format (panel_format, built once per matrix): within a block the CSR records are
 // regrouped panel-major — panel by panel, and within a panel row by row, each row's entries in
-// column order (so every row's sum runs in the CSR's own order) — with the column stored as one
+// column order (so a row's sum within a panel runs in the CSR's order) — with the column stored as one
 // byte, its offset in the panel.  A step (block, panel) therefore reads one contiguous run of
 // records, and no cache line is fetched by two steps; per row and panel the format holds the
 // count (uint16) and the first record (uint32 from the block's base).
@@ -41,7 +41,12 @@
 //     end a block.
 // Work goes to the workgroups XCD by XCD: the 8 XCDs take contiguous eighths of the blocks and
 // an XCD's 32 workgroups sweep theirs side by side, so neighbouring blocks — whose windows
-// overlap by 2H rows — read shared panels close together in time (L2 / Infinity Cache).
+// overlap by 2H rows — read shared panels close together in time (L2 / Infinity Cache).  A
+// block walks its window's np panels from the one = 0 (mod np), wrapping round (kOrder 1): the
+// workgroups, in near lockstep, then read panels of one residue at each step — the same few
+// panels at the same time — instead of panels two steps apart (-2 % at H = 256..2048,
+// profiles/r06_panel_v9_order_ab_b24.txt).  A row's sum thus runs panel by panel in that
+// rotated order (deterministic; the window and gather kernels keep the CSR's order).
 #include <cstdint>
 #include <type_traits>
 #include <utility>
@@ -67,6 +72,14 @@ constexpr unsigned kOob = 0x10000000u;           // a record offset past any blo
 #define RBL_PANEL_ABLATE 0
 #endif
 constexpr int kAbl = RBL_PANEL_ABLATE;
+// the order a block walks its panels: 1 (default) residue-aligned — step pi of a block reads the
+// panel of its window that is = pi (mod np), so the XCD's workgroups, which step through their
+// blocks in near lockstep, read the same few panels at the same time (L2 serves the re-reads);
+// 0 ascending from the window's first panel (probe builds, for A/B)
+#ifndef RBL_PANEL_ORDER
+#define RBL_PANEL_ORDER 1
+#endif
+constexpr int kOrder = RBL_PANEL_ORDER;
 // probe builds only (-DRBL_PANEL_STAMPS=1): workgroups 0 and 128 print the cycles their wave 0
 // spent in each phase of the step loop (s_memtime), once per launch
 #ifndef RBL_PANEL_STAMPS
@@ -183,8 +196,15 @@ __global__ __launch_bounds__(pnl::kThreads) void k_spmm_panel(PanelArgs a) {
   // a step of the workgroup's sweep: (block, panel index within the block's window)
   struct Step {
     int64_t blk;
-    int pi, np, p0;  // panel index, panels of the block, its first panel (global id)
+    int pi, np, p0;  // step index within the block, panels of the block, its first panel (global id)
+    int o;           // the window's panel of step 0 (residue order): step pi takes (pi + o) mod np
     int64_t coff;    // the block's counts
+  };
+  // the panel (index within the block's window) that step s multiplies
+  auto win_panel = [&](const Step& s) -> int {
+    if constexpr (kOrder == 0) return s.pi;
+    const int w = s.pi + s.o;
+    return w >= s.np ? w - s.np : w;
   };
   auto block_step = [&](int64_t b) -> Step {
     Step s;
@@ -192,10 +212,15 @@ __global__ __launch_bounds__(pnl::kThreads) void k_spmm_panel(PanelArgs a) {
     s.pi = 0;
     s.p0 = s.np = 0;
     s.coff = 0;
+    s.o = 0;
     if (b < xb1) {
       s.p0 = bi_s[4 * b];
       s.np = bi_s[4 * b + 1] - s.p0 + 1;
       s.coff = (int64_t)(uint32_t)bi_s[4 * b + 2] | ((int64_t)bi_s[4 * b + 3] << 32);
+      if constexpr (kOrder == 1) {  // p0 + o = 0 (mod np)
+        const int r = s.p0 % s.np;
+        s.o = r == 0 ? 0 : s.np - (r < 0 ? r + s.np : r);
+      }
     }
     return s;
   };
@@ -255,7 +280,7 @@ __global__ __launch_bounds__(pnl::kThreads) void k_spmm_panel(PanelArgs a) {
   auto load_cs = [&](const Step& s, int& m, int& c0) {
     m = c0 = 0;
     if (s.blk >= xb1 || li >= RPG) return;
-    const int64_t i = s.coff + (int64_t)s.pi * R + grp + 64 * li;
+    const int64_t i = s.coff + (int64_t)win_panel(s) * R + grp + 64 * li;
     m = a.cnt[i];
     c0 = (int)a.st[i];
   };
@@ -279,7 +304,7 @@ __global__ __launch_bounds__(pnl::kThreads) void k_spmm_panel(PanelArgs a) {
   });
   int cnt_nxt, s_nxt;
   load_cs(st1, cnt_nxt, s_nxt);
-  load_panel(st.p0, 0);
+  load_panel(st.p0 + win_panel(st), 0);
   __syncthreads();  // (drains everything: the prologue's loads and DMA)
 
   int buf = 0;
@@ -321,7 +346,7 @@ __global__ __launch_bounds__(pnl::kThreads) void k_spmm_panel(PanelArgs a) {
 
     PNL_STAMP(0);
     // (2) the next step's panel, then the loads the next steps need (younger than the DMA)
-    if (have_next) load_panel(sn.p0 + sn.pi, buf ^ 1);
+    if (have_next) load_panel(sn.p0 + win_panel(sn), buf ^ 1);
     asm volatile("" ::: "memory");
     int cnt_nn = 0, s_nn = 0;
     if (have_next) load_cs(sn2, cnt_nn, s_nn);
