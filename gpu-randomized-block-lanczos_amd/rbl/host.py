@@ -14,10 +14,41 @@ Restates Julia/common.jl:9-65 for the product's host loop:
 """
 from __future__ import annotations
 
+import contextlib
 import os
 
 import numpy as np
 from scipy.linalg import lapack
+
+# NumPy advises transparent huge pages (madvise MADV_HUGEPAGE) for every array of >= 4 MiB.  With
+# the kernel's THP defrag policy "madvise" (the MI355X box's), the first touch of such an array
+# compacts memory synchronously, and on the box that stalls the GPU as well: a block step's
+# band-tile SpMM ran 30 ms instead of 3.8 while the host eigensolve first touched its 4.7-MB
+# dense matrix (N = 768), ~27 ms per first slow-spectrum run (profiles/r06_ttk_thp_stall.txt).
+# The eigensolve's arrays (a few MB, used once) gain nothing from huge pages, so they are
+# allocated without the advice; the Ritz vectors' large result array keeps it (its first touch
+# with 4-KiB pages costs 60-90 ms more at C4a).
+try:
+    from numpy._core.multiarray import _set_madvise_hugepage as _np_madvise_hugepage
+except ImportError:  # pragma: no cover - older NumPy layout
+    try:
+        from numpy.core.multiarray import _set_madvise_hugepage as _np_madvise_hugepage
+    except ImportError:
+        _np_madvise_hugepage = None
+
+
+@contextlib.contextmanager
+def small_pages():
+    """NumPy arrays allocated inside use base pages (no MADV_HUGEPAGE); the setting is restored
+    on exit."""
+    if _np_madvise_hugepage is None:
+        yield
+        return
+    prev = _np_madvise_hugepage(False)
+    try:
+        yield
+    finally:
+        _np_madvise_hugepage(prev)
 
 
 class TBand:
@@ -97,12 +128,13 @@ def eig_topk(T: np.ndarray, k: int):
     """sort_eig_abs(*dsbev(T), k) (RBL_gpu.jl:187-188): the k largest-|lambda| eigenpairs of the
     band T (lower, kd = b), ascending |lambda|."""
     N = T.shape[1]
-    if _EIGEN != "auto" or N < SUBSET_MIN_N or 8 * k >= N:
-        return sort_eig_abs(*dsbev(T), k)
-    if _tp_limits is not None:
-        with _tp_limits(limits=1, user_api="blas"):
-            return _eig_topk_dense(T, k)
-    return _eig_topk_dense(T, k)
+    with small_pages():
+        if _EIGEN != "auto" or N < SUBSET_MIN_N or 8 * k >= N:
+            return sort_eig_abs(*dsbev(T), k)
+        if _tp_limits is not None:
+            with _tp_limits(limits=1, user_api="blas"):
+                return _eig_topk_dense(T, k)
+        return _eig_topk_dense(T, k)
 
 
 def _eig_topk_dense(T: np.ndarray, k: int):
