@@ -122,3 +122,43 @@ def test_speculation_rule_from_residual_history():
     r = residual_norms(B, S, b, k)
     assert r.shape == (k,) and np.allclose(r, np.linalg.norm(B @ S[-b:, :k], axis=0))
     assert check_convergence(B, S, b, k, r.max() * 1.001) and not check_convergence(B, S, b, k, r.max() * 0.999)
+
+
+def test_eigensolve_allocates_without_hugepage_advice():
+    """eig_topk's arrays are allocated under small_pages(): NumPy's MADV_HUGEPAGE advice is off
+    inside (THP compaction on their first touch stalled the GPU) and restored after,
+    also when the solve raises; the dense top-k path still matches dsbev's eigenvalues."""
+    import pytest
+    from rbl import host
+    if host._np_madvise_hugepage is None:
+        pytest.skip("this NumPy has no madvise switch")
+    from numpy._core.multiarray import _get_madvise_hugepage
+    before = _get_madvise_hugepage()
+    seen = []
+    real = host._eig_topk_dense
+
+    def spy(T, k):
+        seen.append(_get_madvise_hugepage())
+        return real(T, k)
+
+    rng = np.random.default_rng(3)
+    b, m, k = 16, 40, 5
+    T = host.TBand(b, m)
+    for j in range(1, m + 1):
+        a = rng.standard_normal((b, b))
+        T.insert_A(a + a.T)
+        T.insert_B(np.triu(rng.standard_normal((b, b))), j)
+    host._eig_topk_dense = spy
+    try:
+        D, _ = host.eig_topk(T.view(), k)
+    finally:
+        host._eig_topk_dense = real
+    assert seen == [False] and _get_madvise_hugepage() == before
+    Dr, _ = host.sort_eig_abs(*host.dsbev(T.view()), k)
+    assert np.allclose(np.sort(D), np.sort(Dr), rtol=1e-12)
+    try:
+        with host.small_pages():
+            raise RuntimeError("x")
+    except RuntimeError:
+        pass
+    assert _get_madvise_hugepage() == before
