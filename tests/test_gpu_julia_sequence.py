@@ -18,7 +18,10 @@ only the Julia side uses are exercised on the device:
 Checked against the Python host (`rbl.lanczos`, 0-based CSC, rbl.host's eigensolver) with the same
 seed: every A_i / B_{i+1} bit for bit (the device sees the same matrix and Omega), the same step
 count, eigenvalues within 1e-12 relative (the reference's dsbev vs rbl.host's dsbevd), Ritz vectors
-within 1e-9, residuals < 1e-7."""
+within 1e-9, residuals < 1e-7.  The restarted binding (`RBL_hip_restarted`, restarted.jl:106-146:
+rbl_step with the restart flags, rbl_reorth_last, rbl_lock, rbl_restart, rbl_get_locked) is
+replayed the same way against rbl.RBL_gpu_restarted: the same cycles, locked eigenvalues within
+1e-9, locked vectors' residuals < 1e-7."""
 import ctypes as C
 
 import numpy as np
@@ -155,3 +158,92 @@ def test_julia_call_sequence_matches_python_host(rbl, kind):
     assert np.abs(V - Vp).max() < 1e-9
     res = np.linalg.norm(A @ V - V * D, axis=0) / np.abs(D)
     assert res.max() < 1e-7
+
+
+def _julia_rbl_hip_restarted(A, k, seed, kryl0=100, max_cycles=60):
+    """RBL_hip_restarted(A, k; seed) of julia/RBL_hip.jl (restarted.jl:106-146), line by line."""
+    from rbl import _lib
+    lib = _lib.lib
+    n = A.shape[1]
+    b = 1
+    h = C.c_void_p()
+    assert lib.rbl_create(C.byref(h), 0) == 0
+
+    def check(st, what):
+        if st < 0:
+            raise AssertionError(f"{what}: {st} {lib.rbl_last_error(h)}")
+
+    try:
+        Cm = A.tocsc()
+        Cm.sort_indices()
+        colptr = Cm.indptr.astype(np.int64) + 1
+        rowval = Cm.indices.astype(np.int64) + 1
+        nzval = Cm.data.astype(np.float64)
+        check(lib.rbl_set_matrix_csc(h, n, Cm.nnz, _lib.i64ptr(colptr), _lib.i64ptr(rowval),
+                                     _lib.dptr(nzval), 1), "rbl_set_matrix_csc")
+        check(lib.rbl_start(h, b, kryl0 + 10 * max_cycles, 64, None, seed), "rbl_start")
+        Ai = np.zeros((b, b), order="F")
+        Bi = np.zeros((b, b), order="F")
+
+        def step(i, flags):
+            check(lib.rbl_step(h, i, flags, _lib.dptr(Ai), _lib.dptr(Bi)), "rbl_step")
+
+        D = []
+        count, kryl, cycles = 0, kryl0, 0
+        while count < k and cycles < max_cycles:
+            step(1, 2)                                               # :41-50
+            T = o.insertA(Ai.copy(), b)
+            o.insertB(Bi.copy(), T, b, 1)
+            i = 2
+            while i * b < kryl:                                      # :52-86
+                step(i, 3 if i % 3 == 0 else 0)
+                T = np.hstack([T, o.insertA(Ai.copy(), b)])
+                if (i + 1) * b < kryl:
+                    o.insertB(Bi.copy(), T, b, i)
+                i += 1
+            m = i - 1
+            check(lib.rbl_reorth_last(h, m, 3), "rbl_reorth_last")  # :100-102
+            d, v = o.dsbev(T)                                        # :103
+            conv = Bi @ v[-b:, ::-1]                                 # :104
+            d, v = d[::-1], v[:, ::-1]
+            ncomp, restart = 0, None
+            for j in range(d.size):                                  # :116-137
+                if count + ncomp >= k:
+                    break
+                if np.linalg.norm(conv[:, j]) < 1e-7:
+                    ncomp += 1
+                    s = np.asfortranarray(v[:, j:j + 1])      # Julia's v[:, j:j]
+                    check(lib.rbl_lock(h, m, 1, _lib.dptr(s)), "rbl_lock")
+                    D.append(float(d[j]))
+                else:
+                    restart = np.asfortranarray(v[:, j:j + 1])
+                    break
+            if restart is None:
+                restart = np.zeros((m * b, b), order="F")
+                restart[0, 0] = 1.0
+            check(lib.rbl_restart(h, m, _lib.dptr(restart)), "rbl_restart")
+            kryl += 10
+            count += ncomp
+            cycles += 1
+        L = lib.rbl_num_locked(h)
+        V = np.zeros((n, L), order="F")
+        if L > 0:
+            check(lib.rbl_get_locked(h, _lib.dptr(V)), "rbl_get_locked")
+        return np.asarray(D), V, cycles
+    finally:
+        lib.rbl_free(h)
+
+
+def test_julia_restarted_call_sequence_matches_python_host(rbl):
+    """RBL_hip_restarted's sequence (rbl_step with the restart flags, rbl_reorth_last, rbl_lock,
+    rbl_restart, rbl_get_locked) on a 1-based CSC upload against rbl.RBL_gpu_restarted with the
+    same seed: the same cycles, locked eigenvalues within 1e-9 relative, locked vectors' residuals
+    < 1e-7 (the tolerances of test_gpu_restarted.py)."""
+    k, seed = 5, 77
+    A = matgen.hashwindow_csr(3000, 40, 0.5, 3, matgen.planted_spectrum(k))
+    D, V, cycles = _julia_rbl_hip_restarted(A, k, seed)
+    Dp, Vp, cyc_p = rbl.RBL_gpu_restarted(A, k, seed=seed, return_cycles=True)
+    assert cycles == cyc_p and D.size == Dp.size == k
+    assert np.all(np.abs(D - Dp) <= 1e-9 * np.abs(Dp)), (D, Dp)
+    res = np.linalg.norm(A @ V - V * D[None, :], axis=0) / np.abs(D)
+    assert res.max() < 1e-7, res
