@@ -114,10 +114,12 @@ class Context:
 
     # -- matrix ---------------------------------------------------------------------------
     def set_matrix(self, A) -> None:
-        """Upload a symmetric matrix: a SciPy sparse matrix (any format; CSC arrays passed
-        as-is — Julia SparseMatrixCSC layout, RBL_gpu.jl:209 — symmetry makes them the CSR
-        arrays), or a dense NumPy array (RBL_gpu(A::Matrix{Float64}): panel GEMM on fp64 MFMA;
-        with several ranks each keeps the rows of the even split)."""
+        """Upload A: a SciPy sparse matrix (any format) or a dense NumPy array
+        (RBL_gpu(A::Matrix{Float64}): panel GEMM on fp64 MFMA; with several ranks each keeps
+        the rows of the even split).  The sparse arrays passed are A's rows (CSR): for the
+        symmetric A of RBL_gpu.jl:209 they are exactly Julia's SparseMatrixCSC arrays; for any
+        other A the device then computes A Q, as cuSPARSE does on the CSC matrix (benchmark.jl:58
+        runs an unsymmetric sprandn) and as julia/RBL_hip.jl does by transposing first."""
         if isinstance(A, np.ndarray):
             n = A.shape[0]
             if A.ndim != 2 or A.shape[1] != n:
@@ -126,13 +128,13 @@ class Context:
             r0, r1 = (n * r) // P, (n * (r + 1)) // P
             self.set_matrix_dense_rows(n, r0, r1, A[r0:r1])
             return
-        A = sp.csc_matrix(A)
+        A = sp.csr_matrix(A)
         A.sort_indices()
         n = A.shape[1]
-        colptr = A.indptr.astype(np.int64)
-        rowval = A.indices.astype(np.int64)
+        rowptr = A.indptr.astype(np.int64)
+        colind = A.indices.astype(np.int64)
         nzval = A.data.astype(np.float64)
-        self._check(lib.rbl_set_matrix_csc(self._h, n, A.nnz, i64ptr(colptr), i64ptr(rowval),
+        self._check(lib.rbl_set_matrix_csc(self._h, n, A.nnz, i64ptr(rowptr), i64ptr(colind),
                                            dptr(nzval), 0), "rbl_set_matrix_csc")
 
     def set_matrix_dense_rows(self, n, row_begin, row_end, A_rows) -> None:

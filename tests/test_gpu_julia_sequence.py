@@ -247,3 +247,39 @@ def test_julia_restarted_call_sequence_matches_python_host(rbl):
     assert np.all(np.abs(D - Dp) <= 1e-9 * np.abs(Dp)), (D, Dp)
     res = np.linalg.norm(A @ V - V * D[None, :], axis=0) / np.abs(D)
     assert res.max() < 1e-7, res
+
+
+@pytest.mark.parametrize("b", [8, 32])
+def test_unsymmetric_A_multiplies_by_A(rbl, b):
+    """An unsymmetric A (benchmark.jl:58 runs RBL_gpu on an unsymmetric sprandn; cuSPARSE then
+    multiplies by A itself): the Python host uploads A's rows and julia/RBL_hip.jl uploads the
+    CSC arrays of A^T, 1-based — both make rbl_apply compute A X (not A^T X), within
+    1e-13 |A||X| of SciPy, and the two uploads give the same Y bit for bit."""
+    import scipy.sparse as sp
+    from rbl import _lib
+    lib = _lib.lib
+    n = 3000
+    A = sp.random(n, n, density=0.01, random_state=5, format="csr") + sp.diags(np.arange(1.0, n + 1))
+    A = sp.csr_matrix(A)
+    X = np.asfortranarray(np.random.default_rng(2).standard_normal((n, b)))
+    with rbl.Context(0) as ctx:
+        ctx.set_matrix(A)
+        Y = ctx.apply(X)
+    ref = A @ X
+    assert np.all(np.abs(Y - ref) <= 1e-13 * (abs(A) @ np.abs(X)) + 1e-300)
+    assert np.abs(Y - A.T @ X).max() > 1e-3 * np.abs(ref).max()   # A is far from symmetric
+    Ct = sp.csc_matrix(A.T)                         # SparseMatrixCSC(transpose(A))
+    Ct.sort_indices()
+    colptr = Ct.indptr.astype(np.int64) + 1
+    rowval = Ct.indices.astype(np.int64) + 1
+    nzval = Ct.data.astype(np.float64)
+    h = C.c_void_p()
+    assert lib.rbl_create(C.byref(h), 0) == 0
+    try:
+        assert lib.rbl_set_matrix_csc(h, n, Ct.nnz, _lib.i64ptr(colptr), _lib.i64ptr(rowval),
+                                      _lib.dptr(nzval), 1) == 0
+        Yj = np.zeros((n, b), order="F")
+        assert lib.rbl_apply(h, b, _lib.dptr(X), _lib.dptr(Yj)) == 0
+    finally:
+        lib.rbl_free(h)
+    assert np.array_equal(Yj, Y)
