@@ -455,6 +455,16 @@ void free_seg(rbl_ctx::SegTierBuf& T, bool with_csr) {
   T = rbl_ctx::SegTierBuf();
 }
 
+// the column-panel format (spmm_panel.hip) and its choice
+void free_panels(rbl_ctx* ctx) {
+  hipFree(ctx->d_panel_blk); ctx->d_panel_blk = nullptr; ctx->panel_nblk = 0; ctx->panel_auto = false;
+  ctx->panel_span = 0;
+  hipFree(ctx->d_panel_cnt); ctx->d_panel_cnt = nullptr;
+  hipFree(ctx->d_panel_st); ctx->d_panel_st = nullptr;
+  hipFree(ctx->d_panel_col); ctx->d_panel_col = nullptr;
+  hipFree(ctx->d_panel_val); ctx->d_panel_val = nullptr;
+}
+
 void free_tiers(rbl_ctx* ctx) {
   for (auto& T : ctx->seg_tier) free_seg(T, true);
   ctx->seg_ntiers = 0;
@@ -1150,18 +1160,24 @@ int prepare_window_formats(rbl_ctx* ctx, const std::vector<int64_t>& rp) {
       for (int64_t bk = 0; bk < nb; ++bk) maxblk = std::max(maxblk, zb[bk + 1] - zb[bk]);
     }
     bool fits = maxp <= kPanelMax && ctx->n / pw < INT32_MAX && nb > 0 && maxblk * 8 < INT32_MAX;
-    // the records are a second copy of the matrix: without room for it, no panels (the gathers)
-    if (fits && hipMalloc(&ctx->d_panel_val, std::max<int64_t>(ctx->nnz, 1) * sizeof(double)) != hipSuccess) {
-      (void)hipGetLastError();
-      ctx->d_panel_val = nullptr;
-      fits = false;
+    // the records are a second copy of the matrix: without room for it, no panels (the gathers).
+    // An allocation that fails here is not an error: this rank just runs another kernel (the
+    // several-rank setup after this is collective, so no rank may leave before it)
+    if (fits) {
+      const bool ok =
+          hipMalloc(&ctx->d_panel_val, std::max<int64_t>(ctx->nnz, 1) * sizeof(double)) == hipSuccess &&
+          hipMalloc(&ctx->d_panel_col, std::max<int64_t>(ctx->nnz, 1)) == hipSuccess &&
+          hipMalloc(&ctx->d_panel_blk, 4 * nb * sizeof(int32_t)) == hipSuccess &&
+          hipMalloc(&ctx->d_panel_cnt, std::max<int64_t>(ncnt, 1) * sizeof(uint16_t)) == hipSuccess &&
+          hipMalloc(&ctx->d_panel_st, std::max<int64_t>(ncnt, 1) * sizeof(uint32_t)) == hipSuccess;
+      if (!ok) {
+        (void)hipGetLastError();
+        free_panels(ctx);
+        fits = false;
+      }
     }
     if (fits) {
-      HIPC(hipMalloc(&ctx->d_panel_col, std::max<int64_t>(ctx->nnz, 1)));
-      HIPC(hipMalloc(&ctx->d_panel_blk, 4 * nb * sizeof(int32_t)));
       HIPC(hipMemcpy(ctx->d_panel_blk, bp.data(), 4 * nb * sizeof(int32_t), hipMemcpyHostToDevice));
-      HIPC(hipMalloc(&ctx->d_panel_cnt, std::max<int64_t>(ncnt, 1) * sizeof(uint16_t)));
-      HIPC(hipMalloc(&ctx->d_panel_st, std::max<int64_t>(ncnt, 1) * sizeof(uint32_t)));
       CsrDev A2 = csr(ctx);
       if (panel_format(A2, ctx->d_panel_blk, R, nb, ctx->d_panel_cnt, ctx->d_panel_st, ncnt,
                        ctx->d_panel_col, ctx->d_panel_val, ctx->stream) != 0)
@@ -2130,12 +2146,7 @@ void free_matrix(rbl_ctx* ctx) {
   hipFree(ctx->d_tcmin); ctx->d_tcmin = nullptr;
   hipFree(ctx->d_tcmax); ctx->d_tcmax = nullptr;
   hipFree(ctx->d_tinfo); ctx->d_tinfo = nullptr;
-  hipFree(ctx->d_panel_blk); ctx->d_panel_blk = nullptr; ctx->panel_nblk = 0; ctx->panel_auto = false;
-  ctx->panel_span = 0;
-  hipFree(ctx->d_panel_cnt); ctx->d_panel_cnt = nullptr;
-  hipFree(ctx->d_panel_st); ctx->d_panel_st = nullptr;
-  hipFree(ctx->d_panel_col); ctx->d_panel_col = nullptr;
-  hipFree(ctx->d_panel_val); ctx->d_panel_val = nullptr;
+  free_panels(ctx);
   hipFree(ctx->d_bpos); ctx->d_bpos = nullptr;
   hipFree(ctx->d_bt); ctx->d_bt = nullptr;
   hipFree(ctx->d_bth); ctx->d_bth = nullptr;
