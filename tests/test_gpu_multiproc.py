@@ -47,6 +47,9 @@ CASES = [
      "steps": 10},
     {"name": "hw32", "matrix": "hashwindow", "n": 9000, "W": 64, "p": 0.7734, "seed": 41, "b": 32,
      "steps": 10, "bits": 32},
+    # a wide band (half-width 600): the column panels over the range halo (kernel 7)
+    {"name": "wide", "matrix": "hashwindow", "n": 40000, "W": 600, "p": 0.08, "seed": 43, "b": 32,
+     "steps": 8, "kid": 7},
     {"name": "rmat", **RM, "b": 32, "steps": 10},                    # indexed halo + overlap
     {"name": "rmat_seq", **RM, "b": 32, "steps": 10, "overlap": 0},  # exchange before the SpMM
     {"name": "rmat_pull", **RM, "b": 32, "steps": 10, "push": 0},     # pull-all indexed halo
@@ -169,6 +172,8 @@ def test_rccl_ranks_on_one_gpu(rccl_procs, single, inproc, case):
         assert np.abs(a - a1).max() <= tol * np.abs(a1).max()
     comm = [r[f"{case}__comm"] for r in res]
     assert all(cm[2] > 0 for cm in comm), "no halo exchange"
+    if c.get("kid") is not None:
+        assert all(int(r[f"{case}__kid"]) == c["kid"] for r in res), case
     if c.get("push") is not None:
         assert all(cm[2] == (c["steps"] + 1) * (2 if c["push"] else 1) for cm in comm)
 
@@ -233,6 +238,8 @@ def test_ranks_agree_and_match_inprocess_and_single(procs, single, inproc, case)
         assert kid == 6  # segmented gather with the indexed halo
     if case in ("rmat_b8", "rmat_gather"):
         assert kid == 1  # plain gather over the range halo of a ghost-built context
+    if c.get("kid") is not None:
+        assert all(int(r[f"{case}__kid"]) == c["kid"] for r in res), case
     if c.get("push") is not None:  # the halo plan asked for, with its moved-row count exact
         for cm in comm:
             assert cm[5] == c["push"]
