@@ -192,9 +192,11 @@ int rbl_set_option(rbl_ctx* ctx, int option, int64_t value);
 int rbl_device_memory(rbl_ctx* ctx, int64_t* free_bytes, int64_t* total_bytes);
 
 /* ---- matrix --------------------------------------------------------------------------
- * Replaces `Ag = adapt(CuArray, A)` (RBL_gpu.jl:209).  A is symmetric, so the CSC arrays
- * of Julia's SparseMatrixCSC{Float64,Int64} are the CSR arrays of A; `index_base` 1 accepts
- * them unchanged.  With nranks > 1 every rank passes the whole matrix and keeps the rows
+ * Replaces `Ag = adapt(CuArray, A)` (RBL_gpu.jl:209).  The arrays are read as A's rows (CSR).
+ * A is symmetric, so the CSC arrays of Julia's SparseMatrixCSC{Float64,Int64} are the CSR
+ * arrays of A; `index_base` 1 accepts them unchanged.  For an unsymmetric A (benchmark.jl:58)
+ * pass the CSC arrays of A^T — its CSR arrays — so the device computes A Q as cuSPARSE does
+ * (julia/RBL_hip.jl and rbl.Context.set_matrix both do).  With nranks > 1 every rank passes the whole matrix and keeps the rows
  * [row_begin,row_end) of the nnz-balanced partition (rbl_plan_row_partition). */
 int rbl_set_matrix_csc(rbl_ctx* ctx, int64_t n, int64_t nnz, const int64_t* colptr,
                        const int64_t* rowval, const double* nzval, int index_base);
