@@ -48,7 +48,7 @@ struct rbl_ctx {
   double* d_panel_val = nullptr;    //   and value
   int64_t panel_nblk = 0;
   int panel_rpg = 4;        // rows per 16-lane group: blocks of 64 panel_rpg rows
-  int panel_ch = 32;        // records per row and chunk load
+  int panel_ch = 48;        // records per row and chunk load
   bool panel_auto = false;  // chosen by default: every staged Q row used >= 4 times on average
   int64_t panel_span = 0;   // the widest block window, Q rows
   uint16_t* d_bpos = nullptr;  // band kernel: per-nonzero dense-tile positions
@@ -1135,14 +1135,14 @@ int prepare_window_formats(rbl_ctx* ctx, const std::vector<int64_t>& rp) {
     int64_t maxp = 0, staged = 0;
     plan(512, nullptr, &maxp, &staged);
     // the kernel's shape by the mean count per row and panel at 512-row blocks: 8 rows per
-    // group with 16-record chunks up to a mean of 16, else 4 rows per group with 32-record
-    // chunks (profiles/r06_panel_shape_sweep_b13.txt)
+    // group with 16-record chunks up to a mean of 16, else 4 rows per group with 48-record
+    // chunks (the three shapes forced at H = 128..2048: profiles/r06_panel_shapes_b30.txt)
     const double mean_cnt = (double)ctx->nnz / std::max(1.0, (double)(staged / pw) * 512);
 #ifdef RBL_PANEL_RPG  // (probe builds: tools/build_variant.sh-style A/B of the kernel shape)
     const int rpg = RBL_PANEL_RPG, pch = RBL_PANEL_CH;
 #else
     const int rpg = mean_cnt <= 16.0 ? 8 : 4;
-    const int pch = rpg == 8 ? 16 : 32;
+    const int pch = rpg == 8 ? 16 : 48;
 #endif
     const int R = 64 * rpg;
     std::vector<int32_t> bp;

@@ -359,8 +359,9 @@ __global__ __launch_bounds__(pnl::kThreads) void k_spmm_panel(PanelArgs a) {
     // would wait vmcnt(0) for an ordinary load behind the in-flight DMA, draining the next
     // step's record loads; the epilogue waits vmcnt(kVm) for these itself (the record loads of
     // (3), kVm of them, are the only younger vector-memory ops; the "memory" clobbers keep them
-    // on their side of both asm statements).
-    constexpr bool kQpEarly = EPI && RPG == 4;
+    // on their side of both asm statements).  Not with 48-record chunks: their registers
+    // (128 VGPRs without these; 64 B of scratch with them).
+    constexpr bool kQpEarly = EPI && RPG == 4 && CH <= 32;
     d2v qpe[kQpEarly ? RPG : 1];
     if constexpr (kQpEarly) {
 #pragma unroll
@@ -559,7 +560,9 @@ __global__ __launch_bounds__(pnl::kThreads) void k_spmm_panel(PanelArgs a) {
 }
 
 // RPG / CH by the format's mean count per row and panel (rbl_api.cpp, prepare_window_formats):
-// <8, 16> up to 16, <4, 32> beyond (<8, 32> needs more than 128 VGPRs with the quad read-ahead)
+// <8, 16> up to 16, <4, 48> beyond (<8, 32> needs more than 128 VGPRs with the quad read-ahead;
+// <4, 48> against <4, 32>: a row's ~25-50 entries per panel at half-widths 128-512 in one chunk
+// instead of a chunk and a reload, 0.5-2.4 % faster, profiles/r06_panel_shapes_b30.txt)
 bool spmm_panel(const CsrDev& A, const double* Qin, int64_t col_off, int b, double* U,
                 const double* Qprev, const double* Bi, hipStream_t s) {
   if (b != 32 || !A.panel_blk || A.panel_nblk <= 0 || !A.panel_cnt || !A.panel_st || !A.panel_col ||
@@ -597,7 +600,7 @@ bool spmm_panel(const CsrDev& A, const double* Qin, int64_t col_off, int b, doub
   if (A.panel_rpg == 8) {
     if (Qprev) go(&k_spmm_panel<true, 8, 16>); else go(&k_spmm_panel<false, 8, 16>);
   } else {
-    if (Qprev) go(&k_spmm_panel<true, 4, 32>); else go(&k_spmm_panel<false, 4, 32>);
+    if (Qprev) go(&k_spmm_panel<true, 4, 48>); else go(&k_spmm_panel<false, 4, 48>);
   }
   return true;
 }
